@@ -1,0 +1,223 @@
+"""Benchmark: NN queries/s + motion checks/s on a 10^6-state SE(3) tree (BASELINE.json).
+
+Workload (BASELINE.json configs[2]): an SE(3) tree of 10^6 states
+(translation in [0,1]^3, uniform rotations, seed 42) resident in HBM; per GPU a batch of
+10^5 sampled states (the RRT* sampling step).  One step = for every sample
+    nearestK(k=10)                                   (NearestNeighborsGNAT.h:222-233)
+    steer from its nearest to range 0.2*extent        (RRT.cpp:137-146)
+    checkMotion(nearest, steered) with the HypercubeBenchmark predicate on the
+    translation, resolution 0.01                      (DiscreteMotionValidator.cpp:93-145)
+all on device, inputs resident in HBM.  value = (NN queries + motion checks) per second
+over all ranks.  Multi-GPU: the tree is replicated, samples are sharded (weak scaling,
+no collective in the data path).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "NN queries/sec + motion checks/sec on 10^6-state SE(3) tree"
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector/matrix peak (MI355X_MICROARCH.md)
+F_SE3 = 21                # flops per SE(3) distance, SURVEY.md §8d (sqrt, acos counted as 1 each)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--tree", type=int, default=1_000_000)
+    ap.add_argument("--queries", type=int, default=100_000, help="samples per GPU per step")
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    return ap.parse_args()
+
+
+def cpu_baseline(sp, ck, tree, rng, k, budget_s):
+    """The oracle's GNAT restatement (reference defaults, 1 thread) + oracle motion checks,
+    timed on a bounded sample of the same workload on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+
+    from ompl_amd import workloads as W
+
+    g = O.Gnat(sp)
+    t0 = time.perf_counter()
+    g.add(tree)
+    build_s = time.perf_counter() - t0
+    nq = 500
+    q = W.uniform_se3(rng, nq)
+    t0 = time.perf_counter()
+    ids, _, _ = g.knn(q, k)
+    t_probe = time.perf_counter() - t0
+    nq = int(min(20000, max(nq, 0.6 * budget_s / max(t_probe / nq, 1e-9))))
+    q = W.uniform_se3(rng, nq)
+    t0 = time.perf_counter()
+    ids, d, _ = g.knn(q, k)
+    t_nn = time.perf_counter() - t0
+    maxd = 0.2 * sp.getMaximumExtent()
+    s1 = tree[ids[:, 0].astype(np.int64)]
+    s2 = np.empty_like(q)
+    for i in range(nq):  # steering is not timed on the CPU side (favours the CPU)
+        s2[i] = O.interpolate(sp, s1[i], q[i], maxd / d[i, 0]) if d[i, 0] > maxd else q[i]
+    reps = 1
+    t0 = time.perf_counter()
+    O.check_motions_mt(sp, ck, s1, s2, 1)
+    t_mv = time.perf_counter() - t0
+    if t_mv < 0.3 * budget_s:
+        reps = int(max(1, 0.3 * budget_s / max(t_mv, 1e-9)))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            O.check_motions_mt(sp, ck, s1, s2, 1)
+        t_mv = (time.perf_counter() - t0) / reps
+    qps = nq / t_nn
+    mps = nq / t_mv
+    value = 2.0 / (1.0 / qps + 1.0 / mps)  # same op mix as one GPU step: 1 query + 1 motion check
+    return {
+        "value": value, "unit": "(NN queries + motion checks)/s", "cores": 1, "kind": "port",
+        "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same 10^6-state "
+                   f"SE(3) tree, {nq} nearestK(k={k}) queries; {nq} checkMotion(nearest, steered) x{reps} "
+                   f"with the oracle DiscreteMotionValidator; index build {build_s:.2f} s excluded"),
+        "nn_queries_per_s": qps, "motion_checks_per_s": mps,
+    }
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    from ompl_amd import DiscreteMotionValidatorGPU, NearestNeighborsGPU
+    from ompl_amd import workloads as W
+    from ompl_amd.checkers import HypercubeChecker
+    from ompl_amd.spaces import SE3StateSpace
+
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+    sp = SE3StateSpace(0.0, 1.0)
+    ck = HypercubeChecker(3, 0.1)
+    tree = W.uniform_se3(np.random.default_rng(42), args.tree)      # identical on every rank
+    qrng = np.random.default_rng(1000 + rank)                         # samples sharded by rank
+    nq, k = args.queries, args.k
+    queries = torch.from_numpy(W.uniform_se3(qrng, nq)).to(dev)
+
+    nn = NearestNeighborsGPU(sp, local)
+    nn.add(tree)
+    mv = DiscreteMotionValidatorGPU(sp, ck, local)
+    nn.set_stream(stream.cuda_stream)
+    mv.set_stream(stream.cuda_stream)
+    ids = torch.empty((nq, k), dtype=torch.int32, device=dev)
+    dd = torch.empty((nq, k), dtype=torch.float64, device=dev)
+    s_from = torch.empty_like(queries)
+    s_to = torch.empty_like(queries)
+    valid = torch.empty(nq, dtype=torch.uint8, device=dev)
+    maxd = 0.2 * sp.getMaximumExtent()  # RRT range default (SelfConfig.cpp:98)
+
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+
+    def step(e=None):
+        if e:
+            e[0].record(stream)
+        nn.knn_device(queries.data_ptr(), nq, k, ids.data_ptr(), dd.data_ptr())
+        if e:
+            e[1].record(stream)
+        nn.steer_device(queries.data_ptr(), nq, ids.data_ptr(), k, maxd, s_from.data_ptr(), s_to.data_ptr())
+        if e:
+            e[2].record(stream)
+        mv.check_device(s_from.data_ptr(), s_to.data_ptr(), nq, valid.data_ptr())
+        if e:
+            e[3].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(ev[s])
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    knn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    steer_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    mv_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
+    t = torch.tensor([elapsed, knn_ms, steer_ms, mv_ms], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, knn_ms, steer_ms, mv_ms = t.tolist()
+    valid_frac = float(valid.float().mean().item())
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(sp, ck, tree, np.random.default_rng(7), k, args.cpu_seconds)
+
+    if rank == 0:
+        total_ops = 2.0 * nq * world * args.steps
+        value = total_ops / elapsed
+        flops = float(nq) * args.tree * F_SE3
+        achieved = flops / (knn_ms * 1e-3) / 1e12
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "(NN queries + motion checks)/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (uniform SE(3) states, seeded; tree seed 42, samples seed 1000+rank)",
+            "config": {
+                "workload": "configs[2]: SE(3) RRT*-style batch — nearestK(k=10) + steer + checkMotion "
+                            "(HypercubeBenchmark predicate on translation, edgeWidth 0.1, resolution 0.01)",
+                "tree_states": args.tree, "samples_per_gpu": nq, "k": k, "state_space": "SE3 [0,1]^3",
+                "parallelism": f"samples sharded over {world} GPU(s), tree replicated",
+            },
+            "nn_queries_per_s": nq * world / (knn_ms * 1e-3),
+            "motion_checks_per_s": nq * world / (mv_ms * 1e-3),
+            "phase_ms": {"knn": knn_ms, "steer": steer_ms, "motion": mv_ms},
+            "motion_valid_fraction": valid_frac,
+            "roofline": {
+                "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                "kernel": "knn_tiled_kernel<SE3,7,0,16> + knn_merge_kernel<16> (fp64 VALU-bound)",
+                "algorithmic": f"{nq} x {args.tree} pairs x {F_SE3} flops per launch",
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,194 @@
+/*
+ * ompl_gpu.h — C ABI of the MI355X (gfx950) backend for OMPL's data-parallel
+ * inner loops: NearestNeighbors queries and DiscreteMotionValidator sweeps.
+ *
+ * The ABI is plain C: pointers, sizes and status codes; no C++ or torch types.
+ * It is what the C++ plugin classes in include/ompl_amd/ (drop-ins for the
+ * reference's ompl::NearestNeighbors<_T> and ompl::base::MotionValidator)
+ * call, and what a ctypes / cgo / JNI binding would bind.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference repo, OMPL 1.6.0):
+ *   ompl_gpu_nn_add        NearestNeighbors<_T>::add(data) / add(vector)
+ *                          src/ompl/datastructures/NearestNeighbors.h:76-85,
+ *                          NearestNeighborsGNAT.h:147-176
+ *   ompl_gpu_nn_remove     NearestNeighbors<_T>::remove          NearestNeighbors.h:88,
+ *                          NearestNeighborsGNAT.h:190-207
+ *   ompl_gpu_nn_clear      NearestNeighbors<_T>::clear           NearestNeighbors.h:73
+ *   ompl_gpu_nn_size       NearestNeighbors<_T>::size            NearestNeighbors.h:107
+ *   ompl_gpu_nn_knn        nearest (k=1) / nearestK              NearestNeighbors.h:91-98,
+ *                          NearestNeighborsGNAT.h:209-233, NearestNeighborsLinear.h:98-131
+ *   ompl_gpu_nn_radius     nearestR                              NearestNeighbors.h:100-105,
+ *                          NearestNeighborsGNAT.h:236-245, NearestNeighborsLinear.h:135-142
+ *   ompl_gpu_mv_check      DiscreteMotionValidator::checkMotion(s1,s2) and
+ *                          checkMotion(s1,s2,lastValid)
+ *                          src/ompl/base/src/DiscreteMotionValidator.cpp:48-145
+ *   ompl_gpu_mv_counters   MotionValidator::getValidMotionCount/getInvalidMotionCount
+ *                          src/ompl/base/MotionValidator.h:102-139
+ *   ompl_gpu_svc_check     StateValidityChecker::isValid         src/ompl/base/StateValidityChecker.h:111
+ *   ompl_gpu_steer_device  the RRT extend step (nearest -> interpolate to range)
+ *                          src/ompl/geometric/planners/rrt/src/RRT.cpp:137-146
+ *
+ * Distances are the reference's fp64 formulas in the reference's operation
+ * order (StateSpace.cpp:1068-1076, RealVectorStateSpace.cpp:230-242,
+ * SO3StateSpace.cpp:254-262, demos/KinematicChain.h:105-124).
+ *
+ * State layout across the ABI: AoS rows of `dim` doubles (OMPL copyToReals
+ * order): R^n -> n values; SO3 -> qx,qy,qz,qw; SE3 -> x,y,z,qx,qy,qz,qw;
+ * KCHAIN -> n joint angles.  Ids are insertion indices (0,1,2,...).
+ *
+ * Errors: every call returns ompl_gpu_status and never throws or aborts;
+ * ompl_gpu_last_error() gives the thread's last message.  nearest on an empty
+ * set returns OMPL_GPU_ERR_EMPTY, which the C++ wrapper turns into the
+ * reference's ompl::Exception("No elements found in nearest neighbors data
+ * structure") (NearestNeighborsGNAT.h:218).
+ *
+ * Threading: one handle = one device + one HIP stream + an internal mutex;
+ * const queries on one handle from several threads are serialised safely.
+ * add/remove need external exclusion as in the reference (pRRT.cpp:119-141).
+ */
+#ifndef OMPL_GPU_H
+#define OMPL_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMPL_GPU_ABI_VERSION 1
+
+typedef enum ompl_gpu_status {
+    OMPL_GPU_OK = 0,
+    OMPL_GPU_ERR_INVALID_ARG = 1,
+    OMPL_GPU_ERR_EMPTY = 2,       /* "No elements found in nearest neighbors data structure" */
+    OMPL_GPU_ERR_DEVICE = 3,      /* HIP runtime error / no device */
+    OMPL_GPU_ERR_OOM = 4,
+    OMPL_GPU_ERR_UNSUPPORTED = 5, /* e.g. k above the largest compiled bucket */
+    OMPL_GPU_ERR_NOT_FOUND = 6    /* remove() of an unknown / already removed id */
+} ompl_gpu_status;
+
+/* ---- state spaces (closed set of device metrics) --------------------------
+ * REALVECTOR : RealVectorStateSpace(n)                 RealVectorStateSpace.cpp:230-265
+ * SO3        : SO3StateSpace                           SO3StateSpace.cpp:254-318
+ * SE3        : SE3StateSpace = R^3 (w0) + SO3 (w1)     SE3StateSpace.h:114-121, StateSpace.cpp:1068-1116
+ * KCHAIN     : KinematicChainSpace(n, linkLength)      demos/KinematicChain.h:87-175
+ */
+enum {
+    OMPL_GPU_SPACE_REALVECTOR = 0,
+    OMPL_GPU_SPACE_SO3 = 1,
+    OMPL_GPU_SPACE_SE3 = 2,
+    OMPL_GPU_SPACE_KCHAIN = 3
+};
+
+typedef struct ompl_gpu_space {
+    int32_t kind;
+    int32_t dim;          /* reals per state: n, 4 (SO3), 7 (SE3) */
+    double weight[2];     /* SE3 component weights (CompoundStateSpace::weights_), normally {1,1} */
+    double lvs[2];        /* longestValidSegment_ per component: [0] R^n / chain / SE3's R^3, [1] SE3's SO3 */
+    uint32_t factor[2];   /* longestValidSegmentCountFactor_ per component (StateSpace.cpp:851-854) */
+    double link_length;   /* KCHAIN only */
+} ompl_gpu_space;
+
+/* ---- device validity checkers (closed set) --------------------------------
+ * ALL_VALID : AllValidStateValidityChecker            StateValidityChecker.h:165-183
+ * HYPERCUBE : narrow-passage hypercube on the first ndim reals
+ *                                                     demos/HypercubeBenchmark.cpp:57-72
+ * SPHERES   : 3-D sphere obstacles on the first 3 reals (SE3 translation); the
+ *             3-D extension of Circles2D::noOverlap   tests/resources/circles2D.h:139-150
+ * KCHAIN    : KinematicChainValidityChecker           demos/KinematicChain.h:193-277
+ * CIRCLES2D : Circles2D::noOverlap on (x,y)            tests/resources/circles2D.h:139-150
+ */
+enum {
+    OMPL_GPU_CHECK_ALL_VALID = 0,
+    OMPL_GPU_CHECK_HYPERCUBE = 1,
+    OMPL_GPU_CHECK_SPHERES = 2,
+    OMPL_GPU_CHECK_KCHAIN = 3,
+    OMPL_GPU_CHECK_CIRCLES2D = 4
+};
+
+typedef struct ompl_gpu_checker {
+    int32_t kind;
+    int32_t ndim;         /* HYPERCUBE: number of leading reals tested */
+    double edge_width;    /* HYPERCUBE */
+    int32_t count;        /* SPHERES / CIRCLES2D: obstacles; KCHAIN: environment segments */
+    int32_t reserved;
+    const double *data;   /* SPHERES: count x (cx,cy,cz,r^2); CIRCLES2D: count x (x,y,r^2);
+                             KCHAIN: count x (x0,y0,x1,y1).  Copied at create time. */
+} ompl_gpu_checker;
+
+typedef struct ompl_gpu_nn ompl_gpu_nn;
+typedef struct ompl_gpu_mv ompl_gpu_mv;
+
+/* ---- library ---------------------------------------------------------------- */
+int ompl_gpu_abi_version(void);
+const char *ompl_gpu_last_error(void);
+ompl_gpu_status ompl_gpu_device_count(int *count);
+void ompl_gpu_free(void *p); /* frees buffers the library returned (radius CSR) */
+
+/* ---- nearest neighbours ----------------------------------------------------- */
+ompl_gpu_status ompl_gpu_nn_create(ompl_gpu_nn **out, const ompl_gpu_space *space, int device);
+ompl_gpu_status ompl_gpu_nn_destroy(ompl_gpu_nn *h);
+/* Launch on a caller-owned hipStream_t (NULL restores the handle's own stream). */
+ompl_gpu_status ompl_gpu_nn_set_stream(ompl_gpu_nn *h, void *hip_stream);
+ompl_gpu_status ompl_gpu_nn_sync(ompl_gpu_nn *h);
+/* Append n AoS states; *first_id (may be NULL) receives the id of the first one. */
+ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, uint64_t *first_id);
+ompl_gpu_status ompl_gpu_nn_remove(ompl_gpu_nn *h, uint64_t id);
+ompl_gpu_status ompl_gpu_nn_clear(ompl_gpu_nn *h);
+ompl_gpu_status ompl_gpu_nn_size(const ompl_gpu_nn *h, size_t *live, size_t *total);
+/* Copy back the stored states (AoS), ids [first, first+n). */
+ompl_gpu_status ompl_gpu_nn_get_states(ompl_gpu_nn *h, uint64_t first, size_t n, double *out);
+/* k nearest per query, host buffers, synchronous.  Results sorted by
+ * (distance, id) ascending; out_ids/out_dist are nq x k, out_cnt[q] = number
+ * of valid results (min(k, live)).  k == 0 returns counts of 0.  With no live
+ * element, counts are 0 and the call returns OMPL_GPU_ERR_EMPTY only if k==1
+ * was requested through ompl_gpu_nn_nearest. */
+ompl_gpu_status ompl_gpu_nn_knn(ompl_gpu_nn *h, const double *queries, size_t nq, uint32_t k,
+                                uint64_t *out_ids, double *out_dist, uint32_t *out_cnt);
+ompl_gpu_status ompl_gpu_nn_nearest(ompl_gpu_nn *h, const double *queries, size_t nq,
+                                    uint64_t *out_ids, double *out_dist);
+/* All elements with distance <= r (inclusive), sorted by (distance, id).
+ * *ids / *dists are library-allocated CSR payloads (free with ompl_gpu_free);
+ * offsets has nq+1 entries. */
+ompl_gpu_status ompl_gpu_nn_radius(ompl_gpu_nn *h, const double *queries, size_t nq, double r,
+                                   uint64_t **ids, double **dists, uint64_t *offsets);
+/* Device-resident variants: all pointers are device memory, the call is
+ * asynchronous on the handle's stream.  queries are AoS fp64; ids are uint32
+ * (0xFFFFFFFF = no result); dist fp64. */
+ompl_gpu_status ompl_gpu_nn_knn_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, uint32_t k,
+                                       uint32_t *d_ids, double *d_dist);
+/* RRT extend on device: for each query q with nearest id nid[q*stride]:
+ * from = state[nid]; to = q; if d(from,q) > max_distance, to = interpolate(from,
+ * q, max_distance/d).  Writes AoS from/to rows (RRT.cpp:137-146). */
+ompl_gpu_status ompl_gpu_steer_device(ompl_gpu_nn *h, const double *d_queries, size_t nq,
+                                      const uint32_t *d_nearest, uint32_t stride, double max_distance,
+                                      double *d_from, double *d_to);
+
+/* ---- motion validation ------------------------------------------------------ */
+ompl_gpu_status ompl_gpu_mv_create(ompl_gpu_mv **out, const ompl_gpu_space *space,
+                                   const ompl_gpu_checker *checker, int device);
+ompl_gpu_status ompl_gpu_mv_destroy(ompl_gpu_mv *h);
+ompl_gpu_status ompl_gpu_mv_set_stream(ompl_gpu_mv *h, void *hip_stream);
+ompl_gpu_status ompl_gpu_mv_sync(ompl_gpu_mv *h);
+/* m edges (s1[i] -> s2[i]), host AoS.  valid[i] = checkMotion(s1,s2) (s1 is
+ * assumed valid and never checked, DiscreteMotionValidator.cpp:95-96);
+ * nd[i] = validSegmentCount; first_invalid[i] = first invalid sample of the
+ * lastValid variant (j in [1,nd-1]; nd when only s2 fails; -1 when valid).
+ * nd / first_invalid may be NULL.  Updates the valid/invalid counters. */
+ompl_gpu_status ompl_gpu_mv_check(ompl_gpu_mv *h, const double *s1, const double *s2, size_t m,
+                                  uint8_t *valid, int32_t *nd, int32_t *first_invalid);
+ompl_gpu_status ompl_gpu_mv_check_device(ompl_gpu_mv *h, const double *d_s1, const double *d_s2, size_t m,
+                                         uint8_t *d_valid, int32_t *d_nd, int32_t *d_first_invalid);
+ompl_gpu_status ompl_gpu_mv_counters(ompl_gpu_mv *h, uint64_t *valid, uint64_t *invalid);
+ompl_gpu_status ompl_gpu_mv_reset_counters(ompl_gpu_mv *h);
+/* total isValid() evaluations the bisection variant made (the reference's work). */
+ompl_gpu_status ompl_gpu_mv_state_checks(ompl_gpu_mv *h, uint64_t *checks);
+/* isValid per state (host AoS). */
+ompl_gpu_status ompl_gpu_svc_check(ompl_gpu_mv *h, const double *states, size_t m, uint8_t *valid);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OMPL_GPU_H */

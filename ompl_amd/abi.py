@@ -1,0 +1,138 @@
+"""ctypes binding of the C ABI in include/ompl_gpu.h (libompl_gpu.so).
+
+The library is the product path: there is no CPU fallback.  If the shared
+object is missing this module raises at import time; if no HIP device is present
+every handle constructor raises :class:`GpuError` (``OMPL_GPU_ERR_DEVICE``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("OMPL_GPU_LIB", os.path.join(HERE, "lib", "libompl_gpu.so"))
+
+# ---- enums (include/ompl_gpu.h) ------------------------------------------------
+OK, ERR_INVALID_ARG, ERR_EMPTY, ERR_DEVICE, ERR_OOM, ERR_UNSUPPORTED, ERR_NOT_FOUND = range(7)
+SPACE_REALVECTOR, SPACE_SO3, SPACE_SE3, SPACE_KCHAIN = range(4)
+CHECK_ALL_VALID, CHECK_HYPERCUBE, CHECK_SPHERES, CHECK_KCHAIN, CHECK_CIRCLES2D = range(5)
+NO_ID32 = 0xFFFFFFFF
+NO_ID64 = 0xFFFFFFFFFFFFFFFF
+
+
+class SpaceStruct(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("dim", C.c_int32),
+        ("weight", C.c_double * 2),
+        ("lvs", C.c_double * 2),
+        ("factor", C.c_uint32 * 2),
+        ("link_length", C.c_double),
+    ]
+
+
+class CheckerStruct(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("ndim", C.c_int32),
+        ("edge_width", C.c_double),
+        ("count", C.c_int32),
+        ("reserved", C.c_int32),
+        ("data", C.POINTER(C.c_double)),
+    ]
+
+
+class GpuError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"[ompl_gpu status {status}] {msg}")
+        self.status = status
+
+
+class EmptyError(GpuError):
+    """Raised where the reference throws ompl::Exception("No elements found in
+    nearest neighbors data structure") (NearestNeighborsGNAT.h:218)."""
+
+
+_P = C.c_void_p
+_D = C.POINTER(C.c_double)
+_U8 = C.POINTER(C.c_uint8)
+_U32 = C.POINTER(C.c_uint32)
+_I32 = C.POINTER(C.c_int32)
+_U64 = C.POINTER(C.c_uint64)
+
+# name -> (restype, argtypes); every symbol include/ompl_gpu.h declares
+SIGNATURES = {
+    "ompl_gpu_abi_version": (C.c_int, []),
+    "ompl_gpu_last_error": (C.c_char_p, []),
+    "ompl_gpu_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "ompl_gpu_free": (None, [_P]),
+    "ompl_gpu_nn_create": (C.c_int, [C.POINTER(_P), C.POINTER(SpaceStruct), C.c_int]),
+    "ompl_gpu_nn_destroy": (C.c_int, [_P]),
+    "ompl_gpu_nn_set_stream": (C.c_int, [_P, _P]),
+    "ompl_gpu_nn_sync": (C.c_int, [_P]),
+    "ompl_gpu_nn_add": (C.c_int, [_P, _D, C.c_size_t, _U64]),
+    "ompl_gpu_nn_remove": (C.c_int, [_P, C.c_uint64]),
+    "ompl_gpu_nn_clear": (C.c_int, [_P]),
+    "ompl_gpu_nn_size": (C.c_int, [_P, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "ompl_gpu_nn_get_states": (C.c_int, [_P, C.c_uint64, C.c_size_t, _D]),
+    "ompl_gpu_nn_knn": (C.c_int, [_P, _D, C.c_size_t, C.c_uint32, _U64, _D, _U32]),
+    "ompl_gpu_nn_nearest": (C.c_int, [_P, _D, C.c_size_t, _U64, _D]),
+    "ompl_gpu_nn_radius": (C.c_int, [_P, _D, C.c_size_t, C.c_double, C.POINTER(_U64), C.POINTER(_D), _U64]),
+    "ompl_gpu_nn_knn_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P]),
+    "ompl_gpu_steer_device": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_uint32, C.c_double, _P, _P]),
+    "ompl_gpu_mv_create": (C.c_int, [C.POINTER(_P), C.POINTER(SpaceStruct), C.POINTER(CheckerStruct), C.c_int]),
+    "ompl_gpu_mv_destroy": (C.c_int, [_P]),
+    "ompl_gpu_mv_set_stream": (C.c_int, [_P, _P]),
+    "ompl_gpu_mv_sync": (C.c_int, [_P]),
+    "ompl_gpu_mv_check": (C.c_int, [_P, _D, _D, C.c_size_t, _U8, _I32, _I32]),
+    "ompl_gpu_mv_check_device": (C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, _P]),
+    "ompl_gpu_mv_counters": (C.c_int, [_P, _U64, _U64]),
+    "ompl_gpu_mv_reset_counters": (C.c_int, [_P]),
+    "ompl_gpu_mv_state_checks": (C.c_int, [_P, _U64]),
+    "ompl_gpu_svc_check": (C.c_int, [_P, _D, C.c_size_t, _U8]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"ompl_amd: {LIB_PATH} is missing — build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback for the GPU backend)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(status: int) -> None:
+    if status != OK:
+        msg = (lib.ompl_gpu_last_error() or b"").decode(errors="replace")
+        if status == ERR_EMPTY:
+            raise EmptyError(status, msg)
+        raise GpuError(status, msg)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    st = lib.ompl_gpu_device_count(C.byref(n))
+    return n.value if st == OK else 0
+
+
+def dptr(a: np.ndarray):
+    return a.ctypes.data_as(_D)
+
+
+def as_states(x, dim: int) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    if a.ndim == 1:
+        a = a.reshape(1, -1)
+    if a.shape[-1] != dim:
+        raise ValueError(f"expected states with {dim} reals, got shape {a.shape}")
+    return a

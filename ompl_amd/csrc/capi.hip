@@ -1,0 +1,656 @@
+// capi.hip — implementation of the C ABI declared in include/ompl_gpu.h.
+//
+// Device data layout (HBM):
+//   feat : SoA [F][cap] fp64 feature rows of the stored states (kernels.h FeatGeom),
+//          cap a multiple of kTile; unused / removed slots hold NaN so the kernels
+//          never need bounds or liveness checks (a NaN distance is never selected).
+//   raw  : SoA [dim][cap] raw states for KCHAIN (for the other spaces raw == feat).
+// Ids are insertion indices, as the reference NN stores copies of _T in insertion
+// order (NearestNeighborsLinear.h:78-88); the C++ wrapper maps id <-> _T.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ompl_gpu.h"
+#include "kernels.h"
+#include "topk.h"
+
+using namespace ompl_amd;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+ompl_gpu_status fail(ompl_gpu_status s, const std::string &msg) {
+    g_last_error = msg;
+    return s;
+}
+
+#define HIP_OR_FAIL(expr)                                                                              \
+    do {                                                                                               \
+        hipError_t _e = (expr);                                                                        \
+        if (_e != hipSuccess) {                                                                        \
+            return fail(_e == hipErrorOutOfMemory ? OMPL_GPU_ERR_OOM : OMPL_GPU_ERR_DEVICE,            \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                            \
+        }                                                                                              \
+    } while (0)
+
+bool space_ok(const ompl_gpu_space *s, DevSpace *d, FeatGeom *g) {
+    if (!s) return false;
+    d->kind = s->kind;
+    d->dim = s->dim;
+    d->w0 = s->weight[0];
+    d->w1 = s->weight[1];
+    d->lvs0 = s->lvs[0];
+    d->lvs1 = s->lvs[1];
+    d->f0 = s->factor[0] ? s->factor[0] : 1;
+    d->f1 = s->factor[1] ? s->factor[1] : 1;
+    d->link = s->link_length;
+    if (d->dim > kChainMaxLinks) return false;
+    return feature_geometry(*d, g);
+}
+
+// grow-only device buffer
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t b) {
+        if (b <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t nb = std::max(b, (size_t)4096);
+        hipError_t e = hipMalloc(&p, nb);
+        if (e == hipSuccess) bytes = nb;
+        return e;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+int cu_count(int device) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 256;
+    return prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+}
+
+}  // namespace
+
+struct ompl_gpu_nn {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t own = nullptr, stream = nullptr;
+    DevSpace sp{};
+    FeatGeom g{};
+    double *feat = nullptr;  // [F][cap]
+    double *raw = nullptr;   // [dim][cap] (KCHAIN) or == feat
+    uint64_t cap = 0, n_total = 0, n_live = 0;
+    std::vector<uint8_t> removed;
+    std::mutex mu;
+    DevBuf q, out_d, out_i, ws, stage, counts, offsets, ids, dists, sorted_ids, sorted_d, tmp;
+    std::vector<double> hfeat;
+};
+
+struct ompl_gpu_mv {
+    int device = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    DevSpace sp{};
+    FeatGeom g{};
+    DevChecker ck{};
+    double *ck_data = nullptr;
+    unsigned long long *counters = nullptr;  // valid, invalid, isValid calls
+    std::mutex mu;
+    DevBuf s1, s2, valid, nd, fi;
+};
+
+extern "C" {
+
+int ompl_gpu_abi_version(void) { return OMPL_GPU_ABI_VERSION; }
+
+const char *ompl_gpu_last_error(void) { return g_last_error.c_str(); }
+
+ompl_gpu_status ompl_gpu_device_count(int *count) {
+    if (!count) return fail(OMPL_GPU_ERR_INVALID_ARG, "count is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *count = e == hipSuccess ? c : 0;
+    return e == hipSuccess ? OMPL_GPU_OK : fail(OMPL_GPU_ERR_DEVICE, hipGetErrorString(e));
+}
+
+void ompl_gpu_free(void *p) { std::free(p); }
+
+// ------------------------------------------------------------------------------ NN
+
+ompl_gpu_status ompl_gpu_nn_create(ompl_gpu_nn **out, const ompl_gpu_space *space, int device) {
+    if (!out) return fail(OMPL_GPU_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    DevSpace sp;
+    FeatGeom g;
+    if (!space_ok(space, &sp, &g)) return fail(OMPL_GPU_ERR_UNSUPPORTED, "unsupported state space");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(OMPL_GPU_ERR_DEVICE, "no such HIP device");
+    HIP_OR_FAIL(hipSetDevice(device));
+    auto *h = new ompl_gpu_nn();
+    h->device = device;
+    h->num_cus = cu_count(device);
+    h->sp = sp;
+    h->g = g;
+    hipError_t e = hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete h;
+        return fail(OMPL_GPU_ERR_DEVICE, hipGetErrorString(e));
+    }
+    h->stream = h->own;
+    *out = h;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_destroy(ompl_gpu_nn *h) {
+    if (!h) return OMPL_GPU_OK;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    if (h->raw && h->raw != h->feat) (void)hipFree(h->raw);
+    if (h->feat) (void)hipFree(h->feat);
+    if (h->own) (void)hipStreamDestroy(h->own);
+    delete h;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_set_stream(ompl_gpu_nn *h, void *s) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->stream = s ? (hipStream_t)s : h->own;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_sync(ompl_gpu_nn *h) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
+static ompl_gpu_status grow(ompl_gpu_nn *h, uint64_t need) {
+    if (need <= h->cap) return OMPL_GPU_OK;
+    uint64_t nc = std::max<uint64_t>(h->cap * 2, need);
+    nc = std::max<uint64_t>(nc, 4096);
+    nc = (nc + kTile - 1) / kTile * kTile;
+    const int F = h->g.F;
+    const bool sep_raw = h->sp.kind == OMPL_GPU_SPACE_KCHAIN;
+    double *nf = nullptr, *nr = nullptr;
+    HIP_OR_FAIL(hipMalloc(&nf, sizeof(double) * F * nc));
+    HIP_OR_FAIL(hipMemsetAsync(nf, 0xFF, sizeof(double) * F * nc, h->stream));  // all-ones = NaN
+    if (sep_raw) {
+        HIP_OR_FAIL(hipMalloc(&nr, sizeof(double) * h->sp.dim * nc));
+        HIP_OR_FAIL(hipMemsetAsync(nr, 0xFF, sizeof(double) * h->sp.dim * nc, h->stream));
+    }
+    if (h->n_total) {
+        HIP_OR_FAIL(hipMemcpy2DAsync(nf, nc * sizeof(double), h->feat, h->cap * sizeof(double),
+                                     h->n_total * sizeof(double), F, hipMemcpyDeviceToDevice, h->stream));
+        if (sep_raw)
+            HIP_OR_FAIL(hipMemcpy2DAsync(nr, nc * sizeof(double), h->raw, h->cap * sizeof(double),
+                                         h->n_total * sizeof(double), h->sp.dim, hipMemcpyDeviceToDevice,
+                                         h->stream));
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (h->raw && h->raw != h->feat) (void)hipFree(h->raw);
+    if (h->feat) (void)hipFree(h->feat);
+    h->feat = nf;
+    h->raw = sep_raw ? nr : nf;
+    h->cap = nc;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, uint64_t *first_id) {
+    if (!h || (n && !states)) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    if (first_id) *first_id = h->n_total;
+    if (n == 0) return OMPL_GPU_OK;
+    if (h->n_total + n > 0xFFFFFFF0ull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "more than 2^32-16 states");
+    ompl_gpu_status s = grow(h, h->n_total + n);
+    if (s != OMPL_GPU_OK) return s;
+    const int F = h->g.F, dim = h->sp.dim;
+    h->hfeat.resize((size_t)n * F);
+    for (size_t i = 0; i < n; ++i) host_features(h->sp, h->g, states + i * dim, h->hfeat.data() + i * F);
+    const bool sep_raw = h->raw != h->feat;
+    const size_t stage_bytes = sizeof(double) * n * (F + (sep_raw ? dim : 0));
+    HIP_OR_FAIL(h->stage.ensure(stage_bytes));
+    double *sf = (double *)h->stage.p;
+    HIP_OR_FAIL(hipMemcpyAsync(sf, h->hfeat.data(), sizeof(double) * n * F, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(launch_store_soa(sf, (uint32_t)n, F, h->feat, h->cap, h->n_total, h->stream));
+    if (sep_raw) {
+        double *sr = sf + n * F;
+        HIP_OR_FAIL(hipMemcpyAsync(sr, states, sizeof(double) * n * dim, hipMemcpyHostToDevice, h->stream));
+        HIP_OR_FAIL(launch_store_soa(sr, (uint32_t)n, dim, h->raw, h->cap, h->n_total, h->stream));
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // host staging buffers are reused
+    h->n_total += n;
+    h->n_live += n;
+    h->removed.resize(h->n_total, 0);
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_remove(ompl_gpu_nn *h, uint64_t id) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (id >= h->n_total || h->removed[id]) return fail(OMPL_GPU_ERR_NOT_FOUND, "id not stored");
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    // tombstone: a NaN in feature row 0 makes every distance to this state NaN
+    const double nan = __builtin_nan("");
+    HIP_OR_FAIL(hipMemcpyAsync(h->feat + id, &nan, sizeof(double), hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    h->removed[id] = 1;
+    h->n_live--;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_clear(ompl_gpu_nn *h) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    if (h->cap) {
+        HIP_OR_FAIL(hipMemsetAsync(h->feat, 0xFF, sizeof(double) * h->g.F * h->cap, h->stream));
+        if (h->raw != h->feat)
+            HIP_OR_FAIL(hipMemsetAsync(h->raw, 0xFF, sizeof(double) * h->sp.dim * h->cap, h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    }
+    h->n_total = h->n_live = 0;
+    h->removed.clear();
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_size(const ompl_gpu_nn *h, size_t *live, size_t *total) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    if (live) *live = h->n_live;
+    if (total) *total = h->n_total;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_get_states(ompl_gpu_nn *h, uint64_t first, size_t n, double *out) {
+    if (!h || (n && !out)) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (first + n > h->n_total) return fail(OMPL_GPU_ERR_INVALID_ARG, "range beyond stored states");
+    if (n == 0) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    const int dim = h->sp.dim;
+    std::vector<double> soa((size_t)dim * n);
+    HIP_OR_FAIL(hipMemcpy2DAsync(soa.data(), n * sizeof(double), h->raw + first, h->cap * sizeof(double),
+                                 n * sizeof(double), dim, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    for (size_t i = 0; i < n; ++i)
+        for (int c = 0; c < dim; ++c) out[i * dim + c] = soa[(size_t)c * n + i];
+    return OMPL_GPU_OK;
+}
+
+static uint64_t n_end_of(const ompl_gpu_nn *h) { return (h->n_total + kTile - 1) / kTile * kTile; }
+
+// knn on device-resident features (queries already converted); caller holds the lock
+static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, size_t nq, uint32_t k, uint32_t *d_ids,
+                                           double *d_dist) {
+    if (k > (uint32_t)kMaxK) return fail(OMPL_GPU_ERR_UNSUPPORTED, "k above 64 is not supported yet");
+    const uint64_t n_end = n_end_of(h);
+    if (n_end == 0) {
+        // empty structure: every entry is (inf, none)
+        std::vector<double> inf((size_t)nq * k, __builtin_inf());
+        HIP_OR_FAIL(hipMemsetAsync(d_ids, 0xFF, sizeof(uint32_t) * nq * k, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(d_dist, inf.data(), sizeof(double) * inf.size(), hipMemcpyHostToDevice, h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+        return OMPL_GPU_OK;
+    }
+    const size_t wsb = knn_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus);
+    HIP_OR_FAIL(h->ws.ensure(wsb));
+    HIP_OR_FAIL(launch_knn(h->sp, h->g, h->feat, h->cap, n_end, d_qf, (uint32_t)nq, k, d_dist, d_ids, h->ws.p,
+                           h->ws.bytes, h->num_cus, h->stream));
+    return OMPL_GPU_OK;
+}
+
+static ompl_gpu_status upload_query_features(ompl_gpu_nn *h, const double *queries, size_t nq) {
+    const int F = h->g.F, dim = h->sp.dim;
+    h->hfeat.resize(nq * F);
+    for (size_t i = 0; i < nq; ++i) host_features(h->sp, h->g, queries + i * dim, h->hfeat.data() + i * F);
+    HIP_OR_FAIL(h->q.ensure(sizeof(double) * nq * F));
+    HIP_OR_FAIL(hipMemcpyAsync(h->q.p, h->hfeat.data(), sizeof(double) * nq * F, hipMemcpyHostToDevice, h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_knn(ompl_gpu_nn *h, const double *queries, size_t nq, uint32_t k, uint64_t *out_ids,
+                                double *out_dist, uint32_t *out_cnt) {
+    if (!h || (nq && (!queries || (k && (!out_ids || !out_dist))))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (nq == 0) return OMPL_GPU_OK;
+    if (nq > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many queries in one call");
+    if (k == 0) {  // NearestNeighborsGNAT.h:226-227
+        if (out_cnt) std::fill(out_cnt, out_cnt + nq, 0u);
+        return OMPL_GPU_OK;
+    }
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    ompl_gpu_status s = upload_query_features(h, queries, nq);
+    if (s != OMPL_GPU_OK) return s;
+    HIP_OR_FAIL(h->out_d.ensure(sizeof(double) * nq * k));
+    HIP_OR_FAIL(h->out_i.ensure(sizeof(uint32_t) * nq * k));
+    s = knn_features_locked(h, (const double *)h->q.p, nq, k, (uint32_t *)h->out_i.p, (double *)h->out_d.p);
+    if (s != OMPL_GPU_OK) return s;
+    std::vector<uint32_t> ids32(nq * k);
+    HIP_OR_FAIL(hipMemcpyAsync(out_dist, h->out_d.p, sizeof(double) * nq * k, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(ids32.data(), h->out_i.p, sizeof(uint32_t) * nq * k, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    for (size_t q = 0; q < nq; ++q) {
+        uint32_t c = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t id = ids32[q * k + j];
+            out_ids[q * k + j] = id == kNoId ? UINT64_MAX : (uint64_t)id;
+            if (id != kNoId) ++c;
+        }
+        if (out_cnt) out_cnt[q] = c;
+    }
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_nearest(ompl_gpu_nn *h, const double *queries, size_t nq, uint64_t *out_ids,
+                                    double *out_dist) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    if (h->n_live == 0)  // NearestNeighborsGNAT.h:218
+        return fail(OMPL_GPU_ERR_EMPTY, "No elements found in nearest neighbors data structure");
+    std::vector<double> tmpd;
+    if (!out_dist) {
+        tmpd.resize(nq);
+        out_dist = tmpd.data();
+    }
+    return ompl_gpu_nn_knn(h, queries, nq, 1, out_ids, out_dist, nullptr);
+}
+
+ompl_gpu_status ompl_gpu_nn_radius(ompl_gpu_nn *h, const double *queries, size_t nq, double r, uint64_t **ids_out,
+                                   double **dists_out, uint64_t *offsets_out) {
+    if (!h || !ids_out || !offsets_out || (nq && !queries)) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    *ids_out = nullptr;
+    if (dists_out) *dists_out = nullptr;
+    offsets_out[0] = 0;
+    const uint64_t n_end = n_end_of(h);
+    if (nq == 0) return OMPL_GPU_OK;
+    if (n_end == 0 || !(r >= 0.0)) {  // empty structure, or a radius no distance satisfies
+        for (size_t q = 0; q <= nq; ++q) offsets_out[q] = 0;
+        *ids_out = (uint64_t *)std::malloc(sizeof(uint64_t));
+        if (dists_out) *dists_out = (double *)std::malloc(sizeof(double));
+        return OMPL_GPU_OK;
+    }
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    ompl_gpu_status s = upload_query_features(h, queries, nq);
+    if (s != OMPL_GPU_OK) return s;
+    const RadiusPlan p = radius_plan((uint32_t)nq, n_end, h->num_cus);
+    const size_t nc = nq * p.chunks;
+    HIP_OR_FAIL(h->counts.ensure(sizeof(uint32_t) * nc));
+    HIP_OR_FAIL(launch_radius_count(h->sp, h->g, p, h->feat, h->cap, n_end, (const double *)h->q.p, (uint32_t)nq, r,
+                                    (uint32_t *)h->counts.p, h->stream));
+    std::vector<uint32_t> cnt(nc);
+    HIP_OR_FAIL(hipMemcpyAsync(cnt.data(), h->counts.p, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    std::vector<uint64_t> off(nc);
+    uint64_t tot = 0;
+    for (size_t q = 0; q < nq; ++q) {
+        offsets_out[q] = tot;
+        for (uint32_t c = 0; c < p.chunks; ++c) {
+            off[q * p.chunks + c] = tot;
+            tot += cnt[q * p.chunks + c];
+        }
+    }
+    offsets_out[nq] = tot;
+    uint64_t *hid = (uint64_t *)std::malloc(sizeof(uint64_t) * std::max<uint64_t>(tot, 1));
+    double *hd = (double *)std::malloc(sizeof(double) * std::max<uint64_t>(tot, 1));
+    if (!hid || !hd) {
+        std::free(hid);
+        std::free(hd);
+        return fail(OMPL_GPU_ERR_OOM, "host allocation failed");
+    }
+    auto cleanup_fail = [&](ompl_gpu_status st) {
+        std::free(hid);
+        std::free(hd);
+        return st;
+    };
+    if (tot > 0) {
+        if (tot > 0x7FFFFFFFull) return cleanup_fail(fail(OMPL_GPU_ERR_UNSUPPORTED, "radius result above 2^31 entries"));
+        hipError_t e;
+#define TRY(expr)                                                                                  \
+    if ((e = (expr)) != hipSuccess)                                                                \
+        return cleanup_fail(fail(e == hipErrorOutOfMemory ? OMPL_GPU_ERR_OOM : OMPL_GPU_ERR_DEVICE, \
+                                 std::string(#expr) + ": " + hipGetErrorString(e)));
+        TRY(h->offsets.ensure(sizeof(uint64_t) * (nc + nq + 1)));
+        uint64_t *d_off = (uint64_t *)h->offsets.p;
+        uint64_t *d_qoff = d_off + nc;
+        TRY(hipMemcpyAsync(d_off, off.data(), sizeof(uint64_t) * nc, hipMemcpyHostToDevice, h->stream));
+        TRY(hipMemcpyAsync(d_qoff, offsets_out, sizeof(uint64_t) * (nq + 1), hipMemcpyHostToDevice, h->stream));
+        TRY(h->ids.ensure(sizeof(uint32_t) * tot));
+        TRY(h->dists.ensure(sizeof(double) * tot));
+        TRY(h->sorted_ids.ensure(sizeof(uint32_t) * tot));
+        TRY(h->sorted_d.ensure(sizeof(double) * tot));
+        TRY(launch_radius_fill(h->sp, h->g, p, h->feat, h->cap, n_end, (const double *)h->q.p, (uint32_t)nq, r, d_off,
+                               (uint32_t *)h->ids.p, (double *)h->dists.p, h->stream));
+        // stable sort by distance inside each query segment; ids were written ascending
+        size_t tb = 0;
+        TRY(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            nullptr, tb, (const double *)h->dists.p, (double *)h->sorted_d.p, (const uint32_t *)h->ids.p,
+            (uint32_t *)h->sorted_ids.p, (int)tot, (int)nq, d_qoff, d_qoff + 1, 0, 64, h->stream));
+        TRY(h->tmp.ensure(tb));
+        TRY(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            h->tmp.p, tb, (const double *)h->dists.p, (double *)h->sorted_d.p, (const uint32_t *)h->ids.p,
+            (uint32_t *)h->sorted_ids.p, (int)tot, (int)nq, d_qoff, d_qoff + 1, 0, 64, h->stream));
+        std::vector<uint32_t> i32(tot);
+        TRY(hipMemcpyAsync(i32.data(), h->sorted_ids.p, sizeof(uint32_t) * tot, hipMemcpyDeviceToHost, h->stream));
+        TRY(hipMemcpyAsync(hd, h->sorted_d.p, sizeof(double) * tot, hipMemcpyDeviceToHost, h->stream));
+        TRY(hipStreamSynchronize(h->stream));
+#undef TRY
+        for (uint64_t j = 0; j < tot; ++j) hid[j] = i32[j];
+    }
+    *ids_out = hid;
+    if (dists_out)
+        *dists_out = hd;
+    else
+        std::free(hd);
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_knn_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, uint32_t k,
+                                       uint32_t *d_ids, double *d_dist) {
+    if (!h || (nq && (!d_queries || !d_ids || !d_dist))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (nq == 0 || k == 0) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    const double *qf = d_queries;
+    const bool raw_is_feat = h->sp.kind == OMPL_GPU_SPACE_SE3 || h->sp.kind == OMPL_GPU_SPACE_SO3 ||
+                             (h->sp.kind == OMPL_GPU_SPACE_REALVECTOR && h->g.F == h->sp.dim);
+    if (!raw_is_feat) {
+        HIP_OR_FAIL(h->q.ensure(sizeof(double) * nq * h->g.F));
+        HIP_OR_FAIL(launch_features(h->sp, h->g, d_queries, (uint32_t)nq, (double *)h->q.p, h->stream));
+        qf = (const double *)h->q.p;
+    }
+    return knn_features_locked(h, qf, nq, k, d_ids, d_dist);
+}
+
+ompl_gpu_status ompl_gpu_steer_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, const uint32_t *d_nearest,
+                                      uint32_t stride, double max_distance, double *d_from, double *d_to) {
+    if (!h || (nq && (!d_queries || !d_nearest || !d_from || !d_to))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (nq == 0) return OMPL_GPU_OK;
+    if (h->n_total == 0) return fail(OMPL_GPU_ERR_EMPTY, "No elements found in nearest neighbors data structure");
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(launch_steer(h->sp, h->raw, h->cap, d_queries, (uint32_t)nq, d_nearest, stride, max_distance, d_from,
+                             d_to, h->stream));
+    return OMPL_GPU_OK;
+}
+
+// ------------------------------------------------------------------------------ MV
+
+ompl_gpu_status ompl_gpu_mv_create(ompl_gpu_mv **out, const ompl_gpu_space *space, const ompl_gpu_checker *checker,
+                                   int device) {
+    if (!out || !checker) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    *out = nullptr;
+    DevSpace sp;
+    FeatGeom g;
+    if (!space_ok(space, &sp, &g)) return fail(OMPL_GPU_ERR_UNSUPPORTED, "unsupported state space");
+    if (checker->kind < OMPL_GPU_CHECK_ALL_VALID || checker->kind > OMPL_GPU_CHECK_CIRCLES2D)
+        return fail(OMPL_GPU_ERR_UNSUPPORTED, "unknown validity checker");
+    size_t per = 0;
+    switch (checker->kind) {
+    case OMPL_GPU_CHECK_SPHERES: per = 4; break;
+    case OMPL_GPU_CHECK_CIRCLES2D: per = 3; break;
+    case OMPL_GPU_CHECK_KCHAIN: per = 4; break;
+    default: per = 0;
+    }
+    if (per && checker->count > 0 && !checker->data) return fail(OMPL_GPU_ERR_INVALID_ARG, "checker data is NULL");
+    if (checker->kind == OMPL_GPU_CHECK_HYPERCUBE && (checker->ndim < 1 || checker->ndim > sp.dim))
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "hypercube ndim out of range");
+    if (checker->kind == OMPL_GPU_CHECK_SPHERES && sp.dim < 3) return fail(OMPL_GPU_ERR_INVALID_ARG, "spheres need 3 reals");
+    if (checker->kind == OMPL_GPU_CHECK_CIRCLES2D && sp.dim < 2) return fail(OMPL_GPU_ERR_INVALID_ARG, "circles need 2 reals");
+    if (checker->kind == OMPL_GPU_CHECK_KCHAIN && sp.kind != OMPL_GPU_SPACE_KCHAIN)
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "kinematic chain checker needs a KCHAIN space");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(OMPL_GPU_ERR_DEVICE, "no such HIP device");
+    HIP_OR_FAIL(hipSetDevice(device));
+    auto *h = new ompl_gpu_mv();
+    h->device = device;
+    h->sp = sp;
+    h->g = g;
+    h->ck.kind = checker->kind;
+    h->ck.ndim = checker->ndim;
+    h->ck.edge = checker->edge_width;
+    h->ck.count = per ? checker->count : 0;
+    h->ck.data = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&h->counters, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(h->counters, 0, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess && per && h->ck.count > 0) {
+        e = hipMalloc(&h->ck_data, sizeof(double) * per * h->ck.count);
+        if (e == hipSuccess)
+            e = hipMemcpy(h->ck_data, checker->data, sizeof(double) * per * h->ck.count, hipMemcpyHostToDevice);
+        h->ck.data = h->ck_data;
+    }
+    if (e != hipSuccess) {
+        ompl_gpu_mv_destroy(h);
+        return fail(OMPL_GPU_ERR_DEVICE, hipGetErrorString(e));
+    }
+    h->stream = h->own;
+    *out = h;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_destroy(ompl_gpu_mv *h) {
+    if (!h) return OMPL_GPU_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->ck_data) (void)hipFree(h->ck_data);
+    if (h->counters) (void)hipFree(h->counters);
+    if (h->own) (void)hipStreamDestroy(h->own);
+    delete h;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_set_stream(ompl_gpu_mv *h, void *s) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->stream = s ? (hipStream_t)s : h->own;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_sync(ompl_gpu_mv *h) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_check(ompl_gpu_mv *h, const double *s1, const double *s2, size_t m, uint8_t *valid,
+                                  int32_t *nd, int32_t *first_invalid) {
+    if (!h || (m && (!s1 || !s2 || !valid))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (m == 0) return OMPL_GPU_OK;
+    if (m > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many edges in one call");
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    const size_t sb = sizeof(double) * m * h->sp.dim;
+    HIP_OR_FAIL(h->s1.ensure(sb));
+    HIP_OR_FAIL(h->s2.ensure(sb));
+    HIP_OR_FAIL(h->valid.ensure(m));
+    if (nd) HIP_OR_FAIL(h->nd.ensure(sizeof(int32_t) * m));
+    if (first_invalid) HIP_OR_FAIL(h->fi.ensure(sizeof(int32_t) * m));
+    HIP_OR_FAIL(hipMemcpyAsync(h->s1.p, s1, sb, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(h->s2.p, s2, sb, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(launch_motion(h->sp, h->ck, (const double *)h->s1.p, (const double *)h->s2.p, (uint32_t)m,
+                              (uint8_t *)h->valid.p, nd ? (int32_t *)h->nd.p : nullptr,
+                              first_invalid ? (int32_t *)h->fi.p : nullptr, h->counters, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(valid, h->valid.p, m, hipMemcpyDeviceToHost, h->stream));
+    if (nd) HIP_OR_FAIL(hipMemcpyAsync(nd, h->nd.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, h->stream));
+    if (first_invalid)
+        HIP_OR_FAIL(hipMemcpyAsync(first_invalid, h->fi.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_check_device(ompl_gpu_mv *h, const double *d_s1, const double *d_s2, size_t m,
+                                         uint8_t *d_valid, int32_t *d_nd, int32_t *d_first_invalid) {
+    if (!h || (m && (!d_s1 || !d_s2 || !d_valid))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (m == 0) return OMPL_GPU_OK;
+    if (m > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many edges in one call");
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(launch_motion(h->sp, h->ck, d_s1, d_s2, (uint32_t)m, d_valid, d_nd, d_first_invalid, h->counters,
+                              h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_counters(ompl_gpu_mv *h, uint64_t *valid, uint64_t *invalid) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    unsigned long long c[4];
+    HIP_OR_FAIL(hipMemcpyAsync(c, h->counters, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (valid) *valid = c[0];
+    if (invalid) *invalid = c[1];
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_state_checks(ompl_gpu_mv *h, uint64_t *checks) {
+    if (!h || !checks) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    unsigned long long c[4];
+    HIP_OR_FAIL(hipMemcpyAsync(c, h->counters, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    *checks = c[2];
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_reset_counters(ompl_gpu_mv *h) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(hipMemsetAsync(h->counters, 0, 4 * sizeof(unsigned long long), h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_svc_check(ompl_gpu_mv *h, const double *states, size_t m, uint8_t *valid) {
+    if (!h || (m && (!states || !valid))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (m == 0) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    const size_t sb = sizeof(double) * m * h->sp.dim;
+    HIP_OR_FAIL(h->s1.ensure(sb));
+    HIP_OR_FAIL(h->valid.ensure(m));
+    HIP_OR_FAIL(hipMemcpyAsync(h->s1.p, states, sb, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(launch_state_valid(h->sp, h->ck, (const double *)h->s1.p, (uint32_t)m, (uint8_t *)h->valid.p, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(valid, h->valid.p, m, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
+}  // extern "C"

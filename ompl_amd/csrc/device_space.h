@@ -1,0 +1,288 @@
+// device_space.h — device restatement of the reference's state-space leaves in
+// IEEE fp64 with the reference's operation order.  This translation unit is
+// compiled with -ffp-contract=off: no multiply-add is fused, matching the
+// reference x86-64 build (CMakeModules/CompilerSettings.cmake:8, no -march).
+//
+//   distance   RealVectorStateSpace.cpp:230-242, SO3StateSpace.cpp:254-262,
+//              StateSpace.cpp:1068-1076 (compound), demos/KinematicChain.h:105-124
+//   interpolate RealVectorStateSpace.cpp:257-265, SO3StateSpace.cpp:289-318,
+//              StateSpace.cpp:1109-1116, demos/KinematicChain.h:150-175
+//   segments   StateSpace.cpp:851-854, :1085-1097
+//   isValid    demos/HypercubeBenchmark.cpp:57-72, tests/resources/circles2D.h:139-150,
+//              demos/KinematicChain.h:200-276
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ompl_gpu.h"
+
+namespace ompl_amd {
+
+constexpr double kPi = 3.141592653589793238462643383279502884;
+constexpr double kQuatNormErr = 1e-9;                    // SO3StateSpace.cpp:47
+constexpr double kDblEps = 2.220446049250313080847e-16;  // numeric_limits<double>::epsilon()
+constexpr double kFltEps = 1.1920928955078125e-07;       // numeric_limits<float>::epsilon()
+
+// Plain-old-data copy of ompl_gpu_space passed by value to kernels.
+struct DevSpace {
+    int kind;
+    int dim;
+    double w0, w1;
+    double lvs0, lvs1;
+    uint32_t f0, f1;
+    double link;
+};
+
+// Feature layout per state (what the NN kernels stream):
+//   REALVECTOR(n): n coordinates, zero-padded to the bucket (adding 0*0 to the
+//                  running sum is exact, so padding preserves the bits)
+//   SO3          : qx,qy,qz,qw
+//   SE3          : x,y,z,qx,qy,qz,qw
+//   KCHAIN(n)    : cos(theta_1..n), sin(theta_1..n) of the cumulative angles —
+//                  the reference recomputes them per pair; they are a pure
+//                  function of the state, so precomputing them is bit-identical.
+__host__ __device__ inline int feature_count(int kind, int dim) {
+    return kind == OMPL_GPU_SPACE_KCHAIN ? 2 * dim : dim;
+}
+
+__device__ __forceinline__ double l2_dist(const double *a, const double *b, int n) {
+    double acc = 0.0;
+    for (int i = 0; i < n; ++i) {
+        double diff = a[i] - b[i];
+        acc += diff * diff;
+    }
+    return sqrt(acc);
+}
+
+__device__ __forceinline__ double so3_arc(const double *p, const double *q) {
+    double dq = fabs(p[0] * q[0] + p[1] * q[1] + p[2] * q[2] + p[3] * q[3]);
+    if (dq > 1.0 - kQuatNormErr) return 0.0;
+    return acos(dq);
+}
+
+// chain distance from precomputed cumulative cos/sin features (cs[0..n) = cos, cs[n..2n) = sin)
+template <int NMAX>
+__device__ __forceinline__ double chain_dist_feat(const double *a, const double *b, int n, double link) {
+    double dx = 0., dy = 0., dist = 0.;
+#pragma unroll
+    for (int i = 0; i < NMAX; ++i) {
+        if (i < n) {
+            dx += a[i] - b[i];
+            dy += a[NMAX + i] - b[NMAX + i];
+            dist += sqrt(dx * dx + dy * dy);
+        }
+    }
+    return dist * link;
+}
+
+// raw-angle chain distance (motion validator: validSegmentCount on raw states)
+__device__ __forceinline__ double chain_dist_raw(const double *a, const double *b, int n, double link) {
+    double th1 = 0., th2 = 0., dx = 0., dy = 0., dist = 0.;
+    for (int i = 0; i < n; ++i) {
+        th1 += a[i];
+        th2 += b[i];
+        dx += cos(th1) - cos(th2);
+        dy += sin(th1) - sin(th2);
+        dist += sqrt(dx * dx + dy * dy);
+    }
+    return dist * link;
+}
+
+__device__ __forceinline__ double se3_dist(const double *a, const double *b, double w0, double w1) {
+    double dist = 0.0;
+    dist += w0 * l2_dist(a, b, 3);
+    dist += w1 * so3_arc(a + 3, b + 3);
+    return dist;
+}
+
+// distance on raw AoS states (dim reals)
+__device__ inline double raw_distance(const DevSpace &sp, const double *a, const double *b) {
+    switch (sp.kind) {
+    case OMPL_GPU_SPACE_REALVECTOR: return l2_dist(a, b, sp.dim);
+    case OMPL_GPU_SPACE_SO3: return so3_arc(a, b);
+    case OMPL_GPU_SPACE_SE3: return se3_dist(a, b, sp.w0, sp.w1);
+    default: return chain_dist_raw(a, b, sp.dim, sp.link);
+    }
+}
+
+__device__ __forceinline__ uint32_t seg_count(double d, double lvs, uint32_t f) {
+    return f * (uint32_t)ceil(d / lvs);
+}
+
+__device__ inline uint32_t valid_segment_count(const DevSpace &sp, const double *a, const double *b) {
+    switch (sp.kind) {
+    case OMPL_GPU_SPACE_REALVECTOR: return seg_count(l2_dist(a, b, sp.dim), sp.lvs0, sp.f0);
+    case OMPL_GPU_SPACE_SO3: return seg_count(so3_arc(a, b), sp.lvs0, sp.f0);
+    case OMPL_GPU_SPACE_SE3: {
+        uint32_t sc = 0;
+        uint32_t s0 = seg_count(l2_dist(a, b, 3), sp.lvs0, sp.f0);
+        if (s0 > sc) sc = s0;
+        uint32_t s1 = seg_count(so3_arc(a + 3, b + 3), sp.lvs1, sp.f1);
+        if (s1 > sc) sc = s1;
+        return sc;
+    }
+    default: return seg_count(chain_dist_raw(a, b, sp.dim, sp.link), sp.lvs0, sp.f0);
+    }
+}
+
+__device__ __forceinline__ void lerp(const double *f, const double *t_, double t, double *o, int n) {
+    for (int i = 0; i < n; ++i) o[i] = f[i] + (t_[i] - f[i]) * t;
+}
+
+__device__ inline void slerp(const double *f, const double *to, double t, double *o) {
+    double theta = so3_arc(f, to);
+    if (theta > kDblEps) {
+        double d = 1.0 / sin(theta);
+        double s0 = sin((1.0 - t) * theta);
+        double s1 = sin(t * theta);
+        double dq = f[0] * to[0] + f[1] * to[1] + f[2] * to[2] + f[3] * to[3];
+        if (dq < 0) s1 = -s1;
+        o[0] = (f[0] * s0 + to[0] * s1) * d;
+        o[1] = (f[1] * s0 + to[1] * s1) * d;
+        o[2] = (f[2] * s0 + to[2] * s1) * d;
+        o[3] = (f[3] * s0 + to[3] * s1) * d;
+    } else {
+        o[0] = f[0]; o[1] = f[1]; o[2] = f[2]; o[3] = f[3];
+    }
+}
+
+__device__ inline void chain_interp(const double *f, const double *to, double t, double *o, int n) {
+    for (int i = 0; i < n; ++i) {
+        double diff = to[i] - f[i];
+        if (fabs(diff) <= kPi) {
+            o[i] = f[i] + diff * t;
+        } else {
+            if (diff > 0.0)
+                diff = 2.0 * kPi - diff;
+            else
+                diff = -2.0 * kPi - diff;
+            double v = f[i] - diff * t;
+            if (v > kPi)
+                v -= 2.0 * kPi;
+            else if (v < -kPi)
+                v += 2.0 * kPi;
+            o[i] = v;
+        }
+    }
+}
+
+// interpolate; rot=false skips the SO3 part of SE3 when the validity checker only
+// reads the translation (its output is then unused: the result bit is unchanged).
+__device__ inline void interpolate(const DevSpace &sp, const double *f, const double *to, double t, double *o,
+                                   bool rot = true) {
+    switch (sp.kind) {
+    case OMPL_GPU_SPACE_REALVECTOR: lerp(f, to, t, o, sp.dim); break;
+    case OMPL_GPU_SPACE_SO3: slerp(f, to, t, o); break;
+    case OMPL_GPU_SPACE_SE3:
+        lerp(f, to, t, o, 3);
+        if (rot) slerp(f + 3, to + 3, t, o + 3);
+        break;
+    default: chain_interp(f, to, t, o, sp.dim); break;
+    }
+}
+
+// ---- validity checkers --------------------------------------------------------
+
+struct DevChecker {
+    int kind;
+    int ndim;
+    double edge;
+    int count;
+    const double *data;  // device copy
+};
+
+__device__ __forceinline__ bool hypercube_valid(const double *s, int ndim, double edge) {
+    bool found = false;
+    for (int i = ndim - 1; i >= 0; i--) {
+        if (!found) {
+            if (s[i] > edge) found = true;
+        } else if (s[i] < (1. - edge)) {
+            return false;
+        }
+    }
+    return true;
+}
+
+__device__ __forceinline__ bool spheres_valid(const double *s, const double *c, int count) {
+    for (int i = 0; i < count; ++i) {
+        double dx = c[4 * i + 0] - s[0];
+        double dy = c[4 * i + 1] - s[1];
+        double dz = c[4 * i + 2] - s[2];
+        if (dx * dx + dy * dy + dz * dz < c[4 * i + 3]) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ bool circles_valid(const double *s, const double *c, int count) {
+    for (int i = 0; i < count; ++i) {
+        double dx = c[3 * i + 0] - s[0];
+        double dy = c[3 * i + 1] - s[1];
+        if (dx * dx + dy * dy < c[3 * i + 2]) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ bool seg_intersect(double a0x, double a0y, double a1x, double a1y, double b0x, double b0y,
+                                              double b1x, double b1y) {
+    double s10_x = a1x - a0x;
+    double s10_y = a1y - a0y;
+    double s32_x = b1x - b0x;
+    double s32_y = b1y - b0y;
+    double denom = s10_x * s32_y - s32_x * s10_y;
+    if (fabs(denom) < kDblEps) return false;
+    bool denomPositive = denom > 0;
+    double s02_x = a0x - b0x;
+    double s02_y = a0y - b0y;
+    double s_numer = s10_x * s02_y - s10_y * s02_x;
+    if ((s_numer < kFltEps) == denomPositive) return false;
+    double t_numer = s32_x * s02_y - s32_y * s02_x;
+    if ((t_numer < kFltEps) == denomPositive) return false;
+    if (((s_numer - denom > -kFltEps) == denomPositive) || ((t_numer - denom > kFltEps) == denomPositive))
+        return false;
+    return true;
+}
+
+constexpr int kChainMaxLinks = 32;
+
+__device__ inline bool chain_valid(const double *s, int n, double link, const double *env, int nenv) {
+    double px[kChainMaxLinks + 2], py[kChainMaxLinks + 2];  // segment i = (p[i], p[i+1])
+    double theta = 0., x = 0., y = 0.;
+    px[0] = 0.;
+    py[0] = 0.;
+    for (int i = 0; i < n; ++i) {
+        theta += s[i];
+        double xN = x + cos(theta) * link;
+        double yN = y + sin(theta) * link;
+        px[i + 1] = xN;
+        py[i + 1] = yN;
+        x = xN;
+        y = yN;
+    }
+    px[n + 1] = x + cos(theta) * 0.001;
+    py[n + 1] = y + sin(theta) * 0.001;
+    const int ns = n + 1;
+    for (int i = 0; i < ns; ++i)
+        for (int j = i + 1; j < ns; ++j)
+            if (seg_intersect(px[i], py[i], px[i + 1], py[i + 1], px[j], py[j], px[j + 1], py[j + 1])) return false;
+    for (int i = 0; i < ns; ++i)
+        for (int j = 0; j < nenv; ++j)
+            if (seg_intersect(px[i], py[i], px[i + 1], py[i + 1], env[4 * j], env[4 * j + 1], env[4 * j + 2],
+                              env[4 * j + 3]))
+                return false;
+    return true;
+}
+
+__device__ inline bool is_valid(const DevSpace &sp, const DevChecker &ck, const double *s) {
+    switch (ck.kind) {
+    case OMPL_GPU_CHECK_ALL_VALID: return true;
+    case OMPL_GPU_CHECK_HYPERCUBE: return hypercube_valid(s, ck.ndim, ck.edge);
+    case OMPL_GPU_CHECK_SPHERES: return spheres_valid(s, ck.data, ck.count);
+    case OMPL_GPU_CHECK_CIRCLES2D: return circles_valid(s, ck.data, ck.count);
+    default: return chain_valid(s, sp.dim, sp.link, ck.data, ck.count);
+    }
+}
+
+// Does the checker read the SO3 part of an SE3 state?  (None of the closed set does.)
+__host__ __device__ inline bool checker_reads_rotation(int kind) { return false; }
+
+}  // namespace ompl_amd

@@ -1,0 +1,70 @@
+// kernels.h — host-side launch interface of the HIP kernels (knn.hip, motion.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "device_space.h"
+
+namespace ompl_amd {
+
+constexpr int kTile = 256;          // states per LDS tile / threads per block
+constexpr int kMaxK = 64;           // largest register top-K bucket
+
+// Feature geometry of a space on device.
+struct FeatGeom {
+    int F;       // feature slots per state (padded)
+    int nmax;    // KCHAIN: link bucket (F = 2*nmax); else 0
+};
+bool feature_geometry(const DevSpace &sp, FeatGeom *g);  // false if unsupported
+// host-side feature computation for one AoS state (glibc cos/sin for KCHAIN)
+void host_features(const DevSpace &sp, const FeatGeom &g, const double *raw, double *feat);
+
+int k_bucket(uint32_t k);  // 1,4,16,32,64 or 0 if k > kMaxK
+
+// kNN over features.  feat: SoA [F][cap]; qfeat: AoS [nq][F]; scans ids [0, n_end)
+// (n_end a multiple of kTile, entries >= n_total are NaN).  Output [nq][k] sorted by
+// (distance, id), missing entries = (inf, 0xFFFFFFFF).  ws: device workspace.
+struct KnnWorkspace {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+size_t knn_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k, uint64_t n_end, int num_cus);
+hipError_t launch_knn(const DevSpace &sp, const FeatGeom &g, const double *feat, uint64_t cap, uint64_t n_end,
+                      const double *qfeat, uint32_t nq, uint32_t k, double *out_d, uint32_t *out_i, void *ws,
+                      size_t ws_bytes, int num_cus, hipStream_t st);
+
+// radius search, pass 1 (count per (query, chunk)) and pass 2 (fill CSR in id order).
+struct RadiusPlan {
+    uint32_t chunks;      // chunks per query
+    uint32_t chunk_len;   // states per chunk
+    bool stream;          // wave-chunk mapping (small nq) vs tiled mapping
+};
+RadiusPlan radius_plan(uint32_t nq, uint64_t n_end, int num_cus);
+hipError_t launch_radius_count(const DevSpace &sp, const FeatGeom &g, const RadiusPlan &p, const double *feat,
+                               uint64_t cap, uint64_t n_end, const double *qfeat, uint32_t nq, double r,
+                               uint32_t *counts /* [nq][chunks] */, hipStream_t st);
+hipError_t launch_radius_fill(const DevSpace &sp, const FeatGeom &g, const RadiusPlan &p, const double *feat,
+                              uint64_t cap, uint64_t n_end, const double *qfeat, uint32_t nq, double r,
+                              const uint64_t *offsets /* [nq*chunks] exclusive */, uint32_t *ids, double *dists,
+                              hipStream_t st);
+
+// device feature computation for raw AoS queries (device-resident API)
+hipError_t launch_features(const DevSpace &sp, const FeatGeom &g, const double *raw, uint32_t n, double *feat,
+                           hipStream_t st);
+// scatter AoS features of n new states into SoA storage at [first, first+n)
+hipError_t launch_store_soa(const double *aos, uint32_t n, int width, double *soa, uint64_t cap, uint64_t first,
+                            hipStream_t st);
+// RRT steer: from = raw[nearest], to = q or interpolate(from, q, maxd/d)
+hipError_t launch_steer(const DevSpace &sp, const double *raw_soa, uint64_t cap, const double *q, uint32_t nq,
+                        const uint32_t *nearest, uint32_t stride, double maxd, double *from, double *to,
+                        hipStream_t st);
+
+// motion validation: one thread per edge
+hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double *s1, const double *s2, uint32_t m,
+                         uint8_t *valid, int32_t *nd, int32_t *first_invalid, unsigned long long *counters,
+                         hipStream_t st);
+hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const double *s, uint32_t m, uint8_t *valid,
+                              hipStream_t st);
+
+}  // namespace ompl_amd

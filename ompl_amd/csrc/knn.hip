@@ -1,0 +1,576 @@
+// knn.hip — nearest-neighbour kernels for gfx950 (MI355X / CDNA4).
+//
+// Replaces the reference's per-query tree walk (NearestNeighborsGNAT.h:335-356,
+// :565-662) with exact brute-force scans over a structure-of-arrays state store in
+// HBM.  Two mappings:
+//   * tiled   (batched queries, nq >= kStreamMaxQ): one thread = one query; a 256-
+//             state tile of the store is staged through LDS and read by broadcast;
+//             the store is split into chunks along grid.y so the grid fills 256 CUs;
+//             per-thread register top-K; per-chunk lists merged by knn_merge.
+//   * stream  (small nq, the RRT one-query-per-iteration case): one wave = 64*ITEMS
+//             consecutive states, coalesced SoA loads, per-lane top-K, wave/block
+//             selection by shuffles; partial lists merged per query.
+// Distances are fp64 in the reference's operation order (device_space.h); results
+// are ordered by (distance, id), which is the reference's ascending order with ties
+// resolved by insertion id.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <algorithm>
+
+#include "kernels.h"
+#include "topk.h"
+
+namespace ompl_amd {
+
+constexpr uint32_t kStreamMaxQ = 64;  // below this many queries use the stream mapping
+constexpr int kStreamItems = 16;      // states per lane in the stream mapping
+
+// ---------------------------------------------------------------------------------
+// distance on features (element first, query second: NearestNeighborsLinear.h:104)
+template <int SP, int F, int NMAX>
+__device__ __forceinline__ double feat_dist(const double *s, const double *q, const DevSpace &sp) {
+    if constexpr (SP == OMPL_GPU_SPACE_REALVECTOR) {
+        double acc = 0.0;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            double diff = s[f] - q[f];
+            acc += diff * diff;
+        }
+        return sqrt(acc);
+    } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
+        return so3_arc(s, q);
+    } else if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        return se3_dist(s, q, sp.w0, sp.w1);
+    } else {
+        return chain_dist_feat<NMAX>(s, q, sp.dim, sp.link);
+    }
+}
+
+template <int F>
+struct LdsStride {
+    static constexpr int value = (F + 1) & ~1;  // even -> 16-byte aligned rows for ds_read_b128
+};
+
+// ---------------------------------------------------------------------------------
+// tiled batched kNN
+template <int SP, int F, int NMAX, int K>
+__global__ __launch_bounds__(256) void knn_tiled_kernel(const double *__restrict__ feat, uint64_t cap,
+                                                        uint64_t n_end, const double *__restrict__ qfeat,
+                                                        uint32_t nq, uint32_t chunk_len, DevSpace sp,
+                                                        double *__restrict__ out_d, uint32_t *__restrict__ out_i,
+                                                        uint32_t out_k) {
+    constexpr int FP = LdsStride<F>::value;
+    __shared__ __attribute__((aligned(16))) double tile[kTile * FP];
+    const uint32_t q = blockIdx.x * kTile + threadIdx.x;
+    double qf[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qf[f] = q < nq ? qfeat[(size_t)q * F + f] : __builtin_nan("");
+    TopK<K> top;
+    top.init();
+    const uint64_t c0 = (uint64_t)blockIdx.y * chunk_len;
+    const uint64_t c1 = min(c0 + chunk_len, n_end);
+    for (uint64_t base = c0; base < c1; base += kTile) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) tile[threadIdx.x * FP + f] = feat[(uint64_t)f * cap + base + threadIdx.x];
+        __syncthreads();
+#pragma unroll 2
+        for (int s = 0; s < kTile; ++s) {
+            double sf[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) sf[f] = tile[s * FP + f];
+            const double d = feat_dist<SP, F, NMAX>(sf, qf, sp);
+            const uint32_t id = (uint32_t)(base + s);
+            if (top.admits(d, id)) top.push(d, id);
+        }
+        __syncthreads();
+    }
+    if (q >= nq) return;
+    // out layout: [blockIdx.y][nq][out_k]
+    const size_t o = ((size_t)blockIdx.y * nq + q) * out_k;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (j < (int)out_k) {
+            out_d[o + j] = top.d[j];
+            out_i[o + j] = top.i[j];
+        }
+}
+
+// thread per query: merge S sorted partial lists of K
+template <int K>
+__global__ __launch_bounds__(256) void knn_merge_kernel(const double *__restrict__ pd, const uint32_t *__restrict__ pi,
+                                                        uint32_t S, uint32_t nq, double *__restrict__ out_d,
+                                                        uint32_t *__restrict__ out_i, uint32_t out_k) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    TopK<K> top;
+    top.init();
+    for (uint32_t s = 0; s < S; ++s) {
+        const size_t o = ((size_t)s * nq + q) * K;
+        for (int j = 0; j < K; ++j) {
+            const double d = pd[o + j];
+            const uint32_t id = pi[o + j];
+            if (!top.admits(d, id)) break;  // lists are sorted
+            top.push(d, id);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (j < (int)out_k) {
+            out_d[(size_t)q * out_k + j] = top.d[j];
+            out_i[(size_t)q * out_k + j] = top.i[j];
+        }
+}
+
+// ---------------------------------------------------------------------------------
+// stream kNN (small nq): grid (blocks, nq); wave gw scans [gw*64*ITEMS, (gw+1)*64*ITEMS)
+template <int SP, int F, int NMAX, int K>
+__global__ __launch_bounds__(256) void knn_stream_kernel(const double *__restrict__ feat, uint64_t cap,
+                                                         uint64_t n_end, const double *__restrict__ qfeat,
+                                                         DevSpace sp, double *__restrict__ part_d,
+                                                         uint32_t *__restrict__ part_i) {
+    __shared__ double lds_d[4 * K];
+    __shared__ uint32_t lds_i[4 * K];
+    const uint32_t q = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double qf[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qf[f] = qfeat[(size_t)q * F + f];
+    TopK<K> top;
+    top.init();
+    const uint64_t wbase = ((uint64_t)blockIdx.x * 4 + wave) * (64 * kStreamItems);
+#pragma unroll 4
+    for (int it = 0; it < kStreamItems; ++it) {
+        const uint64_t id = wbase + (uint64_t)it * 64 + lane;
+        if (id < n_end) {
+            double sf[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) sf[f] = feat[(uint64_t)f * cap + id];
+            const double d = feat_dist<SP, F, NMAX>(sf, qf, sp);
+            if (top.admits(d, (uint32_t)id)) top.push(d, (uint32_t)id);
+        }
+    }
+    double rd;
+    uint32_t ri;
+    block_select<K>(top, lds_d, lds_i, rd, ri);
+    if (wave == 0 && lane < K) {
+        const size_t o = ((size_t)q * gridDim.x + blockIdx.x) * K + lane;
+        part_d[o] = rd;
+        part_i[o] = ri;
+    }
+}
+
+// block per query: merge P lists of K
+template <int K>
+__global__ __launch_bounds__(256) void knn_stream_merge_kernel(const double *__restrict__ pd,
+                                                               const uint32_t *__restrict__ pi, uint32_t P,
+                                                               double *__restrict__ out_d,
+                                                               uint32_t *__restrict__ out_i, uint32_t out_k) {
+    __shared__ double lds_d[4 * K];
+    __shared__ uint32_t lds_i[4 * K];
+    const uint32_t q = blockIdx.x;
+    TopK<K> top;
+    top.init();
+    const size_t base = (size_t)q * P * K;
+    for (size_t j = threadIdx.x; j < (size_t)P * K; j += blockDim.x) top.offer(pd[base + j], pi[base + j]);
+    double rd;
+    uint32_t ri;
+    block_select<K>(top, lds_d, lds_i, rd, ri);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (wave == 0 && lane < (int)out_k) {
+        out_d[(size_t)q * out_k + lane] = rd;
+        out_i[(size_t)q * out_k + lane] = ri;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// radius search.  Hits are written per (query, chunk) segment in ascending id order
+// so that a stable sort by distance yields (distance, id) order.
+template <int SP, int F, int NMAX, bool FILL>
+__global__ __launch_bounds__(256) void radius_tiled_kernel(const double *__restrict__ feat, uint64_t cap,
+                                                           uint64_t n_end, const double *__restrict__ qfeat,
+                                                           uint32_t nq, uint32_t chunk_len, uint32_t chunks,
+                                                           DevSpace sp, double r, uint32_t *__restrict__ counts,
+                                                           const uint64_t *__restrict__ offsets,
+                                                           uint32_t *__restrict__ ids, double *__restrict__ dists) {
+    constexpr int FP = LdsStride<F>::value;
+    __shared__ __attribute__((aligned(16))) double tile[kTile * FP];
+    const uint32_t q = blockIdx.x * kTile + threadIdx.x;
+    double qf[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qf[f] = q < nq ? qfeat[(size_t)q * F + f] : __builtin_nan("");
+    const uint64_t c0 = (uint64_t)blockIdx.y * chunk_len;
+    const uint64_t c1 = min(c0 + chunk_len, n_end);
+    uint32_t cnt = 0;
+    uint64_t out = FILL && q < nq ? offsets[(size_t)q * chunks + blockIdx.y] : 0;
+    for (uint64_t base = c0; base < c1; base += kTile) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) tile[threadIdx.x * FP + f] = feat[(uint64_t)f * cap + base + threadIdx.x];
+        __syncthreads();
+#pragma unroll 2
+        for (int s = 0; s < kTile; ++s) {
+            double sf[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) sf[f] = tile[s * FP + f];
+            const double d = feat_dist<SP, F, NMAX>(sf, qf, sp);
+            if (d <= r) {
+                if (FILL) {
+                    ids[out] = (uint32_t)(base + s);
+                    dists[out] = d;
+                    ++out;
+                } else {
+                    ++cnt;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!FILL && q < nq) counts[(size_t)q * chunks + blockIdx.y] = cnt;
+}
+
+// stream radius: chunk = one wave's 64*ITEMS consecutive states; ballot-ordered writes
+template <int SP, int F, int NMAX, bool FILL>
+__global__ __launch_bounds__(256) void radius_stream_kernel(const double *__restrict__ feat, uint64_t cap,
+                                                            uint64_t n_end, const double *__restrict__ qfeat,
+                                                            uint32_t chunks, DevSpace sp, double r,
+                                                            uint32_t *__restrict__ counts,
+                                                            const uint64_t *__restrict__ offsets,
+                                                            uint32_t *__restrict__ ids, double *__restrict__ dists) {
+    const uint32_t q = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t chunk = blockIdx.x * 4 + wave;
+    if (chunk >= chunks) return;
+    double qf[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qf[f] = qfeat[(size_t)q * F + f];
+    const uint64_t wbase = (uint64_t)chunk * (64 * kStreamItems);
+    uint64_t cursor = FILL ? offsets[(size_t)q * chunks + chunk] : 0;
+    uint32_t cnt = 0;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int it = 0; it < kStreamItems; ++it) {
+        const uint64_t id = wbase + (uint64_t)it * 64 + lane;
+        bool hit = false;
+        double d = 0.0;
+        if (id < n_end) {
+            double sf[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) sf[f] = feat[(uint64_t)f * cap + id];
+            d = feat_dist<SP, F, NMAX>(sf, qf, sp);
+            hit = d <= r;
+        }
+        const uint64_t bal = __ballot(hit);
+        if (FILL && hit) {
+            const uint64_t pos = cursor + __popcll(bal & lt_mask);
+            ids[pos] = (uint32_t)id;
+            dists[pos] = d;
+        }
+        cursor += __popcll(bal);
+        cnt += (uint32_t)__popcll(bal);
+    }
+    if (!FILL && lane == 0) counts[(size_t)q * chunks + chunk] = cnt;
+}
+
+// ---------------------------------------------------------------------------------
+// helpers: features, SoA scatter, steer
+__global__ void features_kernel(DevSpace sp, FeatGeom g, const double *__restrict__ raw, uint32_t n,
+                                double *__restrict__ feat) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double *s = raw + (size_t)i * sp.dim;
+    double *o = feat + (size_t)i * g.F;
+    if (sp.kind == OMPL_GPU_SPACE_KCHAIN) {
+        double th = 0.;
+        for (int j = 0; j < g.nmax; ++j) {
+            if (j < sp.dim) {
+                th += s[j];
+                o[j] = cos(th);
+                o[g.nmax + j] = sin(th);
+            } else {
+                o[j] = 0.;
+                o[g.nmax + j] = 0.;
+            }
+        }
+    } else {
+        for (int j = 0; j < g.F; ++j) o[j] = j < sp.dim ? s[j] : 0.0;
+    }
+}
+
+__global__ void store_soa_kernel(const double *__restrict__ aos, uint32_t n, int width, double *__restrict__ soa,
+                                 uint64_t cap, uint64_t first) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)n * width) return;
+    const uint64_t i = t / width, c = t % width;
+    soa[c * cap + first + i] = aos[t];
+}
+
+__global__ void steer_kernel(DevSpace sp, const double *__restrict__ raw, uint64_t cap, const double *__restrict__ q,
+                             uint32_t nq, const uint32_t *__restrict__ nearest, uint32_t stride, double maxd,
+                             double *__restrict__ from, double *__restrict__ to) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const int dim = sp.dim;
+    double a[kChainMaxLinks], b[kChainMaxLinks], o[kChainMaxLinks];
+    const uint32_t nid = nearest[(size_t)i * stride];
+    for (int c = 0; c < dim; ++c) {
+        a[c] = raw[(uint64_t)c * cap + nid];
+        b[c] = q[(size_t)i * dim + c];
+    }
+    const double d = raw_distance(sp, a, b);  // si_->distance(nmotion->state, rstate)  RRT.cpp:141
+    if (d > maxd) {
+        interpolate(sp, a, b, maxd / d, o);  // RRT.cpp:142-145
+    } else {
+        for (int c = 0; c < dim; ++c) o[c] = b[c];
+    }
+    for (int c = 0; c < dim; ++c) {
+        from[(size_t)i * dim + c] = a[c];
+        to[(size_t)i * dim + c] = o[c];
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// host side
+
+bool feature_geometry(const DevSpace &sp, FeatGeom *g) {
+    g->nmax = 0;
+    switch (sp.kind) {
+    case OMPL_GPU_SPACE_REALVECTOR:
+        if (sp.dim < 1 || sp.dim > 16) return false;
+        g->F = sp.dim <= 4 ? 4 : sp.dim <= 8 ? 8 : 16;
+        return true;
+    case OMPL_GPU_SPACE_SO3:
+        if (sp.dim != 4) return false;
+        g->F = 4;
+        return true;
+    case OMPL_GPU_SPACE_SE3:
+        if (sp.dim != 7) return false;
+        g->F = 7;
+        return true;
+    case OMPL_GPU_SPACE_KCHAIN:
+        if (sp.dim < 1 || sp.dim > 16) return false;
+        g->nmax = sp.dim <= 4 ? 4 : sp.dim <= 8 ? 8 : sp.dim <= 12 ? 12 : 16;
+        g->F = 2 * g->nmax;
+        return true;
+    }
+    return false;
+}
+
+void host_features(const DevSpace &sp, const FeatGeom &g, const double *s, double *o) {
+    if (sp.kind == OMPL_GPU_SPACE_KCHAIN) {
+        double th = 0.;
+        for (int j = 0; j < g.nmax; ++j) {
+            if (j < sp.dim) {
+                th += s[j];
+                o[j] = std::cos(th);           // glibc, as the reference (KinematicChain.h:113-116)
+                o[g.nmax + j] = std::sin(th);
+            } else {
+                o[j] = 0.;
+                o[g.nmax + j] = 0.;
+            }
+        }
+    } else {
+        for (int j = 0; j < g.F; ++j) o[j] = j < sp.dim ? s[j] : 0.0;
+    }
+}
+
+int k_bucket(uint32_t k) {
+    if (k <= 1) return 1;
+    if (k <= 4) return 4;
+    if (k <= 16) return 16;
+    if (k <= 32) return 32;
+    if (k <= 64) return 64;
+    return 0;
+}
+
+namespace {
+
+struct KnnPlan {
+    bool stream;
+    uint32_t chunks;      // tiled: grid.y ; stream: blocks per query
+    uint32_t chunk_len;   // tiled only
+    int K;
+};
+
+KnnPlan knn_plan(uint32_t nq, uint32_t k, uint64_t n_end, int num_cus) {
+    KnnPlan p{};
+    p.K = k_bucket(k);
+    const uint64_t tiles = n_end / kTile;
+    if (nq < kStreamMaxQ) {
+        p.stream = true;
+        p.chunks = (uint32_t)((n_end + 256 * kStreamItems - 1) / (256 * kStreamItems));
+        if (p.chunks == 0) p.chunks = 1;
+        return p;
+    }
+    p.stream = false;
+    const uint64_t qblocks = (nq + kTile - 1) / kTile;
+    const uint64_t target = (uint64_t)num_cus * 8;  // ~8 resident blocks per CU
+    uint64_t S = (target + qblocks - 1) / qblocks;
+    S = std::max<uint64_t>(1, std::min<uint64_t>(S, std::max<uint64_t>(tiles, 1)));
+    const uint64_t tiles_per_chunk = (tiles + S - 1) / S;
+    p.chunk_len = (uint32_t)(std::max<uint64_t>(tiles_per_chunk, 1) * kTile);
+    p.chunks = (uint32_t)((n_end + p.chunk_len - 1) / p.chunk_len);
+    if (p.chunks == 0) p.chunks = 1;
+    return p;
+}
+
+// ---- dispatch over (space, feature bucket) then K -------------------------------
+template <int SP, int F, int NMAX, int K>
+hipError_t run_knn_k(const DevSpace &sp, const KnnPlan &p, const double *feat, uint64_t cap, uint64_t n_end,
+                     const double *qf, uint32_t nq, uint32_t k, double *od, uint32_t *oi, void *ws,
+                     hipStream_t st) {
+    double *pd = (double *)ws;
+    if (p.stream) {
+        const size_t np = (size_t)nq * p.chunks * K;
+        uint32_t *pi = (uint32_t *)(pd + np);
+        hipLaunchKernelGGL((knn_stream_kernel<SP, F, NMAX, K>), dim3(p.chunks, nq), dim3(256), 0, st, feat, cap,
+                           n_end, qf, sp, pd, pi);
+        hipLaunchKernelGGL((knn_stream_merge_kernel<K>), dim3(nq), dim3(256), 0, st, pd, pi, p.chunks, od, oi, k);
+        return hipGetLastError();
+    }
+    const dim3 grid((nq + kTile - 1) / kTile, p.chunks);
+    if (p.chunks == 1) {
+        hipLaunchKernelGGL((knn_tiled_kernel<SP, F, NMAX, K>), grid, dim3(kTile), 0, st, feat, cap, n_end, qf, nq,
+                           p.chunk_len, sp, od, oi, k);
+        return hipGetLastError();
+    }
+    const size_t np = (size_t)nq * p.chunks * K;
+    uint32_t *pi = (uint32_t *)(pd + np);
+    hipLaunchKernelGGL((knn_tiled_kernel<SP, F, NMAX, K>), grid, dim3(kTile), 0, st, feat, cap, n_end, qf, nq,
+                       p.chunk_len, sp, pd, pi, (uint32_t)K);
+    hipLaunchKernelGGL((knn_merge_kernel<K>), dim3((nq + 255) / 256), dim3(256), 0, st, pd, pi, p.chunks, nq, od,
+                       oi, k);
+    return hipGetLastError();
+}
+
+template <int SP, int F, int NMAX>
+hipError_t run_knn(const DevSpace &sp, const KnnPlan &p, const double *feat, uint64_t cap, uint64_t n_end,
+                   const double *qf, uint32_t nq, uint32_t k, double *od, uint32_t *oi, void *ws, hipStream_t st) {
+    switch (p.K) {
+    case 1: return run_knn_k<SP, F, NMAX, 1>(sp, p, feat, cap, n_end, qf, nq, k, od, oi, ws, st);
+    case 4: return run_knn_k<SP, F, NMAX, 4>(sp, p, feat, cap, n_end, qf, nq, k, od, oi, ws, st);
+    case 16: return run_knn_k<SP, F, NMAX, 16>(sp, p, feat, cap, n_end, qf, nq, k, od, oi, ws, st);
+    case 32: return run_knn_k<SP, F, NMAX, 32>(sp, p, feat, cap, n_end, qf, nq, k, od, oi, ws, st);
+    case 64: return run_knn_k<SP, F, NMAX, 64>(sp, p, feat, cap, n_end, qf, nq, k, od, oi, ws, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+#define OMPL_AMD_SPACE_DISPATCH(FN, ...)                                                              \
+    switch (sp.kind) {                                                                               \
+    case OMPL_GPU_SPACE_REALVECTOR:                                                                  \
+        if (g.F == 4) return FN<OMPL_GPU_SPACE_REALVECTOR, 4, 0>(__VA_ARGS__);                       \
+        if (g.F == 8) return FN<OMPL_GPU_SPACE_REALVECTOR, 8, 0>(__VA_ARGS__);                       \
+        return FN<OMPL_GPU_SPACE_REALVECTOR, 16, 0>(__VA_ARGS__);                                    \
+    case OMPL_GPU_SPACE_SO3: return FN<OMPL_GPU_SPACE_SO3, 4, 0>(__VA_ARGS__);                       \
+    case OMPL_GPU_SPACE_SE3: return FN<OMPL_GPU_SPACE_SE3, 7, 0>(__VA_ARGS__);                       \
+    case OMPL_GPU_SPACE_KCHAIN:                                                                      \
+        if (g.nmax == 4) return FN<OMPL_GPU_SPACE_KCHAIN, 8, 4>(__VA_ARGS__);                        \
+        if (g.nmax == 8) return FN<OMPL_GPU_SPACE_KCHAIN, 16, 8>(__VA_ARGS__);                       \
+        if (g.nmax == 12) return FN<OMPL_GPU_SPACE_KCHAIN, 24, 12>(__VA_ARGS__);                     \
+        return FN<OMPL_GPU_SPACE_KCHAIN, 32, 16>(__VA_ARGS__);                                       \
+    }                                                                                                \
+    return hipErrorInvalidValue;
+
+template <int SP, int F, int NMAX>
+hipError_t run_radius_count(const DevSpace &sp, const RadiusPlan &p, const double *feat, uint64_t cap,
+                            uint64_t n_end, const double *qf, uint32_t nq, double r, uint32_t *counts,
+                            hipStream_t st) {
+    if (p.stream) {
+        hipLaunchKernelGGL((radius_stream_kernel<SP, F, NMAX, false>), dim3((p.chunks + 3) / 4, nq), dim3(256), 0,
+                           st, feat, cap, n_end, qf, p.chunks, sp, r, counts, nullptr, nullptr, nullptr);
+    } else {
+        hipLaunchKernelGGL((radius_tiled_kernel<SP, F, NMAX, false>), dim3((nq + kTile - 1) / kTile, p.chunks),
+                           dim3(kTile), 0, st, feat, cap, n_end, qf, nq, p.chunk_len, p.chunks, sp, r, counts,
+                           nullptr, nullptr, nullptr);
+    }
+    return hipGetLastError();
+}
+
+template <int SP, int F, int NMAX>
+hipError_t run_radius_fill(const DevSpace &sp, const RadiusPlan &p, const double *feat, uint64_t cap,
+                           uint64_t n_end, const double *qf, uint32_t nq, double r, const uint64_t *offsets,
+                           uint32_t *ids, double *dists, hipStream_t st) {
+    if (p.stream) {
+        hipLaunchKernelGGL((radius_stream_kernel<SP, F, NMAX, true>), dim3((p.chunks + 3) / 4, nq), dim3(256), 0,
+                           st, feat, cap, n_end, qf, p.chunks, sp, r, nullptr, offsets, ids, dists);
+    } else {
+        hipLaunchKernelGGL((radius_tiled_kernel<SP, F, NMAX, true>), dim3((nq + kTile - 1) / kTile, p.chunks),
+                           dim3(kTile), 0, st, feat, cap, n_end, qf, nq, p.chunk_len, p.chunks, sp, r, nullptr,
+                           offsets, ids, dists);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t knn_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k, uint64_t n_end,
+                           int num_cus) {
+    (void)sp;
+    (void)g;
+    const KnnPlan p = knn_plan(nq, k, n_end, num_cus);
+    if (!p.stream && p.chunks == 1) return 0;
+    return (size_t)nq * p.chunks * p.K * (sizeof(double) + sizeof(uint32_t));
+}
+
+hipError_t launch_knn(const DevSpace &sp, const FeatGeom &g, const double *feat, uint64_t cap, uint64_t n_end,
+                      const double *qf, uint32_t nq, uint32_t k, double *od, uint32_t *oi, void *ws, size_t ws_bytes,
+                      int num_cus, hipStream_t st) {
+    if (nq == 0 || k == 0) return hipSuccess;
+    const KnnPlan p = knn_plan(nq, k, n_end, num_cus);
+    if (p.K == 0) return hipErrorInvalidValue;
+    if (knn_workspace_bytes(sp, g, nq, k, n_end, num_cus) > ws_bytes) return hipErrorInvalidValue;
+    OMPL_AMD_SPACE_DISPATCH(run_knn, sp, p, feat, cap, n_end, qf, nq, k, od, oi, ws, st)
+}
+
+RadiusPlan radius_plan(uint32_t nq, uint64_t n_end, int num_cus) {
+    RadiusPlan p{};
+    if (nq < kStreamMaxQ) {
+        p.stream = true;
+        p.chunk_len = 64 * kStreamItems;
+        p.chunks = (uint32_t)std::max<uint64_t>(1, (n_end + p.chunk_len - 1) / p.chunk_len);
+        return p;
+    }
+    const KnnPlan kp = knn_plan(nq, 1, n_end, num_cus);
+    p.stream = false;
+    p.chunk_len = kp.chunk_len;
+    p.chunks = kp.chunks;
+    return p;
+}
+
+hipError_t launch_radius_count(const DevSpace &sp, const FeatGeom &g, const RadiusPlan &p, const double *feat,
+                               uint64_t cap, uint64_t n_end, const double *qf, uint32_t nq, double r,
+                               uint32_t *counts, hipStream_t st) {
+    OMPL_AMD_SPACE_DISPATCH(run_radius_count, sp, p, feat, cap, n_end, qf, nq, r, counts, st)
+}
+
+hipError_t launch_radius_fill(const DevSpace &sp, const FeatGeom &g, const RadiusPlan &p, const double *feat,
+                              uint64_t cap, uint64_t n_end, const double *qf, uint32_t nq, double r,
+                              const uint64_t *offsets, uint32_t *ids, double *dists, hipStream_t st) {
+    OMPL_AMD_SPACE_DISPATCH(run_radius_fill, sp, p, feat, cap, n_end, qf, nq, r, offsets, ids, dists, st)
+}
+
+hipError_t launch_features(const DevSpace &sp, const FeatGeom &g, const double *raw, uint32_t n, double *feat,
+                           hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(features_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sp, g, raw, n, feat);
+    return hipGetLastError();
+}
+
+hipError_t launch_store_soa(const double *aos, uint32_t n, int width, double *soa, uint64_t cap, uint64_t first,
+                            hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t t = (uint64_t)n * width;
+    hipLaunchKernelGGL(store_soa_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, aos, n, width, soa, cap,
+                       first);
+    return hipGetLastError();
+}
+
+hipError_t launch_steer(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
+                        const uint32_t *nearest, uint32_t stride, double maxd, double *from, double *to,
+                        hipStream_t st) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(steer_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, sp, raw, cap, q, nq, nearest, stride,
+                       maxd, from, to);
+    return hipGetLastError();
+}
+
+}  // namespace ompl_amd

@@ -1,0 +1,140 @@
+// motion.hip — discrete motion validation and state validity for gfx950.
+//
+// DiscreteMotionValidator::checkMotion(s1, s2) (DiscreteMotionValidator.cpp:93-145)
+// checks s2, then the interior samples j/nd, j in [1, nd-1], in FIFO-bisection order
+// with early exit; s1 is assumed valid.  The result bit does not depend on the order,
+// but the work does, so each thread walks the same order without a queue: the FIFO
+// visits the implicit interval tree level by level, left to right, so level L is
+// enumerated by the 2^L root-to-node paths and empty intervals are skipped.  The
+// number of isValid() calls therefore equals the reference's exactly (counters[2]).
+//
+// The lastValid variant (DiscreteMotionValidator.cpp:48-91, linear sweep) is served
+// by first_invalid: the first failing j in linear order, nd when only s2 fails.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace ompl_amd {
+
+__device__ __forceinline__ void load_state(const double *__restrict__ p, int dim, double *o) {
+    for (int c = 0; c < dim; ++c) o[c] = p[c];
+}
+
+__global__ __launch_bounds__(256) void motion_kernel(DevSpace sp, DevChecker ck, const double *__restrict__ s1,
+                                                     const double *__restrict__ s2, uint32_t m,
+                                                     uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out,
+                                                     int32_t *__restrict__ fi_out,
+                                                     unsigned long long *__restrict__ counters, int rot) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    bool result = true;
+    uint32_t checks = 0;
+    if (e < m) {
+        const int dim = sp.dim;
+        double a[kChainMaxLinks], b[kChainMaxLinks], t[kChainMaxLinks];
+        load_state(s1 + (size_t)e * dim, dim, a);
+        load_state(s2 + (size_t)e * dim, dim, b);
+        const int nd = (int)valid_segment_count(sp, a, b);
+        if (nd_out) nd_out[e] = nd;
+        ++checks;
+        result = is_valid(sp, ck, b);  // :96
+        if (result && nd >= 2) {
+            // level-order walk of the FIFO bisection :104-134
+            bool any = true;
+            for (int L = 0; any && result && L < 32; ++L) {
+                any = false;
+                const uint32_t np = 1u << L;
+                for (uint32_t p = 0; p < np && result; ++p) {
+                    int lo = 1, hi = nd - 1;
+                    bool empty = false;
+                    for (int bit = L - 1; bit >= 0; --bit) {
+                        const int mid = (lo + hi) / 2;
+                        if ((p >> bit) & 1u)
+                            lo = mid + 1;
+                        else
+                            hi = mid - 1;
+                        if (lo > hi) {
+                            empty = true;
+                            break;
+                        }
+                    }
+                    if (empty) continue;
+                    any = true;
+                    const int mid = (lo + hi) / 2;
+                    interpolate(sp, a, b, (double)mid / (double)nd, t, rot != 0);
+                    ++checks;
+                    if (!is_valid(sp, ck, t)) result = false;
+                }
+            }
+        }
+        if (valid) valid[e] = result ? 1 : 0;
+        if (fi_out) {
+            int fi = -1;
+            if (!result) {
+                // linear sweep :57-69, then s2 :73-79
+                for (int j = 1; j < nd; ++j) {
+                    interpolate(sp, a, b, (double)j / (double)nd, t, rot != 0);
+                    if (!is_valid(sp, ck, t)) {
+                        fi = j;
+                        break;
+                    }
+                }
+                if (fi < 0) fi = nd;
+            }
+            fi_out[e] = fi;
+        }
+    }
+    if (counters) {
+        // wave-aggregated counter updates: valid_, invalid_ (MotionValidator.h:136-139), isValid calls
+        unsigned long long nv = (e < m && result) ? 1ull : 0ull;
+        unsigned long long ni = (e < m && !result) ? 1ull : 0ull;
+        unsigned long long nc = checks;
+        for (int off = 32; off > 0; off >>= 1) {
+            nv += __shfl_xor(nv, off, 64);
+            ni += __shfl_xor(ni, off, 64);
+            nc += __shfl_xor(nc, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (nv) atomicAdd(&counters[0], nv);
+            if (ni) atomicAdd(&counters[1], ni);
+            if (nc) atomicAdd(&counters[2], nc);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void state_valid_kernel(DevSpace sp, DevChecker ck, const double *__restrict__ s,
+                                                          uint32_t m, uint8_t *__restrict__ valid) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    double a[kChainMaxLinks];
+    load_state(s + (size_t)i * sp.dim, sp.dim, a);
+    valid[i] = is_valid(sp, ck, a) ? 1 : 0;
+}
+
+static bool needs_rotation(const DevSpace &sp, const DevChecker &ck) {
+    if (sp.kind != OMPL_GPU_SPACE_SE3) return true;
+    switch (ck.kind) {
+    case OMPL_GPU_CHECK_ALL_VALID: return false;
+    case OMPL_GPU_CHECK_HYPERCUBE: return ck.ndim > 3;
+    case OMPL_GPU_CHECK_SPHERES: return false;
+    case OMPL_GPU_CHECK_CIRCLES2D: return false;
+    default: return true;
+    }
+}
+
+hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double *s1, const double *s2, uint32_t m,
+                         uint8_t *valid, int32_t *nd, int32_t *first_invalid, unsigned long long *counters,
+                         hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(motion_kernel, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd,
+                       first_invalid, counters, needs_rotation(sp, ck) ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const double *s, uint32_t m, uint8_t *valid,
+                              hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(state_valid_kernel, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s, m, valid);
+    return hipGetLastError();
+}
+
+}  // namespace ompl_amd

@@ -1,0 +1,99 @@
+"""Python mirror of ompl::base::DiscreteMotionValidator / StateValidityChecker
+(MotionValidator.h:56-145, DiscreteMotionValidator.cpp:48-145) over the MI355X
+C ABI, for the closed set of device checkers in :mod:`ompl_amd.checkers`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .checkers import Checker
+from .spaces import StateSpace
+
+
+class DiscreteMotionValidatorGPU:
+    def __init__(self, space: StateSpace, checker: Checker, device: int = 0):
+        self.space = space
+        self.checker = checker
+        self.dim = space.dim
+        self._space_struct = space.to_abi()
+        self._checker_struct = checker.to_abi()
+        h = C.c_void_p()
+        abi.check(abi.lib.ompl_gpu_mv_create(C.byref(h), C.byref(self._space_struct),
+                                             C.byref(self._checker_struct), int(device)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            abi.lib.ompl_gpu_mv_destroy(h)
+            self._h = None
+
+    def checkMotions(self, s1, s2, want_nd: bool = False, want_first_invalid: bool = False):
+        a = abi.as_states(s1, self.dim)
+        b = abi.as_states(s2, self.dim)
+        if a.shape != b.shape:
+            raise ValueError("s1 and s2 must have the same shape")
+        m = a.shape[0]
+        valid = np.zeros(m, dtype=np.uint8)
+        nd = np.zeros(m, dtype=np.int32) if want_nd else None
+        fi = np.zeros(m, dtype=np.int32) if want_first_invalid else None
+        abi.check(abi.lib.ompl_gpu_mv_check(
+            self._h, abi.dptr(a), abi.dptr(b), m, valid.ctypes.data_as(abi._U8),
+            nd.ctypes.data_as(abi._I32) if nd is not None else None,
+            fi.ctypes.data_as(abi._I32) if fi is not None else None))
+        out = [valid.astype(bool)]
+        if want_nd:
+            out.append(nd)
+        if want_first_invalid:
+            out.append(fi)
+        return out[0] if len(out) == 1 else tuple(out)
+
+    def checkMotion(self, s1, s2, lastValid: bool = False):
+        """checkMotion(s1,s2) -> bool; with lastValid=True returns (bool, t) where t is
+        lastValid.second = (j-1)/nd of the first invalid sample (DiscreteMotionValidator.cpp:63-77)."""
+        if not lastValid:
+            return bool(self.checkMotions(s1, s2)[0])
+        v, nd, fi = self.checkMotions(s1, s2, want_nd=True, want_first_invalid=True)
+        if v[0]:
+            return True, None
+        j, n = int(fi[0]), int(nd[0])
+        return False, (j - 1) / n if n else float("-inf")
+
+    def getValidMotionCount(self) -> int:
+        v, i = C.c_uint64(0), C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_mv_counters(self._h, C.byref(v), C.byref(i)))
+        return v.value
+
+    def getInvalidMotionCount(self) -> int:
+        v, i = C.c_uint64(0), C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_mv_counters(self._h, C.byref(v), C.byref(i)))
+        return i.value
+
+    def stateChecks(self) -> int:
+        c = C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_mv_state_checks(self._h, C.byref(c)))
+        return c.value
+
+    def resetMotionCounter(self) -> None:
+        abi.check(abi.lib.ompl_gpu_mv_reset_counters(self._h))
+
+    def isValid(self, states) -> np.ndarray:
+        s = abi.as_states(states, self.dim)
+        out = np.zeros(s.shape[0], dtype=np.uint8)
+        abi.check(abi.lib.ompl_gpu_svc_check(self._h, abi.dptr(s), s.shape[0], out.ctypes.data_as(abi._U8)))
+        return out.astype(bool)
+
+    # device-resident
+    def set_stream(self, stream_ptr: int | None) -> None:
+        abi.check(abi.lib.ompl_gpu_mv_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
+
+    def sync(self) -> None:
+        abi.check(abi.lib.ompl_gpu_mv_sync(self._h))
+
+    def check_device(self, d_s1: int, d_s2: int, m: int, d_valid: int, d_nd: int = 0, d_fi: int = 0) -> None:
+        abi.check(abi.lib.ompl_gpu_mv_check_device(self._h, C.c_void_p(d_s1), C.c_void_p(d_s2), m,
+                                                   C.c_void_p(d_valid), C.c_void_p(d_nd or None),
+                                                   C.c_void_p(d_fi or None)))

@@ -1,0 +1,141 @@
+"""Python mirror of the reference's ompl::NearestNeighbors<_T> for integer element
+ids (the form PRM and Blaze use: NearestNeighbors<Vertex>, PRM.h:125), backed by
+the MI355X C ABI.  Method names and semantics follow NearestNeighbors.h:46-115:
+
+  add / remove / clear / size / list / nearest / nearestK / nearestR /
+  reportsSortedResults  — plus batched forms (nearestKBatch, nearestRBatch) and
+  device-resident forms used by the benchmark.
+
+Element ids are insertion indices.  Results are sorted by (distance, id).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .spaces import StateSpace
+
+
+class NearestNeighborsGPU:
+    def __init__(self, space: StateSpace, device: int = 0):
+        self.space = space
+        self.dim = space.dim
+        self._space_struct = space.to_abi()
+        h = C.c_void_p()
+        abi.check(abi.lib.ompl_gpu_nn_create(C.byref(h), C.byref(self._space_struct), int(device)))
+        self._h = h
+        self._removed: set[int] = set()
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            abi.lib.ompl_gpu_nn_destroy(h)
+            self._h = None
+
+    # ---- container ---------------------------------------------------------
+    def reportsSortedResults(self) -> bool:
+        return True
+
+    def add(self, states) -> np.ndarray:
+        s = abi.as_states(states, self.dim)
+        first = C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_nn_add(self._h, abi.dptr(s), s.shape[0], C.byref(first)))
+        return np.arange(first.value, first.value + s.shape[0], dtype=np.uint64)
+
+    def remove(self, elem_id: int) -> bool:
+        st = abi.lib.ompl_gpu_nn_remove(self._h, int(elem_id))
+        if st == abi.ERR_NOT_FOUND:
+            return False
+        abi.check(st)
+        self._removed.add(int(elem_id))
+        return True
+
+    def clear(self) -> None:
+        abi.check(abi.lib.ompl_gpu_nn_clear(self._h))
+        self._removed.clear()
+
+    def size(self) -> int:
+        live, tot = C.c_size_t(0), C.c_size_t(0)
+        abi.check(abi.lib.ompl_gpu_nn_size(self._h, C.byref(live), C.byref(tot)))
+        return live.value
+
+    def total(self) -> int:
+        live, tot = C.c_size_t(0), C.c_size_t(0)
+        abi.check(abi.lib.ompl_gpu_nn_size(self._h, C.byref(live), C.byref(tot)))
+        return tot.value
+
+    def states(self, first: int = 0, n: int | None = None) -> np.ndarray:
+        n = self.total() - first if n is None else n
+        out = np.empty((n, self.dim), dtype=np.float64)
+        abi.check(abi.lib.ompl_gpu_nn_get_states(self._h, int(first), int(n), abi.dptr(out)))
+        return out
+
+    # ---- queries -----------------------------------------------------------
+    def nearest(self, q) -> int:
+        qs = abi.as_states(q, self.dim)
+        ids = np.empty(qs.shape[0], dtype=np.uint64)
+        d = np.empty(qs.shape[0], dtype=np.float64)
+        abi.check(abi.lib.ompl_gpu_nn_nearest(self._h, abi.dptr(qs), qs.shape[0],
+                                              ids.ctypes.data_as(abi._U64), abi.dptr(d)))
+        return int(ids[0])
+
+    def nearestKBatch(self, queries, k: int):
+        """ids [nq, k] (uint64, NO_ID64 padding), dists [nq, k], counts [nq]."""
+        qs = abi.as_states(queries, self.dim)
+        nq = qs.shape[0]
+        ids = np.full((nq, max(k, 1)), abi.NO_ID64, dtype=np.uint64)
+        d = np.full((nq, max(k, 1)), np.inf, dtype=np.float64)
+        cnt = np.zeros(nq, dtype=np.uint32)
+        abi.check(abi.lib.ompl_gpu_nn_knn(self._h, abi.dptr(qs), nq, int(k), ids.ctypes.data_as(abi._U64),
+                                          abi.dptr(d), cnt.ctypes.data_as(abi._U32)))
+        return ids[:, :k], d[:, :k], cnt
+
+    def nearestK(self, q, k: int) -> list:
+        ids, _, cnt = self.nearestKBatch(q, k)
+        return [int(x) for x in ids[0, :cnt[0]]]
+
+    def nearestRBatch(self, queries, radius: float):
+        """CSR: (offsets [nq+1], ids, dists) sorted by (distance, id) per query."""
+        qs = abi.as_states(queries, self.dim)
+        nq = qs.shape[0]
+        pid = abi._U64()
+        pd = abi._D()
+        off = np.zeros(nq + 1, dtype=np.uint64)
+        abi.check(abi.lib.ompl_gpu_nn_radius(self._h, abi.dptr(qs), nq, float(radius), C.byref(pid), C.byref(pd),
+                                             off.ctypes.data_as(abi._U64)))
+        tot = int(off[-1])
+        try:
+            ids = np.ctypeslib.as_array(pid, shape=(max(tot, 1),))[:tot].copy()
+            d = np.ctypeslib.as_array(pd, shape=(max(tot, 1),))[:tot].copy()
+        finally:
+            abi.lib.ompl_gpu_free(C.cast(pid, C.c_void_p))
+            abi.lib.ompl_gpu_free(C.cast(pd, C.c_void_p))
+        return off, ids, d
+
+    def nearestR(self, q, radius: float) -> list:
+        off, ids, _ = self.nearestRBatch(q, radius)
+        return [int(x) for x in ids[int(off[0]):int(off[1])]]
+
+    def list(self) -> list:
+        """Live element ids (insertion order; the reference's order is unspecified)."""
+        return [i for i in range(self.total()) if i not in self._removed]
+
+    # ---- device-resident (benchmark / pipelines); pointers are device addresses
+    def set_stream(self, stream_ptr: int | None) -> None:
+        abi.check(abi.lib.ompl_gpu_nn_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
+
+    def sync(self) -> None:
+        abi.check(abi.lib.ompl_gpu_nn_sync(self._h))
+
+    def knn_device(self, d_queries: int, nq: int, k: int, d_ids: int, d_dist: int) -> None:
+        abi.check(abi.lib.ompl_gpu_nn_knn_device(self._h, C.c_void_p(d_queries), nq, k, C.c_void_p(d_ids),
+                                                 C.c_void_p(d_dist)))
+
+    def steer_device(self, d_queries: int, nq: int, d_nearest: int, stride: int, max_distance: float,
+                     d_from: int, d_to: int) -> None:
+        abi.check(abi.lib.ompl_gpu_steer_device(self._h, C.c_void_p(d_queries), nq, C.c_void_p(d_nearest),
+                                                int(stride), float(max_distance), C.c_void_p(d_from),
+                                                C.c_void_p(d_to)))

@@ -1,0 +1,75 @@
+"""Synthetic inputs of the BASELINE.json configurations (numpy, seeded).
+
+Samplers restate the reference's distributions (not its bit streams — parity is
+defined on identical inputs, which the tests feed to both sides):
+  uniform R^n in bounds          RealVectorStateSampler::sampleUniform (RealVectorStateSpace.cpp:45-53)
+  uniform SO3, Shoemake          RNG::quaternion (util/src/RandomNumbers.cpp:263-279)
+  SE3 = uniform R^3 x SO3        CompoundStateSampler::sampleUniform (base/src/StateSampler.cpp:47-52)
+Environments:
+  createHornEnvironment(d, eps)  demos/KinematicChain.h:279-315
+  sphere field                   32 spheres, r = 0.1, seed 7
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+def uniform_rv(rng: np.random.Generator, n: int, dim: int, low=0.0, high=1.0) -> np.ndarray:
+    return rng.uniform(low, high, size=(n, dim))
+
+
+def uniform_quat(rng: np.random.Generator, n: int) -> np.ndarray:
+    x0 = rng.random(n)
+    r1, r2 = np.sqrt(1.0 - x0), np.sqrt(x0)
+    t1 = 2.0 * math.pi * rng.random(n)
+    t2 = 2.0 * math.pi * rng.random(n)
+    return np.column_stack([np.sin(t1) * r1, np.cos(t1) * r1, np.sin(t2) * r2, np.cos(t2) * r2])
+
+
+def uniform_se3(rng: np.random.Generator, n: int, low=0.0, high=1.0) -> np.ndarray:
+    return np.ascontiguousarray(np.column_stack([rng.uniform(low, high, size=(n, 3)), uniform_quat(rng, n)]))
+
+
+def uniform_chain(rng: np.random.Generator, n: int, links: int) -> np.ndarray:
+    return rng.uniform(-math.pi, math.pi, size=(n, links))
+
+
+def horn_environment(d: int, eps: float) -> np.ndarray:
+    """createHornEnvironment (demos/KinematicChain.h:279-315), segments (x0,y0,x1,y1)."""
+    env = []
+    w = 1.0 / float(d)
+    x, y, theta = w, -eps, 0.0
+    scale = w * (1.0 + math.pi * eps)
+    for _ in range(d - 1):
+        theta += math.pi / float(d)
+        xN = x + math.cos(theta) * scale
+        yN = y + math.sin(theta) * scale
+        env.append((x, y, xN, yN))
+        x, y = xN, yN
+    theta, x, y = 0.0, w, eps
+    scale = w * (1.0 - math.pi * eps)
+    for _ in range(d - 1):
+        theta += math.pi / d
+        xN = x + math.cos(theta) * scale
+        yN = y + math.sin(theta) * scale
+        env.append((x, y, xN, yN))
+        x, y = xN, yN
+    return np.array(env, dtype=np.float64)
+
+
+def sphere_field(count: int = 32, radius: float = 0.1, seed: int = 7, low=0.0, high=1.0):
+    rng = np.random.default_rng(seed)
+    return rng.uniform(low, high, size=(count, 3)), np.full(count, radius)
+
+
+def rrt_star_k(n: int, d: int) -> int:
+    """k_rrt * log(n+1), k_rrt = 1.1 * 2^(d+1) e (1 + 1/d)  (RRTstar.cpp:609, :1147-1159)."""
+    k_rrt = 1.1 * (2.0 ** (d + 1) * math.e * (1.0 + 1.0 / d))
+    return int(math.ceil(k_rrt * math.log(n + 1)))
+
+
+def prm_star_k(n: int, d: int) -> int:
+    """ceil((e + e/d) log n)  (ConnectionStrategy.h:141-149)."""
+    return int(math.ceil((math.e + math.e / d) * math.log(n)))

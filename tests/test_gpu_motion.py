@@ -1,0 +1,93 @@
+"""GPU parity tests of the motion-validation path (through the C ABI): validity bits,
+segment counts, first-invalid samples and isValid-call counts must be identical to the
+oracle restatement of DiscreteMotionValidator and to the golden fixtures."""
+import math
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+from ompl_amd import DiscreteMotionValidatorGPU
+from ompl_amd import workloads as W
+from ompl_amd.checkers import (AllValidChecker, Circles2DChecker, HypercubeChecker, KinematicChainChecker,
+                               SpheresChecker)
+from ompl_amd.spaces import KinematicChainSpace, RealVectorStateSpace, SE3StateSpace
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(name, golden):
+    if name == "se3_hypercube":
+        return SE3StateSpace(), HypercubeChecker(3, 0.1)
+    if name == "se3_spheres":
+        c, r = W.sphere_field(32, 0.1, 7)
+        return SE3StateSpace(), SpheresChecker(c, r)
+    if name == "r6_hypercube":
+        sp = RealVectorStateSpace(6)
+        sp.setLongestValidSegmentFraction(0.001)
+        return sp, HypercubeChecker(6, 0.1)
+    if name == "chain12_horn":
+        return KinematicChainSpace(12, 1.0 / 12), KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))
+    sp = RealVectorStateSpace(2, 0.0, 100.0)
+    sp.setLongestValidSegmentFraction(0.002)
+    return sp, Circles2DChecker(golden("circles2d.npz")["obstacles"])
+
+
+@pytest.mark.parametrize("name", ["se3_hypercube", "se3_spheres", "r6_hypercube", "chain12_horn", "r2_circles"])
+def test_motion_golden(gpu, golden, name):
+    g = golden(f"motion_{name}.npz")
+    sp, ck = _case(name, golden)
+    mv = DiscreteMotionValidatorGPU(sp, ck, gpu)
+    valid, nd, fi = mv.checkMotions(g["s1"], g["s2"], want_nd=True, want_first_invalid=True)
+    np.testing.assert_array_equal(nd, g["nd"])
+    np.testing.assert_array_equal(valid, g["valid"])
+    np.testing.assert_array_equal(fi, g["first_invalid"])
+    assert mv.getValidMotionCount() == int(g["valid"].sum())
+    assert mv.getInvalidMotionCount() == int((~g["valid"]).sum())
+    assert mv.stateChecks() == int(g["checks"])  # same isValid() work as the FIFO bisection
+    np.testing.assert_array_equal(mv.isValid(g["s2"]), g["s2_valid"])
+    mv.resetMotionCounter()
+    assert mv.getValidMotionCount() == 0 and mv.getInvalidMotionCount() == 0
+
+
+def test_motion_random_vs_oracle(gpu):
+    rng = np.random.default_rng(21)
+    sp = SE3StateSpace()
+    c, r = W.sphere_field(32, 0.1, 7)
+    ck = SpheresChecker(c, r)
+    a, b = W.uniform_se3(rng, 100000), W.uniform_se3(rng, 100000)
+    mv = DiscreteMotionValidatorGPU(sp, ck, gpu)
+    valid, nd, fi = mv.checkMotions(a, b, want_nd=True, want_first_invalid=True)
+    ov, ond, ofi, checks = O.check_motions(sp, ck, a, b)
+    np.testing.assert_array_equal(nd, ond)
+    np.testing.assert_array_equal(valid, ov)
+    np.testing.assert_array_equal(fi, ofi)
+    assert mv.stateChecks() == checks
+
+
+def test_motion_edge_cases(gpu):
+    sp = SE3StateSpace()
+    mv = DiscreteMotionValidatorGPU(sp, AllValidChecker(), gpu)
+    rng = np.random.default_rng(3)
+    a = W.uniform_se3(rng, 10)
+    v, nd = mv.checkMotions(a, a, want_nd=True)           # s1 == s2: nd = 0, s2 checked only
+    assert v.all() and (nd == 0).all()
+    assert mv.checkMotion(a[0], a[1]) is True
+    ok, t = mv.checkMotion(a[0], a[1], lastValid=True)
+    assert ok and t is None
+    hc = DiscreteMotionValidatorGPU(sp, HypercubeChecker(3, 0.1), gpu)
+    s1 = np.array([0.05, 0.05, 0.05, 0, 0, 0, 1.0])
+    s2 = np.array([0.5, 0.5, 0.5, 0, 0, 0, 1.0])        # s2 invalid
+    ok, t = hc.checkMotion(s1, s2, lastValid=True)
+    _, ond, ofi, _ = O.check_motions(sp, HypercubeChecker(3, 0.1), s1[None], s2[None])
+    assert not ok and t == (ofi[0] - 1) / ond[0]
+    assert hc.checkMotions(np.zeros((0, 7)), np.zeros((0, 7))).shape == (0,)
+
+
+def test_state_validity_random(gpu):
+    rng = np.random.default_rng(4)
+    sp = KinematicChainSpace(12, 1.0 / 12)
+    ck = KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))
+    x = W.uniform_chain(rng, 50000, 12)
+    mv = DiscreteMotionValidatorGPU(sp, ck, gpu)
+    np.testing.assert_array_equal(mv.isValid(x), O.is_valid(sp, ck, x))
