@@ -116,7 +116,7 @@ def main():
     from ompl_amd.spaces import SE3StateSpace
 
     dev = torch.device("cuda", local)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # a real (non-null) stream shared by torch events and the library
     sp = SE3StateSpace(0.0, 1.0)
     ck = HypercubeChecker(3, 0.1)
     tree = W.uniform_se3(np.random.default_rng(42), args.tree)      # identical on every rank

@@ -95,7 +95,22 @@ SIGNATURES = {
 }
 
 
+def _share_torch_runtime():
+    """PyTorch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so, SONAME
+    libamdhip64.so.7).  Loading torch first makes the dynamic linker bind this library's
+    libamdhip64.so.7 dependency to that same runtime, so device pointers and streams
+    from torch (plumbing for the device-resident API and RCCL) are valid here.  Without
+    torch the system ROCm runtime is used."""
+    if os.environ.get("OMPL_GPU_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _load():
+    _share_torch_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"ompl_amd: {LIB_PATH} is missing — build it with `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -1,0 +1,40 @@
+"""The C++ plugin (include/ompl_amd/NearestNeighborsGPU.h) compiles against the OMPL
+interface — the standalone surface and, where the reference tree is present, the
+reference's own datastructures/NearestNeighbors.h — and on the GPU answers planner-style
+queries identically to the oracle."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "cpp", "plugin_test.cpp")
+REF_SRC = "/root/reference/src"
+
+
+def _build(out, extra):
+    cmd = ["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "include"), *extra, SRC, "-o", out,
+           "-L", os.path.join(ROOT, "ompl_amd", "lib"), "-L", os.path.join(ROOT, "oracle"), "-lompl_gpu", "-loracle",
+           f"-Wl,-rpath,{os.path.join(ROOT, 'ompl_amd', 'lib')}", f"-Wl,-rpath,{os.path.join(ROOT, 'oracle')}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return out
+
+
+def test_plugin_compiles_standalone(tmp_path):
+    exe = _build(str(tmp_path / "plugin_sa"), [])
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0 and "PLUGIN COMPILED" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_SRC, "ompl/datastructures/NearestNeighbors.h")),
+                    reason="reference sources absent")
+def test_plugin_compiles_against_reference_interface(tmp_path):
+    _build(str(tmp_path / "plugin_ref"), ["-DOMPL_AMD_WITH_OMPL", "-I", REF_SRC])
+
+
+@pytest.mark.gpu
+def test_plugin_runs_on_gpu(tmp_path, gpu):
+    exe = _build(str(tmp_path / "plugin_run"), [])
+    r = subprocess.run([exe, "run"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "PLUGIN OK" in r.stdout, r.stdout + r.stderr

@@ -23,3 +23,9 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py
 fi
+if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
+    TAG=${2:-r1}
+    step prof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o trace --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline
+    step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_$TAG -o pmc_fetch --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+    step prof_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_$TAG -o pmc_write --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+fi
