@@ -17,7 +17,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -28,8 +27,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "NN queries/sec + motion checks/sec on 10^6-state SE(3) tree"
-FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector/matrix peak (MI355X_MICROARCH.md)
-F_SE3 = 21                # flops per SE(3) distance, SURVEY.md §8d (sqrt, acos counted as 1 each)
+PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X vector peaks (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0                       # HBM3E spec
+F_SE3 = 21  # flops per SE(3) distance, SURVEY.md §8d (sqrt and acos counted as 1 each)
+B_SE3 = {"f32": 28, "f64": 56}              # bytes per stored SE(3) state streamed by a scan
 
 
 def parse():
@@ -40,8 +41,10 @@ def parse():
     ap.add_argument("--tree", type=int, default=1_000_000)
     ap.add_argument("--queries", type=int, default=100_000, help="samples per GPU per step")
     ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--exact", action="store_true", help="force the exact fp64 scan (no fp32 screen)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--single-query-reps", type=int, default=200, help="RRT-style one-query scans (0 = skip)")
     return ap.parse_args()
 
 
@@ -60,7 +63,7 @@ def cpu_baseline(sp, ck, tree, rng, k, budget_s):
     nq = 500
     q = W.uniform_se3(rng, nq)
     t0 = time.perf_counter()
-    ids, _, _ = g.knn(q, k)
+    g.knn(q, k)
     t_probe = time.perf_counter() - t0
     nq = int(min(20000, max(nq, 0.6 * budget_s / max(t_probe / nq, 1e-9))))
     q = W.uniform_se3(rng, nq)
@@ -72,26 +75,51 @@ def cpu_baseline(sp, ck, tree, rng, k, budget_s):
     s2 = np.empty_like(q)
     for i in range(nq):  # steering is not timed on the CPU side (favours the CPU)
         s2[i] = O.interpolate(sp, s1[i], q[i], maxd / d[i, 0]) if d[i, 0] > maxd else q[i]
-    reps = 1
     t0 = time.perf_counter()
     O.check_motions_mt(sp, ck, s1, s2, 1)
     t_mv = time.perf_counter() - t0
+    reps = 1
     if t_mv < 0.3 * budget_s:
         reps = int(max(1, 0.3 * budget_s / max(t_mv, 1e-9)))
         t0 = time.perf_counter()
         for _ in range(reps):
             O.check_motions_mt(sp, ck, s1, s2, 1)
         t_mv = (time.perf_counter() - t0) / reps
-    qps = nq / t_nn
-    mps = nq / t_mv
-    value = 2.0 / (1.0 / qps + 1.0 / mps)  # same op mix as one GPU step: 1 query + 1 motion check
+    qps, mps = nq / t_nn, nq / t_mv
     return {
-        "value": value, "unit": "(NN queries + motion checks)/s", "cores": 1, "kind": "port",
+        "value": 2.0 / (1.0 / qps + 1.0 / mps),  # same op mix as a GPU step: 1 query + 1 motion check
+        "unit": "(NN queries + motion checks)/s", "cores": 1, "kind": "port",
         "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same 10^6-state "
-                   f"SE(3) tree, {nq} nearestK(k={k}) queries; {nq} checkMotion(nearest, steered) x{reps} "
+                   f"SE(3) tree: {nq} nearestK(k={k}) queries, then {nq} checkMotion(nearest, steered) x{reps} "
                    f"with the oracle DiscreteMotionValidator; index build {build_s:.2f} s excluded"),
         "nn_queries_per_s": qps, "motion_checks_per_s": mps,
     }
+
+
+def single_query_scan(torch, nn, dev, reps, n_tree):
+    """RRT semantics (RRT.cpp:137): one nearest() per iteration -> the stream kernel, HBM/MALL bound."""
+    from ompl_amd import workloads as W
+
+    q = torch.from_numpy(W.uniform_se3(np.random.default_rng(99), reps)).to(dev)
+    ids = torch.empty(reps, dtype=torch.int32, device=dev)
+    dd = torch.empty(reps, dtype=torch.float64, device=dev)
+    for i in range(5):
+        nn.knn_device(q[i].data_ptr(), 1, 1, ids[i].data_ptr(), dd[i].data_ptr())
+    torch.cuda.synchronize(dev)
+    ms0, n0, _ = nn.kernel_time()
+    t0 = time.perf_counter()
+    for i in range(reps):
+        nn.knn_device(q[i].data_ptr(), 1, 1, ids[i].data_ptr(), dd[i].data_ptr())
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    ms1, n1, name = nn.kernel_time()
+    kern_ms = (ms1 - ms0) / max(n1 - n0, 1)
+    achieved = n_tree * B_SE3["f64"] / (kern_ms * 1e-3) / 1e9
+    return {"queries_per_s": reps / wall, "kernel": name, "kernel_us": kern_ms * 1e3,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "algorithmic": f"{n_tree} states x {B_SE3['f64']} B per query (fp64 SoA)",
+                         "note": "the 56 MB store is Infinity-Cache resident across back-to-back scans"}}
 
 
 def main():
@@ -102,13 +130,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
 
     from ompl_amd import DiscreteMotionValidatorGPU, NearestNeighborsGPU
     from ompl_amd import workloads as W
@@ -125,6 +151,7 @@ def main():
     queries = torch.from_numpy(W.uniform_se3(qrng, nq)).to(dev)
 
     nn = NearestNeighborsGPU(sp, local)
+    nn.set_exact(args.exact)
     nn.add(tree)
     mv = DiscreteMotionValidatorGPU(sp, ck, local)
     nn.set_stream(stream.cuda_stream)
@@ -135,7 +162,6 @@ def main():
     s_to = torch.empty_like(queries)
     valid = torch.empty(nq, dtype=torch.uint8, device=dev)
     maxd = 0.2 * sp.getMaximumExtent()  # RRT range default (SelfConfig.cpp:98)
-
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
 
     def step(e=None):
@@ -154,6 +180,9 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    nn.profile(True)
+    nn.kernel_time()
+    scr0, fb0 = nn.stats()
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -165,24 +194,31 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    kern_ms_total, kern_n, kern_name = nn.kernel_time()
+    kern_ms = kern_ms_total / max(kern_n, 1)
+    scr1, fb1 = nn.stats()
     knn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     steer_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     mv_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
-    t = torch.tensor([elapsed, knn_ms, steer_ms, mv_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, knn_ms, steer_ms, mv_ms, kern_ms], dtype=torch.float64, device=dev)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, knn_ms, steer_ms, mv_ms = t.tolist()
+    elapsed, knn_ms, steer_ms, mv_ms, kern_ms = t.tolist()
     valid_frac = float(valid.float().mean().item())
 
+    single = None
+    if rank == 0 and args.single_query_reps > 0:
+        single = single_query_scan(torch, nn, dev, args.single_query_reps, args.tree)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sp, ck, tree, np.random.default_rng(7), k, args.cpu_seconds)
 
     if rank == 0:
-        total_ops = 2.0 * nq * world * args.steps
-        value = total_ops / elapsed
+        value = 2.0 * nq * world * args.steps / elapsed
+        screen = kern_name.startswith("knn32")
+        dt = "f32" if screen else "f64"
         flops = float(nq) * args.tree * F_SE3
-        achieved = flops / (knn_ms * 1e-3) / 1e12
+        achieved = flops / (kern_ms * 1e-3) / 1e12
         line = {
             "metric": METRIC,
             "value": value,
@@ -194,7 +230,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32 screen + f64 certify" if screen else "f64",
             "data": "synthetic (uniform SE(3) states, seeded; tree seed 42, samples seed 1000+rank)",
             "config": {
                 "workload": "configs[2]: SE(3) RRT*-style batch — nearestK(k=10) + steer + checkMotion "
@@ -205,13 +241,16 @@ def main():
             "nn_queries_per_s": nq * world / (knn_ms * 1e-3),
             "motion_checks_per_s": nq * world / (mv_ms * 1e-3),
             "phase_ms": {"knn": knn_ms, "steer": steer_ms, "motion": mv_ms},
+            "fast_path": {"screened": scr1 - scr0, "exact_reruns": fb1 - fb0},
             "motion_valid_fraction": valid_frac,
             "roofline": {
-                "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
-                "kernel": "knn_tiled_kernel<SE3,7,0,16> + knn_merge_kernel<16> (fp64 VALU-bound)",
-                "algorithmic": f"{nq} x {args.tree} pairs x {F_SE3} flops per launch",
+                "bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
+                "frac": achieved / PEAK_TFLOPS[dt], "traffic": None,
+                "kernel": kern_name, "kernel_ms": kern_ms,
+                "algorithmic": f"{nq} x {args.tree} pairs x {F_SE3} flop (SURVEY §8d) per launch, "
+                               f"{dt} vector peak; VALU-bound (no MFMA)",
             },
+            "single_query": single,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -159,6 +159,18 @@ ompl_gpu_status ompl_gpu_nn_radius(ompl_gpu_nn *h, const double *queries, size_t
  * (0xFFFFFFFF = no result); dist fp64. */
 ompl_gpu_status ompl_gpu_nn_knn_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, uint32_t k,
                                        uint32_t *d_ids, double *d_dist);
+/* Path selection and counters.  exact_only=1 forces the exact fp64 scan; by default
+ * batched R^n / SO3 / SE3 queries use the fp32 screen + fp64 certificate (results are
+ * identical: uncertified queries are re-run exactly).  *screened counts queries that took
+ * the screen, *fallbacks those re-run exactly. */
+ompl_gpu_status ompl_gpu_nn_set_exact(ompl_gpu_nn *h, int exact_only);
+ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint64_t *fallbacks);
+/* Profiling: when enabled, each query call brackets its dominant scan kernel with HIP
+ * events recorded on the launch stream; kernel_time synchronises the stream and returns
+ * the summed duration, the number of bracketed launches and the kernel's name. */
+ompl_gpu_status ompl_gpu_nn_profile(ompl_gpu_nn *h, int enable);
+ompl_gpu_status ompl_gpu_nn_kernel_time(ompl_gpu_nn *h, double *total_ms, uint64_t *launches,
+                                        const char **kernel_name);
 /* RRT extend on device: for each query q with nearest id nid[q*stride]:
  * from = state[nid]; to = q; if d(from,q) > max_distance, to = interpolate(from,
  * q, max_distance/d).  Writes AoS from/to rows (RRT.cpp:137-146). */

@@ -81,6 +81,10 @@ SIGNATURES = {
     "ompl_gpu_nn_nearest": (C.c_int, [_P, _D, C.c_size_t, _U64, _D]),
     "ompl_gpu_nn_radius": (C.c_int, [_P, _D, C.c_size_t, C.c_double, C.POINTER(_U64), C.POINTER(_D), _U64]),
     "ompl_gpu_nn_knn_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, _P, _P]),
+    "ompl_gpu_nn_set_exact": (C.c_int, [_P, C.c_int]),
+    "ompl_gpu_nn_stats": (C.c_int, [_P, _U64, _U64]),
+    "ompl_gpu_nn_profile": (C.c_int, [_P, C.c_int]),
+    "ompl_gpu_nn_kernel_time": (C.c_int, [_P, _D, _U64, C.POINTER(C.c_char_p)]),
     "ompl_gpu_steer_device": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_uint32, C.c_double, _P, _P]),
     "ompl_gpu_mv_create": (C.c_int, [C.POINTER(_P), C.POINTER(SpaceStruct), C.POINTER(CheckerStruct), C.c_int]),
     "ompl_gpu_mv_destroy": (C.c_int, [_P]),

@@ -11,7 +11,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -91,12 +93,52 @@ struct ompl_gpu_nn {
     FeatGeom g{};
     double *feat = nullptr;  // [F][cap]
     double *raw = nullptr;   // [dim][cap] (KCHAIN) or == feat
+    float *feat32 = nullptr; // [rows32][cap] fp32 copy for the screening scan (knn_fast.hip)
+    int rows32 = 0;
     uint64_t cap = 0, n_total = 0, n_live = 0;
     std::vector<uint8_t> removed;
     std::mutex mu;
-    DevBuf q, out_d, out_i, ws, stage, counts, offsets, ids, dists, sorted_ids, sorted_d, tmp;
+    DevBuf q, out_d, out_i, ws, stage, counts, offsets, ids, dists, sorted_ids, sorted_d, tmp, fb_q, fb_d, fb_i;
     std::vector<double> hfeat;
+    // screening bounds: box of the first three coordinates and max |coordinate|
+    double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, absmax = 0.0;
+    bool fast = true;        // OMPL_GPU_EXACT_ONLY=1 forces the exact fp64 scan
+    uint64_t fast_queries = 0, fast_fallbacks = 0;
+    // profiling of the dominant scan kernel (HIP events on the launch stream)
+    bool profile = false;
+    std::vector<KernelTimer> pending;
+    double prof_ms = 0.0;
+    uint64_t prof_launches = 0;
+    std::string prof_name;
 };
+
+namespace ompl_amd {
+thread_local KernelTimer *g_kernel_timer = nullptr;
+}
+
+namespace {
+// arms g_kernel_timer for the scope of one query call when the handle profiles
+struct ProfileScope {
+    ompl_gpu_nn *h;
+    KernelTimer t;
+    bool armed = false;
+    explicit ProfileScope(ompl_gpu_nn *hh) : h(hh) {
+        if (!h->profile) return;
+        if (hipEventCreate(&t.begin) != hipSuccess) return;
+        if (hipEventCreate(&t.end) != hipSuccess) {
+            (void)hipEventDestroy(t.begin);
+            return;
+        }
+        armed = true;
+        g_kernel_timer = &t;
+    }
+    ~ProfileScope() {
+        if (!armed) return;
+        g_kernel_timer = nullptr;
+        h->pending.push_back(t);
+    }
+};
+}  // namespace
 
 struct ompl_gpu_mv {
     int device = 0;
@@ -143,6 +185,9 @@ ompl_gpu_status ompl_gpu_nn_create(ompl_gpu_nn **out, const ompl_gpu_space *spac
     h->num_cus = cu_count(device);
     h->sp = sp;
     h->g = g;
+    h->rows32 = fp32_rows(sp, g);
+    const char *exact = std::getenv("OMPL_GPU_EXACT_ONLY");
+    h->fast = !(exact && exact[0] == '1');
     hipError_t e = hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
@@ -159,6 +204,7 @@ ompl_gpu_status ompl_gpu_nn_destroy(ompl_gpu_nn *h) {
     (void)hipStreamSynchronize(h->stream);
     if (h->raw && h->raw != h->feat) (void)hipFree(h->raw);
     if (h->feat) (void)hipFree(h->feat);
+    if (h->feat32) (void)hipFree(h->feat32);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
     return OMPL_GPU_OK;
@@ -186,6 +232,14 @@ static ompl_gpu_status grow(ompl_gpu_nn *h, uint64_t need) {
     const int F = h->g.F;
     const bool sep_raw = h->sp.kind == OMPL_GPU_SPACE_KCHAIN;
     double *nf = nullptr, *nr = nullptr;
+    float *n32 = nullptr;
+    if (h->rows32) {
+        HIP_OR_FAIL(hipMalloc(&n32, sizeof(float) * h->rows32 * nc));
+        HIP_OR_FAIL(hipMemsetAsync(n32, 0xFF, sizeof(float) * h->rows32 * nc, h->stream));  // NaN
+        if (h->n_total)
+            HIP_OR_FAIL(hipMemcpy2DAsync(n32, nc * sizeof(float), h->feat32, h->cap * sizeof(float),
+                                         h->n_total * sizeof(float), h->rows32, hipMemcpyDeviceToDevice, h->stream));
+    }
     HIP_OR_FAIL(hipMalloc(&nf, sizeof(double) * F * nc));
     HIP_OR_FAIL(hipMemsetAsync(nf, 0xFF, sizeof(double) * F * nc, h->stream));  // all-ones = NaN
     if (sep_raw) {
@@ -203,7 +257,9 @@ static ompl_gpu_status grow(ompl_gpu_nn *h, uint64_t need) {
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     if (h->raw && h->raw != h->feat) (void)hipFree(h->raw);
     if (h->feat) (void)hipFree(h->feat);
+    if (h->feat32) (void)hipFree(h->feat32);
     h->feat = nf;
+    h->feat32 = n32;
     h->raw = sep_raw ? nr : nf;
     h->cap = nc;
     return OMPL_GPU_OK;
@@ -232,6 +288,19 @@ ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, 
         HIP_OR_FAIL(hipMemcpyAsync(sr, states, sizeof(double) * n * dim, hipMemcpyHostToDevice, h->stream));
         HIP_OR_FAIL(launch_store_soa(sr, (uint32_t)n, dim, h->raw, h->cap, h->n_total, h->stream));
     }
+    if (h->rows32) HIP_OR_FAIL(launch_to_fp32(h->feat, h->cap, h->rows32, h->n_total, n, h->feat32, h->stream));
+    // screening bounds (knn_fast.hip): box of the first three coordinates, max |coordinate|
+    const int nb = h->sp.kind == OMPL_GPU_SPACE_SO3 ? 0 : std::min(dim, 3);
+    const int na = h->sp.kind == OMPL_GPU_SPACE_SE3 ? 3 : (h->sp.kind == OMPL_GPU_SPACE_SO3 ? 0 : dim);
+    for (size_t i = 0; i < n; ++i) {
+        const double *s = states + i * dim;
+        for (int c = 0; c < nb; ++c) {
+            if (h->n_total == 0 && i == 0) h->lo[c] = h->hi[c] = s[c];
+            h->lo[c] = std::min(h->lo[c], s[c]);
+            h->hi[c] = std::max(h->hi[c], s[c]);
+        }
+        for (int c = 0; c < na; ++c) h->absmax = std::max(h->absmax, std::fabs(s[c]));
+    }
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // host staging buffers are reused
     h->n_total += n;
     h->n_live += n;
@@ -247,6 +316,9 @@ ompl_gpu_status ompl_gpu_nn_remove(ompl_gpu_nn *h, uint64_t id) {
     // tombstone: a NaN in feature row 0 makes every distance to this state NaN
     const double nan = __builtin_nan("");
     HIP_OR_FAIL(hipMemcpyAsync(h->feat + id, &nan, sizeof(double), hipMemcpyHostToDevice, h->stream));
+    const float nanf = __builtin_nanf("");
+    if (h->rows32)
+        HIP_OR_FAIL(hipMemcpyAsync(h->feat32 + id, &nanf, sizeof(float), hipMemcpyHostToDevice, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     h->removed[id] = 1;
     h->n_live--;
@@ -261,9 +333,11 @@ ompl_gpu_status ompl_gpu_nn_clear(ompl_gpu_nn *h) {
         HIP_OR_FAIL(hipMemsetAsync(h->feat, 0xFF, sizeof(double) * h->g.F * h->cap, h->stream));
         if (h->raw != h->feat)
             HIP_OR_FAIL(hipMemsetAsync(h->raw, 0xFF, sizeof(double) * h->sp.dim * h->cap, h->stream));
+        if (h->rows32) HIP_OR_FAIL(hipMemsetAsync(h->feat32, 0xFF, sizeof(float) * h->rows32 * h->cap, h->stream));
         HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     }
     h->n_total = h->n_live = 0;
+    h->absmax = 0.0;
     h->removed.clear();
     return OMPL_GPU_OK;
 }
@@ -304,6 +378,43 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
         HIP_OR_FAIL(hipMemsetAsync(d_ids, 0xFF, sizeof(uint32_t) * nq * k, h->stream));
         HIP_OR_FAIL(hipMemcpyAsync(d_dist, inf.data(), sizeof(double) * inf.size(), hipMemcpyHostToDevice, h->stream));
         HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+        return OMPL_GPU_OK;
+    }
+    ProfileScope prof(h);
+    if (h->fast && fast_k2(h->sp, k, (uint32_t)nq) > 0) {
+        // fp32 screen + fp64 certificate (knn_fast.hip); uncertified queries re-run exactly
+        FastBounds b{};
+        for (int c = 0; c < 3; ++c) {
+            b.lo[c] = (float)h->lo[c];
+            const double ext = h->hi[c] - h->lo[c];
+            b.inv[c] = ext > 0 ? (float)(1023.0 / ext) : 0.f;
+        }
+        b.absmax = (float)h->absmax * (1.0f + 1e-6f);
+        const size_t wsb = knn_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus);
+        HIP_OR_FAIL(h->ws.ensure(wsb));
+        uint32_t *d_fail_count = nullptr, *d_fail_list = nullptr;
+        HIP_OR_FAIL(launch_knn_fast(h->sp, h->g, h->feat, h->feat32, h->cap, n_end, d_qf, (uint32_t)nq, k, b, d_dist,
+                                    d_ids, h->ws.p, h->ws.bytes, h->num_cus, h->stream, &d_fail_count,
+                                    &d_fail_list));
+        uint32_t nfail = 0;
+        HIP_OR_FAIL(hipMemcpyAsync(&nfail, d_fail_count, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+        h->fast_queries += nq;
+        h->fast_fallbacks += nfail;
+        if (nfail == 0) return OMPL_GPU_OK;
+        // exact fp64 re-run of the uncertified queries, then scatter into the outputs
+        const int F = h->g.F;
+        HIP_OR_FAIL(h->fb_q.ensure(sizeof(double) * nfail * F));
+        HIP_OR_FAIL(h->fb_d.ensure(sizeof(double) * nfail * k));
+        HIP_OR_FAIL(h->fb_i.ensure(sizeof(uint32_t) * nfail * k));
+        HIP_OR_FAIL(launch_gather_rows(d_qf, F, d_fail_list, nfail, (double *)h->fb_q.p, h->stream));
+        DevBuf ws2;
+        HIP_OR_FAIL(ws2.ensure(knn_workspace_bytes(h->sp, h->g, nfail, k, n_end, h->num_cus)));
+        HIP_OR_FAIL(launch_knn(h->sp, h->g, h->feat, h->cap, n_end, (const double *)h->fb_q.p, nfail, k,
+                               (double *)h->fb_d.p, (uint32_t *)h->fb_i.p, ws2.p, ws2.bytes, h->num_cus, h->stream));
+        HIP_OR_FAIL(launch_scatter_results((const double *)h->fb_d.p, (const uint32_t *)h->fb_i.p, k, d_fail_list,
+                                           nfail, d_dist, d_ids, h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // ws2 is released on return
         return OMPL_GPU_OK;
     }
     const size_t wsb = knn_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus);
@@ -473,6 +584,50 @@ ompl_gpu_status ompl_gpu_nn_knn_device(ompl_gpu_nn *h, const double *d_queries, 
         qf = (const double *)h->q.p;
     }
     return knn_features_locked(h, qf, nq, k, d_ids, d_dist);
+}
+
+ompl_gpu_status ompl_gpu_nn_set_exact(ompl_gpu_nn *h, int exact_only) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->fast = exact_only == 0;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_profile(ompl_gpu_nn *h, int enable) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->profile = enable != 0;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_kernel_time(ompl_gpu_nn *h, double *total_ms, uint64_t *launches,
+                                        const char **kernel_name) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    for (KernelTimer &t : h->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, t.begin, t.end) == hipSuccess) {
+            h->prof_ms += ms;
+            h->prof_launches++;
+            h->prof_name = t.name;
+        }
+        (void)hipEventDestroy(t.begin);
+        (void)hipEventDestroy(t.end);
+    }
+    h->pending.clear();
+    if (total_ms) *total_ms = h->prof_ms;
+    if (launches) *launches = h->prof_launches;
+    if (kernel_name) *kernel_name = h->prof_name.c_str();
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint64_t *fallbacks) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    if (screened) *screened = h->fast_queries;
+    if (fallbacks) *fallbacks = h->fast_fallbacks;
+    return OMPL_GPU_OK;
 }
 
 ompl_gpu_status ompl_gpu_steer_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, const uint32_t *d_nearest,

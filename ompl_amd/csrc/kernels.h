@@ -10,6 +10,26 @@ namespace ompl_amd {
 
 constexpr int kTile = 256;          // states per LDS tile / threads per block
 constexpr int kMaxK = 64;           // largest register top-K bucket
+constexpr uint32_t kStreamMaxQ = 64; // below this many queries the stream mapping is used
+
+// Optional HIP-event bracket around the dominant kernel of a launch (the scan), armed by
+// the C ABI when profiling is enabled (ompl_gpu_nn_profile).  Events are recorded on the
+// stream the kernel is launched on.
+struct KernelTimer {
+    hipEvent_t begin = nullptr, end = nullptr;
+    const char *name = "";
+};
+extern thread_local KernelTimer *g_kernel_timer;
+inline void timer_begin(hipStream_t st, const char *name) {
+    if (g_kernel_timer) {
+        g_kernel_timer->name = name;
+        (void)hipEventRecord(g_kernel_timer->begin, st);
+    }
+}
+inline void timer_end(hipStream_t st) {  // one bracket per armed call: disarm after it
+    if (g_kernel_timer) (void)hipEventRecord(g_kernel_timer->end, st);
+    g_kernel_timer = nullptr;
+}
 
 // Feature geometry of a space on device.
 struct FeatGeom {
@@ -33,6 +53,29 @@ size_t knn_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq, u
 hipError_t launch_knn(const DevSpace &sp, const FeatGeom &g, const double *feat, uint64_t cap, uint64_t n_end,
                       const double *qfeat, uint32_t nq, uint32_t k, double *out_d, uint32_t *out_i, void *ws,
                       size_t ws_bytes, int num_cus, hipStream_t st);
+
+// ---- fast exact kNN: fp32 screen (top-K2, K2 > k) + fp64 certify / rerank ----------
+// Eligible for REALVECTOR / SO3 / SE3 with nq >= kStreamMaxQ and k + 6 <= kMaxK.  Every
+// result is exact: a query whose certificate fails is listed in *fail_list (device) and
+// must be re-run on the exact path by the caller (count in *fail_count, device).
+struct FastBounds {
+    float lo[3], inv[3];  // Morton box of the first three coordinates (query ordering only)
+    float absmax;         // max |coordinate| stored (error bound of the fp32 screen)
+};
+int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq);  // screening list size, 0 = not eligible
+int fp32_rows(const DevSpace &sp, const FeatGeom &g);     // rows of the fp32 SoA copy
+size_t knn_fast_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k, uint64_t n_end,
+                                int num_cus);
+hipError_t launch_knn_fast(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32,
+                           uint64_t cap, uint64_t n_end, const double *qfeat64, uint32_t nq, uint32_t k,
+                           const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes,
+                           int num_cus, hipStream_t st, uint32_t **fail_count, uint32_t **fail_list);
+hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t first, uint64_t n, float *feat32,
+                          hipStream_t st);
+// gather rows q = list[i] of an AoS [*][F] fp64 array into dst[i]; scatter results back
+hipError_t launch_gather_rows(const double *src, int F, const uint32_t *list, uint32_t n, double *dst, hipStream_t st);
+hipError_t launch_scatter_results(const double *d, const uint32_t *ids, uint32_t k, const uint32_t *list, uint32_t n,
+                                  double *out_d, uint32_t *out_i, hipStream_t st);
 
 // radius search, pass 1 (count per (query, chunk)) and pass 2 (fill CSR in id order).
 struct RadiusPlan {

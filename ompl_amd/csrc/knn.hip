@@ -19,38 +19,13 @@
 #include <algorithm>
 
 #include "kernels.h"
+#include "feat_dist.h"
 #include "topk.h"
 
 namespace ompl_amd {
 
-constexpr uint32_t kStreamMaxQ = 64;  // below this many queries use the stream mapping
 constexpr int kStreamItems = 16;      // states per lane in the stream mapping
 
-// ---------------------------------------------------------------------------------
-// distance on features (element first, query second: NearestNeighborsLinear.h:104)
-template <int SP, int F, int NMAX>
-__device__ __forceinline__ double feat_dist(const double *s, const double *q, const DevSpace &sp) {
-    if constexpr (SP == OMPL_GPU_SPACE_REALVECTOR) {
-        double acc = 0.0;
-#pragma unroll
-        for (int f = 0; f < F; ++f) {
-            double diff = s[f] - q[f];
-            acc += diff * diff;
-        }
-        return sqrt(acc);
-    } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
-        return so3_arc(s, q);
-    } else if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        return se3_dist(s, q, sp.w0, sp.w1);
-    } else {
-        return chain_dist_feat<NMAX>(s, q, sp.dim, sp.link);
-    }
-}
-
-template <int F>
-struct LdsStride {
-    static constexpr int value = (F + 1) & ~1;  // even -> 16-byte aligned rows for ds_read_b128
-};
 
 // ---------------------------------------------------------------------------------
 // tiled batched kNN
@@ -354,24 +329,6 @@ bool feature_geometry(const DevSpace &sp, FeatGeom *g) {
     return false;
 }
 
-void host_features(const DevSpace &sp, const FeatGeom &g, const double *s, double *o) {
-    if (sp.kind == OMPL_GPU_SPACE_KCHAIN) {
-        double th = 0.;
-        for (int j = 0; j < g.nmax; ++j) {
-            if (j < sp.dim) {
-                th += s[j];
-                o[j] = std::cos(th);           // glibc, as the reference (KinematicChain.h:113-116)
-                o[g.nmax + j] = std::sin(th);
-            } else {
-                o[j] = 0.;
-                o[g.nmax + j] = 0.;
-            }
-        }
-    } else {
-        for (int j = 0; j < g.F; ++j) o[j] = j < sp.dim ? s[j] : 0.0;
-    }
-}
-
 int k_bucket(uint32_t k) {
     if (k <= 1) return 1;
     if (k <= 4) return 4;
@@ -421,21 +378,27 @@ hipError_t run_knn_k(const DevSpace &sp, const KnnPlan &p, const double *feat, u
     if (p.stream) {
         const size_t np = (size_t)nq * p.chunks * K;
         uint32_t *pi = (uint32_t *)(pd + np);
+        timer_begin(st, "knn_stream_kernel");
         hipLaunchKernelGGL((knn_stream_kernel<SP, F, NMAX, K>), dim3(p.chunks, nq), dim3(256), 0, st, feat, cap,
                            n_end, qf, sp, pd, pi);
+        timer_end(st);
         hipLaunchKernelGGL((knn_stream_merge_kernel<K>), dim3(nq), dim3(256), 0, st, pd, pi, p.chunks, od, oi, k);
         return hipGetLastError();
     }
     const dim3 grid((nq + kTile - 1) / kTile, p.chunks);
     if (p.chunks == 1) {
+        timer_begin(st, "knn_tiled_kernel");
         hipLaunchKernelGGL((knn_tiled_kernel<SP, F, NMAX, K>), grid, dim3(kTile), 0, st, feat, cap, n_end, qf, nq,
                            p.chunk_len, sp, od, oi, k);
+        timer_end(st);
         return hipGetLastError();
     }
     const size_t np = (size_t)nq * p.chunks * K;
     uint32_t *pi = (uint32_t *)(pd + np);
+    timer_begin(st, "knn_tiled_kernel");
     hipLaunchKernelGGL((knn_tiled_kernel<SP, F, NMAX, K>), grid, dim3(kTile), 0, st, feat, cap, n_end, qf, nq,
                        p.chunk_len, sp, pd, pi, (uint32_t)K);
+    timer_end(st);
     hipLaunchKernelGGL((knn_merge_kernel<K>), dim3((nq + 255) / 256), dim3(256), 0, st, pd, pi, p.chunks, nq, od,
                        oi, k);
     return hipGetLastError();

@@ -57,6 +57,42 @@ struct TopK {
     }
 };
 
+// fp32 screening list: same (distance, id) order, plus the squared admission radius used
+// by the cheap translation pre-reject (inflated by 2^-19 so rounding never rejects an
+// element whose fp32 distance would still be admitted).
+template <int K>
+struct TopK32 {
+    float d[K];
+    uint32_t i[K];
+    float tau2;
+
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            d[j] = __builtin_inff();
+            i[j] = kNoId;
+        }
+        tau2 = __builtin_inff();
+    }
+    __device__ __forceinline__ bool admits(float cd, uint32_t ci) const {
+        return cd < d[K - 1] || (cd == d[K - 1] && ci < i[K - 1]);
+    }
+    __device__ __forceinline__ void push(float cd, uint32_t ci) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            bool sw = cd < d[j] || (cd == d[j] && ci < i[j]);
+            float td = d[j];
+            uint32_t ti = i[j];
+            d[j] = sw ? cd : td;
+            i[j] = sw ? ci : ti;
+            cd = sw ? td : cd;
+            ci = sw ? ti : ci;
+        }
+        const float w = d[K - 1];
+        tau2 = w * w * 1.0000020f;
+    }
+};
+
 __device__ __forceinline__ void wave_argmin(double &d, uint32_t &i) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {

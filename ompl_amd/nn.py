@@ -123,6 +123,26 @@ class NearestNeighborsGPU:
         """Live element ids (insertion order; the reference's order is unspecified)."""
         return [i for i in range(self.total()) if i not in self._removed]
 
+    def set_exact(self, exact_only: bool) -> None:
+        """Force the exact fp64 scan (default: fp32 screen + fp64 certificate)."""
+        abi.check(abi.lib.ompl_gpu_nn_set_exact(self._h, 1 if exact_only else 0))
+
+    def stats(self) -> tuple[int, int]:
+        """(queries that took the fp32 screen, queries re-run exactly after a failed certificate)."""
+        a, b = C.c_uint64(0), C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_nn_stats(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def profile(self, enable: bool = True) -> None:
+        abi.check(abi.lib.ompl_gpu_nn_profile(self._h, 1 if enable else 0))
+
+    def kernel_time(self) -> tuple[float, int, str]:
+        """(summed ms, launches, name) of the dominant scan kernel, from HIP events recorded
+        on the launch stream while profiling was enabled."""
+        ms, n, name = C.c_double(0), C.c_uint64(0), C.c_char_p()
+        abi.check(abi.lib.ompl_gpu_nn_kernel_time(self._h, C.byref(ms), C.byref(n), C.byref(name)))
+        return ms.value, n.value, (name.value or b"").decode()
+
     # ---- device-resident (benchmark / pipelines); pointers are device addresses
     def set_stream(self, stream_ptr: int | None) -> None:
         abi.check(abi.lib.ompl_gpu_nn_set_stream(self._h, C.c_void_p(stream_ptr or 0)))

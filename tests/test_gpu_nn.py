@@ -26,6 +26,19 @@ def _sample(name, rng, n):
             "so3": lambda: W.uniform_quat(rng, n), "chain12": lambda: W.uniform_chain(rng, n, 12)}[name]()
 
 
+@pytest.fixture(params=["fast", "exact"])
+def path(request):
+    """fast = fp32 screen + fp64 certificate (default for batched R^n/SO3/SE3);
+    exact = the fp64 scan.  Both must give the same answers."""
+    return request.param
+
+
+def make_nn(sp, gpu, path):
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.set_exact(path == "exact")
+    return nn
+
+
 def _oracle_ext(sp, data, q, k):
     K = min(k + 8, len(data))
     oi, od, _ = O.knn(sp, data, q, max(K, 1))
@@ -33,10 +46,10 @@ def _oracle_ext(sp, data, q, k):
 
 
 @pytest.mark.parametrize("name", list(SPACES))
-def test_knn_golden(gpu, golden, name):
+def test_knn_golden(gpu, path, golden, name):
     g = golden(f"nn_{name}.npz")
     sp = SPACES[name]()
-    nn = NearestNeighborsGPU(sp, gpu)
+    nn = make_nn(sp, gpu, path)
     nn.add(g["data"])
     assert nn.size() == len(g["data"])
     for k in (1, 10, 41):
@@ -52,11 +65,11 @@ def test_knn_golden(gpu, golden, name):
 
 @pytest.mark.parametrize("name", list(SPACES))
 @pytest.mark.parametrize("nq", [5, 300])
-def test_knn_random_vs_oracle(gpu, name, nq):
+def test_knn_random_vs_oracle(gpu, path, name, nq):
     rng = np.random.default_rng(100 + nq)
     sp = SPACES[name]()
     data, q = _sample(name, rng, 60000), _sample(name, rng, nq)
-    nn = NearestNeighborsGPU(sp, gpu)
+    nn = make_nn(sp, gpu, path)
     nn.add(data[:25000])
     nn.add(data[25000:])  # growth path: the store is reallocated and copied
     oi, od = _oracle_ext(sp, data, q, 64)  # (distance, id)-sorted: top-k is a prefix
@@ -66,13 +79,13 @@ def test_knn_random_vs_oracle(gpu, name, nq):
         assert_knn_parity(ids, d, oi, od, k)
 
 
-def test_knn_bitwise_for_realvector(gpu):
+def test_knn_bitwise_for_realvector(gpu, path):
     """L2 uses only IEEE-exact operations (sub, mul, add, correctly rounded sqrt): the device
     distances must equal the reference formula bit for bit."""
     rng = np.random.default_rng(5)
     sp = RealVectorStateSpace(6)
     data, q = W.uniform_rv(rng, 20000, 6), W.uniform_rv(rng, 100, 6)
-    nn = NearestNeighborsGPU(sp, gpu)
+    nn = make_nn(sp, gpu, path)
     nn.add(data)
     ids, d, _ = nn.nearestKBatch(q, 16)
     oi, od, _ = O.knn(sp, data, q, 16)
@@ -80,13 +93,13 @@ def test_knn_bitwise_for_realvector(gpu):
     np.testing.assert_array_equal(ids.astype(np.int64), oi.astype(np.int64))
 
 
-def test_ties_resolved_by_id(gpu):
+def test_ties_resolved_by_id(gpu, path):
     """Exact distance ties (grid data): results ordered by (distance, id), like the oracle."""
     sp = RealVectorStateSpace(2)
     g = np.stack(np.meshgrid(np.arange(0, 1, 0.1), np.arange(0, 1, 0.1)), -1).reshape(-1, 2)
     data = np.concatenate([g, g])  # every state twice
     q = g[::7] + 0.0
-    nn = NearestNeighborsGPU(sp, gpu)
+    nn = make_nn(sp, gpu, path)
     nn.add(data)
     for k in (1, 4, 16, 64):
         for sub in (q, q[:3]):
@@ -117,11 +130,11 @@ def test_k_edge_cases(gpu):
         nn.nearestKBatch(data[:2], 65)                    # above the register top-K buckets
 
 
-def test_remove_and_clear(gpu):
+def test_remove_and_clear(gpu, path):
     sp = SE3StateSpace()
     rng = np.random.default_rng(2)
     data, q = W.uniform_se3(rng, 3000), W.uniform_se3(rng, 80)
-    nn = NearestNeighborsGPU(sp, gpu)
+    nn = make_nn(sp, gpu, path)
     nn.add(data)
     removed = rng.choice(3000, 700, replace=False)
     for i in removed:
@@ -172,13 +185,13 @@ def test_radius_random_vs_oracle(gpu, nq):
         assert_dist_close(d, od)
 
 
-def test_large_tree_properties(gpu):
+def test_large_tree_properties(gpu, path):
     """1e6 SE(3) tree (the headline size): stream and tiled mappings agree, results are sorted,
     radius and kNN are consistent, and a sample of queries matches the oracle."""
     rng = np.random.default_rng(42)
     sp = SE3StateSpace()
     data, q = W.uniform_se3(rng, 1_000_000), W.uniform_se3(rng, 2000)
-    nn = NearestNeighborsGPU(sp, gpu)
+    nn = make_nn(sp, gpu, path)
     nn.add(data)
     ids, d, _ = nn.nearestKBatch(q, 10)
     ids_s, d_s, _ = nn.nearestKBatch(q[:40], 10)          # stream mapping
@@ -241,3 +254,36 @@ def test_chain_features_exact(gpu):
     st = nn.states(0, 5)
     np.testing.assert_array_equal(st, data[:5])
     assert math.isfinite(float(st.sum()))
+
+
+@pytest.mark.parametrize("name", ["se3", "r6", "so3"])
+def test_fast_path_is_used_and_certified(gpu, name):
+    rng = np.random.default_rng(31)
+    sp = SPACES[name]()
+    data, q = _sample(name, rng, 200000), _sample(name, rng, 2000)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    ids, d, _ = nn.nearestKBatch(q, 10)
+    screened, fallbacks = nn.stats()
+    assert screened == 2000 and fallbacks < 200
+    oi, od = _oracle_ext(sp, data, q[:50], 10)
+    assert_knn_parity(ids[:50], d[:50], oi, od, 10)
+
+
+def test_fast_path_fallback_when_certificate_fails(gpu):
+    """Rotations within 1e-3 rad of each other: the fp32 screen's error bound exceeds the
+    distance gaps, certificates fail, and the exact re-run must give the exact answer."""
+    rng = np.random.default_rng(32)
+    sp = SO3StateSpace()
+    v = rng.normal(0, 1e-3, (60000, 3))
+    data = np.column_stack([v, np.ones(60000)])
+    data /= np.linalg.norm(data, axis=1, keepdims=True)
+    q = data[rng.choice(60000, 300, replace=False)] + rng.normal(0, 1e-5, (300, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    ids, d, _ = nn.nearestKBatch(q, 10)
+    screened, fallbacks = nn.stats()
+    assert screened == 300 and fallbacks > 0
+    oi, od = _oracle_ext(sp, data, q, 10)
+    assert_knn_parity(ids, d, oi, od, 10)
