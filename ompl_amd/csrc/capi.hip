@@ -370,7 +370,9 @@ static uint64_t n_end_of(const ompl_gpu_nn *h) { return (h->n_total + kTile - 1)
 // knn on device-resident features (queries already converted); caller holds the lock
 static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, size_t nq, uint32_t k, uint32_t *d_ids,
                                            double *d_dist) {
-    if (k > (uint32_t)kMaxK) return fail(OMPL_GPU_ERR_UNSUPPORTED, "k above 64 is not supported yet");
+    const bool large = k > 32 && large_k_supported(h->sp) && (h->fast || k > (uint32_t)kMaxK);
+    if (k > (uint32_t)kMaxK && !large)
+        return fail(OMPL_GPU_ERR_UNSUPPORTED, "k above 64 is not supported for this state space");
     const uint64_t n_end = n_end_of(h);
     if (n_end == 0) {
         // empty structure: every entry is (inf, none)
@@ -381,6 +383,24 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
         return OMPL_GPU_OK;
     }
     ProfileScope prof(h);
+    if (large) {
+        // distance bound for the histogram range (knn_large.hip)
+        double dmax;
+        if (h->sp.kind == OMPL_GPU_SPACE_SO3) {
+            dmax = 0.5 * M_PI;
+        } else if (h->sp.kind == OMPL_GPU_SPACE_SE3) {
+            double e = 0.0;
+            for (int c = 0; c < 3; ++c) e += (h->hi[c] - h->lo[c]) * (h->hi[c] - h->lo[c]);
+            dmax = h->sp.w0 * std::sqrt(e) + h->sp.w1 * 0.5 * M_PI;
+        } else {
+            dmax = 2.0 * h->absmax * std::sqrt((double)h->sp.dim);
+        }
+        dmax = std::max(dmax * 1.0001, 1e-30);
+        HIP_OR_FAIL(launch_knn_large(h->sp, h->g, h->feat, h->feat32, h->cap, n_end, d_qf, (uint32_t)nq, k,
+                                     (float)h->absmax * (1.0f + 1e-6f), (float)dmax, d_dist, d_ids,
+                                     size_t(4) << 30, h->num_cus, h->stream));
+        return OMPL_GPU_OK;
+    }
     if (h->fast && fast_k2(h->sp, k, (uint32_t)nq) > 0) {
         // fp32 screen + fp64 certificate (knn_fast.hip); uncertified queries re-run exactly
         FastBounds b{};

@@ -70,6 +70,14 @@ hipError_t launch_knn_fast(const DevSpace &sp, const FeatGeom &g, const double *
                            uint64_t cap, uint64_t n_end, const double *qfeat64, uint32_t nq, uint32_t k,
                            const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes,
                            int num_cus, hipStream_t st, uint32_t **fail_count, uint32_t **fail_list);
+// ---- large k (k > 32; RRT* k ~ 6e3): histogram threshold + candidate sort (knn_large.hip)
+// dmax: bound of the distances between stored states (the histogram's range; larger
+// distances fall into an overflow bin and are still handled exactly).
+bool large_k_supported(const DevSpace &sp);
+hipError_t launch_knn_large(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32,
+                            uint64_t cap, uint64_t n_end, const double *qfeat64, uint32_t nq, uint32_t k, float absmax,
+                            float dmax, double *out_d, uint32_t *out_i, size_t mem_budget, int num_cus,
+                            hipStream_t st);
 hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t first, uint64_t n, float *feat32,
                           hipStream_t st);
 // gather rows q = list[i] of an AoS [*][F] fp64 array into dst[i]; scatter results back

@@ -1,0 +1,59 @@
+"""GPU parity of the large-k path (k > 32: histogram threshold + candidate sort), the
+RRT* neighbourhood size k = ceil(k_rrt log(n+1)) (RRTstar.cpp:603-618)."""
+import numpy as np
+import pytest
+
+import pyoracle as O
+from ompl_amd import NearestNeighborsGPU
+from ompl_amd import workloads as W
+from ompl_amd.spaces import RealVectorStateSpace, SE3StateSpace, SO3StateSpace
+from parity import assert_knn_parity
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nq", [3, 150])
+def test_large_k_se3_rrtstar(gpu, nq):
+    rng = np.random.default_rng(50 + nq)
+    sp = SE3StateSpace()
+    n = 100_000
+    data, q = W.uniform_se3(rng, n), W.uniform_se3(rng, nq)
+    k_rrt = W.rrt_star_k(n, 6)  # 5,141 at n = 1e5
+    assert k_rrt == 5141
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    oi, od, _ = O.knn(sp, data, q, k_rrt + 8)
+    for k in (33, 64, 100, 1000, k_rrt):
+        ids, d, cnt = nn.nearestKBatch(q, k)
+        assert (cnt == k).all()
+        assert_knn_parity(ids, d, oi, od, k)
+
+
+@pytest.mark.parametrize("name", ["r6", "so3"])
+def test_large_k_other_spaces(gpu, name):
+    rng = np.random.default_rng(7)
+    if name == "r6":
+        sp, data, q = RealVectorStateSpace(6), W.uniform_rv(rng, 50000, 6), W.uniform_rv(rng, 100, 6)
+    else:
+        sp, data, q = SO3StateSpace(), W.uniform_quat(rng, 50000), W.uniform_quat(rng, 100)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    oi, od, _ = O.knn(sp, data, q, 508)
+    for k in (40, 500):
+        ids, d, _ = nn.nearestKBatch(q, k)
+        assert_knn_parity(ids, d, oi, od, k)
+
+
+def test_large_k_more_than_stored(gpu):
+    rng = np.random.default_rng(8)
+    sp = SE3StateSpace()
+    data, q = W.uniform_se3(rng, 300), W.uniform_se3(rng, 70)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    nn.remove(5)
+    ids, d, cnt = nn.nearestKBatch(q, 1000)
+    assert (cnt == 299).all()
+    keep = np.setdiff1d(np.arange(300), [5])
+    oi, od, _ = O.knn(sp, data[keep], q, 299)
+    assert_knn_parity(ids[:, :299], d[:, :299], keep[oi], od, 299)
+    assert np.isinf(d[:, 299:]).all()

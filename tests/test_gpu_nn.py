@@ -126,8 +126,12 @@ def test_k_edge_cases(gpu):
     assert res == [int(x) for x in oi[0]]
     assert sorted(nn.nearestR(data[3], float("inf"))) == list(range(50))  # nearestR(inf) = all
     assert nn.nearestR(data[3], float("inf"))[0] == 3
+    ids, d, cnt = nn.nearestKBatch(data[:2], 65)          # large-k path: k > n -> n results
+    assert (cnt == 50).all() and list(ids[0, :50]) == [int(x) for x in oi[0]]
+    ch = NearestNeighborsGPU(KinematicChainSpace(12, 1 / 12), gpu)
+    ch.add(W.uniform_chain(rng, 100, 12))
     with pytest.raises(abi.GpuError):
-        nn.nearestKBatch(data[:2], 65)                    # above the register top-K buckets
+        ch.nearestKBatch(W.uniform_chain(rng, 2, 12), 65)  # chain: register buckets only (k <= 64)
 
 
 def test_remove_and_clear(gpu, path):
