@@ -159,10 +159,11 @@ ompl_gpu_status ompl_gpu_nn_radius(ompl_gpu_nn *h, const double *queries, size_t
  * (0xFFFFFFFF = no result); dist fp64. */
 ompl_gpu_status ompl_gpu_nn_knn_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, uint32_t k,
                                        uint32_t *d_ids, double *d_dist);
-/* Path selection and counters.  exact_only=1 forces the exact fp64 scan; by default
- * batched R^n / SO3 / SE3 queries use the fp32 screen + fp64 certificate (results are
- * identical: uncertified queries are re-run exactly).  *screened counts queries that took
- * the screen, *fallbacks those re-run exactly. */
+/* Path selection and counters.  mode (exact_only) 0 = default: batched R^n / SO3 / SE3
+ * queries use the fp32 screen + fp64 certificate, culled over a Morton-sorted copy of the
+ * store for R^n and SE3; 1 = the exact fp64 scan only; 2 = the screen without culling.
+ * Results are identical in every mode (uncertified queries are re-run exactly).
+ * *screened counts queries that took the screen, *fallbacks those re-run exactly. */
 ompl_gpu_status ompl_gpu_nn_set_exact(ompl_gpu_nn *h, int exact_only);
 ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint64_t *fallbacks);
 /* Profiling: when enabled, each query call brackets its dominant scan kernel with HIP

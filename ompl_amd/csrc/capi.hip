@@ -101,7 +101,12 @@ struct ompl_gpu_nn {
     DevBuf q, out_d, out_i, ws, stage, counts, offsets, ids, dists, sorted_ids, sorted_d, tmp, fb_q, fb_d, fb_i;
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
-    double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, absmax = 0.0;
+    double lo[kKeyDims] = {0}, hi[kKeyDims] = {0}, absmax = 0.0;
+    // Morton-sorted fp32 copy for the culled screen (rebuilt lazily after add/remove)
+    SortedStore sorted;
+    FastBounds sorted_bounds{};
+    bool sorted_dirty = true;
+    bool cull = true;         // ompl_gpu_nn_set_exact(h, 2) disables the culled screen
     bool fast = true;        // OMPL_GPU_EXACT_ONLY=1 forces the exact fp64 scan
     uint64_t fast_queries = 0, fast_fallbacks = 0;
     // profiling of the dominant scan kernel (HIP events on the launch stream)
@@ -117,6 +122,24 @@ thread_local KernelTimer *g_kernel_timer = nullptr;
 }
 
 namespace {
+// coordinates that carry the Morton key / culling box: SE3 translation, R^n first <= 6
+int key_dims(const DevSpace &sp) {
+    if (sp.kind == OMPL_GPU_SPACE_SE3) return 3;
+    if (sp.kind == OMPL_GPU_SPACE_REALVECTOR) return std::min(sp.dim, kKeyDims);
+    return 0;
+}
+
+FastBounds current_bounds(const ompl_gpu_nn *h) {
+    FastBounds b{};
+    b.nkey = key_dims(h->sp);
+    for (int c = 0; c < b.nkey; ++c) {
+        b.lo[c] = (float)h->lo[c];
+        const double ext = h->hi[c] - h->lo[c];
+        b.inv[c] = ext > 0 ? (float)(1.0 / ext) : 0.f;
+    }
+    b.absmax = (float)h->absmax;
+    return b;
+}
 // arms g_kernel_timer for the scope of one query call when the handle profiles
 struct ProfileScope {
     ompl_gpu_nn *h;
@@ -205,6 +228,7 @@ ompl_gpu_status ompl_gpu_nn_destroy(ompl_gpu_nn *h) {
     if (h->raw && h->raw != h->feat) (void)hipFree(h->raw);
     if (h->feat) (void)hipFree(h->feat);
     if (h->feat32) (void)hipFree(h->feat32);
+    free_sorted_store(&h->sorted);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
     return OMPL_GPU_OK;
@@ -289,8 +313,9 @@ ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, 
         HIP_OR_FAIL(launch_store_soa(sr, (uint32_t)n, dim, h->raw, h->cap, h->n_total, h->stream));
     }
     if (h->rows32) HIP_OR_FAIL(launch_to_fp32(h->feat, h->cap, h->rows32, h->n_total, n, h->feat32, h->stream));
-    // screening bounds (knn_fast.hip): box of the first three coordinates, max |coordinate|
-    const int nb = h->sp.kind == OMPL_GPU_SPACE_SO3 ? 0 : std::min(dim, 3);
+    // screening bounds (knn_fast.hip): key box of the first <= 6 coordinates, max |coordinate|
+    const int nb = key_dims(h->sp);
+    h->sorted_dirty = true;
     const int na = h->sp.kind == OMPL_GPU_SPACE_SE3 ? 3 : (h->sp.kind == OMPL_GPU_SPACE_SO3 ? 0 : dim);
     for (size_t i = 0; i < n; ++i) {
         const double *s = states + i * dim;
@@ -321,6 +346,7 @@ ompl_gpu_status ompl_gpu_nn_remove(ompl_gpu_nn *h, uint64_t id) {
         HIP_OR_FAIL(hipMemcpyAsync(h->feat32 + id, &nanf, sizeof(float), hipMemcpyHostToDevice, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     h->removed[id] = 1;
+    h->sorted_dirty = true;
     h->n_live--;
     return OMPL_GPU_OK;
 }
@@ -338,6 +364,7 @@ ompl_gpu_status ompl_gpu_nn_clear(ompl_gpu_nn *h) {
     }
     h->n_total = h->n_live = 0;
     h->absmax = 0.0;
+    h->sorted_dirty = true;
     h->removed.clear();
     return OMPL_GPU_OK;
 }
@@ -403,19 +430,21 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
     }
     if (h->fast && fast_k2(h->sp, k, (uint32_t)nq) > 0) {
         // fp32 screen + fp64 certificate (knn_fast.hip); uncertified queries re-run exactly
-        FastBounds b{};
-        for (int c = 0; c < 3; ++c) {
-            b.lo[c] = (float)h->lo[c];
-            const double ext = h->hi[c] - h->lo[c];
-            b.inv[c] = ext > 0 ? (float)(1023.0 / ext) : 0.f;
+        const bool cull = h->cull && cull_supported(h->sp);
+        if (cull && (h->sorted_dirty || h->sorted.n != h->n_total)) {
+            h->sorted_bounds = current_bounds(h);
+            HIP_OR_FAIL(build_sorted_store(h->sp, h->g, h->feat32, h->cap, (uint32_t)h->n_total, h->sorted_bounds,
+                                           &h->sorted, h->stream));
+            h->sorted_dirty = false;
         }
+        FastBounds b = cull ? h->sorted_bounds : current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
-        const size_t wsb = knn_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus);
+        const size_t wsb = knn_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus, cull);
         HIP_OR_FAIL(h->ws.ensure(wsb));
         uint32_t *d_fail_count = nullptr, *d_fail_list = nullptr;
-        HIP_OR_FAIL(launch_knn_fast(h->sp, h->g, h->feat, h->feat32, h->cap, n_end, d_qf, (uint32_t)nq, k, b, d_dist,
-                                    d_ids, h->ws.p, h->ws.bytes, h->num_cus, h->stream, &d_fail_count,
-                                    &d_fail_list));
+        HIP_OR_FAIL(launch_knn_fast(h->sp, h->g, h->feat, h->feat32, h->cap, n_end, cull ? &h->sorted : nullptr, d_qf,
+                                    (uint32_t)nq, k, b, d_dist, d_ids, h->ws.p, h->ws.bytes, h->num_cus, h->stream,
+                                    &d_fail_count, &d_fail_list));
         uint32_t nfail = 0;
         HIP_OR_FAIL(hipMemcpyAsync(&nfail, d_fail_count, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
         HIP_OR_FAIL(hipStreamSynchronize(h->stream));
@@ -609,7 +638,8 @@ ompl_gpu_status ompl_gpu_nn_knn_device(ompl_gpu_nn *h, const double *d_queries, 
 ompl_gpu_status ompl_gpu_nn_set_exact(ompl_gpu_nn *h, int exact_only) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
-    h->fast = exact_only == 0;
+    h->fast = exact_only != 1;
+    h->cull = exact_only != 2;
     return OMPL_GPU_OK;
 }
 

@@ -58,17 +58,41 @@ hipError_t launch_knn(const DevSpace &sp, const FeatGeom &g, const double *feat,
 // Eligible for REALVECTOR / SO3 / SE3 with nq >= kStreamMaxQ and k + 6 <= kMaxK.  Every
 // result is exact: a query whose certificate fails is listed in *fail_list (device) and
 // must be re-run on the exact path by the caller (count in *fail_count, device).
+constexpr int kKeyDims = 6;  // Morton key over at most 6 coordinates
 struct FastBounds {
-    float lo[3], inv[3];  // Morton box of the first three coordinates (query ordering only)
-    float absmax;         // max |coordinate| stored (error bound of the fp32 screen)
+    float lo[kKeyDims], inv[kKeyDims];  // key box (inv = 1 / extent) of the first nkey coordinates
+    int nkey;                           // SE3: 3 (translation); R^n: min(n, 6); SO3: 0
+    float absmax;                       // max |coordinate| stored (error bound of the fp32 screen)
 };
+
+// Spatially sorted fp32 copy of the store for the culled screen (SE3 and R^n): states in
+// Morton order, 64-state tiles (one state per lane) and 32-tile super-tiles with
+// axis-aligned boxes over the distance's Euclidean part (SE3 translation / all of R^n).
+constexpr int kCullTile = 64;
+constexpr int kSuperTiles = 32;
+struct SortedStore {
+    float *rows = nullptr;       // [rows32][n_pad]
+    uint32_t *ids = nullptr;     // [n_pad] original id of each sorted slot (kNoId = padding)
+    float *tbox = nullptr;       // [ntiles][2*NB] lo.., hi..
+    float *sbox = nullptr;       // [nsuper][2*NB]
+    uint32_t *tkey0 = nullptr;   // [ntiles] Morton key of each tile's first state
+    uint32_t n = 0, n_pad = 0, ntiles = 0, nsuper = 0;
+    size_t bytes = 0;
+};
+bool cull_supported(const DevSpace &sp);
+// (re)build the sorted copy of ids [0, n) from the fp32 store; allocates into *s
+hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, uint64_t cap, uint32_t n,
+                              const FastBounds &b, SortedStore *s, hipStream_t st);
+void free_sorted_store(SortedStore *s);
+
 int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq);  // screening list size, 0 = not eligible
 int fp32_rows(const DevSpace &sp, const FeatGeom &g);     // rows of the fp32 SoA copy
 size_t knn_fast_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k, uint64_t n_end,
-                                int num_cus);
+                                int num_cus, bool cull);
+// sorted == nullptr: chunked brute-force screen; else the culled screen over *sorted
 hipError_t launch_knn_fast(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32,
-                           uint64_t cap, uint64_t n_end, const double *qfeat64, uint32_t nq, uint32_t k,
-                           const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes,
+                           uint64_t cap, uint64_t n_end, const SortedStore *sorted, const double *qfeat64, uint32_t nq,
+                           uint32_t k, const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes,
                            int num_cus, hipStream_t st, uint32_t **fail_count, uint32_t **fail_list);
 // ---- large k (k > 32; RRT* k ~ 6e3): histogram threshold + candidate sort (knn_large.hip)
 // dmax: bound of the distances between stored states (the histogram's range; larger

@@ -125,7 +125,12 @@ class NearestNeighborsGPU:
 
     def set_exact(self, exact_only: bool) -> None:
         """Force the exact fp64 scan (default: fp32 screen + fp64 certificate)."""
-        abi.check(abi.lib.ompl_gpu_nn_set_exact(self._h, 1 if exact_only else 0))
+        self.set_mode(1 if exact_only else 0)
+
+    def set_mode(self, mode: int) -> None:
+        """0: fp32 screen (culled for R^n / SE3) + fp64 certificate; 1: exact fp64 scan;
+        2: fp32 screen without culling.  All modes return identical results."""
+        abi.check(abi.lib.ompl_gpu_nn_set_exact(self._h, int(mode)))
 
     def stats(self) -> tuple[int, int]:
         """(queries that took the fp32 screen, queries re-run exactly after a failed certificate)."""

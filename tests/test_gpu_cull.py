@@ -1,0 +1,61 @@
+"""The culled screen keeps a Morton-sorted copy of the store; it must stay exact across
+incremental adds, removals, queries outside the stored bounding box and degenerate
+(duplicate-heavy) data."""
+import numpy as np
+import pytest
+
+import pyoracle as O
+from ompl_amd import NearestNeighborsGPU
+from ompl_amd import workloads as W
+from ompl_amd.spaces import RealVectorStateSpace, SE3StateSpace
+from parity import assert_knn_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(nn, sp, data_live, ids_live, q, k):
+    ids, d, _ = nn.nearestKBatch(q, k)
+    oi, od, _ = O.knn(sp, data_live, q, min(k + 8, len(data_live)))
+    assert_knn_parity(ids, d, ids_live[oi], od, k)
+
+
+def test_sorted_store_tracks_adds_and_removes(gpu):
+    rng = np.random.default_rng(61)
+    sp = SE3StateSpace()
+    data = W.uniform_se3(rng, 120000)
+    q = W.uniform_se3(rng, 500)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data[:50000])
+    _check(nn, sp, data[:50000], np.arange(50000), q, 10)
+    nn.add(data[50000:])                        # sorted copy is now stale -> rebuilt
+    _check(nn, sp, data, np.arange(120000), q, 10)
+    gone = rng.choice(120000, 20000, replace=False)
+    for i in gone:
+        nn.remove(int(i))
+    keep = np.setdiff1d(np.arange(120000), gone)
+    _check(nn, sp, data[keep], keep, q, 16)
+    screened, _ = nn.stats()
+    assert screened == 1500
+
+
+def test_queries_outside_the_stored_box(gpu):
+    rng = np.random.default_rng(62)
+    sp = RealVectorStateSpace(6, -1.0, 1.0)
+    data = W.uniform_rv(rng, 80000, 6, 0.0, 1.0)
+    q = np.concatenate([W.uniform_rv(rng, 200, 6, -1.0, 0.0), W.uniform_rv(rng, 200, 6, 1.0, 3.0)])
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    _check(nn, sp, data, np.arange(80000), q, 10)
+
+
+def test_clustered_and_duplicate_states(gpu):
+    rng = np.random.default_rng(63)
+    sp = SE3StateSpace()
+    base = W.uniform_se3(rng, 300)
+    data = np.repeat(base, 40, axis=0) + np.concatenate(
+        [rng.normal(0, 1e-4, (12000, 3)), np.zeros((12000, 4))], axis=1)
+    data[:, 3:] /= np.linalg.norm(data[:, 3:], axis=1, keepdims=True)
+    q = base[rng.choice(300, 100)] + np.concatenate([rng.normal(0, 1e-3, (100, 3)), np.zeros((100, 4))], axis=1)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    _check(nn, sp, data, np.arange(len(data)), q, 16)

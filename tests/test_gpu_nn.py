@@ -26,16 +26,17 @@ def _sample(name, rng, n):
             "so3": lambda: W.uniform_quat(rng, n), "chain12": lambda: W.uniform_chain(rng, n, 12)}[name]()
 
 
-@pytest.fixture(params=["fast", "exact"])
+@pytest.fixture(params=["fast", "exact", "nocull"])
 def path(request):
-    """fast = fp32 screen + fp64 certificate (default for batched R^n/SO3/SE3);
-    exact = the fp64 scan.  Both must give the same answers."""
+    """fast = fp32 screen (culled over the Morton-sorted copy for R^n / SE3) + fp64
+    certificate, the default for batched queries; exact = the fp64 scan; nocull = the
+    chunked fp32 screen.  All must give the same answers."""
     return request.param
 
 
 def make_nn(sp, gpu, path):
     nn = NearestNeighborsGPU(sp, gpu)
-    nn.set_exact(path == "exact")
+    nn.set_mode({"fast": 0, "exact": 1, "nocull": 2}[path])
     return nn
 
 
@@ -126,7 +127,7 @@ def test_k_edge_cases(gpu):
     assert res == [int(x) for x in oi[0]]
     assert sorted(nn.nearestR(data[3], float("inf"))) == list(range(50))  # nearestR(inf) = all
     assert nn.nearestR(data[3], float("inf"))[0] == 3
-    ids, d, cnt = nn.nearestKBatch(data[:2], 65)          # large-k path: k > n -> n results
+    ids, d, cnt = nn.nearestKBatch(data[3:5], 65)         # large-k path: k > n -> n results
     assert (cnt == 50).all() and list(ids[0, :50]) == [int(x) for x in oi[0]]
     ch = NearestNeighborsGPU(KinematicChainSpace(12, 1 / 12), gpu)
     ch.add(W.uniform_chain(rng, 100, 12))
