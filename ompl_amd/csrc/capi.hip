@@ -107,6 +107,8 @@ struct ompl_gpu_nn {
     FastBounds sorted_bounds{};
     bool sorted_dirty = true;
     bool cull = true;         // ompl_gpu_nn_set_exact(h, 2) disables the culled screen
+    DevBuf cull_counter;      // tiles scanned by the culled screen (device)
+    uint64_t tiles_total = 0; // tiles a brute-force walk would have scanned
     bool fast = true;        // OMPL_GPU_EXACT_ONLY=1 forces the exact fp64 scan
     uint64_t fast_queries = 0, fast_fallbacks = 0;
     // profiling of the dominant scan kernel (HIP events on the launch stream)
@@ -436,7 +438,13 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
             HIP_OR_FAIL(build_sorted_store(h->sp, h->g, h->feat32, h->cap, (uint32_t)h->n_total, h->sorted_bounds,
                                            &h->sorted, h->stream));
             h->sorted_dirty = false;
+            if (!h->cull_counter.p) {
+                HIP_OR_FAIL(h->cull_counter.ensure(sizeof(unsigned long long)));
+                HIP_OR_FAIL(hipMemsetAsync(h->cull_counter.p, 0, sizeof(unsigned long long), h->stream));
+            }
+            h->sorted.counters = (unsigned long long *)h->cull_counter.p;
         }
+        if (cull) h->tiles_total += (uint64_t)((nq + kCullTile - 1) / kCullTile) * h->sorted.ntiles;
         FastBounds b = cull ? h->sorted_bounds : current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
         const size_t wsb = knn_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus, cull);
@@ -670,6 +678,20 @@ ompl_gpu_status ompl_gpu_nn_kernel_time(ompl_gpu_nn *h, double *total_ms, uint64
     if (total_ms) *total_ms = h->prof_ms;
     if (launches) *launches = h->prof_launches;
     if (kernel_name) *kernel_name = h->prof_name.c_str();
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *tiles_total) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    unsigned long long c = 0;
+    if (h->cull_counter.p) {
+        HIP_OR_FAIL(hipSetDevice(h->device));
+        HIP_OR_FAIL(hipMemcpyAsync(&c, h->cull_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    }
+    if (tiles_scanned) *tiles_scanned = c;
+    if (tiles_total) *tiles_total = h->tiles_total;
     return OMPL_GPU_OK;
 }
 

@@ -78,6 +78,7 @@ struct SortedStore {
     uint32_t *tkey0 = nullptr;   // [ntiles] Morton key of each tile's first state
     uint32_t n = 0, n_pad = 0, ntiles = 0, nsuper = 0;
     size_t bytes = 0;
+    unsigned long long *counters = nullptr;  // optional device counter: tiles scanned (owned by the caller)
 };
 bool cull_supported(const DevSpace &sp);
 // (re)build the sorted copy of ids [0, n) from the fp32 store; allocates into *s

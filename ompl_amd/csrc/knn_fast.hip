@@ -179,10 +179,33 @@ __global__ void super_box_kernel(const float *__restrict__ tbox, uint32_t ntiles
 }
 
 // ---- screening --------------------------------------------------------------------------
+// acos on [0, 1] (Abramowitz & Stegun 4.4.46, |error| <= 2e-8; fp32 evaluation adds
+// < 1e-6, inside the screen's error bound).  NaN propagates.
+__device__ __forceinline__ float acos01(float x) {
+    float p = -0.0012624911f;
+    p = fmaf(p, x, 0.0066700901f);
+    p = fmaf(p, x, -0.0170881256f);
+    p = fmaf(p, x, 0.0308918810f);
+    p = fmaf(p, x, -0.0501743046f);
+    p = fmaf(p, x, 0.0889789874f);
+    p = fmaf(p, x, -0.2145988016f);
+    p = fmaf(p, x, 1.5707963050f);
+    return __builtin_amdgcn_sqrtf(1.f - x) * p;
+}
+
+// Rotation pre-reject threshold: an element with |dot| <= cos(tau/w1 + 1e-5) has
+// acos(|dot|) > tau/w1 even after every fp32 error, hence distance > tau: skip it without
+// the square root and the arc cosine.  ctau < 0 rejects nothing.
+__device__ __forceinline__ float rot_threshold(float tau, float w1) {
+    const float x = tau / w1 + 1e-5f;
+    return x < 1.5707963f ? cosf(x) : -1.f;
+}
+
 // fp32 distance of LDS state j to the lane's query, with the SE3 translation pre-reject
+// and the rotation pre-reject
 template <int SP, int FS, int K2>
 __device__ __forceinline__ void screen_pair(const float *tile, int j, const float *qf, float w0, float w0sq, float w1,
-                                            uint32_t id, TopK32<K2> &top) {
+                                            uint32_t id, TopK32<K2> &top, float &ctau) {
     if constexpr (SP == OMPL_GPU_SPACE_SE3) {
         const float4 a = reinterpret_cast<const float4 *>(tile)[j * 2];
         const float dx = a.x - qf[0], dy = a.y - qf[1], dz = a.z - qf[2];
@@ -195,8 +218,14 @@ __device__ __forceinline__ void screen_pair(const float *tile, int j, const floa
             dot = fmaf(r.y, qf[5], dot);
             dot = fmaf(r.z, qf[6], dot);
             dot = fmaf(r.w, qf[7], dot);
-            const float d = w0 * sqrtf(t) + w1 * acosf(abs1(dot));
-            if (top.admits(d, id)) top.push(d, id);
+            const float c = abs1(dot);
+            if (c > ctau) {
+                const float d = w0 * __builtin_amdgcn_sqrtf(t) + w1 * acos01(c);
+                if (top.admits(d, id)) {
+                    top.push(d, id);
+                    ctau = rot_threshold(top.d[K2 - 1], w1);
+                }
+            }
         }
     } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
         const float4 r = reinterpret_cast<const float4 *>(tile)[j];
@@ -204,8 +233,14 @@ __device__ __forceinline__ void screen_pair(const float *tile, int j, const floa
         dot = fmaf(r.y, qf[1], dot);
         dot = fmaf(r.z, qf[2], dot);
         dot = fmaf(r.w, qf[3], dot);
-        const float d = acosf(abs1(dot));
-        if (top.admits(d, id)) top.push(d, id);
+        const float c = abs1(dot);
+        if (c > ctau) {
+            const float d = acos01(c);
+            if (top.admits(d, id)) {
+                top.push(d, id);
+                ctau = rot_threshold(top.d[K2 - 1], 1.f);
+            }
+        }
     } else {
         float acc = 0.f;
 #pragma unroll
@@ -214,7 +249,7 @@ __device__ __forceinline__ void screen_pair(const float *tile, int j, const floa
             acc = fmaf(diff, diff, acc);
         }
         if (acc < top.tau2) {
-            const float d = sqrtf(acc);
+            const float d = __builtin_amdgcn_sqrtf(acc);
             if (top.admits(d, id)) top.push(d, id);
         }
     }
@@ -250,13 +285,15 @@ __global__ __launch_bounds__(256) void knn32_screen_kernel(const float *__restri
     const float w0sq = w0 * w0;
     TopK32<K2> top;
     top.init();
+    float ctau = -1.f;
     const uint64_t c0 = (uint64_t)blockIdx.y * chunk_len;
     const uint64_t c1 = min(c0 + chunk_len, n_end);
     for (uint64_t base = c0; base < c1; base += kTile) {
         stage_row<SP, FS>(tile, threadIdx.x, f32, cap, base + threadIdx.x);
         __syncthreads();
 #pragma unroll 4
-        for (int s = 0; s < kTile; ++s) screen_pair<SP, FS, K2>(tile, s, qf, w0, w0sq, w1, (uint32_t)(base + s), top);
+        for (int s = 0; s < kTile; ++s)
+            screen_pair<SP, FS, K2>(tile, s, qf, w0, w0sq, w1, (uint32_t)(base + s), top, ctau);
         __syncthreads();
     }
     if (qs >= nq) return;
@@ -275,7 +312,8 @@ __global__ __launch_bounds__(64) void knn32_cull_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
     const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
-    uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi) {
+    uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi,
+    unsigned long long *__restrict__ counters) {
     constexpr int FS = Geo<SP, F>::FS;
     constexpr int NB = Geo<SP, F>::NB;
     __shared__ __attribute__((aligned(16))) float tile[kCullTile * FS];
@@ -289,6 +327,8 @@ __global__ __launch_bounds__(64) void knn32_cull_kernel(
     const float w0sq = w0 * w0;
     TopK32<K2> top;
     top.init();
+    float ctau = -1.f;
+    uint32_t visited = 0;
     // start at the tile holding this wave's middle query on the Morton curve
     const uint32_t key = qkeys[min(blockIdx.x * kCullTile + kCullTile / 2, nq - 1)];
     uint32_t lo = 0, hi = ntiles;  // first tile with tkey0 > key
@@ -321,10 +361,13 @@ __global__ __launch_bounds__(64) void knn32_cull_kernel(
             tid[lane] = ids[p];
             __syncthreads();
 #pragma unroll 4
-            for (int j = 0; j < kCullTile; ++j) screen_pair<SP, FS, K2>(tile, j, qf, w0, w0sq, w1, tid[j], top);
+            for (int j = 0; j < kCullTile; ++j)
+                screen_pair<SP, FS, K2>(tile, j, qf, w0, w0sq, w1, tid[j], top, ctau);
+            ++visited;
             __syncthreads();
         }
     }
+    if (counters && lane == 0) atomicAdd(counters, (unsigned long long)visited);  // tiles scanned
     if (!active) return;
     const size_t o = (size_t)qs * K2;
 #pragma unroll
@@ -339,9 +382,9 @@ __device__ __forceinline__ double screen_error(const DevSpace &sp, double B, dou
     double e = 0.0;
     if constexpr (SP == OMPL_GPU_SPACE_SE3) {
         e = sp.w0 * (6.0 * 1.7320508075688772 * kU * B) + 6.0 * kU * L +
-            sp.w1 * (1.1 * sqrt(12.0 * kU) + 1e-6 + 4.5e-5);
+            sp.w1 * (1.1 * sqrt(12.0 * kU) + 2e-6 + 4.5e-5);
     } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
-        e = 1.1 * sqrt(12.0 * kU) + 1e-6 + 4.5e-5;
+        e = 1.1 * sqrt(12.0 * kU) + 2e-6 + 4.5e-5;
     } else {
         e = 6.0 * sqrt((double)sp.dim) * kU * B + 6.0 * kU * L;
     }
@@ -517,7 +560,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         timer_begin(st, "knn32_cull_kernel");
         hipLaunchKernelGGL((knn32_cull_kernel<SP, F, K2>), dim3((nq + kCullTile - 1) / kCullTile), dim3(kCullTile), 0,
                            st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0,
-                           q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi);
+                           q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters);
         timer_end(st);
     } else {
         timer_begin(st, "knn32_screen_kernel");
