@@ -107,8 +107,7 @@ struct ompl_gpu_nn {
     FastBounds sorted_bounds{};
     bool sorted_dirty = true;
     bool cull = true;         // ompl_gpu_nn_set_exact(h, 2) disables the culled screen
-    DevBuf cull_counter;      // tiles scanned by the culled screen (device)
-    uint64_t tiles_total = 0; // tiles a brute-force walk would have scanned
+    DevBuf cull_counter;      // [tiles scanned by the group walk, tiles of a brute-force walk] (device)
     bool fast = true;        // OMPL_GPU_EXACT_ONLY=1 forces the exact fp64 scan
     uint64_t fast_queries = 0, fast_fallbacks = 0;
     // profiling of the dominant scan kernel (HIP events on the launch stream)
@@ -124,20 +123,27 @@ thread_local KernelTimer *g_kernel_timer = nullptr;
 }
 
 namespace {
-// coordinates that carry the Morton key / culling box: SE3 translation, R^n first <= 6
-int key_dims(const DevSpace &sp) {
+// coordinates whose running box the handle tracks: SE3 translation, R^n first <= 6
+int tracked_dims(const DevSpace &sp) {
     if (sp.kind == OMPL_GPU_SPACE_SE3) return 3;
     if (sp.kind == OMPL_GPU_SPACE_REALVECTOR) return std::min(sp.dim, kKeyDims);
     return 0;
 }
 
+// Morton key box: the tracked coordinates, plus for SE3 the vector part of the
+// sign-canonical quaternion, which lies in [-1, 1]
 FastBounds current_bounds(const ompl_gpu_nn *h) {
     FastBounds b{};
-    b.nkey = key_dims(h->sp);
-    for (int c = 0; c < b.nkey; ++c) {
+    const int nt = tracked_dims(h->sp);
+    b.nkey = h->sp.kind == OMPL_GPU_SPACE_SE3 ? 6 : nt;
+    for (int c = 0; c < nt; ++c) {
         b.lo[c] = (float)h->lo[c];
         const double ext = h->hi[c] - h->lo[c];
         b.inv[c] = ext > 0 ? (float)(1.0 / ext) : 0.f;
+    }
+    for (int c = nt; c < b.nkey; ++c) {
+        b.lo[c] = -1.f;
+        b.inv[c] = 0.5f;
     }
     b.absmax = (float)h->absmax;
     return b;
@@ -316,7 +322,7 @@ ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, 
     }
     if (h->rows32) HIP_OR_FAIL(launch_to_fp32(h->feat, h->cap, h->rows32, h->n_total, n, h->feat32, h->stream));
     // screening bounds (knn_fast.hip): key box of the first <= 6 coordinates, max |coordinate|
-    const int nb = key_dims(h->sp);
+    const int nb = tracked_dims(h->sp);
     h->sorted_dirty = true;
     const int na = h->sp.kind == OMPL_GPU_SPACE_SE3 ? 3 : (h->sp.kind == OMPL_GPU_SPACE_SO3 ? 0 : dim);
     for (size_t i = 0; i < n; ++i) {
@@ -439,12 +445,11 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
                                            &h->sorted, h->stream));
             h->sorted_dirty = false;
             if (!h->cull_counter.p) {
-                HIP_OR_FAIL(h->cull_counter.ensure(sizeof(unsigned long long)));
-                HIP_OR_FAIL(hipMemsetAsync(h->cull_counter.p, 0, sizeof(unsigned long long), h->stream));
+                HIP_OR_FAIL(h->cull_counter.ensure(2 * sizeof(unsigned long long)));
+                HIP_OR_FAIL(hipMemsetAsync(h->cull_counter.p, 0, 2 * sizeof(unsigned long long), h->stream));
             }
             h->sorted.counters = (unsigned long long *)h->cull_counter.p;
         }
-        if (cull) h->tiles_total += (uint64_t)((nq + kCullTile - 1) / kCullTile) * h->sorted.ntiles;
         FastBounds b = cull ? h->sorted_bounds : current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
         const size_t wsb = knn_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus, cull);
@@ -684,14 +689,14 @@ ompl_gpu_status ompl_gpu_nn_kernel_time(ompl_gpu_nn *h, double *total_ms, uint64
 ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *tiles_total) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
-    unsigned long long c = 0;
+    unsigned long long c[2] = {0, 0};
     if (h->cull_counter.p) {
         HIP_OR_FAIL(hipSetDevice(h->device));
-        HIP_OR_FAIL(hipMemcpyAsync(&c, h->cull_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(c, h->cull_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
         HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     }
-    if (tiles_scanned) *tiles_scanned = c;
-    if (tiles_total) *tiles_total = h->tiles_total;
+    if (tiles_scanned) *tiles_scanned = c[0];
+    if (tiles_total) *tiles_total = c[1];
     return OMPL_GPU_OK;
 }
 

@@ -60,25 +60,30 @@ hipError_t launch_knn(const DevSpace &sp, const FeatGeom &g, const double *feat,
 // must be re-run on the exact path by the caller (count in *fail_count, device).
 constexpr int kKeyDims = 6;  // Morton key over at most 6 coordinates
 struct FastBounds {
-    float lo[kKeyDims], inv[kKeyDims];  // key box (inv = 1 / extent) of the first nkey coordinates
-    int nkey;                           // SE3: 3 (translation); R^n: min(n, 6); SO3: 0
+    float lo[kKeyDims], inv[kKeyDims];  // key box (inv = 1 / extent) of the first nkey key coordinates
+    int nkey;                           // SE3: 6 (translation + canonical quaternion xyz); R^n: min(n, 6); SO3: 0
     float absmax;                       // max |coordinate| stored (error bound of the fp32 screen)
 };
 
-// Spatially sorted fp32 copy of the store for the culled screen (SE3 and R^n): states in
-// Morton order, 64-state tiles (one state per lane) and 32-tile super-tiles with
-// axis-aligned boxes over the distance's Euclidean part (SE3 translation / all of R^n).
+// Spatially sorted fp32 copy of the store for the group walk (SE3 and R^n): states in
+// Morton order over the key coordinates, 64-state tiles (one state per lane) and 32-tile
+// super-tiles with axis-aligned boxes over every coordinate of the metric (SE3: the
+// translation and the sign-canonical quaternion, plus the largest quaternion norm excess,
+// so the box yields a lower bound of the full SE3 distance).
 constexpr int kCullTile = 64;
 constexpr int kSuperTiles = 32;
+constexpr int kGroup = 8;  // queries per wave in the group walk
 struct SortedStore {
-    float *rows = nullptr;       // [rows32][n_pad]
+    float *rows = nullptr;       // [rows32][n_pad] (SE3 quaternions sign-canonical: w >= 0)
     uint32_t *ids = nullptr;     // [n_pad] original id of each sorted slot (kNoId = padding)
-    float *tbox = nullptr;       // [ntiles][2*NB] lo.., hi..
-    float *sbox = nullptr;       // [nsuper][2*NB]
+    float *tbox = nullptr;       // [ntiles][box_w] lo.., hi.. (, eta, pad)
+    float *sbox = nullptr;       // [nsuper][box_w]
     uint32_t *tkey0 = nullptr;   // [ntiles] Morton key of each tile's first state
     uint32_t n = 0, n_pad = 0, ntiles = 0, nsuper = 0;
     size_t bytes = 0;
-    unsigned long long *counters = nullptr;  // optional device counter: tiles scanned (owned by the caller)
+    // optional device counters (owned by the caller): [0] tiles scanned, [1] tiles a
+    // brute-force walk of the same query groups would have scanned
+    unsigned long long *counters = nullptr;
 };
 bool cull_supported(const DevSpace &sp);
 // (re)build the sorted copy of ids [0, n) from the fp32 store; allocates into *s
@@ -90,7 +95,7 @@ int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq);  // screening list siz
 int fp32_rows(const DevSpace &sp, const FeatGeom &g);     // rows of the fp32 SoA copy
 size_t knn_fast_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k, uint64_t n_end,
                                 int num_cus, bool cull);
-// sorted == nullptr: chunked brute-force screen; else the culled screen over *sorted
+// sorted == nullptr: chunked brute-force screen; else the group walk over *sorted
 hipError_t launch_knn_fast(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32,
                            uint64_t cap, uint64_t n_end, const SortedStore *sorted, const double *qfeat64, uint32_t nq,
                            uint32_t k, const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes,

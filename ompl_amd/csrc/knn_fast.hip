@@ -48,8 +48,10 @@ constexpr double kU = 5.9604644775390625e-08;  // 2^-24
 template <int SP, int F>
 struct Geo {
     static constexpr int FS = SP == OMPL_GPU_SPACE_SE3 ? 8 : F;  // fp32 row width (LDS / queries)
-    static constexpr int NB = SP == OMPL_GPU_SPACE_SE3 ? 3 : F;  // box dims (Euclidean part)
+    static constexpr int NB = SP == OMPL_GPU_SPACE_SE3 ? 7 : F;  // box dims (every stored coordinate)
     static constexpr int R = SP == OMPL_GPU_SPACE_SE3 ? 7 : F;   // rows of the fp32 SoA store
+    // box record: lo[NB], hi[NB]; SE3 adds eta (largest |q|^2 - 1 >= 0 of the quaternions) + pad
+    static constexpr int BW = SP == OMPL_GPU_SPACE_SE3 ? 16 : 2 * F;
 };
 
 __device__ __forceinline__ float abs1(float x) {  // |x| clamped to 1; NaN stays NaN
@@ -57,7 +59,7 @@ __device__ __forceinline__ float abs1(float x) {  // |x| clamped to 1; NaN stays
     return a > 1.f ? 1.f : a;
 }
 
-// 30-bit Morton key of a fp32 row (SE3 row layout x y z . qx qy qz qw); NaN -> max key
+// 30-bit Morton key of the key coordinates c[0..nkey); NaN -> max key
 __device__ __forceinline__ uint32_t morton_key(const float *c, const FastBounds &b) {
     if (!(c[0] == c[0])) return 0xFFFFFFFFu;
     const int D = b.nkey;
@@ -76,6 +78,20 @@ __device__ __forceinline__ uint32_t morton_key(const float *c, const FastBounds 
     return key;
 }
 
+// key coordinates of a state given as its R stored coordinates (SE3: x y z qx qy qz qw):
+// SE3 keys on the translation and the vector part of the sign-canonical (w >= 0)
+// quaternion, so that tiles are compact in rotation too; R^n on its first coordinates.
+template <int SP>
+__device__ __forceinline__ void key_coords(const float *x, float *c, int nkey) {
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        const float sg = x[6] < 0.f ? -1.f : 1.f;
+        c[0] = x[0]; c[1] = x[1]; c[2] = x[2];
+        c[3] = sg * x[3]; c[4] = sg * x[4]; c[5] = sg * x[5];
+    } else {
+        for (int d = 0; d < nkey; ++d) c[d] = x[d];
+    }
+}
+
 // ---- queries: fp32 rows, keys, order ---------------------------------------------------
 template <int SP, int F>
 __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, FastBounds b, float *__restrict__ q32u,
@@ -85,14 +101,25 @@ __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, Fa
     if (i >= nq) return;
     const double *s = qf + (size_t)i * F;
     float o[FS];
+    float x[kKeyDims + 1];
     if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        o[0] = (float)s[0]; o[1] = (float)s[1]; o[2] = (float)s[2]; o[3] = 0.f;
+        o[0] = (float)s[0]; o[1] = (float)s[1]; o[2] = (float)s[2];
         o[4] = (float)s[3]; o[5] = (float)s[4]; o[6] = (float)s[5]; o[7] = (float)s[6];
+        // slot 3: the quaternion's norm excess max(|q|^2 - 1, 0), used by the box bound
+        float n2 = o[4] * o[4];
+        n2 = fmaf(o[5], o[5], n2);
+        n2 = fmaf(o[6], o[6], n2);
+        n2 = fmaf(o[7], o[7], n2);
+        o[3] = fmaxf(n2 - 1.f, 0.f) * 1.00001f;
+        x[0] = o[0]; x[1] = o[1]; x[2] = o[2]; x[3] = o[4]; x[4] = o[5]; x[5] = o[6]; x[6] = o[7];
     } else {
         for (int f = 0; f < FS; ++f) o[f] = (float)s[f];
+        for (int d = 0; d < b.nkey; ++d) x[d] = o[d];
     }
     for (int f = 0; f < FS; ++f) q32u[(size_t)i * FS + f] = o[f];
-    keys[i] = morton_key(o, b);
+    float c[kKeyDims];
+    key_coords<SP>(x, c, b.nkey);
+    keys[i] = morton_key(c, b);
     idx[i] = i;
 }
 
@@ -111,10 +138,13 @@ __global__ void tree_key_kernel(const float *__restrict__ f32, uint64_t cap, uin
                                 uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    constexpr int R = Geo<SP, F>::R;
+    float x[R > kKeyDims ? R : kKeyDims + 1];
+    const int D = SP == OMPL_GPU_SPACE_SE3 ? 7 : b.nkey;
+    for (int d = 0; d < D; ++d) x[d] = f32[(uint64_t)d * cap + i];
     float c[kKeyDims];
-    const int D = b.nkey;
-    for (int d = 0; d < D; ++d) c[d] = f32[(uint64_t)d * cap + i];
-    keys[i] = D > 0 ? morton_key(c, b) : (c[0] == c[0] ? 0u : 0xFFFFFFFFu);
+    key_coords<SP>(x, c, b.nkey);
+    keys[i] = b.nkey > 0 ? morton_key(c, b) : (x[0] == x[0] ? 0u : 0xFFFFFFFFu);
     ids[i] = i;
 }
 
@@ -126,7 +156,13 @@ __global__ void tree_gather_kernel(const float *__restrict__ f32, uint64_t cap, 
     if (p >= n_pad) return;
     if (p < n) {
         const uint32_t id = ids_sorted[p];
-        for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = f32[(uint64_t)r * cap + id];
+        float x[R];
+        for (int r = 0; r < R; ++r) x[r] = f32[(uint64_t)r * cap + id];
+        if constexpr (SP == OMPL_GPU_SPACE_SE3) {  // |dot| is sign-invariant: store w >= 0
+            if (x[6] < 0.f)
+                for (int r = 3; r < 7; ++r) x[r] = -x[r];
+        }
+        for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = x[r];
         ids[p] = id;
     } else {
         for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = __builtin_nanf("");
@@ -138,7 +174,7 @@ template <int SP, int F>
 __global__ void tile_box_kernel(const float *__restrict__ rows, uint32_t n_pad, uint32_t ntiles,
                                 const uint32_t *__restrict__ keys_sorted, uint32_t n, float *__restrict__ tbox,
                                 uint32_t *__restrict__ tkey0) {
-    constexpr int NB = Geo<SP, F>::NB;
+    constexpr int NB = Geo<SP, F>::NB, BW = Geo<SP, F>::BW;
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
     float lo[NB], hi[NB];
@@ -146,35 +182,57 @@ __global__ void tile_box_kernel(const float *__restrict__ rows, uint32_t n_pad, 
         lo[c] = __builtin_inff();
         hi[c] = -__builtin_inff();
     }
+    float eta = 0.f;
     for (int j = 0; j < kCullTile; ++j) {
         const uint32_t p = t * kCullTile + j;
+        float x[NB];
+        for (int c = 0; c < NB; ++c) x[c] = rows[(size_t)c * n_pad + p];
+        if (!(x[0] == x[0])) continue;  // padding / removed
         for (int c = 0; c < NB; ++c) {
-            const float v = rows[(size_t)c * n_pad + p];
-            if (v == v) {
-                lo[c] = fminf(lo[c], v);
-                hi[c] = fmaxf(hi[c], v);
-            }
+            lo[c] = fminf(lo[c], x[c]);
+            hi[c] = fmaxf(hi[c], x[c]);
+        }
+        if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+            float n2 = x[3] * x[3];
+            n2 = fmaf(x[4], x[4], n2);
+            n2 = fmaf(x[5], x[5], n2);
+            n2 = fmaf(x[6], x[6], n2);
+            eta = fmaxf(eta, n2 - 1.f);
         }
     }
+    float *o = tbox + (size_t)t * BW;
     for (int c = 0; c < NB; ++c) {
-        tbox[(size_t)t * 2 * NB + c] = lo[c];
-        tbox[(size_t)t * 2 * NB + NB + c] = hi[c];
+        o[c] = lo[c];
+        o[NB + c] = hi[c];
+    }
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        o[2 * NB] = eta * 1.00001f;
+        o[2 * NB + 1] = 0.f;
     }
     tkey0[t] = t * kCullTile < n ? keys_sorted[t * kCullTile] : 0xFFFFFFFFu;
 }
 
-__global__ void super_box_kernel(const float *__restrict__ tbox, uint32_t ntiles, int NB, uint32_t nsuper,
+template <int SP, int F>
+__global__ void super_box_kernel(const float *__restrict__ tbox, uint32_t ntiles, uint32_t nsuper,
                                  float *__restrict__ sbox) {
+    constexpr int NB = Geo<SP, F>::NB, BW = Geo<SP, F>::BW;
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nsuper) return;
+    const uint32_t t0 = s * kSuperTiles, t1 = min((s + 1) * kSuperTiles, ntiles);
     for (int c = 0; c < NB; ++c) {
         float lo = __builtin_inff(), hi = -__builtin_inff();
-        for (uint32_t t = s * kSuperTiles; t < min((s + 1) * kSuperTiles, ntiles); ++t) {
-            lo = fminf(lo, tbox[(size_t)t * 2 * NB + c]);
-            hi = fmaxf(hi, tbox[(size_t)t * 2 * NB + NB + c]);
+        for (uint32_t t = t0; t < t1; ++t) {
+            lo = fminf(lo, tbox[(size_t)t * BW + c]);
+            hi = fmaxf(hi, tbox[(size_t)t * BW + NB + c]);
         }
-        sbox[(size_t)s * 2 * NB + c] = lo;
-        sbox[(size_t)s * 2 * NB + NB + c] = hi;
+        sbox[(size_t)s * BW + c] = lo;
+        sbox[(size_t)s * BW + NB + c] = hi;
+    }
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        float eta = 0.f;
+        for (uint32_t t = t0; t < t1; ++t) eta = fmaxf(eta, tbox[(size_t)t * BW + 2 * NB]);
+        sbox[(size_t)s * BW + 2 * NB] = eta;
+        sbox[(size_t)s * BW + 2 * NB + 1] = 0.f;
     }
 }
 
@@ -201,56 +259,87 @@ __device__ __forceinline__ float rot_threshold(float tau, float w1) {
     return x < 1.5707963f ? cosf(x) : -1.f;
 }
 
-// fp32 distance of LDS state j to the lane's query, with the SE3 translation pre-reject
-// and the rotation pre-reject
-template <int SP, int FS, int K2>
-__device__ __forceinline__ void screen_pair(const float *tile, int j, const float *qf, float w0, float w0sq, float w1,
-                                            uint32_t id, TopK32<K2> &top, float &ctau) {
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        const float4 a = reinterpret_cast<const float4 *>(tile)[j * 2];
-        const float dx = a.x - qf[0], dy = a.y - qf[1], dz = a.z - qf[2];
-        float t = dx * dx;
-        t = fmaf(dy, dy, t);
-        t = fmaf(dz, dz, t);
-        if (t * w0sq < top.tau2) {
-            const float4 r = reinterpret_cast<const float4 *>(tile)[j * 2 + 1];
-            float dot = r.x * qf[4];
-            dot = fmaf(r.y, qf[5], dot);
-            dot = fmaf(r.z, qf[6], dot);
-            dot = fmaf(r.w, qf[7], dot);
-            const float c = abs1(dot);
-            if (c > ctau) {
-                const float d = w0 * __builtin_amdgcn_sqrtf(t) + w1 * acos01(c);
-                if (top.admits(d, id)) {
-                    top.push(d, id);
-                    ctau = rot_threshold(top.d[K2 - 1], w1);
+// fp32 screen of NS LDS states against the lane's query, in batches of kBatch: the cheap
+// part (SE3 translation, SO3 dot, R^n squared distance) of a whole batch is computed from
+// back-to-back LDS reads before any data-dependent branch, so one LDS latency is paid per
+// batch, not per state.  Pre-rejects: SE3 translation vs tau, rotation |dot| vs ctau.
+constexpr int kBatch = 8;
+
+template <int SP, int FS, int K2, int NS, class IdOf>
+__device__ __forceinline__ void screen_tile(const float *tile, const float *qf, float w0, float w0sq, float w1,
+                                            IdOf id_of, TopK32<K2> &top, float &ctau) {
+    const float4 *t4 = reinterpret_cast<const float4 *>(tile);
+#pragma unroll 2
+    for (int j0 = 0; j0 < NS; j0 += kBatch) {
+        float v[kBatch];
+        if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+#pragma unroll
+            for (int u = 0; u < kBatch; ++u) {
+                const float4 a = t4[(j0 + u) * 2];
+                const float dx = a.x - qf[0], dy = a.y - qf[1], dz = a.z - qf[2];
+                float t = dx * dx;
+                t = fmaf(dy, dy, t);
+                v[u] = fmaf(dz, dz, t);
+            }
+#pragma unroll
+            for (int u = 0; u < kBatch; ++u) {
+                if (v[u] * w0sq < top.tau2) {
+                    const float4 r = t4[(j0 + u) * 2 + 1];
+                    float dot = r.x * qf[4];
+                    dot = fmaf(r.y, qf[5], dot);
+                    dot = fmaf(r.z, qf[6], dot);
+                    dot = fmaf(r.w, qf[7], dot);
+                    const float c = abs1(dot);
+                    if (c > ctau) {
+                        const float d = w0 * __builtin_amdgcn_sqrtf(v[u]) + w1 * acos01(c);
+                        const uint32_t id = id_of(j0 + u);
+                        if (top.admits(d, id)) {
+                            top.push(d, id);
+                            ctau = rot_threshold(top.d[K2 - 1], w1);
+                        }
+                    }
                 }
             }
-        }
-    } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
-        const float4 r = reinterpret_cast<const float4 *>(tile)[j];
-        float dot = r.x * qf[0];
-        dot = fmaf(r.y, qf[1], dot);
-        dot = fmaf(r.z, qf[2], dot);
-        dot = fmaf(r.w, qf[3], dot);
-        const float c = abs1(dot);
-        if (c > ctau) {
-            const float d = acos01(c);
-            if (top.admits(d, id)) {
-                top.push(d, id);
-                ctau = rot_threshold(top.d[K2 - 1], 1.f);
-            }
-        }
-    } else {
-        float acc = 0.f;
+        } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
 #pragma unroll
-        for (int f = 0; f < FS; ++f) {
-            const float diff = tile[j * FS + f] - qf[f];
-            acc = fmaf(diff, diff, acc);
-        }
-        if (acc < top.tau2) {
-            const float d = __builtin_amdgcn_sqrtf(acc);
-            if (top.admits(d, id)) top.push(d, id);
+            for (int u = 0; u < kBatch; ++u) {
+                const float4 r = t4[j0 + u];
+                float dot = r.x * qf[0];
+                dot = fmaf(r.y, qf[1], dot);
+                dot = fmaf(r.z, qf[2], dot);
+                dot = fmaf(r.w, qf[3], dot);
+                v[u] = abs1(dot);
+            }
+#pragma unroll
+            for (int u = 0; u < kBatch; ++u) {
+                if (v[u] > ctau) {
+                    const float d = acos01(v[u]);
+                    const uint32_t id = id_of(j0 + u);
+                    if (top.admits(d, id)) {
+                        top.push(d, id);
+                        ctau = rot_threshold(top.d[K2 - 1], 1.f);
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kBatch; ++u) {
+                float acc = 0.f;
+#pragma unroll
+                for (int f = 0; f < FS; ++f) {
+                    const float diff = tile[(j0 + u) * FS + f] - qf[f];
+                    acc = fmaf(diff, diff, acc);
+                }
+                v[u] = acc;
+            }
+#pragma unroll
+            for (int u = 0; u < kBatch; ++u) {
+                if (v[u] < top.tau2) {
+                    const float d = __builtin_amdgcn_sqrtf(v[u]);
+                    const uint32_t id = id_of(j0 + u);
+                    if (top.admits(d, id)) top.push(d, id);
+                }
+            }
         }
     }
 }
@@ -291,9 +380,8 @@ __global__ __launch_bounds__(256) void knn32_screen_kernel(const float *__restri
     for (uint64_t base = c0; base < c1; base += kTile) {
         stage_row<SP, FS>(tile, threadIdx.x, f32, cap, base + threadIdx.x);
         __syncthreads();
-#pragma unroll 4
-        for (int s = 0; s < kTile; ++s)
-            screen_pair<SP, FS, K2>(tile, s, qf, w0, w0sq, w1, (uint32_t)(base + s), top, ctau);
+        screen_tile<SP, FS, K2, kTile>(tile, qf, w0, w0sq, w1, [&](int j) { return (uint32_t)(base + j); }, top,
+                                       ctau);
         __syncthreads();
     }
     if (qs >= nq) return;
@@ -305,32 +393,211 @@ __global__ __launch_bounds__(256) void knn32_screen_kernel(const float *__restri
     }
 }
 
-// culled screen: one wave = 64 spatially adjacent queries, nearest-first walk over
-// super-tiles with box culling (the Euclidean part is a lower bound of the distance)
-template <int SP, int F, int K2>
-__global__ __launch_bounds__(64) void knn32_cull_kernel(
+// ---- group walk (SE3, R^n) ----------------------------------------------------------------
+// One wave serves G queries that are neighbours on the Morton curve.  Lanes hold the states
+// of a 64-state tile (registers), the G queries are broadcast from LDS, and every query keeps
+// its K2-list spread over the wave (lane j holds entry j, sorted by (distance, id)), so an
+// insertion is one shift by a lane.  Tiles and super-tiles whose box is farther than every
+// query's current K2-th distance are skipped; the box bound covers the whole metric.
+
+// lower bound of the fp32 distance from query row q (FS layout) to any state inside box bx
+template <int SP, int F>
+__device__ __forceinline__ float box_lb(const float *bx, const float *q, float w0, float w1) {
+    constexpr int NB = Geo<SP, F>::NB;
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        float tg = 0.f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float g = fmaxf(fmaxf(bx[c] - q[c], q[c] - bx[NB + c]), 0.f);
+            tg = fmaf(g, g, tg);
+        }
+        // rotation: acos|<q,p>| >= chord min(|q - p|, |q + p|) for unit quaternions; a norm
+        // excess eta of either side lowers the chord^2 bound by at most eta_q + eta_p
+        float rp = 0.f, rm = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float lo = bx[3 + c], hi = bx[NB + 3 + c], v = q[4 + c];
+            const float gp = fmaxf(fmaxf(lo - v, v - hi), 0.f);
+            const float gm = fmaxf(fmaxf(lo + v, -v - hi), 0.f);
+            rp = fmaf(gp, gp, rp);
+            rm = fmaf(gm, gm, rm);
+        }
+        const float r2 = fminf(rp, rm) - (bx[2 * NB] + q[3]);
+        return w0 * __builtin_amdgcn_sqrtf(tg) + w1 * __builtin_amdgcn_sqrtf(fmaxf(r2, 0.f));
+    } else {
+        float acc = 0.f;
+#pragma unroll
+        for (int c = 0; c < F; ++c) {
+            const float g = fmaxf(fmaxf(bx[c] - q[c], q[c] - bx[F + c]), 0.f);
+            acc = fmaf(g, g, acc);
+        }
+        return __builtin_amdgcn_sqrtf(acc);
+    }
+}
+
+// fp32 screened distance of a lane's state x (R stored coordinates) to query row q; the
+// operation sequence is screen_tile's, so screen_error bounds it too
+template <int SP, int F>
+__device__ __forceinline__ float state_dist32(const float *x, const float *q, float w0, float w1) {
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        const float dx = x[0] - q[0], dy = x[1] - q[1], dz = x[2] - q[2];
+        float t = dx * dx;
+        t = fmaf(dy, dy, t);
+        t = fmaf(dz, dz, t);
+        float dot = x[3] * q[4];
+        dot = fmaf(x[4], q[5], dot);
+        dot = fmaf(x[5], q[6], dot);
+        dot = fmaf(x[6], q[7], dot);
+        return w0 * __builtin_amdgcn_sqrtf(t) + w1 * acos01(abs1(dot));
+    } else {
+        float acc = 0.f;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            const float diff = x[f] - q[f];
+            acc = fmaf(diff, diff, acc);
+        }
+        return __builtin_amdgcn_sqrtf(acc);
+    }
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ uint32_t readlane_u(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+// value of lane - 1 (wave-wide DPP shift); lane 0 receives `first`
+__device__ __forceinline__ float shr1_f(float v, float first) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(first), __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint32_t shr1_u(uint32_t v, uint32_t first) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t fold_tiles(uint64_t m) {  // lanes t and t+32 describe tile t
+    return (uint32_t)(m | (m >> 32));
+}
+
+template <int SP, int F, int K2, int G>
+__global__ __launch_bounds__(64) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
     const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
     uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi,
     unsigned long long *__restrict__ counters) {
-    constexpr int FS = Geo<SP, F>::FS;
-    constexpr int NB = Geo<SP, F>::NB;
-    __shared__ __attribute__((aligned(16))) float tile[kCullTile * FS];
-    __shared__ uint32_t tid[kCullTile];
+    constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
+    constexpr int GH = G / 2;
+    static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
+    __shared__ __attribute__((aligned(16))) float qrow[G * FS];
     const int lane = threadIdx.x;
-    const uint32_t qs = blockIdx.x * kCullTile + lane;
-    const bool active = qs < nq;
-    float qf[FS];
+    const int half = lane >> 5;
+    const uint32_t g0 = blockIdx.x * G;
+    for (int t = lane; t < G * FS; t += 64) {
+        const uint32_t qi = g0 + t / FS;
+        qrow[t] = qi < nq ? q32[(size_t)qi * FS + t % FS] : __builtin_nanf("");
+    }
+    __syncthreads();
+    // the lists (lane j = entry j) and their K2-th entries (wave-uniform); a padding query
+    // gets threshold -inf so that it admits nothing and needs no tile
+    float Ld[G];
+    uint32_t Li[G];
+    float td[G];
+    uint32_t ti[G];
 #pragma unroll
-    for (int f = 0; f < FS; ++f) qf[f] = active ? q32[(size_t)qs * FS + f] : __builtin_nanf("");
-    const float w0sq = w0 * w0;
-    TopK32<K2> top;
-    top.init();
-    float ctau = -1.f;
+    for (int g = 0; g < G; ++g) {
+        Ld[g] = __builtin_inff();
+        Li[g] = kNoId;
+        td[g] = g0 + g < nq ? __builtin_inff() : -__builtin_inff();
+        ti[g] = kNoId;
+    }
     uint32_t visited = 0;
-    // start at the tile holding this wave's middle query on the Morton curve
-    const uint32_t key = qkeys[min(blockIdx.x * kCullTile + kCullTile / 2, nq - 1)];
+
+    // tiles of super-tile s some query may still need; lb[j]: this lane's bound for tile
+    // (lane & 31) and query half * GH + j
+    auto tile_mask = [&](uint32_t s, float (&lb)[GH]) -> uint32_t {
+        const uint32_t t = s * kSuperTiles + (lane & 31);
+        bool need = false;
+        if (t < ntiles) {
+            float bx[BW];
+            const float4 *b4 = reinterpret_cast<const float4 *>(tbox + (size_t)t * BW);
+#pragma unroll
+            for (int c = 0; c < BW / 4; ++c) {
+                const float4 v = b4[c];
+                bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
+            }
+#pragma unroll
+            for (int j = 0; j < GH; ++j) {
+                lb[j] = box_lb<SP, F>(bx, &qrow[(half * GH + j) * FS], w0, w1);
+                need |= lb[j] < (half ? td[GH + j] : td[j]);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < GH; ++j) lb[j] = __builtin_inff();
+        }
+        return fold_tiles(__ballot(need));
+    };
+    auto load_state = [&](uint32_t t, float (&x)[R], uint32_t &id) {
+        const uint64_t p = (uint64_t)t * kCullTile + lane;
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r] = rows[(uint64_t)r * n_pad + p];
+        id = ids[p];
+    };
+    auto scan_state = [&](const float (&x)[R], uint32_t id) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float d = state_dist32<SP, F>(x, &qrow[g * FS], w0, w1);
+            uint64_t bm = __ballot(d < td[g] || (d == td[g] && id < ti[g]));
+            while (bm) {
+                const int l = __builtin_ctzll(bm);
+                bm &= bm - 1;
+                const float cd = readlane_f(d, l);
+                const uint32_t ci = readlane_u(id, l);
+                if (cd < td[g] || (cd == td[g] && ci < ti[g])) {
+                    const float pv = shr1_f(Ld[g], -__builtin_inff());
+                    const uint32_t pv_i = shr1_u(Li[g], 0u);
+                    const bool lt_cur = cd < Ld[g] || (cd == Ld[g] && ci < Li[g]);
+                    const bool lt_prev = lane > 0 && (cd < pv || (cd == pv && ci < pv_i));
+                    const float nd = lt_prev ? pv : (lt_cur ? cd : Ld[g]);
+                    const uint32_t ni = lt_prev ? pv_i : (lt_cur ? ci : Li[g]);
+                    Ld[g] = nd;
+                    Li[g] = ni;
+                    td[g] = readlane_f(Ld[g], K2 - 1);
+                    ti[g] = readlane_u(Li[g], K2 - 1);
+                }
+            }
+        }
+    };
+    auto visit = [&](uint32_t s) {
+        float lb[GH];
+        uint32_t m = tile_mask(s, lb);
+        if (!m) return;
+        float x[R], xn[R];
+        uint32_t id, idn = kNoId;
+        int t = __builtin_ctz(m);
+        m &= m - 1;
+        load_state(s * kSuperTiles + t, x, id);
+        while (true) {
+            const bool more = m != 0;
+            if (more) {  // prefetch the next tile while this one is scanned
+                const int tn = __builtin_ctz(m);
+                m &= m - 1;
+                load_state(s * kSuperTiles + tn, xn, idn);
+            }
+            scan_state(x, id);
+            ++visited;
+            // drop the remaining tiles that the tightened thresholds exclude
+            bool still = false;
+#pragma unroll
+            for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
+            m &= fold_tiles(__ballot(still));
+            if (!more) break;
+#pragma unroll
+            for (int r = 0; r < R; ++r) x[r] = xn[r];
+            id = idn;
+        }
+    };
+
+    // start at the super-tile holding the group's middle query on the Morton curve
+    const uint32_t key = qkeys[min(g0 + G / 2, nq - 1)];
     uint32_t lo = 0, hi = ntiles;  // first tile with tkey0 > key
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -339,42 +606,49 @@ __global__ __launch_bounds__(64) void knn32_cull_kernel(
         else
             hi = mid;
     }
-    const int s0 = (int)((lo > 0 ? lo - 1 : 0) / kSuperTiles);
-    auto culled = [&](const float *box) {
-        float lb2 = 0.f;
+    const uint32_t s0 = (lo > 0 ? lo - 1 : 0) / kSuperTiles;
+    // visit order: s0 - 1, s0, s0 + 1 (the group's neighbourhood, which sets the thresholds),
+    // then every other super-tile in curve order, 64 box tests at a time.  One call site
+    // keeps the kernel's code small.
+    uint32_t base = s0 > 0 ? s0 - 1 : 0;
+    uint64_t sm = (s0 > 0 ? 7ull : 3ull) & ((nsuper - base >= 64) ? ~0ull : ((1ull << (nsuper - base)) - 1));
+    uint32_t sb = 0;
+    while (true) {
+        if (!sm) {
+            if (sb >= nsuper) break;
+            const uint32_t s = sb + lane;
+            bool need = false;
+            if (s < nsuper && (s + 1 < s0 || s > s0 + 1)) {
+                float bx[BW];
+                const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
 #pragma unroll
-        for (int c = 0; c < NB; ++c) {
-            const float g = fmaxf(fmaxf(box[c] - qf[c], qf[c] - box[NB + c]), 0.f);
-            lb2 = fmaf(g, g, lb2);
-        }
-        return __all(!active || lb2 * w0sq >= top.tau2);
-    };
-    for (int step = 0; step < 2 * (int)nsuper; ++step) {
-        const int s = (step & 1) ? s0 + (step + 1) / 2 : s0 - step / 2;  // s0, s0+1, s0-1, s0+2, ...
-        if (s < 0 || s >= (int)nsuper) continue;
-        if (culled(sbox + (size_t)s * 2 * NB)) continue;
-        const uint32_t t_end = min((uint32_t)(s + 1) * kSuperTiles, ntiles);
-        for (uint32_t t = (uint32_t)s * kSuperTiles; t < t_end; ++t) {
-            if (culled(tbox + (size_t)t * 2 * NB)) continue;
-            const uint64_t p = (uint64_t)t * kCullTile + lane;
-            stage_row<SP, FS>(tile, lane, rows, n_pad, p);
-            tid[lane] = ids[p];
-            __syncthreads();
-#pragma unroll 4
-            for (int j = 0; j < kCullTile; ++j)
-                screen_pair<SP, FS, K2>(tile, j, qf, w0, w0sq, w1, tid[j], top, ctau);
-            ++visited;
-            __syncthreads();
-        }
-    }
-    if (counters && lane == 0) atomicAdd(counters, (unsigned long long)visited);  // tiles scanned
-    if (!active) return;
-    const size_t o = (size_t)qs * K2;
+                for (int c = 0; c < BW / 4; ++c) {
+                    const float4 v = b4[c];
+                    bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
+                }
 #pragma unroll
-    for (int j = 0; j < K2; ++j) {
-        pd[o + j] = top.d[j];
-        pi[o + j] = top.i[j];
+                for (int g = 0; g < G; ++g) need |= box_lb<SP, F>(bx, &qrow[g * FS], w0, w1) < td[g];
+            }
+            sm = __ballot(need);
+            base = sb;
+            sb += 64;
+            continue;
+        }
+        const int l = __builtin_ctzll(sm);
+        sm &= sm - 1;
+        visit(base + l);
     }
+    if (counters && lane == 0) {
+        atomicAdd(&counters[0], (unsigned long long)visited);  // tiles scanned
+        atomicAdd(&counters[1], (unsigned long long)ntiles);   // tiles of a brute-force walk
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+        if (g0 + g < nq && lane < K2) {
+            const size_t o = (size_t)(g0 + g) * K2 + lane;
+            pd[o] = Ld[g];
+            pi[o] = Li[g];
+        }
 }
 
 template <int SP>
@@ -488,7 +762,7 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
     p.K2 = fast_k2(sp, k, nq);
     p.K = k_bucket(k);
     p.cull = cull;
-    if (cull) {
+    if (cull) {  // group walk: one list per query
         p.chunks = 1;
         p.chunk_len = 0;
         return p;
@@ -556,13 +830,19 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
     e = hipMemsetAsync(fail, 0, 4, st);
     if (e != hipSuccess) return e;
-    if (p.cull) {
-        timer_begin(st, "knn32_cull_kernel");
-        hipLaunchKernelGGL((knn32_cull_kernel<SP, F, K2>), dim3((nq + kCullTile - 1) / kCullTile), dim3(kCullTile), 0,
-                           st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0,
-                           q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters);
-        timer_end(st);
-    } else {
+    bool walked = false;
+    if constexpr (SP != OMPL_GPU_SPACE_SO3) {  // SO3 has no group walk (cull_supported)
+        if (p.cull) {
+            timer_begin(st, "knn32_group_kernel");
+            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, kGroup>), dim3((nq + kGroup - 1) / kGroup), dim3(64),
+                               0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
+                               ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters);
+            timer_end(st);
+            walked = true;
+        }
+    }
+    if (p.cull && !walked) return hipErrorInvalidValue;
+    if (!walked) {
         timer_begin(st, "knn32_screen_kernel");
         hipLaunchKernelGGL((knn32_screen_kernel<SP, F, K2>), dim3((nq + kTile - 1) / kTile, p.chunks), dim3(kTile), 0,
                            st, f32, cap, n_end, q32, nq, p.chunk_len, (float)sp.w0, (float)sp.w1, pd, pi);
@@ -603,7 +883,7 @@ hipError_t run_fast_space(const DevSpace &sp, const FastPlan &p, const FastLayou
 template <int SP, int F>
 hipError_t build_sorted(const float *f32, uint64_t cap, uint32_t n, const FastBounds &b, SortedStore *s,
                         hipStream_t st) {
-    constexpr int R = Geo<SP, F>::R, NB = Geo<SP, F>::NB;
+    constexpr int R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
     free_sorted_store(s);
     s->n = n;
     s->ntiles = std::max<uint32_t>(1, (n + kCullTile - 1) / kCullTile);
@@ -627,10 +907,10 @@ hipError_t build_sorted(const float *f32, uint64_t cap, uint32_t n, const FastBo
     if ((e = hipMalloc(&tmp, std::max<size_t>(tb, 1))) != hipSuccess) return done(e);
     if ((e = hipMalloc(&s->rows, 4ull * R * s->n_pad)) != hipSuccess) return done(e);
     if ((e = hipMalloc(&s->ids, 4ull * s->n_pad)) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->tbox, 8ull * NB * s->ntiles)) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->sbox, 8ull * NB * s->nsuper)) != hipSuccess) return done(e);
+    if ((e = hipMalloc(&s->tbox, 4ull * BW * s->ntiles)) != hipSuccess) return done(e);
+    if ((e = hipMalloc(&s->sbox, 4ull * BW * s->nsuper)) != hipSuccess) return done(e);
     if ((e = hipMalloc(&s->tkey0, 4ull * s->ntiles)) != hipSuccess) return done(e);
-    s->bytes = 4ull * R * s->n_pad + 4ull * s->n_pad + 8ull * NB * (s->ntiles + s->nsuper) + 4ull * s->ntiles;
+    s->bytes = 4ull * R * s->n_pad + 4ull * s->n_pad + 4ull * BW * (s->ntiles + s->nsuper) + 4ull * s->ntiles;
     if (n) {
         hipLaunchKernelGGL((tree_key_kernel<SP, F>), dim3((n + 255) / 256), dim3(256), 0, st, f32, cap, n, b, keys,
                            ids0);
@@ -642,8 +922,8 @@ hipError_t build_sorted(const float *f32, uint64_t cap, uint32_t n, const FastBo
                        n, s->n_pad, s->rows, s->ids);
     hipLaunchKernelGGL((tile_box_kernel<SP, F>), dim3((s->ntiles + 255) / 256), dim3(256), 0, st, s->rows, s->n_pad,
                        s->ntiles, keys_s, n, s->tbox, s->tkey0);
-    hipLaunchKernelGGL(super_box_kernel, dim3((s->nsuper + 255) / 256), dim3(256), 0, st, s->tbox, s->ntiles, NB,
-                       s->nsuper, s->sbox);
+    hipLaunchKernelGGL((super_box_kernel<SP, F>), dim3((s->nsuper + 255) / 256), dim3(256), 0, st, s->tbox,
+                       s->ntiles, s->nsuper, s->sbox);
     if ((e = hipGetLastError()) != hipSuccess) return done(e);
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);  // temporaries freed below
     return done(hipSuccess);

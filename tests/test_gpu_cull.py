@@ -59,3 +59,32 @@ def test_clustered_and_duplicate_states(gpu):
     nn = NearestNeighborsGPU(sp, gpu)
     nn.add(data)
     _check(nn, sp, data, np.arange(len(data)), q, 16)
+
+
+def test_se3_quaternion_signs_and_norms(gpu):
+    """The group walk stores sign-canonical quaternions and bounds the rotation part by the
+    chord to the box, corrected for norm excess: stored and query quaternions with w < 0 and
+    norms away from 1 must not lose a neighbour."""
+    rng = np.random.default_rng(64)
+    sp = SE3StateSpace()
+    data = W.uniform_se3(rng, 60000)
+    data[:, 3:] *= rng.choice([-1.0, 1.0], size=(60000, 1)) * rng.uniform(0.97, 1.03, size=(60000, 1))
+    q = W.uniform_se3(rng, 700)
+    q[:, 3:] *= rng.choice([-1.0, 1.0], size=(700, 1)) * rng.uniform(0.97, 1.03, size=(700, 1))
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    _check(nn, sp, data, np.arange(len(data)), q, 10)
+    scanned, total = nn.cull_stats()
+    assert 0 < scanned <= total
+
+
+def test_group_tail_and_small_batches(gpu):
+    """Query counts that leave the last group of the walk partly empty."""
+    rng = np.random.default_rng(65)
+    sp = RealVectorStateSpace(5, 0.0, 1.0)
+    data = W.uniform_rv(rng, 30000, 5)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    for nq in (64, 67, 131, 1001):
+        q = W.uniform_rv(rng, nq, 5)
+        _check(nn, sp, data, np.arange(len(data)), q, 7)
