@@ -31,6 +31,22 @@ PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X vector peaks (MI355X_MICROAR
 HBM_PEAK_GBS = 8000.0                       # HBM3E spec
 F_SE3 = 21  # flops per SE(3) distance, SURVEY.md §8d (sqrt and acos counted as 1 each)
 B_SE3 = {"f32": 28, "f64": 56}              # bytes per stored SE(3) state streamed by a scan
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r1_group_walk", "pmc_summary.json")
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
+    (FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction, + WRITE_SIZE)."""
+    try:
+        with open(PMC_PROFILE) as f:
+            per = json.load(f)["per_kernel_mean"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for name, c in per.items():
+        if name.split("<")[0].endswith(kernel) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            return {"bytes": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0,
+                    "source": os.path.relpath(PMC_PROFILE, ROOT) + f" [{name}]"}
+    return None
 
 
 def parse():
@@ -183,6 +199,7 @@ def main():
     nn.profile(True)
     nn.kernel_time()
     scr0, fb0 = nn.stats()
+    cul0 = nn.cull_stats()
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -197,6 +214,7 @@ def main():
     kern_ms_total, kern_n, kern_name = nn.kernel_time()
     kern_ms = kern_ms_total / max(kern_n, 1)
     scr1, fb1 = nn.stats()
+    cul1 = nn.cull_stats()
     knn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     steer_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     mv_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
@@ -217,8 +235,17 @@ def main():
         value = 2.0 * nq * world * args.steps / elapsed
         screen = kern_name.startswith("knn32")
         dt = "f32" if screen else "f64"
-        flops = float(nq) * args.tree * F_SE3
-        achieved = flops / (kern_ms * 1e-3) / 1e12
+        # work the dominant kernel actually did: the group walk evaluates the 64 states of a
+        # tile for each query whose own box bound admits the tile (cull counters, device
+        # atomics); the brute-force kernels evaluate every (query, state) pair
+        launches = max(args.steps, 1)
+        if kern_name == "knn32_group_kernel" and cul1[1] > cul0[1]:
+            pairs = (cul1[2] - cul0[2]) * 64 / launches
+            scanned_frac = pairs / (float(nq) * args.tree)
+        else:
+            pairs, scanned_frac = float(nq) * args.tree, 1.0
+        achieved = pairs * F_SE3 / (kern_ms * 1e-3) / 1e12
+        traffic = pmc_traffic(kern_name)
         line = {
             "metric": METRIC,
             "value": value,
@@ -245,10 +272,13 @@ def main():
             "motion_valid_fraction": valid_frac,
             "roofline": {
                 "bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
-                "frac": achieved / PEAK_TFLOPS[dt], "traffic": None,
+                "frac": achieved / PEAK_TFLOPS[dt], "traffic": traffic["bytes"] if traffic else None,
                 "kernel": kern_name, "kernel_ms": kern_ms,
-                "algorithmic": f"{nq} x {args.tree} pairs x {F_SE3} flop (SURVEY §8d) per launch, "
-                               f"{dt} vector peak; VALU-bound (no MFMA)",
+                "algorithmic": (f"{pairs:.4g} (query, state) distance evaluations per launch x {F_SE3} flop "
+                                f"(SURVEY §8d); the culled walk scanned {scanned_frac:.4%} of the "
+                                f"{nq} x {args.tree} pairs; {dt} VALU peak (compute-bound on VALU, no MFMA)"),
+                "brute_force_equivalent_tflops": float(nq) * args.tree * F_SE3 / (kern_ms * 1e-3) / 1e12,
+                "traffic_source": traffic["source"] if traffic else None,
             },
             "single_query": single,
             "cpu_baseline": cpu,

@@ -166,9 +166,11 @@ ompl_gpu_status ompl_gpu_nn_knn_device(ompl_gpu_nn *h, const double *d_queries, 
  * *screened counts queries that took the screen, *fallbacks those re-run exactly. */
 ompl_gpu_status ompl_gpu_nn_set_exact(ompl_gpu_nn *h, int exact_only);
 ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint64_t *fallbacks);
-/* Group walk: 64-state tiles scanned, summed over query groups, vs the tiles a full scan
- * by the same groups would have touched. */
-ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *tiles_total);
+/* Group walk: 64-state tiles fetched, summed over query groups, vs the tiles a full scan
+ * by the same groups would have touched; *query_tiles counts (tile, query) scans, i.e.
+ * 64 distance evaluations each.  Any output may be NULL. */
+ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *tiles_total,
+                                       uint64_t *query_tiles);
 /* Profiling: when enabled, each query call brackets its dominant scan kernel with HIP
  * events recorded on the launch stream; kernel_time synchronises the stream and returns
  * the summed duration, the number of bracketed launches and the kernel's name. */

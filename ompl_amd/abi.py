@@ -84,7 +84,7 @@ SIGNATURES = {
     "ompl_gpu_nn_set_exact": (C.c_int, [_P, C.c_int]),
     "ompl_gpu_nn_stats": (C.c_int, [_P, _U64, _U64]),
     "ompl_gpu_nn_profile": (C.c_int, [_P, C.c_int]),
-    "ompl_gpu_nn_cull_stats": (C.c_int, [_P, _U64, _U64]),
+    "ompl_gpu_nn_cull_stats": (C.c_int, [_P, _U64, _U64, _U64]),
     "ompl_gpu_nn_kernel_time": (C.c_int, [_P, _D, _U64, C.POINTER(C.c_char_p)]),
     "ompl_gpu_steer_device": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_uint32, C.c_double, _P, _P]),
     "ompl_gpu_mv_create": (C.c_int, [C.POINTER(_P), C.POINTER(SpaceStruct), C.POINTER(CheckerStruct), C.c_int]),

@@ -107,7 +107,8 @@ struct ompl_gpu_nn {
     FastBounds sorted_bounds{};
     bool sorted_dirty = true;
     bool cull = true;         // ompl_gpu_nn_set_exact(h, 2) disables the culled screen
-    DevBuf cull_counter;      // [tiles scanned by the group walk, tiles of a brute-force walk] (device)
+    DevBuf cull_counter;      // [tiles fetched by the group walk, tiles of a brute-force walk,
+                              //  (tile, query) pairs scanned] (device)
     bool fast = true;        // OMPL_GPU_EXACT_ONLY=1 forces the exact fp64 scan
     uint64_t fast_queries = 0, fast_fallbacks = 0;
     // profiling of the dominant scan kernel (HIP events on the launch stream)
@@ -445,8 +446,8 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
                                            &h->sorted, h->stream));
             h->sorted_dirty = false;
             if (!h->cull_counter.p) {
-                HIP_OR_FAIL(h->cull_counter.ensure(2 * sizeof(unsigned long long)));
-                HIP_OR_FAIL(hipMemsetAsync(h->cull_counter.p, 0, 2 * sizeof(unsigned long long), h->stream));
+                HIP_OR_FAIL(h->cull_counter.ensure(3 * sizeof(unsigned long long)));
+                HIP_OR_FAIL(hipMemsetAsync(h->cull_counter.p, 0, 3 * sizeof(unsigned long long), h->stream));
             }
             h->sorted.counters = (unsigned long long *)h->cull_counter.p;
         }
@@ -686,10 +687,11 @@ ompl_gpu_status ompl_gpu_nn_kernel_time(ompl_gpu_nn *h, double *total_ms, uint64
     return OMPL_GPU_OK;
 }
 
-ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *tiles_total) {
+ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *tiles_total,
+                                       uint64_t *query_tiles) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
-    unsigned long long c[2] = {0, 0};
+    unsigned long long c[3] = {0, 0, 0};
     if (h->cull_counter.p) {
         HIP_OR_FAIL(hipSetDevice(h->device));
         HIP_OR_FAIL(hipMemcpyAsync(c, h->cull_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
@@ -697,6 +699,7 @@ ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, 
     }
     if (tiles_scanned) *tiles_scanned = c[0];
     if (tiles_total) *tiles_total = c[1];
+    if (query_tiles) *query_tiles = c[2];
     return OMPL_GPU_OK;
 }
 

@@ -1,936 +1,9 @@
-// knn_fast.hip — exact batched kNN via an fp32 screen and an fp64 certificate (gfx950).
-//
-// The reference ranks in fp64 (NearestNeighborsGNAT.h:544-558 on StateSpace::distance).
-// fp64 VALU issues at half the fp32 rate on CDNA4 and the fp64 sqrt / acos expansions
-// are long, so the scan runs in fp32 and fp64 is spent only on a short candidate list:
-//
-//   1. queries are ordered along a Morton curve (SE3: translation; R^n: first <= 6 dims)
-//      so the 64 queries of a wave are spatial neighbours;
-//   2. screen (fp32), one thread per query, register list of the K2 > k smallest fp32
-//      distances.  Two variants:
-//        culled (SE3, R^n): the store is kept in a Morton-sorted copy with 64-state tiles
-//          and 2048-state super-tiles carrying boxes of the Euclidean part of the metric;
-//          a wave walks super-tiles outward from its own position on the curve and skips
-//          every (super-)tile whose box is farther than each lane's current K2-th
-//          distance (a lower bound: the SO3 part of an SE3 distance is >= 0);
-//        chunked (SO3): the whole store, split in chunks along grid.y.
-//      Inside a tile, for SE3 the translation part is computed first and the rotation
-//      (acos) only where sqrt(t) can still beat the K2-th distance: with spatially
-//      ordered queries that branch is coherent across the wave.
-//   3. certify (fp64): merge the lists, recompute the K2 candidates exactly in the
-//      reference's operation order, keep the k best by (distance, id), and prove that no
-//      element outside the list can enter: |d32 - d64| <= e for every element, so if the
-//      exact k-th distance + e < the list's K2-th fp32 distance L the answer is exact.
-//      Queries that fail the proof are listed; the caller re-runs them on the exact fp64
-//      path (knn.hip), so the results always equal the exact path's.
-//
-// Error bound e (u = 2^-24, B = max |coordinate|, D = dims, L as above), doubled for slack:
-//   translation / R^n : 6 sqrt(D) u B + 6 u L   (fp32 conversion + sum of squares + sqrt)
-//   rotation          : 1.1 sqrt(2 * 6u) + 1e-6 + 4.5e-5
-//                       (|dot32 - dot| <= 6u; acos is 1/2-Hoelder near 1; the reference
-//                        returns 0 for dot > 1 - 1e-9, SO3StateSpace.cpp:258-260)
-#include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
-
-#include <algorithm>
-#include <cmath>
-
-#include "feat_dist.h"
-#include "kernels.h"
-#include "topk.h"
+// knn_fast.hip — dispatch of the exact batched kNN (fp32 screen + fp64 certificate).
+// The kernels and their host orchestration live in knn_fast_impl.h, instantiated per
+// space in knn_fast_se3.hip / knn_fast_so3.hip / knn_fast_rv.hip.
+#include "knn_fast_impl.h"
 
 namespace ompl_amd {
-
-namespace {
-
-constexpr double kU = 5.9604644775390625e-08;  // 2^-24
-
-template <int SP, int F>
-struct Geo {
-    static constexpr int FS = SP == OMPL_GPU_SPACE_SE3 ? 8 : F;  // fp32 row width (LDS / queries)
-    static constexpr int NB = SP == OMPL_GPU_SPACE_SE3 ? 7 : F;  // box dims (every stored coordinate)
-    static constexpr int R = SP == OMPL_GPU_SPACE_SE3 ? 7 : F;   // rows of the fp32 SoA store
-    // box record: lo[NB], hi[NB]; SE3 adds eta (largest |q|^2 - 1 >= 0 of the quaternions) + pad
-    static constexpr int BW = SP == OMPL_GPU_SPACE_SE3 ? 16 : 2 * F;
-};
-
-__device__ __forceinline__ float abs1(float x) {  // |x| clamped to 1; NaN stays NaN
-    float a = fabsf(x);
-    return a > 1.f ? 1.f : a;
-}
-
-// 30-bit Morton key of the key coordinates c[0..nkey); NaN -> max key
-__device__ __forceinline__ uint32_t morton_key(const float *c, const FastBounds &b) {
-    if (!(c[0] == c[0])) return 0xFFFFFFFFu;
-    const int D = b.nkey;
-    if (D <= 0) return 0u;
-    const int bits = 30 / D;
-    const float scale = (float)((1u << bits) - 1u);
-    uint32_t v[kKeyDims];
-    for (int d = 0; d < D; ++d) {
-        float t = (c[d] - b.lo[d]) * b.inv[d] * scale;
-        t = t > 0.f ? (t < scale ? t : scale) : 0.f;
-        v[d] = (uint32_t)t;
-    }
-    uint32_t key = 0;
-    for (int bit = bits - 1; bit >= 0; --bit)
-        for (int d = 0; d < D; ++d) key = (key << 1) | ((v[d] >> bit) & 1u);
-    return key;
-}
-
-// key coordinates of a state given as its R stored coordinates (SE3: x y z qx qy qz qw):
-// SE3 keys on the translation and the vector part of the sign-canonical (w >= 0)
-// quaternion, so that tiles are compact in rotation too; R^n on its first coordinates.
-template <int SP>
-__device__ __forceinline__ void key_coords(const float *x, float *c, int nkey) {
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        const float sg = x[6] < 0.f ? -1.f : 1.f;
-        c[0] = x[0]; c[1] = x[1]; c[2] = x[2];
-        c[3] = sg * x[3]; c[4] = sg * x[4]; c[5] = sg * x[5];
-    } else {
-        for (int d = 0; d < nkey; ++d) c[d] = x[d];
-    }
-}
-
-// ---- queries: fp32 rows, keys, order ---------------------------------------------------
-template <int SP, int F>
-__global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, FastBounds b, float *__restrict__ q32u,
-                                  uint32_t *__restrict__ keys, uint32_t *__restrict__ idx) {
-    constexpr int FS = Geo<SP, F>::FS;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nq) return;
-    const double *s = qf + (size_t)i * F;
-    float o[FS];
-    float x[kKeyDims + 1];
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        o[0] = (float)s[0]; o[1] = (float)s[1]; o[2] = (float)s[2];
-        o[4] = (float)s[3]; o[5] = (float)s[4]; o[6] = (float)s[5]; o[7] = (float)s[6];
-        // slot 3: the quaternion's norm excess max(|q|^2 - 1, 0), used by the box bound
-        float n2 = o[4] * o[4];
-        n2 = fmaf(o[5], o[5], n2);
-        n2 = fmaf(o[6], o[6], n2);
-        n2 = fmaf(o[7], o[7], n2);
-        o[3] = fmaxf(n2 - 1.f, 0.f) * 1.00001f;
-        x[0] = o[0]; x[1] = o[1]; x[2] = o[2]; x[3] = o[4]; x[4] = o[5]; x[5] = o[6]; x[6] = o[7];
-    } else {
-        for (int f = 0; f < FS; ++f) o[f] = (float)s[f];
-        for (int d = 0; d < b.nkey; ++d) x[d] = o[d];
-    }
-    for (int f = 0; f < FS; ++f) q32u[(size_t)i * FS + f] = o[f];
-    float c[kKeyDims];
-    key_coords<SP>(x, c, b.nkey);
-    keys[i] = morton_key(c, b);
-    idx[i] = i;
-}
-
-template <int FS>
-__global__ void query_gather_kernel(const float *__restrict__ q32u, const uint32_t *__restrict__ perm, uint32_t nq,
-                                    float *__restrict__ q32) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nq * (uint32_t)FS) return;
-    const uint32_t qs = t / FS, f = t % FS;
-    q32[t] = q32u[(size_t)perm[qs] * FS + f];
-}
-
-// ---- sorted store (culled screen) ----------------------------------------------------------
-template <int SP, int F>
-__global__ void tree_key_kernel(const float *__restrict__ f32, uint64_t cap, uint32_t n, FastBounds b,
-                                uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    constexpr int R = Geo<SP, F>::R;
-    float x[R > kKeyDims ? R : kKeyDims + 1];
-    const int D = SP == OMPL_GPU_SPACE_SE3 ? 7 : b.nkey;
-    for (int d = 0; d < D; ++d) x[d] = f32[(uint64_t)d * cap + i];
-    float c[kKeyDims];
-    key_coords<SP>(x, c, b.nkey);
-    keys[i] = b.nkey > 0 ? morton_key(c, b) : (x[0] == x[0] ? 0u : 0xFFFFFFFFu);
-    ids[i] = i;
-}
-
-template <int SP, int F>
-__global__ void tree_gather_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ ids_sorted,
-                                   uint32_t n, uint32_t n_pad, float *__restrict__ rows, uint32_t *__restrict__ ids) {
-    constexpr int R = Geo<SP, F>::R;
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_pad) return;
-    if (p < n) {
-        const uint32_t id = ids_sorted[p];
-        float x[R];
-        for (int r = 0; r < R; ++r) x[r] = f32[(uint64_t)r * cap + id];
-        if constexpr (SP == OMPL_GPU_SPACE_SE3) {  // |dot| is sign-invariant: store w >= 0
-            if (x[6] < 0.f)
-                for (int r = 3; r < 7; ++r) x[r] = -x[r];
-        }
-        for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = x[r];
-        ids[p] = id;
-    } else {
-        for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = __builtin_nanf("");
-        ids[p] = kNoId;
-    }
-}
-
-template <int SP, int F>
-__global__ void tile_box_kernel(const float *__restrict__ rows, uint32_t n_pad, uint32_t ntiles,
-                                const uint32_t *__restrict__ keys_sorted, uint32_t n, float *__restrict__ tbox,
-                                uint32_t *__restrict__ tkey0) {
-    constexpr int NB = Geo<SP, F>::NB, BW = Geo<SP, F>::BW;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntiles) return;
-    float lo[NB], hi[NB];
-    for (int c = 0; c < NB; ++c) {
-        lo[c] = __builtin_inff();
-        hi[c] = -__builtin_inff();
-    }
-    float eta = 0.f;
-    for (int j = 0; j < kCullTile; ++j) {
-        const uint32_t p = t * kCullTile + j;
-        float x[NB];
-        for (int c = 0; c < NB; ++c) x[c] = rows[(size_t)c * n_pad + p];
-        if (!(x[0] == x[0])) continue;  // padding / removed
-        for (int c = 0; c < NB; ++c) {
-            lo[c] = fminf(lo[c], x[c]);
-            hi[c] = fmaxf(hi[c], x[c]);
-        }
-        if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-            float n2 = x[3] * x[3];
-            n2 = fmaf(x[4], x[4], n2);
-            n2 = fmaf(x[5], x[5], n2);
-            n2 = fmaf(x[6], x[6], n2);
-            eta = fmaxf(eta, n2 - 1.f);
-        }
-    }
-    float *o = tbox + (size_t)t * BW;
-    for (int c = 0; c < NB; ++c) {
-        o[c] = lo[c];
-        o[NB + c] = hi[c];
-    }
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        o[2 * NB] = eta * 1.00001f;
-        o[2 * NB + 1] = 0.f;
-    }
-    tkey0[t] = t * kCullTile < n ? keys_sorted[t * kCullTile] : 0xFFFFFFFFu;
-}
-
-template <int SP, int F>
-__global__ void super_box_kernel(const float *__restrict__ tbox, uint32_t ntiles, uint32_t nsuper,
-                                 float *__restrict__ sbox) {
-    constexpr int NB = Geo<SP, F>::NB, BW = Geo<SP, F>::BW;
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nsuper) return;
-    const uint32_t t0 = s * kSuperTiles, t1 = min((s + 1) * kSuperTiles, ntiles);
-    for (int c = 0; c < NB; ++c) {
-        float lo = __builtin_inff(), hi = -__builtin_inff();
-        for (uint32_t t = t0; t < t1; ++t) {
-            lo = fminf(lo, tbox[(size_t)t * BW + c]);
-            hi = fmaxf(hi, tbox[(size_t)t * BW + NB + c]);
-        }
-        sbox[(size_t)s * BW + c] = lo;
-        sbox[(size_t)s * BW + NB + c] = hi;
-    }
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        float eta = 0.f;
-        for (uint32_t t = t0; t < t1; ++t) eta = fmaxf(eta, tbox[(size_t)t * BW + 2 * NB]);
-        sbox[(size_t)s * BW + 2 * NB] = eta;
-        sbox[(size_t)s * BW + 2 * NB + 1] = 0.f;
-    }
-}
-
-// ---- screening --------------------------------------------------------------------------
-// acos on [0, 1] (Abramowitz & Stegun 4.4.46, |error| <= 2e-8; fp32 evaluation adds
-// < 1e-6, inside the screen's error bound).  NaN propagates.
-__device__ __forceinline__ float acos01(float x) {
-    float p = -0.0012624911f;
-    p = fmaf(p, x, 0.0066700901f);
-    p = fmaf(p, x, -0.0170881256f);
-    p = fmaf(p, x, 0.0308918810f);
-    p = fmaf(p, x, -0.0501743046f);
-    p = fmaf(p, x, 0.0889789874f);
-    p = fmaf(p, x, -0.2145988016f);
-    p = fmaf(p, x, 1.5707963050f);
-    return __builtin_amdgcn_sqrtf(1.f - x) * p;
-}
-
-// Rotation pre-reject threshold: an element with |dot| <= cos(tau/w1 + 1e-5) has
-// acos(|dot|) > tau/w1 even after every fp32 error, hence distance > tau: skip it without
-// the square root and the arc cosine.  ctau < 0 rejects nothing.
-__device__ __forceinline__ float rot_threshold(float tau, float w1) {
-    const float x = tau / w1 + 1e-5f;
-    return x < 1.5707963f ? cosf(x) : -1.f;
-}
-
-// fp32 screen of NS LDS states against the lane's query, in batches of kBatch: the cheap
-// part (SE3 translation, SO3 dot, R^n squared distance) of a whole batch is computed from
-// back-to-back LDS reads before any data-dependent branch, so one LDS latency is paid per
-// batch, not per state.  Pre-rejects: SE3 translation vs tau, rotation |dot| vs ctau.
-constexpr int kBatch = 8;
-
-template <int SP, int FS, int K2, int NS, class IdOf>
-__device__ __forceinline__ void screen_tile(const float *tile, const float *qf, float w0, float w0sq, float w1,
-                                            IdOf id_of, TopK32<K2> &top, float &ctau) {
-    const float4 *t4 = reinterpret_cast<const float4 *>(tile);
-#pragma unroll 2
-    for (int j0 = 0; j0 < NS; j0 += kBatch) {
-        float v[kBatch];
-        if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-#pragma unroll
-            for (int u = 0; u < kBatch; ++u) {
-                const float4 a = t4[(j0 + u) * 2];
-                const float dx = a.x - qf[0], dy = a.y - qf[1], dz = a.z - qf[2];
-                float t = dx * dx;
-                t = fmaf(dy, dy, t);
-                v[u] = fmaf(dz, dz, t);
-            }
-#pragma unroll
-            for (int u = 0; u < kBatch; ++u) {
-                if (v[u] * w0sq < top.tau2) {
-                    const float4 r = t4[(j0 + u) * 2 + 1];
-                    float dot = r.x * qf[4];
-                    dot = fmaf(r.y, qf[5], dot);
-                    dot = fmaf(r.z, qf[6], dot);
-                    dot = fmaf(r.w, qf[7], dot);
-                    const float c = abs1(dot);
-                    if (c > ctau) {
-                        const float d = w0 * __builtin_amdgcn_sqrtf(v[u]) + w1 * acos01(c);
-                        const uint32_t id = id_of(j0 + u);
-                        if (top.admits(d, id)) {
-                            top.push(d, id);
-                            ctau = rot_threshold(top.d[K2 - 1], w1);
-                        }
-                    }
-                }
-            }
-        } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
-#pragma unroll
-            for (int u = 0; u < kBatch; ++u) {
-                const float4 r = t4[j0 + u];
-                float dot = r.x * qf[0];
-                dot = fmaf(r.y, qf[1], dot);
-                dot = fmaf(r.z, qf[2], dot);
-                dot = fmaf(r.w, qf[3], dot);
-                v[u] = abs1(dot);
-            }
-#pragma unroll
-            for (int u = 0; u < kBatch; ++u) {
-                if (v[u] > ctau) {
-                    const float d = acos01(v[u]);
-                    const uint32_t id = id_of(j0 + u);
-                    if (top.admits(d, id)) {
-                        top.push(d, id);
-                        ctau = rot_threshold(top.d[K2 - 1], 1.f);
-                    }
-                }
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < kBatch; ++u) {
-                float acc = 0.f;
-#pragma unroll
-                for (int f = 0; f < FS; ++f) {
-                    const float diff = tile[(j0 + u) * FS + f] - qf[f];
-                    acc = fmaf(diff, diff, acc);
-                }
-                v[u] = acc;
-            }
-#pragma unroll
-            for (int u = 0; u < kBatch; ++u) {
-                if (v[u] < top.tau2) {
-                    const float d = __builtin_amdgcn_sqrtf(v[u]);
-                    const uint32_t id = id_of(j0 + u);
-                    if (top.admits(d, id)) top.push(d, id);
-                }
-            }
-        }
-    }
-}
-
-template <int SP, int FS>
-__device__ __forceinline__ void stage_row(float *tile, int slot, const float *__restrict__ src, uint64_t stride,
-                                          uint64_t g) {
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        float4 a, r;
-        a.x = src[g]; a.y = src[stride + g]; a.z = src[2 * stride + g]; a.w = 0.f;
-        r.x = src[3 * stride + g]; r.y = src[4 * stride + g]; r.z = src[5 * stride + g]; r.w = src[6 * stride + g];
-        reinterpret_cast<float4 *>(tile)[slot * 2] = a;
-        reinterpret_cast<float4 *>(tile)[slot * 2 + 1] = r;
-    } else {
-#pragma unroll
-        for (int f = 0; f < FS; ++f) tile[slot * FS + f] = src[(uint64_t)f * stride + g];
-    }
-}
-
-// chunked brute-force screen (SO3, or when no sorted copy exists)
-template <int SP, int F, int K2>
-__global__ __launch_bounds__(256) void knn32_screen_kernel(const float *__restrict__ f32, uint64_t cap,
-                                                           uint64_t n_end, const float *__restrict__ q32,
-                                                           uint32_t nq, uint32_t chunk_len, float w0, float w1,
-                                                           float *__restrict__ pd, uint32_t *__restrict__ pi) {
-    constexpr int FS = Geo<SP, F>::FS;
-    __shared__ __attribute__((aligned(16))) float tile[kTile * FS];
-    const uint32_t qs = blockIdx.x * kTile + threadIdx.x;
-    float qf[FS];
-#pragma unroll
-    for (int f = 0; f < FS; ++f) qf[f] = qs < nq ? q32[(size_t)qs * FS + f] : __builtin_nanf("");
-    const float w0sq = w0 * w0;
-    TopK32<K2> top;
-    top.init();
-    float ctau = -1.f;
-    const uint64_t c0 = (uint64_t)blockIdx.y * chunk_len;
-    const uint64_t c1 = min(c0 + chunk_len, n_end);
-    for (uint64_t base = c0; base < c1; base += kTile) {
-        stage_row<SP, FS>(tile, threadIdx.x, f32, cap, base + threadIdx.x);
-        __syncthreads();
-        screen_tile<SP, FS, K2, kTile>(tile, qf, w0, w0sq, w1, [&](int j) { return (uint32_t)(base + j); }, top,
-                                       ctau);
-        __syncthreads();
-    }
-    if (qs >= nq) return;
-    const size_t o = ((size_t)blockIdx.y * nq + qs) * K2;
-#pragma unroll
-    for (int j = 0; j < K2; ++j) {
-        pd[o + j] = top.d[j];
-        pi[o + j] = top.i[j];
-    }
-}
-
-// ---- group walk (SE3, R^n) ----------------------------------------------------------------
-// One wave serves G queries that are neighbours on the Morton curve.  Lanes hold the states
-// of a 64-state tile (registers), the G queries are broadcast from LDS, and every query keeps
-// its K2-list spread over the wave (lane j holds entry j, sorted by (distance, id)), so an
-// insertion is one shift by a lane.  Tiles and super-tiles whose box is farther than every
-// query's current K2-th distance are skipped; the box bound covers the whole metric.
-
-// lower bound of the fp32 distance from query row q (FS layout) to any state inside box bx
-template <int SP, int F>
-__device__ __forceinline__ float box_lb(const float *bx, const float *q, float w0, float w1) {
-    constexpr int NB = Geo<SP, F>::NB;
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        float tg = 0.f;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float g = fmaxf(fmaxf(bx[c] - q[c], q[c] - bx[NB + c]), 0.f);
-            tg = fmaf(g, g, tg);
-        }
-        // rotation: acos|<q,p>| >= chord min(|q - p|, |q + p|) for unit quaternions; a norm
-        // excess eta of either side lowers the chord^2 bound by at most eta_q + eta_p
-        float rp = 0.f, rm = 0.f;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const float lo = bx[3 + c], hi = bx[NB + 3 + c], v = q[4 + c];
-            const float gp = fmaxf(fmaxf(lo - v, v - hi), 0.f);
-            const float gm = fmaxf(fmaxf(lo + v, -v - hi), 0.f);
-            rp = fmaf(gp, gp, rp);
-            rm = fmaf(gm, gm, rm);
-        }
-        const float r2 = fminf(rp, rm) - (bx[2 * NB] + q[3]);
-        return w0 * __builtin_amdgcn_sqrtf(tg) + w1 * __builtin_amdgcn_sqrtf(fmaxf(r2, 0.f));
-    } else {
-        float acc = 0.f;
-#pragma unroll
-        for (int c = 0; c < F; ++c) {
-            const float g = fmaxf(fmaxf(bx[c] - q[c], q[c] - bx[F + c]), 0.f);
-            acc = fmaf(g, g, acc);
-        }
-        return __builtin_amdgcn_sqrtf(acc);
-    }
-}
-
-// fp32 screened distance of a lane's state x (R stored coordinates) to query row q; the
-// operation sequence is screen_tile's, so screen_error bounds it too
-template <int SP, int F>
-__device__ __forceinline__ float state_dist32(const float *x, const float *q, float w0, float w1) {
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        const float dx = x[0] - q[0], dy = x[1] - q[1], dz = x[2] - q[2];
-        float t = dx * dx;
-        t = fmaf(dy, dy, t);
-        t = fmaf(dz, dz, t);
-        float dot = x[3] * q[4];
-        dot = fmaf(x[4], q[5], dot);
-        dot = fmaf(x[5], q[6], dot);
-        dot = fmaf(x[6], q[7], dot);
-        return w0 * __builtin_amdgcn_sqrtf(t) + w1 * acos01(abs1(dot));
-    } else {
-        float acc = 0.f;
-#pragma unroll
-        for (int f = 0; f < F; ++f) {
-            const float diff = x[f] - q[f];
-            acc = fmaf(diff, diff, acc);
-        }
-        return __builtin_amdgcn_sqrtf(acc);
-    }
-}
-
-__device__ __forceinline__ float readlane_f(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-__device__ __forceinline__ uint32_t readlane_u(uint32_t v, int l) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
-}
-// value of lane - 1 (wave-wide DPP shift); lane 0 receives `first`
-__device__ __forceinline__ float shr1_f(float v, float first) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(first), __float_as_int(v), 0x138, 0xF, 0xF, false));
-}
-__device__ __forceinline__ uint32_t shr1_u(uint32_t v, uint32_t first) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
-}
-__device__ __forceinline__ uint32_t fold_tiles(uint64_t m) {  // lanes t and t+32 describe tile t
-    return (uint32_t)(m | (m >> 32));
-}
-
-template <int SP, int F, int K2, int G>
-__global__ __launch_bounds__(64) void knn32_group_kernel(
-    const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
-    const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
-    const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
-    uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi,
-    unsigned long long *__restrict__ counters) {
-    constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
-    constexpr int GH = G / 2;
-    static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
-    __shared__ __attribute__((aligned(16))) float qrow[G * FS];
-    const int lane = threadIdx.x;
-    const int half = lane >> 5;
-    const uint32_t g0 = blockIdx.x * G;
-    for (int t = lane; t < G * FS; t += 64) {
-        const uint32_t qi = g0 + t / FS;
-        qrow[t] = qi < nq ? q32[(size_t)qi * FS + t % FS] : __builtin_nanf("");
-    }
-    __syncthreads();
-    // the lists (lane j = entry j) and their K2-th entries (wave-uniform); a padding query
-    // gets threshold -inf so that it admits nothing and needs no tile
-    float Ld[G];
-    uint32_t Li[G];
-    float td[G];
-    uint32_t ti[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        Ld[g] = __builtin_inff();
-        Li[g] = kNoId;
-        td[g] = g0 + g < nq ? __builtin_inff() : -__builtin_inff();
-        ti[g] = kNoId;
-    }
-    uint32_t visited = 0;
-
-    // tiles of super-tile s some query may still need; lb[j]: this lane's bound for tile
-    // (lane & 31) and query half * GH + j
-    auto tile_mask = [&](uint32_t s, float (&lb)[GH]) -> uint32_t {
-        const uint32_t t = s * kSuperTiles + (lane & 31);
-        bool need = false;
-        if (t < ntiles) {
-            float bx[BW];
-            const float4 *b4 = reinterpret_cast<const float4 *>(tbox + (size_t)t * BW);
-#pragma unroll
-            for (int c = 0; c < BW / 4; ++c) {
-                const float4 v = b4[c];
-                bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
-            }
-#pragma unroll
-            for (int j = 0; j < GH; ++j) {
-                lb[j] = box_lb<SP, F>(bx, &qrow[(half * GH + j) * FS], w0, w1);
-                need |= lb[j] < (half ? td[GH + j] : td[j]);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < GH; ++j) lb[j] = __builtin_inff();
-        }
-        return fold_tiles(__ballot(need));
-    };
-    auto load_state = [&](uint32_t t, float (&x)[R], uint32_t &id) {
-        const uint64_t p = (uint64_t)t * kCullTile + lane;
-#pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = rows[(uint64_t)r * n_pad + p];
-        id = ids[p];
-    };
-    auto scan_state = [&](const float (&x)[R], uint32_t id) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float d = state_dist32<SP, F>(x, &qrow[g * FS], w0, w1);
-            uint64_t bm = __ballot(d < td[g] || (d == td[g] && id < ti[g]));
-            while (bm) {
-                const int l = __builtin_ctzll(bm);
-                bm &= bm - 1;
-                const float cd = readlane_f(d, l);
-                const uint32_t ci = readlane_u(id, l);
-                if (cd < td[g] || (cd == td[g] && ci < ti[g])) {
-                    const float pv = shr1_f(Ld[g], -__builtin_inff());
-                    const uint32_t pv_i = shr1_u(Li[g], 0u);
-                    const bool lt_cur = cd < Ld[g] || (cd == Ld[g] && ci < Li[g]);
-                    const bool lt_prev = lane > 0 && (cd < pv || (cd == pv && ci < pv_i));
-                    const float nd = lt_prev ? pv : (lt_cur ? cd : Ld[g]);
-                    const uint32_t ni = lt_prev ? pv_i : (lt_cur ? ci : Li[g]);
-                    Ld[g] = nd;
-                    Li[g] = ni;
-                    td[g] = readlane_f(Ld[g], K2 - 1);
-                    ti[g] = readlane_u(Li[g], K2 - 1);
-                }
-            }
-        }
-    };
-    auto visit = [&](uint32_t s) {
-        float lb[GH];
-        uint32_t m = tile_mask(s, lb);
-        if (!m) return;
-        float x[R], xn[R];
-        uint32_t id, idn = kNoId;
-        int t = __builtin_ctz(m);
-        m &= m - 1;
-        load_state(s * kSuperTiles + t, x, id);
-        while (true) {
-            const bool more = m != 0;
-            if (more) {  // prefetch the next tile while this one is scanned
-                const int tn = __builtin_ctz(m);
-                m &= m - 1;
-                load_state(s * kSuperTiles + tn, xn, idn);
-            }
-            scan_state(x, id);
-            ++visited;
-            // drop the remaining tiles that the tightened thresholds exclude
-            bool still = false;
-#pragma unroll
-            for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
-            m &= fold_tiles(__ballot(still));
-            if (!more) break;
-#pragma unroll
-            for (int r = 0; r < R; ++r) x[r] = xn[r];
-            id = idn;
-        }
-    };
-
-    // start at the super-tile holding the group's middle query on the Morton curve
-    const uint32_t key = qkeys[min(g0 + G / 2, nq - 1)];
-    uint32_t lo = 0, hi = ntiles;  // first tile with tkey0 > key
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (tkey0[mid] <= key)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    const uint32_t s0 = (lo > 0 ? lo - 1 : 0) / kSuperTiles;
-    // visit order: s0 - 1, s0, s0 + 1 (the group's neighbourhood, which sets the thresholds),
-    // then every other super-tile in curve order, 64 box tests at a time.  One call site
-    // keeps the kernel's code small.
-    uint32_t base = s0 > 0 ? s0 - 1 : 0;
-    uint64_t sm = (s0 > 0 ? 7ull : 3ull) & ((nsuper - base >= 64) ? ~0ull : ((1ull << (nsuper - base)) - 1));
-    uint32_t sb = 0;
-    while (true) {
-        if (!sm) {
-            if (sb >= nsuper) break;
-            const uint32_t s = sb + lane;
-            bool need = false;
-            if (s < nsuper && (s + 1 < s0 || s > s0 + 1)) {
-                float bx[BW];
-                const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
-#pragma unroll
-                for (int c = 0; c < BW / 4; ++c) {
-                    const float4 v = b4[c];
-                    bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
-                }
-#pragma unroll
-                for (int g = 0; g < G; ++g) need |= box_lb<SP, F>(bx, &qrow[g * FS], w0, w1) < td[g];
-            }
-            sm = __ballot(need);
-            base = sb;
-            sb += 64;
-            continue;
-        }
-        const int l = __builtin_ctzll(sm);
-        sm &= sm - 1;
-        visit(base + l);
-    }
-    if (counters && lane == 0) {
-        atomicAdd(&counters[0], (unsigned long long)visited);  // tiles scanned
-        atomicAdd(&counters[1], (unsigned long long)ntiles);   // tiles of a brute-force walk
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-        if (g0 + g < nq && lane < K2) {
-            const size_t o = (size_t)(g0 + g) * K2 + lane;
-            pd[o] = Ld[g];
-            pi[o] = Li[g];
-        }
-}
-
-template <int SP>
-__device__ __forceinline__ double screen_error(const DevSpace &sp, double B, double L) {
-    double e = 0.0;
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        e = sp.w0 * (6.0 * 1.7320508075688772 * kU * B) + 6.0 * kU * L +
-            sp.w1 * (1.1 * sqrt(12.0 * kU) + 2e-6 + 4.5e-5);
-    } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
-        e = 1.1 * sqrt(12.0 * kU) + 2e-6 + 4.5e-5;
-    } else {
-        e = 6.0 * sqrt((double)sp.dim) * kU * B + 6.0 * kU * L;
-    }
-    return 2.0 * e;
-}
-
-template <int SP, int F, int K2, int K>
-__global__ __launch_bounds__(256) void knn_certify_kernel(const float *__restrict__ pd, const uint32_t *__restrict__ pi,
-                                                          uint32_t S, uint32_t nq, const uint32_t *__restrict__ perm,
-                                                          const double *__restrict__ feat64, uint64_t cap,
-                                                          const double *__restrict__ qf64, DevSpace sp,
-                                                          float absmax, double *__restrict__ out_d,
-                                                          uint32_t *__restrict__ out_i, uint32_t out_k,
-                                                          uint32_t *__restrict__ fail_count,
-                                                          uint32_t *__restrict__ fail_list) {
-    const uint32_t qs = blockIdx.x * blockDim.x + threadIdx.x;
-    if (qs >= nq) return;
-    TopK32<K2> t;
-    t.init();
-    for (uint32_t s = 0; s < S; ++s) {
-        const size_t o = ((size_t)s * nq + qs) * K2;
-        for (int j = 0; j < K2; ++j) {
-            const float d = pd[o + j];
-            const uint32_t id = pi[o + j];
-            if (!t.admits(d, id)) break;  // lists are sorted
-            t.push(d, id);
-        }
-    }
-    const uint32_t q = perm[qs];
-    double qv[F];
-#pragma unroll
-    for (int f = 0; f < F; ++f) qv[f] = qf64[(size_t)q * F + f];
-    TopK<K> ex;
-    ex.init();
-#pragma unroll
-    for (int j = 0; j < K2; ++j) {
-        const uint32_t id = t.i[j];
-        if (id != kNoId) {
-            double sv[F];
-#pragma unroll
-            for (int f = 0; f < F; ++f) sv[f] = feat64[(uint64_t)f * cap + id];
-            ex.offer(feat_dist<SP, F, 0>(sv, qv, sp), id);  // the reference formula, fp64
-        }
-    }
-    bool ok = true;
-    if (t.i[K2 - 1] != kNoId) {  // the list is full: prove that no excluded element can enter
-        double B = absmax;
-        const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_SO3 ? 0 : F);
-        for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qv[c]));
-        const double L = (double)t.d[K2 - 1];
-        double dk = ex.d[K - 1];
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            if (j == (int)out_k - 1) dk = ex.d[j];
-        ok = dk + screen_error<SP>(sp, B, L) < L * (1.0 - 8.0 * kU);
-    }
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-        if (j < (int)out_k) {
-            out_d[(size_t)q * out_k + j] = ex.d[j];
-            out_i[(size_t)q * out_k + j] = ex.i[j];
-        }
-    if (!ok) fail_list[atomicAdd(fail_count, 1u)] = q;
-}
-
-__global__ void to_fp32_kernel(const double *__restrict__ f64, uint64_t cap, int rows, uint64_t first, uint64_t n,
-                               float *__restrict__ f32) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * rows) return;
-    const uint64_t r = t / n, i = first + t % n;
-    f32[r * cap + i] = (float)f64[r * cap + i];
-}
-
-__global__ void gather_rows_kernel(const double *__restrict__ src, int F, const uint32_t *__restrict__ list,
-                                   uint32_t n, double *__restrict__ dst) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * (uint32_t)F) return;
-    const uint32_t i = t / F, f = t % F;
-    dst[t] = src[(size_t)list[i] * F + f];
-}
-
-__global__ void scatter_results_kernel(const double *__restrict__ d, const uint32_t *__restrict__ ids, uint32_t k,
-                                       const uint32_t *__restrict__ list, uint32_t n, double *__restrict__ out_d,
-                                       uint32_t *__restrict__ out_i) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * k) return;
-    const uint32_t i = t / k, j = t % k;
-    out_d[(size_t)list[i] * k + j] = d[t];
-    out_i[(size_t)list[i] * k + j] = ids[t];
-}
-
-// ---- host orchestration -----------------------------------------------------------------
-struct FastPlan {
-    int K2, K;
-    bool cull;
-    uint32_t chunks, chunk_len;
-};
-
-FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, int num_cus, bool cull) {
-    FastPlan p{};
-    p.K2 = fast_k2(sp, k, nq);
-    p.K = k_bucket(k);
-    p.cull = cull;
-    if (cull) {  // group walk: one list per query
-        p.chunks = 1;
-        p.chunk_len = 0;
-        return p;
-    }
-    const uint64_t tiles = std::max<uint64_t>(n_end / kTile, 1);
-    const uint64_t qblocks = (nq + kTile - 1) / kTile;
-    const uint64_t target = (uint64_t)num_cus * 8;
-    uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>((target + qblocks - 1) / qblocks, tiles));
-    const uint64_t per = (tiles + S - 1) / S;
-    p.chunk_len = (uint32_t)(per * kTile);
-    p.chunks = (uint32_t)((n_end + p.chunk_len - 1) / p.chunk_len);
-    return p;
-}
-
-inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
-
-struct FastLayout {
-    size_t keys, keys2, idx, perm, cub, q32u, q32, pd, pi, fail, total;
-    size_t cub_bytes;
-};
-
-FastLayout fast_layout(const DevSpace &sp, const FeatGeom &g, const FastPlan &p, uint32_t nq) {
-    FastLayout L{};
-    size_t off = 0;
-    auto take = [&](size_t b) {
-        size_t o = off;
-        off += align_up(b);
-        return o;
-    };
-    L.keys = take(4ull * nq);
-    L.keys2 = take(4ull * nq);
-    L.idx = take(4ull * nq);
-    L.perm = take(4ull * nq);
-    size_t cb = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                             (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nq, 0, 32);
-    L.cub_bytes = cb;
-    L.cub = take(cb);
-    const int FS = sp.kind == OMPL_GPU_SPACE_SE3 ? 8 : g.F;
-    L.q32u = take(4ull * nq * FS);
-    L.q32 = take(4ull * nq * FS);
-    L.pd = take(4ull * p.chunks * nq * p.K2);
-    L.pi = take(4ull * p.chunks * nq * p.K2);
-    L.fail = take(4ull * (nq + 1));
-    L.total = off;
-    return L;
-}
-
-template <int SP, int F, int K2, int K>
-hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, char *ws, const float *f32,
-                    const double *f64, uint64_t cap, uint64_t n_end, const SortedStore *ss, const double *qf64,
-                    uint32_t nq, uint32_t k, const FastBounds &b, double *od, uint32_t *oi, hipStream_t st) {
-    constexpr int FS = Geo<SP, F>::FS;
-    uint32_t *keys = (uint32_t *)(ws + L.keys), *keys2 = (uint32_t *)(ws + L.keys2);
-    uint32_t *idx = (uint32_t *)(ws + L.idx), *perm = (uint32_t *)(ws + L.perm);
-    float *q32u = (float *)(ws + L.q32u), *q32 = (float *)(ws + L.q32);
-    float *pd = (float *)(ws + L.pd);
-    uint32_t *pi = (uint32_t *)(ws + L.pi);
-    uint32_t *fail = (uint32_t *)(ws + L.fail);
-    const dim3 b256(256);
-    hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys, idx);
-    size_t cb = L.cub_bytes;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + L.cub, cb, keys, keys2, idx, perm, (int)nq, 0, 32, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
-    e = hipMemsetAsync(fail, 0, 4, st);
-    if (e != hipSuccess) return e;
-    bool walked = false;
-    if constexpr (SP != OMPL_GPU_SPACE_SO3) {  // SO3 has no group walk (cull_supported)
-        if (p.cull) {
-            timer_begin(st, "knn32_group_kernel");
-            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, kGroup>), dim3((nq + kGroup - 1) / kGroup), dim3(64),
-                               0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
-                               ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters);
-            timer_end(st);
-            walked = true;
-        }
-    }
-    if (p.cull && !walked) return hipErrorInvalidValue;
-    if (!walked) {
-        timer_begin(st, "knn32_screen_kernel");
-        hipLaunchKernelGGL((knn32_screen_kernel<SP, F, K2>), dim3((nq + kTile - 1) / kTile, p.chunks), dim3(kTile), 0,
-                           st, f32, cap, n_end, q32, nq, p.chunk_len, (float)sp.w0, (float)sp.w1, pd, pi);
-        timer_end(st);
-    }
-    hipLaunchKernelGGL((knn_certify_kernel<SP, F, K2, K>), dim3((nq + 255) / 256), b256, 0, st, pd, pi, p.chunks, nq,
-                       perm, f64, cap, qf64, sp, b.absmax, od, oi, k, fail, fail + 1);
-    return hipGetLastError();
-}
-
-template <int SP, int F, int K2>
-hipError_t run_fast_k(const DevSpace &sp, const FastPlan &p, const FastLayout &L, char *ws, const float *f32,
-                      const double *f64, uint64_t cap, uint64_t n_end, const SortedStore *ss, const double *qf64,
-                      uint32_t nq, uint32_t k, const FastBounds &b, double *od, uint32_t *oi, hipStream_t st) {
-    switch (p.K) {
-    case 1: return run_fast<SP, F, K2, 1>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
-    case 4: return run_fast<SP, F, K2, 4>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
-    case 16: return run_fast<SP, F, K2, 16>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
-    case 32:
-        if constexpr (K2 >= 32)
-            return run_fast<SP, F, K2, 32>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
-    }
-    return hipErrorInvalidValue;
-}
-
-template <int SP, int F>
-hipError_t run_fast_space(const DevSpace &sp, const FastPlan &p, const FastLayout &L, char *ws, const float *f32,
-                          const double *f64, uint64_t cap, uint64_t n_end, const SortedStore *ss, const double *qf64,
-                          uint32_t nq, uint32_t k, const FastBounds &b, double *od, uint32_t *oi, hipStream_t st) {
-    switch (p.K2) {
-    case 16: return run_fast_k<SP, F, 16>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
-    case 32: return run_fast_k<SP, F, 32>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
-    case 64: return run_fast_k<SP, F, 64>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
-    }
-    return hipErrorInvalidValue;
-}
-
-template <int SP, int F>
-hipError_t build_sorted(const float *f32, uint64_t cap, uint32_t n, const FastBounds &b, SortedStore *s,
-                        hipStream_t st) {
-    constexpr int R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
-    free_sorted_store(s);
-    s->n = n;
-    s->ntiles = std::max<uint32_t>(1, (n + kCullTile - 1) / kCullTile);
-    s->n_pad = s->ntiles * kCullTile;
-    s->nsuper = (s->ntiles + kSuperTiles - 1) / kSuperTiles;
-    uint32_t *keys = nullptr, *ids0 = nullptr, *keys_s = nullptr, *ids_s = nullptr;
-    void *tmp = nullptr;
-    size_t tb = 0;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, keys_s, ids0, ids_s, (int)n, 0, 32, st);
-    auto done = [&](hipError_t r) {
-        for (void *x : {(void *)keys, (void *)ids0, (void *)keys_s, (void *)ids_s, tmp})
-            if (x) (void)hipFree(x);
-        if (r != hipSuccess) free_sorted_store(s);
-        return r;
-    };
-    if (e != hipSuccess) return done(e);
-    if ((e = hipMalloc(&keys, 4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&ids0, 4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&keys_s, 4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&ids_s, 4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&tmp, std::max<size_t>(tb, 1))) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->rows, 4ull * R * s->n_pad)) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->ids, 4ull * s->n_pad)) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->tbox, 4ull * BW * s->ntiles)) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->sbox, 4ull * BW * s->nsuper)) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->tkey0, 4ull * s->ntiles)) != hipSuccess) return done(e);
-    s->bytes = 4ull * R * s->n_pad + 4ull * s->n_pad + 4ull * BW * (s->ntiles + s->nsuper) + 4ull * s->ntiles;
-    if (n) {
-        hipLaunchKernelGGL((tree_key_kernel<SP, F>), dim3((n + 255) / 256), dim3(256), 0, st, f32, cap, n, b, keys,
-                           ids0);
-        if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_s, ids0, ids_s, (int)n, 0, 32, st)) !=
-            hipSuccess)
-            return done(e);
-    }
-    hipLaunchKernelGGL((tree_gather_kernel<SP, F>), dim3((s->n_pad + 255) / 256), dim3(256), 0, st, f32, cap, ids_s,
-                       n, s->n_pad, s->rows, s->ids);
-    hipLaunchKernelGGL((tile_box_kernel<SP, F>), dim3((s->ntiles + 255) / 256), dim3(256), 0, st, s->rows, s->n_pad,
-                       s->ntiles, keys_s, n, s->tbox, s->tkey0);
-    hipLaunchKernelGGL((super_box_kernel<SP, F>), dim3((s->nsuper + 255) / 256), dim3(256), 0, st, s->tbox,
-                       s->ntiles, s->nsuper, s->sbox);
-    if ((e = hipGetLastError()) != hipSuccess) return done(e);
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);  // temporaries freed below
-    return done(hipSuccess);
-}
-
-}  // namespace
-
 // K2: the smallest list bucket >= max(k + 6, 16); the certify kernel's K bucket fits inside it.
 int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq) {
     if (sp.kind == OMPL_GPU_SPACE_KCHAIN || nq < kStreamMaxQ || k == 0) return 0;
@@ -957,11 +30,8 @@ void free_sorted_store(SortedStore *s) {
 hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, uint64_t cap, uint32_t n,
                               const FastBounds &b, SortedStore *s, hipStream_t st) {
     switch (sp.kind) {
-    case OMPL_GPU_SPACE_SE3: return build_sorted<OMPL_GPU_SPACE_SE3, 7>(feat32, cap, n, b, s, st);
-    case OMPL_GPU_SPACE_REALVECTOR:
-        if (g.F == 4) return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 4>(feat32, cap, n, b, s, st);
-        if (g.F == 8) return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 8>(feat32, cap, n, b, s, st);
-        return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 16>(feat32, cap, n, b, s, st);
+    case OMPL_GPU_SPACE_SE3: return fast_se3_build(g, feat32, cap, n, b, s, st);
+    case OMPL_GPU_SPACE_REALVECTOR: return fast_rv_build(g, feat32, cap, n, b, s, st);
     }
     return hipErrorInvalidValue;
 }
@@ -977,29 +47,16 @@ hipError_t launch_knn_fast(const DevSpace &sp, const FeatGeom &g, const double *
                            uint64_t cap, uint64_t n_end, const SortedStore *sorted, const double *qfeat64, uint32_t nq,
                            uint32_t k, const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes,
                            int num_cus, hipStream_t st, uint32_t **fail_count, uint32_t **fail_list) {
-    const FastPlan p = fast_plan(sp, nq, k, n_end, num_cus, sorted != nullptr);
-    if (p.K2 == 0) return hipErrorInvalidValue;
-    const FastLayout L = fast_layout(sp, g, p, nq);
-    if (L.total > ws_bytes) return hipErrorInvalidValue;
-    char *w = (char *)ws;
-    *fail_count = (uint32_t *)(w + L.fail);
-    *fail_list = *fail_count + 1;
     switch (sp.kind) {
     case OMPL_GPU_SPACE_SE3:
-        return run_fast_space<OMPL_GPU_SPACE_SE3, 7>(sp, p, L, w, feat32, feat64, cap, n_end, sorted, qfeat64, nq, k,
-                                                      b, out_d, out_i, st);
+        return fast_se3(sp, g, feat64, feat32, cap, n_end, sorted, qfeat64, nq, k, b, out_d, out_i, ws, ws_bytes,
+                        num_cus, st, fail_count, fail_list);
     case OMPL_GPU_SPACE_SO3:
-        return run_fast_space<OMPL_GPU_SPACE_SO3, 4>(sp, p, L, w, feat32, feat64, cap, n_end, nullptr, qfeat64, nq,
-                                                      k, b, out_d, out_i, st);
+        return fast_so3(sp, g, feat64, feat32, cap, n_end, nullptr, qfeat64, nq, k, b, out_d, out_i, ws, ws_bytes,
+                        num_cus, st, fail_count, fail_list);
     case OMPL_GPU_SPACE_REALVECTOR:
-        if (g.F == 4)
-            return run_fast_space<OMPL_GPU_SPACE_REALVECTOR, 4>(sp, p, L, w, feat32, feat64, cap, n_end, sorted,
-                                                                 qfeat64, nq, k, b, out_d, out_i, st);
-        if (g.F == 8)
-            return run_fast_space<OMPL_GPU_SPACE_REALVECTOR, 8>(sp, p, L, w, feat32, feat64, cap, n_end, sorted,
-                                                                 qfeat64, nq, k, b, out_d, out_i, st);
-        return run_fast_space<OMPL_GPU_SPACE_REALVECTOR, 16>(sp, p, L, w, feat32, feat64, cap, n_end, sorted,
-                                                              qfeat64, nq, k, b, out_d, out_i, st);
+        return fast_rv(sp, g, feat64, feat32, cap, n_end, sorted, qfeat64, nq, k, b, out_d, out_i, ws, ws_bytes,
+                       num_cus, st, fail_count, fail_list);
     }
     return hipErrorInvalidValue;
 }

@@ -1,0 +1,27 @@
+// knn_fast_rv.hip — R^n instantiations (4 / 8 / 16 padded coordinates) of the fp32 screen +
+// fp64 certificate (knn_fast_impl.h).
+#include "knn_fast_impl.h"
+
+namespace ompl_amd {
+
+hipError_t fast_rv(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32, uint64_t cap,
+                   uint64_t n_end, const SortedStore *sorted, const double *qfeat64, uint32_t nq, uint32_t k,
+                   const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes, int num_cus,
+                   hipStream_t st, uint32_t **fail_count, uint32_t **fail_list) {
+#define OMPL_AMD_RV(FF)                                                                                         \
+    return fast_entry<OMPL_GPU_SPACE_REALVECTOR, FF>(sp, g, feat64, feat32, cap, n_end, sorted, qfeat64, nq, k, b, \
+                                                     out_d, out_i, ws, ws_bytes, num_cus, st, fail_count, fail_list)
+    if (g.F == 4) OMPL_AMD_RV(4);
+    if (g.F == 8) OMPL_AMD_RV(8);
+    OMPL_AMD_RV(16);
+#undef OMPL_AMD_RV
+}
+
+hipError_t fast_rv_build(const FeatGeom &g, const float *feat32, uint64_t cap, uint32_t n, const FastBounds &b,
+                         SortedStore *s, hipStream_t st) {
+    if (g.F == 4) return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 4>(feat32, cap, n, b, s, st);
+    if (g.F == 8) return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 8>(feat32, cap, n, b, s, st);
+    return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 16>(feat32, cap, n, b, s, st);
+}
+
+}  // namespace ompl_amd

@@ -138,11 +138,12 @@ class NearestNeighborsGPU:
         abi.check(abi.lib.ompl_gpu_nn_stats(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
-    def cull_stats(self) -> tuple[int, int]:
-        """(64-state tiles the culled screen scanned, tiles a full scan would have scanned)."""
-        a, b = C.c_uint64(0), C.c_uint64(0)
-        abi.check(abi.lib.ompl_gpu_nn_cull_stats(self._h, C.byref(a), C.byref(b)))
-        return a.value, b.value
+    def cull_stats(self) -> tuple[int, int, int]:
+        """(64-state tiles the culled screen fetched, tiles a full scan would have fetched,
+        (tile, query) pairs scanned — 64 distance evaluations each)."""
+        a, b, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_nn_cull_stats(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
 
     def profile(self, enable: bool = True) -> None:
         abi.check(abi.lib.ompl_gpu_nn_profile(self._h, 1 if enable else 0))

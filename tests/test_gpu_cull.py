@@ -74,8 +74,9 @@ def test_se3_quaternion_signs_and_norms(gpu):
     nn = NearestNeighborsGPU(sp, gpu)
     nn.add(data)
     _check(nn, sp, data, np.arange(len(data)), q, 10)
-    scanned, total = nn.cull_stats()
+    scanned, total, qtiles = nn.cull_stats()
     assert 0 < scanned <= total
+    assert scanned <= qtiles <= 8 * scanned  # each fetched tile is scanned by 1..G queries
 
 
 def test_group_tail_and_small_batches(gpu):

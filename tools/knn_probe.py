@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--modes", default="0,2,1")
+    ap.add_argument("--only", default=None, help="run only this workload")
     args = ap.parse_args()
     import torch
 
@@ -42,6 +43,8 @@ def main():
         if sp is None:
             sp, data, q = prev
         prev = (sp, data, q)
+        if args.only and name != args.only:
+            continue
         nn = NearestNeighborsGPU(sp, 0)
         nn.add(data)
         dq = torch.from_numpy(q).to(dev)
@@ -71,9 +74,10 @@ def main():
             s1 = nn.stats()
             nn.profile(False)
             scanned = (c1[0] - c0[0]) / max(c1[1] - c0[1], 1)
+            pair_frac = (c1[2] - c0[2]) * 64 / reps / (len(q) * len(data))
             print(json.dumps({"workload": name, "mode": mode, "kernel": kname,
                               "kernel_ms": (ms1 - ms0) / max(n1 - n0, 1), "call_ms": wall * 1e3,
-                              "queries_per_s": len(q) / wall, "tiles_scanned_frac": scanned,
+                              "queries_per_s": len(q) / wall, "tiles_scanned_frac": scanned, "pairs_scanned_frac": pair_frac,
                               "exact_reruns": s1[1] - s0[1]}), flush=True)
         del nn
 
