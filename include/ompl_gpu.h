@@ -28,6 +28,9 @@
  *   ompl_gpu_svc_check     StateValidityChecker::isValid         src/ompl/base/StateValidityChecker.h:111
  *   ompl_gpu_steer_device  the RRT extend step (nearest -> interpolate to range)
  *                          src/ompl/geometric/planners/rrt/src/RRT.cpp:137-146
+ *   ompl_gpu_rrt_grow_device  the RRT loop itself                 RRT.cpp:128-192
+ *   ompl_gpu_nn_edges_device  the edges PRM / BIT* check after a neighbour query
+ *                          prm/src/PRM.cpp:577-582, informedtrees/src/BITstar.cpp:815
  *
  * Distances are the reference's fp64 formulas in the reference's operation
  * order (StateSpace.cpp:1068-1076, RealVectorStateSpace.cpp:230-242,
@@ -177,6 +180,28 @@ ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, 
 ompl_gpu_status ompl_gpu_nn_profile(ompl_gpu_nn *h, int enable);
 ompl_gpu_status ompl_gpu_nn_kernel_time(ompl_gpu_nn *h, double *total_ms, uint64_t *launches,
                                         const char **kernel_name);
+/* Device-resident nearestR: d_queries AoS fp64 (device).  The CSR result goes to
+ * caller-owned device buffers: d_offsets (nq+1 entries, uint64), d_ids (uint32) / d_dist
+ * (fp64) of `capacity` entries, sorted by (distance, id) inside each query's segment
+ * (NearestNeighborsGNAT.h:236-245, NearestNeighborsLinear.h:135-142).  *total receives the
+ * number of results; when it exceeds capacity only d_offsets is written and the call
+ * returns OMPL_GPU_ERR_INVALID_ARG (call again with *total entries).  Synchronous. */
+ompl_gpu_status ompl_gpu_nn_radius_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, double r,
+                                          uint64_t *d_offsets, uint32_t *d_ids, double *d_dist, uint64_t capacity,
+                                          uint64_t *total);
+/* Radius walk: 64-state tiles fetched and (tile, query) pairs scanned (64 distance
+ * evaluations each), summed over nearestR calls.  Either output may be NULL. */
+ompl_gpu_status ompl_gpu_nn_radius_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *query_tiles);
+/* Motion endpoints of a batch of neighbour results — the edges the planners check after a
+ * neighbour query: PRM checkMotion(state[n], state[m]) (PRM.cpp:577-582, from_query = 0),
+ * BIT* checkMotion(vertex, sample) (BITstar.cpp:815, from_query = 1).  Edge e pairs query q
+ * (d_queries, AoS) with stored state d_ids[e]: e in [d_offsets[q], d_offsets[q+1]) for a CSR
+ * result (nn_radius_device), or, with d_offsets NULL, e = q * stride + j for a dense
+ * nq x stride id matrix (nn_knn_device; m == nq * stride).  A missing id (0xFFFFFFFF)
+ * pairs q with itself.  Writes m AoS rows to d_from / d_to; asynchronous. */
+ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, const uint64_t *d_offsets,
+                                         const uint32_t *d_ids, uint32_t stride, size_t m, int from_query,
+                                         double *d_from, double *d_to);
 /* RRT extend on device: for each query q with nearest id nid[q*stride]:
  * from = state[nid]; to = q; if d(from,q) > max_distance, to = interpolate(from,
  * q, max_distance/d).  Writes AoS from/to rows (RRT.cpp:137-146). */
@@ -205,6 +230,19 @@ ompl_gpu_status ompl_gpu_mv_reset_counters(ompl_gpu_mv *h);
 ompl_gpu_status ompl_gpu_mv_state_checks(ompl_gpu_mv *h, uint64_t *checks);
 /* isValid per state (host AoS). */
 ompl_gpu_status ompl_gpu_svc_check(ompl_gpu_mv *h, const double *states, size_t m, uint8_t *valid);
+
+/* ---- RRT growth on device ----------------------------------------------------
+ * The RRT loop (RRT.cpp:128-192) without its goal test, for ns samples in order: nearest
+ * stored state (:137), steer to max_distance (:141-146), mv's checkMotion(nearest,
+ * steered) (:148) and, when valid, append the steered state to the NN store (:170-173).
+ * Sample i sees every state samples < i appended, as in the sequential loop.
+ * d_nearest[i] = id of sample i's nearest state, d_added[i] = id of the appended state or
+ * 0xFFFFFFFF.  d_samples are ns AoS rows (device).  Both handles must describe the same
+ * space (R^n, SO3 or SE3) on the same device; mv's valid / invalid counters are updated.
+ * All iterations are queued on the NN handle's stream with no host round trip;
+ * synchronous on return. */
+ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
+                                         double max_distance, uint32_t *d_nearest, uint32_t *d_added);
 
 #ifdef __cplusplus
 }

@@ -87,6 +87,10 @@ SIGNATURES = {
     "ompl_gpu_nn_cull_stats": (C.c_int, [_P, _U64, _U64, _U64]),
     "ompl_gpu_nn_kernel_time": (C.c_int, [_P, _D, _U64, C.POINTER(C.c_char_p)]),
     "ompl_gpu_steer_device": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_uint32, C.c_double, _P, _P]),
+    "ompl_gpu_nn_radius_device": (C.c_int, [_P, _P, C.c_size_t, C.c_double, _P, _P, _P, C.c_uint64, _U64]),
+    "ompl_gpu_nn_radius_cull_stats": (C.c_int, [_P, _U64, _U64]),
+    "ompl_gpu_nn_edges_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P, C.c_uint32, C.c_size_t, C.c_int, _P, _P]),
+    "ompl_gpu_rrt_grow_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, _P, _P]),
     "ompl_gpu_mv_create": (C.c_int, [C.POINTER(_P), C.POINTER(SpaceStruct), C.POINTER(CheckerStruct), C.c_int]),
     "ompl_gpu_mv_destroy": (C.c_int, [_P]),
     "ompl_gpu_mv_set_stream": (C.c_int, [_P, _P]),

@@ -98,7 +98,9 @@ struct ompl_gpu_nn {
     uint64_t cap = 0, n_total = 0, n_live = 0;
     std::vector<uint8_t> removed;
     std::mutex mu;
-    DevBuf q, out_d, out_i, ws, stage, counts, offsets, ids, dists, sorted_ids, sorted_d, tmp, fb_q, fb_d, fb_i;
+    DevBuf q, out_d, out_i, ws, ws2, stage, counts, offsets, qoff, ids, dists, sorted_ids, sorted_d, tmp, fb_q, fb_d,
+        fb_i;
+    DevBuf rrt_n, rrt_pd, rrt_pi;  // device RRT growth: live size, per-block partial minima
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
     double lo[kKeyDims] = {0}, hi[kKeyDims] = {0}, absmax = 0.0;
@@ -107,8 +109,8 @@ struct ompl_gpu_nn {
     FastBounds sorted_bounds{};
     bool sorted_dirty = true;
     bool cull = true;         // ompl_gpu_nn_set_exact(h, 2) disables the culled screen
-    DevBuf cull_counter;      // [tiles fetched by the group walk, tiles of a brute-force walk,
-                              //  (tile, query) pairs scanned] (device)
+    DevBuf cull_counter;      // SortedStore::counters: kNN walk [tiles fetched, tiles of a brute-force
+                              // walk, (tile, query) pairs scanned], radius walk [tiles, pairs] (device)
     bool fast = true;        // OMPL_GPU_EXACT_ONLY=1 forces the exact fp64 scan
     uint64_t fast_queries = 0, fast_fallbacks = 0;
     // profiling of the dominant scan kernel (HIP events on the launch stream)
@@ -403,6 +405,23 @@ ompl_gpu_status ompl_gpu_nn_get_states(ompl_gpu_nn *h, uint64_t first, size_t n,
 
 static uint64_t n_end_of(const ompl_gpu_nn *h) { return (h->n_total + kTile - 1) / kTile * kTile; }
 
+constexpr int kCullCounters = 5;
+
+// (re)build the Morton-sorted fp32 copy the culled walks read, if adds or removes made it stale
+static ompl_gpu_status ensure_sorted(ompl_gpu_nn *h) {
+    if (!h->sorted_dirty && h->sorted.n == h->n_total) return OMPL_GPU_OK;
+    h->sorted_bounds = current_bounds(h);
+    HIP_OR_FAIL(build_sorted_store(h->sp, h->g, h->feat32, h->cap, (uint32_t)h->n_total, h->sorted_bounds, &h->sorted,
+                                   h->stream));
+    h->sorted_dirty = false;
+    if (!h->cull_counter.p) {
+        HIP_OR_FAIL(h->cull_counter.ensure(kCullCounters * sizeof(unsigned long long)));
+        HIP_OR_FAIL(hipMemsetAsync(h->cull_counter.p, 0, kCullCounters * sizeof(unsigned long long), h->stream));
+    }
+    h->sorted.counters = (unsigned long long *)h->cull_counter.p;
+    return OMPL_GPU_OK;
+}
+
 // knn on device-resident features (queries already converted); caller holds the lock
 static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, size_t nq, uint32_t k, uint32_t *d_ids,
                                            double *d_dist) {
@@ -440,16 +459,9 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
     if (h->fast && fast_k2(h->sp, k, (uint32_t)nq) > 0) {
         // fp32 screen + fp64 certificate (knn_fast.hip); uncertified queries re-run exactly
         const bool cull = h->cull && cull_supported(h->sp);
-        if (cull && (h->sorted_dirty || h->sorted.n != h->n_total)) {
-            h->sorted_bounds = current_bounds(h);
-            HIP_OR_FAIL(build_sorted_store(h->sp, h->g, h->feat32, h->cap, (uint32_t)h->n_total, h->sorted_bounds,
-                                           &h->sorted, h->stream));
-            h->sorted_dirty = false;
-            if (!h->cull_counter.p) {
-                HIP_OR_FAIL(h->cull_counter.ensure(3 * sizeof(unsigned long long)));
-                HIP_OR_FAIL(hipMemsetAsync(h->cull_counter.p, 0, 3 * sizeof(unsigned long long), h->stream));
-            }
-            h->sorted.counters = (unsigned long long *)h->cull_counter.p;
+        if (cull) {
+            ompl_gpu_status s = ensure_sorted(h);
+            if (s != OMPL_GPU_OK) return s;
         }
         FastBounds b = cull ? h->sorted_bounds : current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
@@ -471,13 +483,12 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
         HIP_OR_FAIL(h->fb_d.ensure(sizeof(double) * nfail * k));
         HIP_OR_FAIL(h->fb_i.ensure(sizeof(uint32_t) * nfail * k));
         HIP_OR_FAIL(launch_gather_rows(d_qf, F, d_fail_list, nfail, (double *)h->fb_q.p, h->stream));
-        DevBuf ws2;
-        HIP_OR_FAIL(ws2.ensure(knn_workspace_bytes(h->sp, h->g, nfail, k, n_end, h->num_cus)));
+        HIP_OR_FAIL(h->ws2.ensure(knn_workspace_bytes(h->sp, h->g, nfail, k, n_end, h->num_cus)));
         HIP_OR_FAIL(launch_knn(h->sp, h->g, h->feat, h->cap, n_end, (const double *)h->fb_q.p, nfail, k,
-                               (double *)h->fb_d.p, (uint32_t *)h->fb_i.p, ws2.p, ws2.bytes, h->num_cus, h->stream));
+                               (double *)h->fb_d.p, (uint32_t *)h->fb_i.p, h->ws2.p, h->ws2.bytes, h->num_cus,
+                               h->stream));
         HIP_OR_FAIL(launch_scatter_results((const double *)h->fb_d.p, (const uint32_t *)h->fb_i.p, k, d_fail_list,
                                            nfail, d_dist, d_ids, h->stream));
-        HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // ws2 is released on return
         return OMPL_GPU_OK;
     }
     const size_t wsb = knn_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus);
@@ -542,6 +553,129 @@ ompl_gpu_status ompl_gpu_nn_nearest(ompl_gpu_nn *h, const double *queries, size_
     return ompl_gpu_nn_knn(h, queries, nq, 1, out_ids, out_dist, nullptr);
 }
 
+// nearestR on device-resident query features (caller holds the lock).  Leaves the CSR
+// result on device: the per-query offsets (nq + 1 entries) in h->qoff and, inside every
+// segment, the (id, distance) pairs sorted by (distance, id) in *res_i / *res_d;
+// *total = number of entries.
+static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf, size_t nq, double r,
+                                              uint64_t *total, const uint32_t **res_i, const double **res_d) {
+    *total = 0;
+    *res_i = nullptr;
+    *res_d = nullptr;
+    HIP_OR_FAIL(h->qoff.ensure(sizeof(uint64_t) * (nq + 1)));
+    uint64_t *d_qoff = (uint64_t *)h->qoff.p;
+    const uint64_t n_end = n_end_of(h);
+    if (n_end == 0 || !(r >= 0.0)) {  // empty structure, or a radius no distance satisfies
+        HIP_OR_FAIL(hipMemsetAsync(d_qoff, 0, sizeof(uint64_t) * (nq + 1), h->stream));
+        return OMPL_GPU_OK;
+    }
+    if (h->fast && h->cull && cull_supported(h->sp) && nq <= 0x7FFFFFFFull) {
+        // culled walk over the Morton-sorted copy (knn_fast_impl.h)
+        ompl_gpu_status s = ensure_sorted(h);
+        if (s != OMPL_GPU_OK) return s;
+        FastBounds b = h->sorted_bounds;
+        b.absmax = (float)h->absmax * (1.0f + 1e-6f);
+        HIP_OR_FAIL(h->ws.ensure(radius_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq)));
+        uint64_t *d_off = nullptr;
+        HIP_OR_FAIL(launch_radius_fast(h->sp, h->g, h->feat, h->cap, &h->sorted, d_qf, (uint32_t)nq, r, b, h->ws.p,
+                                       h->ws.bytes, 0, &d_off, nullptr, nullptr, h->stream));
+        uint64_t tm[2] = {0, 0};  // total, longest segment
+        HIP_OR_FAIL(hipMemcpyAsync(tm, d_off + nq, sizeof(tm), hipMemcpyDeviceToHost, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(d_qoff, d_off, sizeof(uint64_t) * (nq + 1), hipMemcpyDeviceToDevice, h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+        *total = tm[0];
+        if (tm[0] == 0) return OMPL_GPU_OK;
+        if (tm[0] > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "radius result above 2^31 entries");
+        const uint64_t tot = tm[0];
+        HIP_OR_FAIL(h->ids.ensure(sizeof(uint32_t) * tot));
+        HIP_OR_FAIL(h->dists.ensure(sizeof(double) * tot));
+        HIP_OR_FAIL(h->sorted_ids.ensure(sizeof(uint32_t) * tot));
+        HIP_OR_FAIL(h->sorted_d.ensure(sizeof(double) * tot));
+        uint32_t *ui = (uint32_t *)h->ids.p, *si = (uint32_t *)h->sorted_ids.p;
+        double *ud = (double *)h->dists.p, *sd = (double *)h->sorted_d.p;
+        {
+            ProfileScope prof(h);
+            HIP_OR_FAIL(launch_radius_fast(h->sp, h->g, h->feat, h->cap, &h->sorted, d_qf, (uint32_t)nq, r, b, h->ws.p,
+                                           h->ws.bytes, 1, &d_off, ui, ud, h->stream));
+        }
+        if (tm[1] <= kRankSortMax) {
+            HIP_OR_FAIL(launch_segment_rank_sort(d_qoff, ui, ud, (uint32_t)nq, si, sd, h->stream));
+            *res_i = si;
+            *res_d = sd;
+            return OMPL_GPU_OK;
+        }
+        // long segments: two stable radix passes, by id and then by distance
+        size_t tb1 = 0, tb2 = 0;
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb1, (const uint32_t *)ui, si,
+                                                                (const double *)ud, sd, (int)tot, (int)nq, d_qoff,
+                                                                d_qoff + 1, 0, 32, h->stream));
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb2, (const double *)sd, ud,
+                                                                (const uint32_t *)si, ui, (int)tot, (int)nq, d_qoff,
+                                                                d_qoff + 1, 0, 64, h->stream));
+        HIP_OR_FAIL(h->tmp.ensure(std::max(tb1, tb2)));
+        tb1 = tb2 = h->tmp.bytes;
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb1, (const uint32_t *)ui, si,
+                                                                (const double *)ud, sd, (int)tot, (int)nq, d_qoff,
+                                                                d_qoff + 1, 0, 32, h->stream));
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb2, (const double *)sd, ud,
+                                                                (const uint32_t *)si, ui, (int)tot, (int)nq, d_qoff,
+                                                                d_qoff + 1, 0, 64, h->stream));
+        *res_i = ui;
+        *res_d = ud;
+        return OMPL_GPU_OK;
+    }
+    // exact fp64 scan (OMPL_GPU_EXACT_ONLY / set_exact, SO3, KCHAIN): hits per (query, chunk)
+    // written in id order, then a stable sort by distance gives (distance, id) order
+    const RadiusPlan p = radius_plan((uint32_t)nq, n_end, h->num_cus);
+    const size_t nc = nq * p.chunks;
+    HIP_OR_FAIL(h->counts.ensure(sizeof(uint32_t) * nc));
+    HIP_OR_FAIL(launch_radius_count(h->sp, h->g, p, h->feat, h->cap, n_end, d_qf, (uint32_t)nq, r,
+                                    (uint32_t *)h->counts.p, h->stream));
+    std::vector<uint32_t> cnt(nc);
+    HIP_OR_FAIL(hipMemcpyAsync(cnt.data(), h->counts.p, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    std::vector<uint64_t> off(nc), qoff(nq + 1);
+    uint64_t tot = 0;
+    for (size_t q = 0; q < nq; ++q) {
+        qoff[q] = tot;
+        for (uint32_t c = 0; c < p.chunks; ++c) {
+            off[q * p.chunks + c] = tot;
+            tot += cnt[q * p.chunks + c];
+        }
+    }
+    qoff[nq] = tot;
+    *total = tot;
+    HIP_OR_FAIL(hipMemcpyAsync(d_qoff, qoff.data(), sizeof(uint64_t) * (nq + 1), hipMemcpyHostToDevice, h->stream));
+    if (tot > 0x7FFFFFFFull) {
+        (void)hipStreamSynchronize(h->stream);
+        return fail(OMPL_GPU_ERR_UNSUPPORTED, "radius result above 2^31 entries");
+    }
+    if (tot > 0) {
+        HIP_OR_FAIL(h->offsets.ensure(sizeof(uint64_t) * nc));
+        HIP_OR_FAIL(hipMemcpyAsync(h->offsets.p, off.data(), sizeof(uint64_t) * nc, hipMemcpyHostToDevice, h->stream));
+        HIP_OR_FAIL(h->ids.ensure(sizeof(uint32_t) * tot));
+        HIP_OR_FAIL(h->dists.ensure(sizeof(double) * tot));
+        HIP_OR_FAIL(h->sorted_ids.ensure(sizeof(uint32_t) * tot));
+        HIP_OR_FAIL(h->sorted_d.ensure(sizeof(double) * tot));
+        HIP_OR_FAIL(launch_radius_fill(h->sp, h->g, p, h->feat, h->cap, n_end, d_qf, (uint32_t)nq, r,
+                                       (const uint64_t *)h->offsets.p, (uint32_t *)h->ids.p, (double *)h->dists.p,
+                                       h->stream));
+        size_t tb = 0;
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            nullptr, tb, (const double *)h->dists.p, (double *)h->sorted_d.p, (const uint32_t *)h->ids.p,
+            (uint32_t *)h->sorted_ids.p, (int)tot, (int)nq, d_qoff, d_qoff + 1, 0, 64, h->stream));
+        HIP_OR_FAIL(h->tmp.ensure(tb));
+        tb = h->tmp.bytes;
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            h->tmp.p, tb, (const double *)h->dists.p, (double *)h->sorted_d.p, (const uint32_t *)h->ids.p,
+            (uint32_t *)h->sorted_ids.p, (int)tot, (int)nq, d_qoff, d_qoff + 1, 0, 64, h->stream));
+        *res_i = (const uint32_t *)h->sorted_ids.p;
+        *res_d = (const double *)h->sorted_d.p;
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // the host offset vectors are released on return
+    return OMPL_GPU_OK;
+}
+
 ompl_gpu_status ompl_gpu_nn_radius(ompl_gpu_nn *h, const double *queries, size_t nq, double r, uint64_t **ids_out,
                                    double **dists_out, uint64_t *offsets_out) {
     if (!h || !ids_out || !offsets_out || (nq && !queries)) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
@@ -549,86 +683,109 @@ ompl_gpu_status ompl_gpu_nn_radius(ompl_gpu_nn *h, const double *queries, size_t
     *ids_out = nullptr;
     if (dists_out) *dists_out = nullptr;
     offsets_out[0] = 0;
-    const uint64_t n_end = n_end_of(h);
     if (nq == 0) return OMPL_GPU_OK;
-    if (n_end == 0 || !(r >= 0.0)) {  // empty structure, or a radius no distance satisfies
-        for (size_t q = 0; q <= nq; ++q) offsets_out[q] = 0;
-        *ids_out = (uint64_t *)std::malloc(sizeof(uint64_t));
-        if (dists_out) *dists_out = (double *)std::malloc(sizeof(double));
-        return OMPL_GPU_OK;
-    }
     HIP_OR_FAIL(hipSetDevice(h->device));
     ompl_gpu_status s = upload_query_features(h, queries, nq);
     if (s != OMPL_GPU_OK) return s;
-    const RadiusPlan p = radius_plan((uint32_t)nq, n_end, h->num_cus);
-    const size_t nc = nq * p.chunks;
-    HIP_OR_FAIL(h->counts.ensure(sizeof(uint32_t) * nc));
-    HIP_OR_FAIL(launch_radius_count(h->sp, h->g, p, h->feat, h->cap, n_end, (const double *)h->q.p, (uint32_t)nq, r,
-                                    (uint32_t *)h->counts.p, h->stream));
-    std::vector<uint32_t> cnt(nc);
-    HIP_OR_FAIL(hipMemcpyAsync(cnt.data(), h->counts.p, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, h->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
-    std::vector<uint64_t> off(nc);
     uint64_t tot = 0;
-    for (size_t q = 0; q < nq; ++q) {
-        offsets_out[q] = tot;
-        for (uint32_t c = 0; c < p.chunks; ++c) {
-            off[q * p.chunks + c] = tot;
-            tot += cnt[q * p.chunks + c];
-        }
-    }
-    offsets_out[nq] = tot;
+    const uint32_t *ri = nullptr;
+    const double *rd = nullptr;
+    s = radius_features_locked(h, (const double *)h->q.p, nq, r, &tot, &ri, &rd);
+    if (s != OMPL_GPU_OK) return s;
     uint64_t *hid = (uint64_t *)std::malloc(sizeof(uint64_t) * std::max<uint64_t>(tot, 1));
     double *hd = (double *)std::malloc(sizeof(double) * std::max<uint64_t>(tot, 1));
-    if (!hid || !hd) {
+    std::vector<uint32_t> i32(tot);
+    hipError_t e = hid && hd ? hipSuccess : hipErrorOutOfMemory;
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(offsets_out, h->qoff.p, sizeof(uint64_t) * (nq + 1), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && tot) e = hipMemcpyAsync(i32.data(), ri, sizeof(uint32_t) * tot, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && tot) e = hipMemcpyAsync(hd, rd, sizeof(double) * tot, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
         std::free(hid);
         std::free(hd);
-        return fail(OMPL_GPU_ERR_OOM, "host allocation failed");
+        return fail(e == hipErrorOutOfMemory ? OMPL_GPU_ERR_OOM : OMPL_GPU_ERR_DEVICE,
+                    std::string("nearestR copy-back: ") + hipGetErrorString(e));
     }
-    auto cleanup_fail = [&](ompl_gpu_status st) {
-        std::free(hid);
-        std::free(hd);
-        return st;
-    };
-    if (tot > 0) {
-        if (tot > 0x7FFFFFFFull) return cleanup_fail(fail(OMPL_GPU_ERR_UNSUPPORTED, "radius result above 2^31 entries"));
-        hipError_t e;
-#define TRY(expr)                                                                                  \
-    if ((e = (expr)) != hipSuccess)                                                                \
-        return cleanup_fail(fail(e == hipErrorOutOfMemory ? OMPL_GPU_ERR_OOM : OMPL_GPU_ERR_DEVICE, \
-                                 std::string(#expr) + ": " + hipGetErrorString(e)));
-        TRY(h->offsets.ensure(sizeof(uint64_t) * (nc + nq + 1)));
-        uint64_t *d_off = (uint64_t *)h->offsets.p;
-        uint64_t *d_qoff = d_off + nc;
-        TRY(hipMemcpyAsync(d_off, off.data(), sizeof(uint64_t) * nc, hipMemcpyHostToDevice, h->stream));
-        TRY(hipMemcpyAsync(d_qoff, offsets_out, sizeof(uint64_t) * (nq + 1), hipMemcpyHostToDevice, h->stream));
-        TRY(h->ids.ensure(sizeof(uint32_t) * tot));
-        TRY(h->dists.ensure(sizeof(double) * tot));
-        TRY(h->sorted_ids.ensure(sizeof(uint32_t) * tot));
-        TRY(h->sorted_d.ensure(sizeof(double) * tot));
-        TRY(launch_radius_fill(h->sp, h->g, p, h->feat, h->cap, n_end, (const double *)h->q.p, (uint32_t)nq, r, d_off,
-                               (uint32_t *)h->ids.p, (double *)h->dists.p, h->stream));
-        // stable sort by distance inside each query segment; ids were written ascending
-        size_t tb = 0;
-        TRY(hipcub::DeviceSegmentedRadixSort::SortPairs(
-            nullptr, tb, (const double *)h->dists.p, (double *)h->sorted_d.p, (const uint32_t *)h->ids.p,
-            (uint32_t *)h->sorted_ids.p, (int)tot, (int)nq, d_qoff, d_qoff + 1, 0, 64, h->stream));
-        TRY(h->tmp.ensure(tb));
-        TRY(hipcub::DeviceSegmentedRadixSort::SortPairs(
-            h->tmp.p, tb, (const double *)h->dists.p, (double *)h->sorted_d.p, (const uint32_t *)h->ids.p,
-            (uint32_t *)h->sorted_ids.p, (int)tot, (int)nq, d_qoff, d_qoff + 1, 0, 64, h->stream));
-        std::vector<uint32_t> i32(tot);
-        TRY(hipMemcpyAsync(i32.data(), h->sorted_ids.p, sizeof(uint32_t) * tot, hipMemcpyDeviceToHost, h->stream));
-        TRY(hipMemcpyAsync(hd, h->sorted_d.p, sizeof(double) * tot, hipMemcpyDeviceToHost, h->stream));
-        TRY(hipStreamSynchronize(h->stream));
-#undef TRY
-        for (uint64_t j = 0; j < tot; ++j) hid[j] = i32[j];
-    }
+    for (uint64_t j = 0; j < tot; ++j) hid[j] = i32[j];
     *ids_out = hid;
     if (dists_out)
         *dists_out = hd;
     else
         std::free(hd);
+    return OMPL_GPU_OK;
+}
+
+// device features of AoS raw queries (the NN's own buffer when they differ from the reals)
+static ompl_gpu_status device_query_features(ompl_gpu_nn *h, const double *d_queries, size_t nq, const double **qf) {
+    *qf = d_queries;
+    const bool raw_is_feat = h->sp.kind == OMPL_GPU_SPACE_SE3 || h->sp.kind == OMPL_GPU_SPACE_SO3 ||
+                             (h->sp.kind == OMPL_GPU_SPACE_REALVECTOR && h->g.F == h->sp.dim);
+    if (raw_is_feat) return OMPL_GPU_OK;
+    HIP_OR_FAIL(h->q.ensure(sizeof(double) * nq * h->g.F));
+    HIP_OR_FAIL(launch_features(h->sp, h->g, d_queries, (uint32_t)nq, (double *)h->q.p, h->stream));
+    *qf = (const double *)h->q.p;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_radius_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, double r,
+                                          uint64_t *d_offsets, uint32_t *d_ids, double *d_dist, uint64_t capacity,
+                                          uint64_t *total) {
+    if (!h || !total || (nq && (!d_queries || !d_offsets))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    *total = 0;
+    if (nq == 0) return OMPL_GPU_OK;
+    if (nq > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many queries in one call");
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    const double *qf = nullptr;
+    ompl_gpu_status s = device_query_features(h, d_queries, nq, &qf);
+    if (s != OMPL_GPU_OK) return s;
+    uint64_t tot = 0;
+    const uint32_t *ri = nullptr;
+    const double *rd = nullptr;
+    s = radius_features_locked(h, qf, nq, r, &tot, &ri, &rd);
+    if (s != OMPL_GPU_OK) return s;
+    *total = tot;
+    HIP_OR_FAIL(hipMemcpyAsync(d_offsets, h->qoff.p, sizeof(uint64_t) * (nq + 1), hipMemcpyDeviceToDevice, h->stream));
+    if (tot > capacity) {
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "radius result exceeds the output capacity (see *total)");
+    }
+    if (tot) {
+        if (!d_ids || !d_dist) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL output buffer");
+        HIP_OR_FAIL(hipMemcpyAsync(d_ids, ri, sizeof(uint32_t) * tot, hipMemcpyDeviceToDevice, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(d_dist, rd, sizeof(double) * tot, hipMemcpyDeviceToDevice, h->stream));
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, const uint64_t *d_offsets,
+                                         const uint32_t *d_ids, uint32_t stride, size_t m, int from_query,
+                                         double *d_from, double *d_to) {
+    if (!h || (m && (!d_queries || !d_ids || !d_from || !d_to))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (!d_offsets && m && (stride == 0 || m != nq * (size_t)stride))
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "dense neighbour ids need m == nq * stride");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (m == 0) return OMPL_GPU_OK;
+    if (nq == 0 || nq > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_INVALID_ARG, "query count out of range");
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(launch_edges(h->sp, h->raw, h->cap, d_queries, (uint32_t)nq, d_offsets, d_ids, stride, m, from_query,
+                             d_from, d_to, h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_radius_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *query_tiles) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    unsigned long long c[kCullCounters] = {0, 0, 0, 0, 0};
+    if (h->cull_counter.p) {
+        HIP_OR_FAIL(hipSetDevice(h->device));
+        HIP_OR_FAIL(hipMemcpyAsync(c, h->cull_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    }
+    if (tiles_scanned) *tiles_scanned = c[3];
+    if (query_tiles) *query_tiles = c[4];
     return OMPL_GPU_OK;
 }
 
@@ -638,14 +795,9 @@ ompl_gpu_status ompl_gpu_nn_knn_device(ompl_gpu_nn *h, const double *d_queries, 
     std::lock_guard<std::mutex> lk(h->mu);
     if (nq == 0 || k == 0) return OMPL_GPU_OK;
     HIP_OR_FAIL(hipSetDevice(h->device));
-    const double *qf = d_queries;
-    const bool raw_is_feat = h->sp.kind == OMPL_GPU_SPACE_SE3 || h->sp.kind == OMPL_GPU_SPACE_SO3 ||
-                             (h->sp.kind == OMPL_GPU_SPACE_REALVECTOR && h->g.F == h->sp.dim);
-    if (!raw_is_feat) {
-        HIP_OR_FAIL(h->q.ensure(sizeof(double) * nq * h->g.F));
-        HIP_OR_FAIL(launch_features(h->sp, h->g, d_queries, (uint32_t)nq, (double *)h->q.p, h->stream));
-        qf = (const double *)h->q.p;
-    }
+    const double *qf = nullptr;
+    ompl_gpu_status s = device_query_features(h, d_queries, nq, &qf);
+    if (s != OMPL_GPU_OK) return s;
     return knn_features_locked(h, qf, nq, k, d_ids, d_dist);
 }
 
@@ -691,7 +843,7 @@ ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, 
                                        uint64_t *query_tiles) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
-    unsigned long long c[3] = {0, 0, 0};
+    unsigned long long c[kCullCounters] = {0, 0, 0, 0, 0};
     if (h->cull_counter.p) {
         HIP_OR_FAIL(hipSetDevice(h->device));
         HIP_OR_FAIL(hipMemcpyAsync(c, h->cull_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
@@ -885,6 +1037,60 @@ ompl_gpu_status ompl_gpu_svc_check(ompl_gpu_mv *h, const double *states, size_t 
     HIP_OR_FAIL(launch_state_valid(h->sp, h->ck, (const double *)h->s1.p, (uint32_t)m, (uint8_t *)h->valid.p, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(valid, h->valid.p, m, hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
+// ------------------------------------------------------------------------------ RRT
+
+ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
+                                         double max_distance, uint32_t *d_nearest, uint32_t *d_added) {
+    if (!h || !mv || (ns && (!d_samples || !d_nearest || !d_added))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (h->device != mv->device) return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles are on different devices");
+    if (h->sp.kind != mv->sp.kind || h->sp.dim != mv->sp.dim)
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles describe different state spaces");
+    if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN)
+        return fail(OMPL_GPU_ERR_UNSUPPORTED, "device RRT growth needs a space whose stored features are its reals");
+    if (!(max_distance > 0.0)) return fail(OMPL_GPU_ERR_INVALID_ARG, "max_distance must be positive");
+    std::scoped_lock lk(h->mu, mv->mu);
+    if (ns == 0) return OMPL_GPU_OK;
+    if (ns > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many samples in one call");
+    if (h->n_live == 0) return fail(OMPL_GPU_ERR_EMPTY, "No elements found in nearest neighbors data structure");
+    if (h->n_total + ns > 0xFFFFFFF0ull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "more than 2^32-16 states");
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    ompl_gpu_status s = grow(h, h->n_total + ns);
+    if (s != OMPL_GPU_OK) return s;
+    // screening bounds: an appended state lies on a segment from a stored state towards a
+    // sample, so the box / largest coordinate over stored states and samples still bound it
+    const int dim = h->sp.dim;
+    std::vector<double> hs((size_t)ns * dim);
+    HIP_OR_FAIL(hipMemcpyAsync(hs.data(), d_samples, sizeof(double) * hs.size(), hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(h->rrt_n.ensure(sizeof(uint64_t)));
+    const size_t parts = rrt_part_entries(h->n_total + ns);
+    HIP_OR_FAIL(h->rrt_pd.ensure(sizeof(double) * parts));
+    HIP_OR_FAIL(h->rrt_pi.ensure(sizeof(uint32_t) * parts));
+    const uint64_t n0 = h->n_total;
+    HIP_OR_FAIL(hipMemcpyAsync(h->rrt_n.p, &n0, sizeof(uint64_t), hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    const int nb = tracked_dims(h->sp);
+    const int na = h->sp.kind == OMPL_GPU_SPACE_SE3 ? 3 : (h->sp.kind == OMPL_GPU_SPACE_SO3 ? 0 : dim);
+    for (size_t i = 0; i < ns; ++i) {
+        const double *x = hs.data() + i * dim;
+        for (int c = 0; c < nb; ++c) {
+            h->lo[c] = std::min(h->lo[c], x[c]);
+            h->hi[c] = std::max(h->hi[c], x[c]);
+        }
+        for (int c = 0; c < na; ++c) h->absmax = std::max(h->absmax, std::fabs(x[c]));
+    }
+    HIP_OR_FAIL(launch_rrt_grow(h->sp, mv->sp, mv->ck, h->g, h->feat, h->feat32, h->rows32, h->cap, n0,
+                                (uint64_t *)h->rrt_n.p, d_samples, (uint32_t)ns, max_distance, (double *)h->rrt_pd.p,
+                                (uint32_t *)h->rrt_pi.p, d_nearest, d_added, mv->counters, h->stream));
+    uint64_t n1 = n0;
+    HIP_OR_FAIL(hipMemcpyAsync(&n1, h->rrt_n.p, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    h->n_live += n1 - n0;
+    h->n_total = n1;
+    h->removed.resize(h->n_total, 0);
+    h->sorted_dirty = true;
     return OMPL_GPU_OK;
 }
 

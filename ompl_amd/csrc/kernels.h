@@ -84,9 +84,9 @@ struct SortedStore {
     uint32_t *tkey0 = nullptr;   // [ntiles] Morton key of each tile's first state
     uint32_t n = 0, n_pad = 0, ntiles = 0, nsuper = 0;
     size_t bytes = 0;
-    // optional device counters (owned by the caller): [0] tiles fetched, [2] (tile, query)
-    // pairs scanned, [1] tiles a
-    // brute-force walk of the same query groups would have scanned
+    // optional device counters (owned by the caller), kNN walk: [0] tiles fetched, [1] tiles
+    // a brute-force walk of the same query groups would have fetched, [2] (tile, query) pairs
+    // scanned; radius walk: [3] tiles fetched, [4] (tile, query) pairs scanned
     unsigned long long *counters = nullptr;
 };
 bool cull_supported(const DevSpace &sp);
@@ -118,6 +118,32 @@ hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t
 hipError_t launch_gather_rows(const double *src, int F, const uint32_t *list, uint32_t n, double *dst, hipStream_t st);
 hipError_t launch_scatter_results(const double *d, const uint32_t *ids, uint32_t k, const uint32_t *list, uint32_t n,
                                   double *out_d, uint32_t *out_i, hipStream_t st);
+
+// ---- culled radius search (SE3, R^n) over the sorted store (knn_fast_impl.h) ---------------
+size_t radius_fast_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq);
+// phase 0: queries ordered on the Morton curve and their hits counted; *d_offsets (device,
+// inside ws) then holds nq + 2 entries: the exclusive offsets [0, nq] (so [nq] = total) and
+// the longest segment at [nq + 1].  phase 1 (same ws, same queries): every hit's (id, fp64
+// distance) written into its query's segment, in walk order.
+hipError_t launch_radius_fast(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap,
+                              const SortedStore *sorted, const double *qfeat64, uint32_t nq, double r,
+                              const FastBounds &b, void *ws, size_t ws_bytes, int phase, uint64_t **d_offsets,
+                              uint32_t *out_i, double *out_d, hipStream_t st);
+// sort every CSR segment (at most kRankSortMax long) by (distance, id): rank placement in LDS
+constexpr uint32_t kRankSortMax = 1024;
+hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_i, const double *in_d, uint32_t nq,
+                                    uint32_t *out_i, double *out_d, hipStream_t st);
+// motion endpoints of neighbour results: edge e pairs query q with stored state ids[e]
+// (CSR offsets, or offsets == nullptr and e = q * stride + j)
+hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
+                        const uint64_t *offsets, const uint32_t *ids, uint32_t stride, uint64_t m, int from_query,
+                        double *from, double *to, hipStream_t st);
+// ---- RRT growth on device (rrt.hip) -------------------------------------------------------
+size_t rrt_part_entries(uint64_t n_max);
+hipError_t launch_rrt_grow(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck, const FeatGeom &g,
+                           double *feat, float *feat32, int rows32, uint64_t cap, uint64_t n0, uint64_t *n_dev,
+                           const double *samples, uint32_t ns, double maxd, double *part_d, uint32_t *part_i,
+                           uint32_t *nearest, uint32_t *added, unsigned long long *counters, hipStream_t st);
 
 // radius search, pass 1 (count per (query, chunk)) and pass 2 (fill CSR in id order).
 struct RadiusPlan {

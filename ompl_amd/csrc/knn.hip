@@ -24,7 +24,7 @@
 
 namespace ompl_amd {
 
-constexpr int kStreamItems = 16;      // states per lane in the stream mapping
+constexpr int kStreamItems = 16;      // states per lane in the stream radius mapping
 
 
 // ---------------------------------------------------------------------------------
@@ -98,7 +98,14 @@ __global__ __launch_bounds__(256) void knn_merge_kernel(const double *__restrict
 }
 
 // ---------------------------------------------------------------------------------
-// stream kNN (small nq): grid (blocks, nq); wave gw scans [gw*64*ITEMS, (gw+1)*64*ITEMS)
+// stream kNN (small nq): grid (blocks, nq); wave gw scans [gw*64*ITEMS, (gw+1)*64*ITEMS).
+// HBM/MALL-bound: every wave issues all of its ITEMS x F row loads before the first
+// distance, and the grid has ~4 waves per SIMD, so the whole store is in flight at once
+// instead of a few serial load rounds per wave.  n_end is a multiple of kTile = 64*ITEMS,
+// so a wave is either wholly inside the store or wholly past it (wave-uniform guard).
+constexpr int kScanItems = 4;
+static_assert(64 * kScanItems == kTile, "stream waves must tile n_end exactly");
+
 template <int SP, int F, int NMAX, int K>
 __global__ __launch_bounds__(256) void knn_stream_kernel(const double *__restrict__ feat, uint64_t cap,
                                                          uint64_t n_end, const double *__restrict__ qfeat,
@@ -113,16 +120,30 @@ __global__ __launch_bounds__(256) void knn_stream_kernel(const double *__restric
     for (int f = 0; f < F; ++f) qf[f] = qfeat[(size_t)q * F + f];
     TopK<K> top;
     top.init();
-    const uint64_t wbase = ((uint64_t)blockIdx.x * 4 + wave) * (64 * kStreamItems);
-#pragma unroll 4
-    for (int it = 0; it < kStreamItems; ++it) {
-        const uint64_t id = wbase + (uint64_t)it * 64 + lane;
-        if (id < n_end) {
-            double sf[F];
+    const uint64_t wbase = ((uint64_t)blockIdx.x * 4 + wave) * (64 * kScanItems);
+    if (wbase < n_end) {
+        double sf[kScanItems][F];
 #pragma unroll
-            for (int f = 0; f < F; ++f) sf[f] = feat[(uint64_t)f * cap + id];
-            const double d = feat_dist<SP, F, NMAX>(sf, qf, sp);
-            if (top.admits(d, (uint32_t)id)) top.push(d, (uint32_t)id);
+        for (int it = 0; it < kScanItems; ++it)
+#pragma unroll
+            for (int f = 0; f < F; ++f) sf[it][f] = feat[(uint64_t)f * cap + wbase + (uint64_t)it * 64 + lane];
+#pragma unroll
+        for (int it = 0; it < kScanItems; ++it) {
+            const uint32_t id = (uint32_t)(wbase + (uint64_t)it * 64 + lane);
+            if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+                // se3_dist is (0 + w0 * |dt|) + w1 * arc with arc >= 0, so in fp64 it is >= the
+                // first term computed by the same operations: a state whose translation term
+                // alone exceeds the current K-th distance cannot enter, and its acos is skipped
+                const double a = sp.w0 * l2_dist(sf[it], qf, 3);
+                if (!(a > top.d[K - 1])) {
+                    double d = 0.0;
+                    d += a;
+                    d += sp.w1 * so3_arc(sf[it] + 3, qf + 3);
+                    top.offer(d, id);
+                }
+            } else {
+                top.offer(feat_dist<SP, F, NMAX>(sf[it], qf, sp), id);
+            }
         }
     }
     double rd;
@@ -302,6 +323,70 @@ __global__ void steer_kernel(DevSpace sp, const double *__restrict__ raw, uint64
     }
 }
 
+// Sort each CSR segment by (distance, id) by rank placement: one wave per segment stages
+// it in LDS and every element's rank is the number of elements ordered before it, so it
+// goes to offsets[q] + rank (ids are unique inside a segment: the ranks are a permutation).
+__global__ __launch_bounds__(64) void segment_rank_sort_kernel(const uint64_t *__restrict__ off,
+                                                               const uint32_t *__restrict__ in_i,
+                                                               const double *__restrict__ in_d,
+                                                               uint32_t *__restrict__ out_i,
+                                                               double *__restrict__ out_d) {
+    __shared__ double sd[kRankSortMax];
+    __shared__ uint32_t si[kRankSortMax];
+    const uint32_t q = blockIdx.x;
+    const uint64_t b = off[q];
+    const uint32_t L = (uint32_t)(off[q + 1] - b);
+    if (L > kRankSortMax) return;  // the caller sorts with radix passes instead
+    for (uint32_t j = threadIdx.x; j < L; j += blockDim.x) {
+        sd[j] = in_d[b + j];
+        si[j] = in_i[b + j];
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < L; j += blockDim.x) {
+        const double dj = sd[j];
+        const uint32_t ij = si[j];
+        uint32_t rank = 0;
+        for (uint32_t t = 0; t < L; ++t) rank += lex_less(sd[t], si[t], dj, ij) ? 1u : 0u;
+        out_d[b + rank] = dj;
+        out_i[b + rank] = ij;
+    }
+}
+
+// Motion endpoints of a batch of neighbour results, the edges the planners check after a
+// neighbour query: PRM checkMotion(state[n], state[m]) (PRM.cpp:577-582, from_query = 0),
+// BIT* checkMotion(vertex, sample) (BITstar.cpp:815, from_query = 1).  Edge e pairs query q
+// with stored state ids[e]; a missing id (fewer stored states than k) pairs q with itself.
+__global__ void edges_kernel(DevSpace sp, const double *__restrict__ raw, uint64_t cap, const double *__restrict__ q,
+                             uint32_t nq, const uint64_t *__restrict__ off, const uint32_t *__restrict__ ids,
+                             uint32_t stride, uint64_t m, int from_query, double *__restrict__ from,
+                             double *__restrict__ to) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    uint32_t qi;
+    if (off) {  // the segment holding e: off[qi] <= e < off[qi + 1]
+        uint32_t lo = 0, hi = nq;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (off[mid] <= e)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        qi = lo;
+    } else {
+        qi = (uint32_t)(e / stride);
+    }
+    const int dim = sp.dim;
+    const uint32_t id = ids[e];
+    double *qd = (from_query ? from : to) + e * dim;
+    double *nd = (from_query ? to : from) + e * dim;
+    for (int c = 0; c < dim; ++c) {
+        const double qv = q[(size_t)qi * dim + c];
+        qd[c] = qv;
+        nd[c] = id == kNoId ? qv : raw[(uint64_t)c * cap + id];
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // host side
 
@@ -353,7 +438,7 @@ KnnPlan knn_plan(uint32_t nq, uint32_t k, uint64_t n_end, int num_cus) {
     const uint64_t tiles = n_end / kTile;
     if (nq < kStreamMaxQ) {
         p.stream = true;
-        p.chunks = (uint32_t)((n_end + 256 * kStreamItems - 1) / (256 * kStreamItems));
+        p.chunks = (uint32_t)((n_end + 256 * kScanItems - 1) / (256 * kScanItems));
         if (p.chunks == 0) p.chunks = 1;
         return p;
     }
@@ -524,6 +609,22 @@ hipError_t launch_store_soa(const double *aos, uint32_t n, int width, double *so
     const uint64_t t = (uint64_t)n * width;
     hipLaunchKernelGGL(store_soa_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, aos, n, width, soa, cap,
                        first);
+    return hipGetLastError();
+}
+
+hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_i, const double *in_d, uint32_t nq,
+                                    uint32_t *out_i, double *out_d, hipStream_t st) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(segment_rank_sort_kernel, dim3(nq), dim3(64), 0, st, offsets, in_i, in_d, out_i, out_d);
+    return hipGetLastError();
+}
+
+hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
+                        const uint64_t *offsets, const uint32_t *ids, uint32_t stride, uint64_t m, int from_query,
+                        double *from, double *to, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(edges_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, sp, raw, cap, q, nq, offsets,
+                       ids, stride, m, from_query, from, to);
     return hipGetLastError();
 }
 

@@ -61,6 +61,25 @@ hipError_t launch_knn_fast(const DevSpace &sp, const FeatGeom &g, const double *
     return hipErrorInvalidValue;
 }
 
+size_t radius_fast_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq) {
+    return radius_layout(sp, g, nq).total;
+}
+
+hipError_t launch_radius_fast(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap,
+                              const SortedStore *sorted, const double *qfeat64, uint32_t nq, double r,
+                              const FastBounds &b, void *ws, size_t ws_bytes, int phase, uint64_t **d_offsets,
+                              uint32_t *out_i, double *out_d, hipStream_t st) {
+    switch (sp.kind) {
+    case OMPL_GPU_SPACE_SE3:
+        return fast_se3_radius(sp, g, feat64, cap, sorted, qfeat64, nq, r, b, ws, ws_bytes, phase, d_offsets, out_i,
+                               out_d, st);
+    case OMPL_GPU_SPACE_REALVECTOR:
+        return fast_rv_radius(sp, g, feat64, cap, sorted, qfeat64, nq, r, b, ws, ws_bytes, phase, d_offsets, out_i,
+                              out_d, st);
+    }
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t first, uint64_t n, float *feat32,
                           hipStream_t st) {
     if (n == 0 || rows == 0) return hipSuccess;

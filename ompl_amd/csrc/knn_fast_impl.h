@@ -831,6 +831,149 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(const float *__restric
     if (!ok) fail_list[atomicAdd(fail_count, 1u)] = q;
 }
 
+// ---- culled radius search (SE3, R^n) ------------------------------------------------------
+// nearestR (NearestNeighborsGNAT.h:236-245; Linear :135-142: d <= r inclusive, ascending).
+// The bound is fixed, so no step of the walk waits on an earlier result: a wave serves G
+// Morton-adjacent queries, tests 64 super-tile boxes per ballot and the 32 tile boxes of a
+// passing super-tile at once, and scans a tile only for the queries whose own box bound
+// comes within their inflated radius.  The fp32 screen keeps d32 <= r + e (e = the screen's
+// error bound, the same as the kNN certificate's, so no element with d <= r is lost); every
+// kept element is then decided by its exact fp64 distance in the reference's operation
+// order.  FILL = false counts the hits of each query, FILL = true writes (id, d) into the
+// query's CSR segment in tile order; the caller sorts each segment by (distance, id).
+template <int SP, int F, int G, bool FILL>
+__global__ __launch_bounds__(64) void radius32_group_kernel(
+    const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
+    const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ q32,
+    const uint32_t *__restrict__ perm, uint32_t nq, const double *__restrict__ feat64, uint64_t cap,
+    const double *__restrict__ qf64, DevSpace sp, float absmax, double r, uint64_t *__restrict__ counts,
+    const uint64_t *__restrict__ offsets, uint32_t *__restrict__ out_i, double *__restrict__ out_d,
+    unsigned long long *__restrict__ counters) {
+    constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
+    constexpr int GH = G / 2;
+    static_assert(G % 2 == 0, "radius walk shape");
+    __shared__ __attribute__((aligned(16))) float qrow[G * FS];
+    const int lane = threadIdx.x;
+    const int half = lane >> 5;
+    const float w0 = (float)sp.w0, w1 = (float)sp.w1;
+    // XCD-aware group order, as in knn32_group_kernel
+    const uint32_t nb = gridDim.x, xq = nb / 8, xr = nb % 8, xb = blockIdx.x % 8;
+    const uint32_t blk = (xb < xr ? xb * (xq + 1) : xr * (xq + 1) + (xb - xr) * xq) + blockIdx.x / 8;
+    const uint32_t g0 = blk * G;
+    for (int t = lane; t < G * FS; t += 64) {
+        const uint32_t qi = g0 + t / FS;
+        qrow[t] = qi < nq ? q32[(size_t)qi * FS + t % FS] : __builtin_nanf("");
+    }
+    __syncthreads();
+    double qv[G][F];
+    uint32_t qo[G];
+    float thr[G];
+    uint64_t cur[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const bool live = g0 + g < nq;
+        qo[g] = live ? perm[g0 + g] : 0u;
+#pragma unroll
+        for (int f = 0; f < F; ++f) qv[g][f] = live ? qf64[(size_t)qo[g] * F + f] : 0.0;
+        double B = absmax;
+        const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : F;
+        for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qv[g][c]));
+        // every element with d <= r has d32 <= r + e; rounding to fp32 is covered by the 16 u
+        const double t = (r + screen_error<SP>(sp, B, r)) * (1.0 + 16.0 * kU);
+        thr[g] = live ? (float)t : -__builtin_inff();
+        cur[g] = (FILL && live) ? offsets[qo[g]] : 0ull;
+    }
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint64_t cnt[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) cnt[g] = 0;
+    uint32_t visited = 0, qscans = 0;
+    for (uint32_t sb = 0; sb < nsuper; sb += 64) {
+        const uint32_t s = sb + lane;
+        bool need = false;
+        if (s < nsuper) {
+            float bx[BW];
+            const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
+#pragma unroll
+            for (int c = 0; c < BW / 4; ++c) {
+                const float4 v = b4[c];
+                bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) need |= box_lb<SP, F>(bx, &qrow[g * FS], w0, w1) <= thr[g];
+        }
+        uint64_t sm = __ballot(need);
+        while (sm) {
+            const uint32_t ss = sb + (uint32_t)__builtin_ctzll(sm);
+            sm &= sm - 1;
+            // this lane's tile (lane & 31) of super-tile ss, bounds for queries half * GH + j
+            const uint32_t tt = ss * kSuperTiles + (lane & 31);
+            float lb[GH];
+            bool tneed = false;
+            if (tt < ntiles) {
+                float bx[BW];
+                const float4 *b4 = reinterpret_cast<const float4 *>(tbox + (size_t)tt * BW);
+#pragma unroll
+                for (int c = 0; c < BW / 4; ++c) {
+                    const float4 v = b4[c];
+                    bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
+                }
+#pragma unroll
+                for (int j = 0; j < GH; ++j) {
+                    lb[j] = box_lb<SP, F>(bx, &qrow[(half * GH + j) * FS], w0, w1);
+                    tneed |= lb[j] <= (half ? thr[GH + j] : thr[j]);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < GH; ++j) lb[j] = __builtin_inff();
+            }
+            uint32_t m = fold_tiles(__ballot(tneed));
+            while (m) {
+                const int t = __builtin_ctz(m);
+                m &= m - 1;
+                const uint64_t p = (uint64_t)(ss * kSuperTiles + t) * kCullTile + lane;
+                float x[R];
+#pragma unroll
+                for (int rr = 0; rr < R; ++rr) x[rr] = rows[(uint64_t)rr * n_pad + p];
+                const uint32_t id = ids[p];
+                ++visited;
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    if (!(readlane_f(lb[g % GH], t + (g < GH ? 0 : 32)) <= thr[g])) continue;
+                    ++qscans;
+                    bool hit = state_dist32<SP, F>(x, &qrow[g * FS], w0, w1) <= thr[g];  // NaN never hits
+                    double dd = 0.0;
+                    if (hit) {
+                        double sv[F];
+#pragma unroll
+                        for (int f = 0; f < F; ++f) sv[f] = feat64[(uint64_t)f * cap + id];
+                        dd = feat_dist<SP, F, 0>(sv, qv[g], sp);
+                        hit = dd <= r;
+                    }
+                    const uint64_t bm = __ballot(hit);
+                    if (FILL && hit) {
+                        const uint64_t pos = cur[g] + (uint64_t)__popcll(bm & lt);
+                        out_i[pos] = id;
+                        out_d[pos] = dd;
+                    }
+                    cur[g] += (uint64_t)__popcll(bm);
+                    cnt[g] += (uint64_t)__popcll(bm);
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        if (!FILL) {
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                if (g0 + g < nq) counts[qo[g]] = cnt[g];
+        } else if (counters) {
+            atomicAdd(&counters[3], (unsigned long long)visited);  // tiles fetched by the radius walk
+            atomicAdd(&counters[4], (unsigned long long)qscans);   // (tile, query) pairs scanned
+        }
+    }
+}
+
 __global__ void to_fp32_kernel(const double *__restrict__ f64, uint64_t cap, int rows, uint64_t first, uint64_t n,
                                float *__restrict__ f32) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -988,6 +1131,86 @@ hipError_t run_fast_space(const DevSpace &sp, const FastPlan &p, const FastLayou
     return hipErrorInvalidValue;
 }
 
+// radius workspace: query order + fp32 rows (as the kNN walk), per-query counts (nq + 1,
+// the last one zero) and the offsets their exclusive scan gives (nq + 2: [nq] = total,
+// [nq + 1] = longest segment)
+constexpr int kRadiusGroup = 2;
+
+struct RadiusLayout {
+    size_t keys, keys2, idx, perm, cub, q32u, q32, counts, off, scan, red, total;
+    size_t cub_bytes, scan_bytes, red_bytes;
+};
+
+RadiusLayout radius_layout(const DevSpace &sp, const FeatGeom &g, uint32_t nq) {
+    RadiusLayout L{};
+    size_t off = 0;
+    auto take = [&](size_t b) {
+        size_t o = off;
+        off += align_up(b);
+        return o;
+    };
+    L.keys = take(4ull * nq);
+    L.keys2 = take(4ull * nq);
+    L.idx = take(4ull * nq);
+    L.perm = take(4ull * nq);
+    size_t cb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                             (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nq, 0, 32);
+    L.cub_bytes = cb;
+    L.cub = take(cb);
+    const int FS = sp.kind == OMPL_GPU_SPACE_SE3 ? 8 : g.F;
+    L.q32u = take(4ull * nq * FS);
+    L.q32 = take(4ull * nq * FS);
+    L.counts = take(8ull * (nq + 1));
+    L.off = take(8ull * (nq + 2));
+    size_t sb = 0, rb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)nq + 1);
+    (void)hipcub::DeviceReduce::Max(nullptr, rb, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)nq);
+    L.scan_bytes = sb;
+    L.red_bytes = rb;
+    L.scan = take(sb);
+    L.red = take(rb);
+    L.total = off;
+    return L;
+}
+
+template <int SP, int F>
+hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, const double *f64, uint64_t cap,
+                           const SortedStore *ss, const double *qf64, uint32_t nq, double r, const FastBounds &b,
+                           int phase, uint32_t *out_i, double *out_d, hipStream_t st) {
+    constexpr int FS = Geo<SP, F>::FS;
+    uint32_t *keys = (uint32_t *)(ws + L.keys), *keys2 = (uint32_t *)(ws + L.keys2);
+    uint32_t *idx = (uint32_t *)(ws + L.idx), *perm = (uint32_t *)(ws + L.perm);
+    float *q32u = (float *)(ws + L.q32u), *q32 = (float *)(ws + L.q32);
+    uint64_t *counts = (uint64_t *)(ws + L.counts), *offs = (uint64_t *)(ws + L.off);
+    const dim3 grid((nq + kRadiusGroup - 1) / kRadiusGroup), b64(64), b256(256);
+    hipError_t e;
+    if (phase == 0) {
+        hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys,
+                           idx);
+        size_t cb = L.cub_bytes;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(ws + L.cub, cb, keys, keys2, idx, perm, (int)nq, 0, 32, st)) !=
+            hipSuccess)
+            return e;
+        hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
+        if ((e = hipMemsetAsync(counts + nq, 0, 8, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, false>), grid, b64, 0, st, ss->rows, ss->n_pad,
+                           ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, f64, cap, qf64, sp,
+                           b.absmax, r, counts, nullptr, nullptr, nullptr, nullptr);
+        size_t sb = L.scan_bytes, rb = L.red_bytes;
+        if ((e = hipcub::DeviceScan::ExclusiveSum(ws + L.scan, sb, counts, offs, (int)nq + 1, st)) != hipSuccess)
+            return e;
+        if ((e = hipcub::DeviceReduce::Max(ws + L.red, rb, counts, offs + nq + 1, (int)nq, st)) != hipSuccess) return e;
+        return hipGetLastError();
+    }
+    timer_begin(st, "radius32_group_kernel");
+    hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, true>), grid, b64, 0, st, ss->rows, ss->n_pad,
+                       ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, f64, cap, qf64, sp,
+                       b.absmax, r, nullptr, offs, out_i, out_d, ss->counters);
+    timer_end(st);
+    return hipGetLastError();
+}
+
 template <int SP, int F>
 hipError_t build_sorted(const float *f32, uint64_t cap, uint32_t n, const FastBounds &b, SortedStore *s,
                         hipStream_t st) {
@@ -1046,7 +1269,11 @@ hipError_t build_sorted(const float *f32, uint64_t cap, uint32_t n, const FastBo
                     uint32_t k, const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes,  \
                     int num_cus, hipStream_t st, uint32_t **fail_count, uint32_t **fail_list);                  \
     hipError_t NAME##_build(const FeatGeom &g, const float *feat32, uint64_t cap, uint32_t n, const FastBounds &b, \
-                            SortedStore *s, hipStream_t st);
+                            SortedStore *s, hipStream_t st);                                                   \
+    hipError_t NAME##_radius(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap,          \
+                             const SortedStore *sorted, const double *qfeat64, uint32_t nq, double r,          \
+                             const FastBounds &b, void *ws, size_t ws_bytes, int phase, uint64_t **d_offsets,  \
+                             uint32_t *out_i, double *out_d, hipStream_t st);
 OMPL_AMD_FAST_DECL(fast_se3)
 OMPL_AMD_FAST_DECL(fast_so3)
 OMPL_AMD_FAST_DECL(fast_rv)
@@ -1066,6 +1293,19 @@ hipError_t fast_entry(const DevSpace &sp, const FeatGeom &g, const double *feat6
     *fail_list = *fail_count + 1;
     return run_fast_space<SP, F>(sp, p, L, w, feat32, feat64, cap, n_end, sorted, qfeat64, nq, k, b, out_d, out_i,
                                  st);
+}
+
+template <int SP, int F>
+hipError_t fast_radius_entry(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap,
+                             const SortedStore *sorted, const double *qfeat64, uint32_t nq, double r,
+                             const FastBounds &b, void *ws, size_t ws_bytes, int phase, uint64_t **d_offsets,
+                             uint32_t *out_i, double *out_d, hipStream_t st) {
+    if (!sorted || nq == 0) return hipErrorInvalidValue;
+    const RadiusLayout L = radius_layout(sp, g, nq);
+    if (L.total > ws_bytes) return hipErrorInvalidValue;
+    char *w = (char *)ws;
+    *d_offsets = (uint64_t *)(w + L.off);
+    return run_radius_fast<SP, F>(sp, L, w, feat64, cap, sorted, qfeat64, nq, r, b, phase, out_i, out_d, st);
 }
 
 }  // namespace ompl_amd

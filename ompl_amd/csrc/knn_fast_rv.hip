@@ -24,4 +24,17 @@ hipError_t fast_rv_build(const FeatGeom &g, const float *feat32, uint64_t cap, u
     return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 16>(feat32, cap, n, b, s, st);
 }
 
+hipError_t fast_rv_radius(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap,
+                          const SortedStore *sorted, const double *qfeat64, uint32_t nq, double r, const FastBounds &b,
+                          void *ws, size_t ws_bytes, int phase, uint64_t **d_offsets, uint32_t *out_i, double *out_d,
+                          hipStream_t st) {
+#define OMPL_AMD_RV(FF)                                                                                          \
+    return fast_radius_entry<OMPL_GPU_SPACE_REALVECTOR, FF>(sp, g, feat64, cap, sorted, qfeat64, nq, r, b, ws,     \
+                                                            ws_bytes, phase, d_offsets, out_i, out_d, st)
+    if (g.F == 4) OMPL_AMD_RV(4);
+    if (g.F == 8) OMPL_AMD_RV(8);
+    OMPL_AMD_RV(16);
+#undef OMPL_AMD_RV
+}
+
 }  // namespace ompl_amd

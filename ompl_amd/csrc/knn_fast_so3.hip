@@ -17,4 +17,10 @@ hipError_t fast_so3_build(const FeatGeom &, const float *, uint64_t, uint32_t, c
     return hipErrorInvalidValue;
 }
 
+hipError_t fast_so3_radius(const DevSpace &, const FeatGeom &, const double *, uint64_t, const SortedStore *,
+                           const double *, uint32_t, double, const FastBounds &, void *, size_t, int, uint64_t **,
+                           uint32_t *, double *, hipStream_t) {
+    return hipErrorInvalidValue;  // no sorted store for SO3: nearestR runs the exact scan
+}
+
 }  // namespace ompl_amd

@@ -166,6 +166,39 @@ class NearestNeighborsGPU:
         abi.check(abi.lib.ompl_gpu_nn_knn_device(self._h, C.c_void_p(d_queries), nq, k, C.c_void_p(d_ids),
                                                  C.c_void_p(d_dist)))
 
+    def radius_device(self, d_queries: int, nq: int, radius: float, d_offsets: int, d_ids: int, d_dist: int,
+                      capacity: int) -> int:
+        """nearestR into caller device buffers: offsets [nq+1] (int64), ids (int32) and dists
+        (fp64) of `capacity` entries, sorted by (distance, id) per query.  Returns the number of
+        results; when it exceeds capacity only the offsets are written."""
+        tot = C.c_uint64(0)
+        st = abi.lib.ompl_gpu_nn_radius_device(self._h, C.c_void_p(d_queries), nq, float(radius),
+                                               C.c_void_p(d_offsets), C.c_void_p(d_ids or None),
+                                               C.c_void_p(d_dist or None), int(capacity), C.byref(tot))
+        if st != abi.OK and not (st == abi.ERR_INVALID_ARG and tot.value > capacity):
+            abi.check(st)
+        return tot.value
+
+    def radius_cull_stats(self) -> tuple[int, int]:
+        """(64-state tiles the radius walk fetched, (tile, query) pairs it scanned)."""
+        a, b = C.c_uint64(0), C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_nn_radius_cull_stats(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def edges_device(self, d_queries: int, nq: int, d_offsets: int | None, d_ids: int, stride: int, m: int,
+                     from_query: bool, d_from: int, d_to: int) -> None:
+        """Motion endpoints of neighbour results (PRM.cpp:582 from_query=False, BITstar.cpp:815
+        from_query=True): CSR offsets from radius_device, or None with a dense nq x stride id matrix."""
+        abi.check(abi.lib.ompl_gpu_nn_edges_device(self._h, C.c_void_p(d_queries), nq, C.c_void_p(d_offsets or None),
+                                                   C.c_void_p(d_ids), int(stride), int(m), 1 if from_query else 0,
+                                                   C.c_void_p(d_from), C.c_void_p(d_to)))
+
+    def rrt_grow_device(self, mv, d_samples: int, ns: int, max_distance: float, d_nearest: int, d_added: int) -> None:
+        """ns RRT iterations on device (RRT.cpp:128-192 without the goal test) with motion
+        validator `mv` (a DiscreteMotionValidatorGPU over the same space)."""
+        abi.check(abi.lib.ompl_gpu_rrt_grow_device(self._h, mv._h, C.c_void_p(d_samples), int(ns), float(max_distance),
+                                                   C.c_void_p(d_nearest), C.c_void_p(d_added)))
+
     def steer_device(self, d_queries: int, nq: int, d_nearest: int, stride: int, max_distance: float,
                      d_from: int, d_to: int) -> None:
         abi.check(abi.lib.ompl_gpu_steer_device(self._h, C.c_void_p(d_queries), nq, C.c_void_p(d_nearest),

@@ -73,3 +73,16 @@ def rrt_star_k(n: int, d: int) -> int:
 def prm_star_k(n: int, d: int) -> int:
     """ceil((e + e/d) log n)  (ConnectionStrategy.h:141-149)."""
     return int(math.ceil((math.e + math.e / d) * math.log(n)))
+
+
+def unit_ball_measure(d: int) -> float:
+    """Volume of the unit d-ball (util/src/GeometricEquations.cpp:55-60)."""
+    return math.pi ** (d / 2.0) / math.gamma(d / 2.0 + 1.0)
+
+
+def bitstar_radius(n: int, d: int, measure: float, rewire: float = 1.1) -> float:
+    """BIT* radius r = rewire * r_RGG,min * (ln n / n)^(1/d), r_RGG,min = (2 (1 + 1/d) measure / zeta_d)^(1/d)
+    (ImplicitGraph.cpp:1372-1381, :1389-1400).  SE(3) over [0,1]^3: d = 6, measure = 1 * pi^2
+    (SO3StateSpace.cpp:171-175) -> 0.1528 at n = 1e7."""
+    r_rgg = (2.0 * (1.0 + 1.0 / d) * (measure / unit_ball_measure(d))) ** (1.0 / d)
+    return rewire * r_rgg * (math.log(n) / n) ** (1.0 / d)
