@@ -1,6 +1,6 @@
 """Benchmark: NN queries/s + motion checks/s on a 10^6-state SE(3) tree (BASELINE.json).
 
-Workload (BASELINE.json configs[2]): an SE(3) tree of 10^6 states
+Default workload (BASELINE.json configs[2]): an SE(3) tree of 10^6 states
 (translation in [0,1]^3, uniform rotations, seed 42) resident in HBM; per GPU a batch of
 10^5 sampled states (the RRT* sampling step).  One step = for every sample
     nearestK(k=10)                                   (NearestNeighborsGNAT.h:222-233)
@@ -11,12 +11,22 @@ all on device, inputs resident in HBM.  value = (NN queries + motion checks) per
 over all ranks.  Multi-GPU: the tree is replicated, samples are sharded (weak scaling,
 no collective in the data path).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+The other configurations are measured with --workload (same JSON line, same unit):
+    cfg2  R^6, 10^5 states, batched nearestK(k=10)                       (configs[1], M1)
+    cfg4  PRM* milestone batch in the KinematicChain R^12 space: 10^6 valid roadmap
+          vertices, per step B new valid milestones -> nearestK(k = 41, KStarStrategy)
+          + checkMotion(neighbour, milestone) for every edge          (configs[3], M3)
+    cfg5  BIT* batch on SE(3): 10^7 valid samples, per step 10^5 vertices -> nearestR
+          (r = 0.1528, ImplicitGraph.cpp:1372-1381) + checkMotion(vertex, sample) for every
+          edge, 32-sphere checker                                     (configs[4], M4)
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg2|cfg4|cfg5]
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -27,25 +37,34 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "NN queries/sec + motion checks/sec on 10^6-state SE(3) tree"
+UNIT = "(NN queries + motion checks)/s"
 PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # MI355X vector peaks (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0                       # HBM3E spec
-F_SE3 = 21  # flops per SE(3) distance, SURVEY.md §8d (sqrt and acos counted as 1 each)
+# flops per distance evaluation (SURVEY.md §8d constants; sqrt and acos counted as 1 each)
+F_SE3, F_L2_6, F_CHAIN = 21, 18, 84
 B_SE3 = {"f32": 28, "f64": 56}              # bytes per stored SE(3) state streamed by a scan
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r1_group_walk", "pmc_summary.json")
+PMC_PROFILES = {"cfg3": "r1_group_walk", "cfg2": "r1_cfg2", "cfg4": "r1_cfg4", "cfg5": "r1_cfg5"}
+DEFAULTS = {  # tree states, queries (samples / milestones / vertices) per GPU per step, k
+    "cfg3": (1_000_000, 100_000, 10),
+    "cfg2": (100_000, 100_000, 10),
+    "cfg4": (1_000_000, 8_192, 0),
+    "cfg5": (10_000_000, 100_000, 0),
+}
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(workload, kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
     (FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction, + WRITE_SIZE)."""
+    path = os.path.join(ROOT, "profiles", PMC_PROFILES[workload], "pmc_summary.json")
     try:
-        with open(PMC_PROFILE) as f:
+        with open(path) as f:
             per = json.load(f)["per_kernel_mean"]
     except (OSError, ValueError, KeyError):
         return None
     for name, c in per.items():
         if name.split("<")[0].endswith(kernel) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             return {"bytes": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0,
-                    "source": os.path.relpath(PMC_PROFILE, ROOT) + f" [{name}]"}
+                    "source": os.path.relpath(path, ROOT) + f" [{name}]"}
     return None
 
 
@@ -54,62 +73,128 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--tree", type=int, default=1_000_000)
-    ap.add_argument("--queries", type=int, default=100_000, help="samples per GPU per step")
-    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--workload", default="cfg3", choices=sorted(DEFAULTS))
+    ap.add_argument("--tree", type=int, default=None)
+    ap.add_argument("--queries", type=int, default=None, help="samples / milestones / vertices per GPU per step")
+    ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--exact", action="store_true", help="force the exact fp64 scan (no fp32 screen)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--single-query-reps", type=int, default=200, help="RRT-style one-query scans (0 = skip)")
-    return ap.parse_args()
+    ap.add_argument("--rrt-iters", type=int, default=2000, help="device RRT iterations after the bench (0 = skip)")
+    a = ap.parse_args()
+    t, q, k = DEFAULTS[a.workload]
+    a.tree = t if a.tree is None else a.tree
+    a.queries = q if a.queries is None else a.queries
+    a.k = k if a.k is None else a.k
+    return a
 
 
-def cpu_baseline(sp, ck, tree, rng, k, budget_s):
-    """The oracle's GNAT restatement (reference defaults, 1 thread) + oracle motion checks,
-    timed on a bounded sample of the same workload on this host."""
+def _valid_states(mv, sampler, rng, n, chunk=1_000_000):
+    """n valid states by rejection (the roadmap / sample sets of PRM* and BIT* hold only valid
+    states: PRM.cpp:356-378, ImplicitGraph.cpp:981), the predicate evaluated on the device."""
+    out, have = [], 0
+    while have < n:
+        x = sampler(rng, chunk)
+        x = x[mv.isValid(x)]
+        out.append(x[: n - have])
+        have += len(out[-1])
+    return np.ascontiguousarray(np.concatenate(out))
+
+
+def _gnat_knn_rate(sp, tree, queries, k, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
-
-    from ompl_amd import workloads as W
 
     g = O.Gnat(sp)
     t0 = time.perf_counter()
     g.add(tree)
     build_s = time.perf_counter() - t0
-    nq = 500
-    q = W.uniform_se3(rng, nq)
     t0 = time.perf_counter()
-    g.knn(q, k)
-    t_probe = time.perf_counter() - t0
-    nq = int(min(20000, max(nq, 0.6 * budget_s / max(t_probe / nq, 1e-9))))
-    q = W.uniform_se3(rng, nq)
+    g.knn(queries[:200], k)
+    per = (time.perf_counter() - t0) / 200
+    nq = int(min(len(queries), max(200, 0.6 * budget_s / max(per, 1e-9))))
     t0 = time.perf_counter()
-    ids, d, _ = g.knn(q, k)
-    t_nn = time.perf_counter() - t0
-    maxd = 0.2 * sp.getMaximumExtent()
-    s1 = tree[ids[:, 0].astype(np.int64)]
-    s2 = np.empty_like(q)
-    for i in range(nq):  # steering is not timed on the CPU side (favours the CPU)
-        s2[i] = O.interpolate(sp, s1[i], q[i], maxd / d[i, 0]) if d[i, 0] > maxd else q[i]
+    ids, d, _ = g.knn(queries[:nq], k)
+    return nq, nq / (time.perf_counter() - t0), build_s, ids, d
+
+
+def _motion_rate(sp, ck, s1, s2, budget_s):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+
     t0 = time.perf_counter()
     O.check_motions_mt(sp, ck, s1, s2, 1)
-    t_mv = time.perf_counter() - t0
+    t = time.perf_counter() - t0
     reps = 1
-    if t_mv < 0.3 * budget_s:
-        reps = int(max(1, 0.3 * budget_s / max(t_mv, 1e-9)))
+    if t < budget_s:
+        reps = int(max(1, budget_s / max(t, 1e-9)))
         t0 = time.perf_counter()
         for _ in range(reps):
             O.check_motions_mt(sp, ck, s1, s2, 1)
-        t_mv = (time.perf_counter() - t0) / reps
-    qps, mps = nq / t_nn, nq / t_mv
-    return {
-        "value": 2.0 / (1.0 / qps + 1.0 / mps),  # same op mix as a GPU step: 1 query + 1 motion check
-        "unit": "(NN queries + motion checks)/s", "cores": 1, "kind": "port",
-        "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same 10^6-state "
-                   f"SE(3) tree: {nq} nearestK(k={k}) queries, then {nq} checkMotion(nearest, steered) x{reps} "
-                   f"with the oracle DiscreteMotionValidator; index build {build_s:.2f} s excluded"),
-        "nn_queries_per_s": qps, "motion_checks_per_s": mps,
-    }
+        t = (time.perf_counter() - t0) / reps
+    return len(s1) / t, reps
+
+
+def cpu_baseline(workload, sp, ck, tree, rng, k, budget_s, radius=None):
+    """The oracle restatement, 1 thread, on a bounded sample of the same workload on this host:
+    GNAT (oracle/gnat.cpp, reference defaults) where building it over the tree is affordable
+    (cfg2, cfg3), else the Linear brute force (cfg4: 10^6 chain states, cfg5: 10^7 SE(3)
+    samples) — a slower CPU path than the reference's GNAT, said so in `sample`."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+
+    from ompl_amd import workloads as W
+
+    if workload in ("cfg3", "cfg2"):
+        q = W.uniform_se3(rng, 20000) if workload == "cfg3" else W.uniform_rv(rng, 20000, 6)
+        nq, qps, build_s, ids, d = _gnat_knn_rate(sp, tree, q, k, budget_s)
+        if workload == "cfg2":
+            return {"value": qps, "unit": "NN queries/s", "cores": 1, "kind": "port",
+                    "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same 10^5-state "
+                               f"R^6 store: {nq} nearestK(k={k}) queries; index build {build_s:.2f} s excluded"),
+                    "nn_queries_per_s": qps}
+        maxd = 0.2 * sp.getMaximumExtent()
+        s1 = tree[ids[:, 0].astype(np.int64)]
+        s2 = np.empty_like(q[:nq])
+        for i in range(nq):  # steering is not timed on the CPU side (favours the CPU)
+            s2[i] = O.interpolate(sp, s1[i], q[i], maxd / d[i, 0]) if d[i, 0] > maxd else q[i]
+        mps, reps = _motion_rate(sp, ck, s1, s2, 0.3 * budget_s)
+        return {"value": 2.0 / (1.0 / qps + 1.0 / mps), "unit": UNIT, "cores": 1, "kind": "port",
+                "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same 10^6-state "
+                           f"SE(3) tree: {nq} nearestK(k={k}) queries, then {nq} checkMotion(nearest, steered) x{reps} "
+                           f"with the oracle DiscreteMotionValidator; index build {build_s:.2f} s excluded"),
+                "nn_queries_per_s": qps, "motion_checks_per_s": mps}
+    # brute force over 10^6 chain / 10^7 SE(3) states: time a few queries
+    dim = sp.dim
+    q = (W.uniform_chain(rng, 64, 12) if workload == "cfg4" else W.uniform_se3(rng, 64))
+    t0 = time.perf_counter()
+    if workload == "cfg4":
+        O.knn(sp, tree, q[:1], k)
+    else:
+        O.radius(sp, tree, q[:1], radius)
+    per = time.perf_counter() - t0
+    nq = int(min(64, max(1, 0.6 * budget_s / max(per, 1e-9))))
+    t0 = time.perf_counter()
+    if workload == "cfg4":
+        ids, _, _ = O.knn(sp, tree, q[:nq], k)
+        nb = tree[ids.reshape(-1).astype(np.int64)]
+        s1, s2 = nb, np.repeat(q[:nq], k, axis=0)                    # checkMotion(state[n], state[m])
+    else:
+        off, ids, _ = O.radius(sp, tree, q[:nq], radius)
+        s1 = np.repeat(q[:nq], np.diff(off).astype(np.int64), axis=0)  # checkMotion(vertex, sample)
+        s2 = tree[ids.astype(np.int64)]
+    t_nn = time.perf_counter() - t0
+    mps, reps = _motion_rate(sp, ck, s1.reshape(-1, dim), s2.reshape(-1, dim), 0.3 * budget_s)
+    m = len(s1)
+    t_mv = m / mps
+    what = (f"nearestK(k={k})" if workload == "cfg4" else f"nearestR(r={radius:.4f})")
+    return {"value": (nq + m) / (t_nn + t_mv), "unit": UNIT, "cores": 1, "kind": "port",
+            "sample": (f"oracle Linear brute force (NearestNeighborsLinear semantics; the reference's GNAT is faster, "
+                       f"its index over {len(tree)} states is not built here) : {nq} {what} queries over the same "
+                       f"{len(tree)}-state set, then their {m} checkMotion edges x{reps} with the oracle "
+                       f"DiscreteMotionValidator"),
+            "nn_queries_per_s": nq / t_nn, "motion_checks_per_s": mps}
 
 
 def single_query_scan(torch, nn, dev, reps, n_tree):
@@ -138,6 +223,191 @@ def single_query_scan(torch, nn, dev, reps, n_tree):
                          "note": "the 56 MB store is Infinity-Cache resident across back-to-back scans"}}
 
 
+def rrt_device(torch, nn, mv, sp, dev, iters):
+    """The RRT loop itself (RRT.cpp:128-192 without the goal test), `iters` dependent iterations
+    queued on the device with no host round trip (ompl_gpu_rrt_grow_device).  Grows the tree,
+    so it runs after every other measurement."""
+    from ompl_amd import workloads as W
+
+    s = torch.from_numpy(W.uniform_se3(np.random.default_rng(98), iters)).to(dev)
+    near = torch.empty(iters, dtype=torch.int32, device=dev)
+    added = torch.empty(iters, dtype=torch.int32, device=dev)
+    maxd = 0.2 * sp.getMaximumExtent()
+    nn.rrt_grow_device(mv, s.data_ptr(), 8, maxd, near.data_ptr(), added.data_ptr())  # warm
+    torch.cuda.synchronize(dev)
+    n0 = nn.size()
+    t0 = time.perf_counter()
+    nn.rrt_grow_device(mv, s.data_ptr(), iters, maxd, near.data_ptr(), added.data_ptr())
+    wall = time.perf_counter() - t0
+    return {"iterations_per_s": iters / wall, "iterations": iters, "states_added": nn.size() - n0,
+            "semantics": "nearest + steer + checkMotion + add per iteration, each iteration seeing the previous ones"}
+
+
+class Runner:
+    """One workload: builds the inputs, the step, and the roofline of its dominant kernel."""
+
+    def __init__(self, args, torch, dev, local, rank, stream):
+        from ompl_amd import DiscreteMotionValidatorGPU, NearestNeighborsGPU
+        from ompl_amd import workloads as W
+        from ompl_amd.checkers import HypercubeChecker, KinematicChainChecker, SpheresChecker
+        from ompl_amd.spaces import KinematicChainSpace, RealVectorStateSpace, SE3StateSpace
+
+        self.args, self.torch, self.dev = args, torch, dev
+        wl, nq, k = args.workload, args.queries, args.k
+        self.radius = None
+        qrng = np.random.default_rng(1000 + rank)                       # samples sharded by rank
+        if wl == "cfg3":
+            self.sp, self.ck = SE3StateSpace(0.0, 1.0), HypercubeChecker(3, 0.1)
+            self.tree = W.uniform_se3(np.random.default_rng(42), args.tree)   # identical on every rank
+            q = W.uniform_se3(qrng, nq)
+        elif wl == "cfg2":
+            self.sp, self.ck = RealVectorStateSpace(6), HypercubeChecker(6, 0.1)
+            self.tree = W.uniform_rv(np.random.default_rng(42), args.tree, 6)
+            q = W.uniform_rv(qrng, nq, 6)
+        elif wl == "cfg4":
+            self.sp = KinematicChainSpace(12, 1.0 / 12)                   # KinematicChainBenchmark.cpp:48-49
+            self.ck = KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))
+            self.k = k or W.prm_star_k(args.tree + 1, 12)                # KStarStrategy, n counts the milestone
+        else:
+            self.sp = SE3StateSpace(0.0, 1.0)
+            c, r = W.sphere_field(32, 0.1, 7)
+            self.ck = SpheresChecker(c, r)
+            self.radius = W.bitstar_radius(args.tree, 6, math.pi ** 2)
+        if wl in ("cfg3", "cfg2"):
+            self.k = k
+        elif wl == "cfg5":
+            self.k = 0
+        self.mv = DiscreteMotionValidatorGPU(self.sp, self.ck, local)
+        if wl == "cfg4":
+            self.tree = _valid_states(self.mv, lambda g, n: W.uniform_chain(g, n, 12), np.random.default_rng(42),
+                                      args.tree)
+            q = _valid_states(self.mv, lambda g, n: W.uniform_chain(g, n, 12), qrng, nq, chunk=max(4 * nq, 4096))
+        elif wl == "cfg5":
+            self.tree = _valid_states(self.mv, W.uniform_se3, np.random.default_rng(42), args.tree, chunk=2_000_000)
+            q = _valid_states(self.mv, W.uniform_se3, qrng, nq, chunk=2 * nq)
+        self.nq = nq
+        self.queries = torch.from_numpy(q).to(dev)
+        self.nn = NearestNeighborsGPU(self.sp, local)
+        self.nn.set_exact(args.exact)
+        self.nn.add(self.tree)
+        self.nn.set_stream(stream.cuda_stream)
+        self.mv.set_stream(stream.cuda_stream)
+        dim = self.sp.dim
+        if wl in ("cfg3", "cfg2", "cfg4"):
+            self.ids = torch.empty((nq, self.k), dtype=torch.int32, device=dev)
+            self.dd = torch.empty((nq, self.k), dtype=torch.float64, device=dev)
+        m = nq * self.k if wl == "cfg4" else nq
+        if wl == "cfg5":
+            self.off = torch.empty(nq + 1, dtype=torch.int64, device=dev)
+            m = self.nn.radius_device(self.queries.data_ptr(), nq, self.radius, self.off.data_ptr(), 0, 0, 0)
+            self.cap = m
+            self.ids = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+            self.dd = torch.empty(max(m, 1), dtype=torch.float64, device=dev)
+        self.m = m
+        self.s_from = torch.empty((max(m, 1), dim), dtype=torch.float64, device=dev)
+        self.s_to = torch.empty_like(self.s_from)
+        self.valid = torch.empty(max(m, 1), dtype=torch.uint8, device=dev)
+        self.maxd = 0.2 * self.sp.getMaximumExtent()                    # RRT range default (SelfConfig.cpp:98)
+
+    def step(self, e=None):
+        a, nn, mv, q = self.args, self.nn, self.mv, self.queries.data_ptr()
+        if e:
+            e[0].record(self.stream)
+        if a.workload == "cfg5":
+            self.m = nn.radius_device(q, self.nq, self.radius, self.off.data_ptr(), self.ids.data_ptr(),
+                                      self.dd.data_ptr(), self.cap)
+        else:
+            nn.knn_device(q, self.nq, self.k, self.ids.data_ptr(), self.dd.data_ptr())
+        if e:
+            e[1].record(self.stream)
+        if a.workload in ("cfg3", "cfg2"):   # RRT extend: nearest -> steer (RRT.cpp:137-146)
+            nn.steer_device(q, self.nq, self.ids.data_ptr(), self.k, self.maxd, self.s_from.data_ptr(),
+                            self.s_to.data_ptr())
+        elif a.workload == "cfg4":           # PRM: checkMotion(state[n], state[m])  PRM.cpp:582
+            nn.edges_device(q, self.nq, None, self.ids.data_ptr(), self.k, self.m, False, self.s_from.data_ptr(),
+                            self.s_to.data_ptr())
+        else:                                # BIT*: checkMotion(vertex, sample)  BITstar.cpp:815
+            nn.edges_device(q, self.nq, self.off.data_ptr(), self.ids.data_ptr(), 0, self.m, True,
+                            self.s_from.data_ptr(), self.s_to.data_ptr())
+        if e:
+            e[2].record(self.stream)
+        if a.workload != "cfg2":
+            mv.check_device(self.s_from.data_ptr(), self.s_to.data_ptr(), self.m, self.valid.data_ptr())
+        if e:
+            e[3].record(self.stream)
+
+    def units_per_step(self):
+        """NN queries + motion checks one step issues on this rank."""
+        if self.args.workload == "cfg2":
+            return self.nq
+        return self.nq + self.m
+
+    def metric(self):
+        wl = self.args.workload
+        if wl == "cfg2":
+            return "NN queries/sec, R^6 10^5 states, batched nearestK(k=10)", "NN queries/s"
+        if wl == "cfg4":
+            return "NN queries/sec + motion checks/sec, PRM* KinematicChain R^12, 10^6-vertex roadmap", UNIT
+        if wl == "cfg5":
+            return "NN queries/sec + motion checks/sec, BIT* SE(3) radius batch, 10^7 samples", UNIT
+        return METRIC, UNIT
+
+    def config(self, world):
+        a = self.args
+        base = {"tree_states": a.tree, "queries_per_gpu": self.nq,
+                "parallelism": f"queries sharded over {world} GPU(s), tree replicated"}
+        if a.workload == "cfg3":
+            base.update(workload="configs[2]: SE(3) RRT*-style batch — nearestK(k=10) + steer + checkMotion "
+                                 "(HypercubeBenchmark predicate on translation, edgeWidth 0.1, resolution 0.01)",
+                        k=self.k, state_space="SE3 [0,1]^3")
+        elif a.workload == "cfg2":
+            base.update(workload="configs[1]: R^6 RealVectorStateSpace, batched nearestK(k=10)", k=self.k,
+                        state_space="R^6 [0,1]^6")
+        elif a.workload == "cfg4":
+            base.update(workload="configs[3]: PRM* milestone batch, KinematicChain R^12 (horn environment) — "
+                                 "nearestK(k = ceil((e + e/12) ln n)) + checkMotion(neighbour, milestone) per edge",
+                        k=self.k, state_space="KinematicChain 12 links, linkLength 1/12",
+                        edges_per_step=self.m, note="roadmap vertices and milestones are valid states (rejection)")
+        else:
+            base.update(workload="configs[4]: BIT* batch on SE(3) — nearestR(r = 1.1 r_RGG (ln n / n)^(1/6)) + "
+                                 "checkMotion(vertex, sample) per edge, 32 spheres r=0.1",
+                        radius=self.radius, state_space="SE3 [0,1]^3", edges_per_step=self.m,
+                        note="samples and vertices are valid states (rejection)")
+        return base
+
+    def roofline(self, kern_ms, kern_name, before, after, launches):
+        wl, nq, n = self.args.workload, self.nq, self.args.tree
+        traffic = pmc_traffic(wl, kern_name)
+        if kern_name == "radius32_group_kernel":
+            pairs = (after["rq"] - before["rq"]) * 64 / launches
+            flop, dt, frac_of = F_SE3, "f32", f"{pairs / (float(nq) * n):.4%}"
+            what = (f"{pairs:.4g} (query, state) fp32 distance evaluations per launch x {F_SE3} flop (SURVEY §8d); "
+                    f"the culled radius walk scanned {frac_of} of the {nq} x {n} pairs")
+        elif kern_name == "knn32_group_kernel":
+            pairs = (after["kq"] - before["kq"]) * 64 / launches
+            flop = F_SE3 if wl == "cfg3" else F_L2_6
+            dt = "f32"
+            what = (f"{pairs:.4g} (query, state) fp32 distance evaluations per launch x {flop} flop (SURVEY §8d); "
+                    f"the culled walk scanned {pairs / (float(nq) * n):.4%} of the {nq} x {n} pairs")
+        else:  # brute-force scans (exact fp64 tiled kernel, or the chunked fp32 screen)
+            pairs = float(nq) * n
+            flop = {"cfg3": F_SE3, "cfg2": F_L2_6, "cfg4": F_CHAIN, "cfg5": F_SE3}[wl]
+            dt = "f32" if kern_name.startswith("knn32") else "f64"
+            what = f"{nq} x {n} (query, state) pairs per launch x {flop} flop (SURVEY §8d), brute force"
+        achieved = pairs * flop / (kern_ms * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
+                "frac": achieved / PEAK_TFLOPS[dt], "traffic": traffic["bytes"] if traffic else None,
+                "kernel": kern_name, "kernel_ms": kern_ms,
+                "algorithmic": what + f"; {dt} VALU peak (compute-bound on VALU, no MFMA)",
+                "brute_force_equivalent_tflops": float(nq) * n * flop / (kern_ms * 1e-3) / 1e12,
+                "traffic_source": traffic["source"] if traffic else None}
+
+    def counters(self):
+        k = self.nn.cull_stats()
+        r = self.nn.radius_cull_stats()
+        return {"kq": k[2], "rq": r[1]}
+
+
 def main():
     args = parse()
     import torch
@@ -152,104 +422,65 @@ def main():
 
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
 
-    from ompl_amd import DiscreteMotionValidatorGPU, NearestNeighborsGPU
-    from ompl_amd import workloads as W
-    from ompl_amd.checkers import HypercubeChecker
-    from ompl_amd.spaces import SE3StateSpace
-
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(dev)  # a real (non-null) stream shared by torch events and the library
-    sp = SE3StateSpace(0.0, 1.0)
-    ck = HypercubeChecker(3, 0.1)
-    tree = W.uniform_se3(np.random.default_rng(42), args.tree)      # identical on every rank
-    qrng = np.random.default_rng(1000 + rank)                         # samples sharded by rank
-    nq, k = args.queries, args.k
-    queries = torch.from_numpy(W.uniform_se3(qrng, nq)).to(dev)
-
-    nn = NearestNeighborsGPU(sp, local)
-    nn.set_exact(args.exact)
-    nn.add(tree)
-    mv = DiscreteMotionValidatorGPU(sp, ck, local)
-    nn.set_stream(stream.cuda_stream)
-    mv.set_stream(stream.cuda_stream)
-    ids = torch.empty((nq, k), dtype=torch.int32, device=dev)
-    dd = torch.empty((nq, k), dtype=torch.float64, device=dev)
-    s_from = torch.empty_like(queries)
-    s_to = torch.empty_like(queries)
-    valid = torch.empty(nq, dtype=torch.uint8, device=dev)
-    maxd = 0.2 * sp.getMaximumExtent()  # RRT range default (SelfConfig.cpp:98)
+    run = Runner(args, torch, dev, local, rank, stream)
+    run.stream = stream
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
 
-    def step(e=None):
-        if e:
-            e[0].record(stream)
-        nn.knn_device(queries.data_ptr(), nq, k, ids.data_ptr(), dd.data_ptr())
-        if e:
-            e[1].record(stream)
-        nn.steer_device(queries.data_ptr(), nq, ids.data_ptr(), k, maxd, s_from.data_ptr(), s_to.data_ptr())
-        if e:
-            e[2].record(stream)
-        mv.check_device(s_from.data_ptr(), s_to.data_ptr(), nq, valid.data_ptr())
-        if e:
-            e[3].record(stream)
-
     for _ in range(args.warmup):
-        step()
+        run.step()
     torch.cuda.synchronize(dev)
-    nn.profile(True)
-    nn.kernel_time()
-    scr0, fb0 = nn.stats()
-    cul0 = nn.cull_stats()
+    run.nn.profile(True)
+    run.nn.kernel_time()
+    scr0, fb0 = run.nn.stats()
+    c0 = run.counters()
+    units = 0
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.steps):
-        step(ev[s])
+        run.step(ev[s])
+        units += run.units_per_step()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms_total, kern_n, kern_name = nn.kernel_time()
+    kern_ms_total, kern_n, kern_name = run.nn.kernel_time()
     kern_ms = kern_ms_total / max(kern_n, 1)
-    scr1, fb1 = nn.stats()
-    cul1 = nn.cull_stats()
-    knn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    steer_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    scr1, fb1 = run.nn.stats()
+    c1 = run.counters()
+    nn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    edge_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     mv_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
-    t = torch.tensor([elapsed, knn_ms, steer_ms, mv_ms, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, nn_ms, edge_ms, mv_ms, kern_ms], dtype=torch.float64, device=dev)
+    u = torch.tensor([units], dtype=torch.float64, device=dev)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, knn_ms, steer_ms, mv_ms, kern_ms = t.tolist()
-    valid_frac = float(valid.float().mean().item())
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+    elapsed, nn_ms, edge_ms, mv_ms, kern_ms = t.tolist()
+    total_units = float(u.item())
+    valid_frac = float(run.valid[: max(run.m, 1)].float().mean().item()) if args.workload != "cfg2" else None
 
-    single = None
-    if rank == 0 and args.single_query_reps > 0:
-        single = single_query_scan(torch, nn, dev, args.single_query_reps, args.tree)
+    single = rrt = None
+    if rank == 0 and args.workload == "cfg3" and args.single_query_reps > 0:
+        single = single_query_scan(torch, run.nn, dev, args.single_query_reps, args.tree)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(sp, ck, tree, np.random.default_rng(7), k, args.cpu_seconds)
+        cpu = cpu_baseline(args.workload, run.sp, run.ck, run.tree, np.random.default_rng(7), run.k,
+                           args.cpu_seconds, run.radius)
+    if rank == 0 and args.workload == "cfg3" and args.rrt_iters > 0:
+        rrt = rrt_device(torch, run.nn, run.mv, run.sp, dev, args.rrt_iters)
 
     if rank == 0:
-        value = 2.0 * nq * world * args.steps / elapsed
-        screen = kern_name.startswith("knn32")
-        dt = "f32" if screen else "f64"
-        # work the dominant kernel actually did: the group walk evaluates the 64 states of a
-        # tile for each query whose own box bound admits the tile (cull counters, device
-        # atomics); the brute-force kernels evaluate every (query, state) pair
-        launches = max(args.steps, 1)
-        if kern_name == "knn32_group_kernel" and cul1[1] > cul0[1]:
-            pairs = (cul1[2] - cul0[2]) * 64 / launches
-            scanned_frac = pairs / (float(nq) * args.tree)
-        else:
-            pairs, scanned_frac = float(nq) * args.tree, 1.0
-        achieved = pairs * F_SE3 / (kern_ms * 1e-3) / 1e12
-        traffic = pmc_traffic(kern_name)
+        metric, unit = run.metric()
+        screen = kern_name.startswith(("knn32", "radius32"))
         line = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "(NN queries + motion checks)/s",
+            "metric": metric,
+            "value": total_units / elapsed,
+            "unit": unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -258,31 +489,21 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32 screen + f64 certify" if screen else "f64",
-            "data": "synthetic (uniform SE(3) states, seeded; tree seed 42, samples seed 1000+rank)",
-            "config": {
-                "workload": "configs[2]: SE(3) RRT*-style batch — nearestK(k=10) + steer + checkMotion "
-                            "(HypercubeBenchmark predicate on translation, edgeWidth 0.1, resolution 0.01)",
-                "tree_states": args.tree, "samples_per_gpu": nq, "k": k, "state_space": "SE3 [0,1]^3",
-                "parallelism": f"samples sharded over {world} GPU(s), tree replicated",
-            },
-            "nn_queries_per_s": nq * world / (knn_ms * 1e-3),
-            "motion_checks_per_s": nq * world / (mv_ms * 1e-3),
-            "phase_ms": {"knn": knn_ms, "steer": steer_ms, "motion": mv_ms},
+            "data": "synthetic (seeded uniform states; tree seed 42, queries seed 1000+rank)",
+            "config": run.config(world),
+            "nn_queries_per_s": run.nq * world / (nn_ms * 1e-3),
+            "phase_ms": {"nn": nn_ms, "steer_or_edges": edge_ms, "motion": mv_ms},
             "fast_path": {"screened": scr1 - scr0, "exact_reruns": fb1 - fb0},
-            "motion_valid_fraction": valid_frac,
-            "roofline": {
-                "bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
-                "frac": achieved / PEAK_TFLOPS[dt], "traffic": traffic["bytes"] if traffic else None,
-                "kernel": kern_name, "kernel_ms": kern_ms,
-                "algorithmic": (f"{pairs:.4g} (query, state) distance evaluations per launch x {F_SE3} flop "
-                                f"(SURVEY §8d); the culled walk scanned {scanned_frac:.4%} of the "
-                                f"{nq} x {args.tree} pairs; {dt} VALU peak (compute-bound on VALU, no MFMA)"),
-                "brute_force_equivalent_tflops": float(nq) * args.tree * F_SE3 / (kern_ms * 1e-3) / 1e12,
-                "traffic_source": traffic["source"] if traffic else None,
-            },
-            "single_query": single,
+            "roofline": run.roofline(kern_ms, kern_name, c0, c1, max(args.steps, 1)),
             "cpu_baseline": cpu,
         }
+        if args.workload != "cfg2":
+            line["motion_checks_per_s"] = run.m * world / (mv_ms * 1e-3)
+            line["motion_valid_fraction"] = valid_frac
+        if single:
+            line["single_query"] = single
+        if rrt:
+            line["rrt_device"] = rrt
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
