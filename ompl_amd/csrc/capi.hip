@@ -323,7 +323,7 @@ ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, 
         HIP_OR_FAIL(hipMemcpyAsync(sr, states, sizeof(double) * n * dim, hipMemcpyHostToDevice, h->stream));
         HIP_OR_FAIL(launch_store_soa(sr, (uint32_t)n, dim, h->raw, h->cap, h->n_total, h->stream));
     }
-    if (h->rows32) HIP_OR_FAIL(launch_to_fp32(h->feat, h->cap, h->rows32, h->n_total, n, h->feat32, h->stream));
+    if (h->rows32) HIP_OR_FAIL(launch_rows32(h->sp, h->g, h->feat, h->cap, h->n_total, n, h->feat32, h->stream));
     // screening bounds (knn_fast.hip): key box of the first <= 6 coordinates, max |coordinate|
     const int nb = tracked_dims(h->sp);
     h->sorted_dirty = true;

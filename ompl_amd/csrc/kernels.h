@@ -97,6 +97,12 @@ void free_sorted_store(SortedStore *s);
 
 int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq);  // screening list size, 0 = not eligible
 int fp32_rows(const DevSpace &sp, const FeatGeom &g);     // rows of the fp32 SoA copy
+// fp32 screening rows of stored states [first, first + n): the features, or for KCHAIN the
+// joint positions (prefix sums of the cos / sin features)
+hipError_t launch_rows32(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap, uint64_t first,
+                         uint64_t n, float *feat32, hipStream_t st);
+hipError_t launch_chain_rows32(const double *feat64, uint64_t cap, int nmax, uint64_t first, uint64_t n, float *feat32,
+                               hipStream_t st);
 size_t knn_fast_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k, uint64_t n_end,
                                 int num_cus, bool cull);
 // sorted == nullptr: chunked brute-force screen; else the group walk over *sorted

@@ -6,16 +6,24 @@
 namespace ompl_amd {
 // K2: the smallest list bucket >= max(k + 6, 16); the certify kernel's K bucket fits inside it.
 int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq) {
-    if (sp.kind == OMPL_GPU_SPACE_KCHAIN || nq < kStreamMaxQ || k == 0) return 0;
+    if (nq < kStreamMaxQ || k == 0) return 0;
     const int K = k_bucket(k);
-    if (K == 0 || K > 32) return 0;  // the exact path serves k > 32
+    // the exact path serves k > 32 (k > 58 for the chain, whose k = 41 of PRM* takes the screen)
+    if (K == 0 || (K > 32 && sp.kind != OMPL_GPU_SPACE_KCHAIN)) return 0;
     int K2 = k_bucket(k + 6);
     if (K2 < 16) K2 = 16;
     if (K2 == 0 || K2 < K) return 0;
     return K2;
 }
 
-int fp32_rows(const DevSpace &sp, const FeatGeom &g) { return sp.kind == OMPL_GPU_SPACE_KCHAIN ? 0 : g.F; }
+// fp32 screening rows: the features (R^n, SO3, SE3) or the joint positions (KCHAIN)
+int fp32_rows(const DevSpace &sp, const FeatGeom &g) { (void)sp; return g.F; }
+
+hipError_t launch_rows32(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap, uint64_t first,
+                         uint64_t n, float *feat32, hipStream_t st) {
+    if (sp.kind == OMPL_GPU_SPACE_KCHAIN) return launch_chain_rows32(feat64, cap, g.nmax, first, n, feat32, st);
+    return launch_to_fp32(feat64, cap, g.F, first, n, feat32, st);
+}
 
 bool cull_supported(const DevSpace &sp) {
     return sp.kind == OMPL_GPU_SPACE_SE3 || sp.kind == OMPL_GPU_SPACE_REALVECTOR;
@@ -57,6 +65,9 @@ hipError_t launch_knn_fast(const DevSpace &sp, const FeatGeom &g, const double *
     case OMPL_GPU_SPACE_REALVECTOR:
         return fast_rv(sp, g, feat64, feat32, cap, n_end, sorted, qfeat64, nq, k, b, out_d, out_i, ws, ws_bytes,
                        num_cus, st, fail_count, fail_list);
+    case OMPL_GPU_SPACE_KCHAIN:
+        return fast_chain(sp, g, feat64, feat32, cap, n_end, nullptr, qfeat64, nq, k, b, out_d, out_i, ws, ws_bytes,
+                          num_cus, st, fail_count, fail_list);
     }
     return hipErrorInvalidValue;
 }

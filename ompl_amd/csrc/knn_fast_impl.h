@@ -95,6 +95,21 @@ __device__ __forceinline__ void key_coords(const float *x, float *c, int nkey) {
     }
 }
 
+// KinematicChain screening rows: the joint positions P_i = (sum_{j<=i} cos t_j, sum_{j<=i} sin t_j)
+// from the cumulative cos / sin features (summed in fp64, then rounded), so that the chain
+// distance (demos/KinematicChain.h:105-124) becomes link * sum_i |P_i(a) - P_i(b)|
+template <int NM>
+__device__ __forceinline__ void chain_positions(const double *feat, float *o) {
+    double cx = 0.0, cy = 0.0;
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        cx += feat[i];
+        cy += feat[NM + i];
+        o[i] = (float)cx;
+        o[NM + i] = (float)cy;
+    }
+}
+
 // ---- queries: fp32 rows, keys, order ---------------------------------------------------
 template <int SP, int F>
 __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, FastBounds b, float *__restrict__ q32u,
@@ -115,14 +130,20 @@ __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, Fa
         n2 = fmaf(o[7], o[7], n2);
         o[3] = fmaxf(n2 - 1.f, 0.f) * 1.00001f;
         x[0] = o[0]; x[1] = o[1]; x[2] = o[2]; x[3] = o[4]; x[4] = o[5]; x[5] = o[6]; x[6] = o[7];
+    } else if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+        chain_positions<FS / 2>(s, o);
     } else {
         for (int f = 0; f < FS; ++f) o[f] = (float)s[f];
         for (int d = 0; d < b.nkey; ++d) x[d] = o[d];
     }
     for (int f = 0; f < FS; ++f) q32u[(size_t)i * FS + f] = o[f];
-    float c[kKeyDims];
-    key_coords<SP>(x, c, b.nkey);
-    keys[i] = morton_key(c, b);
+    if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+        keys[i] = 0u;  // no spatial order for the chain metric (no culled walk)
+    } else {
+        float c[kKeyDims];
+        key_coords<SP>(x, c, b.nkey);
+        keys[i] = morton_key(c, b);
+    }
     idx[i] = i;
 }
 
@@ -270,7 +291,7 @@ constexpr int kBatch = 8;
 
 template <int SP, int FS, int K2, int NS, class IdOf>
 __device__ __forceinline__ void screen_tile(const float *tile, const float *qf, float w0, float w0sq, float w1,
-                                            IdOf id_of, TopK32<K2> &top, float &ctau) {
+                                            int nlinks, IdOf id_of, TopK32<K2> &top, float &ctau) {
     const float4 *t4 = reinterpret_cast<const float4 *>(tile);
 #pragma unroll 2
     for (int j0 = 0; j0 < NS; j0 += kBatch) {
@@ -324,6 +345,27 @@ __device__ __forceinline__ void screen_tile(const float *tile, const float *qf, 
                     }
                 }
             }
+        } else if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+            // w0 = link length; rows are joint positions (chain_positions)
+            constexpr int NM = FS / 2;
+#pragma unroll
+            for (int u = 0; u < kBatch; ++u) {
+                const float *t = tile + (j0 + u) * FS;
+                float acc = 0.f;
+#pragma unroll
+                for (int i = 0; i < NM; ++i) {
+                    if (i < nlinks) {
+                        const float dx = t[i] - qf[i], dy = t[NM + i] - qf[NM + i];
+                        acc += __builtin_amdgcn_sqrtf(fmaf(dy, dy, dx * dx));
+                    }
+                }
+                v[u] = acc * w0;
+            }
+#pragma unroll
+            for (int u = 0; u < kBatch; ++u) {
+                const uint32_t id = id_of(j0 + u);
+                if (top.admits(v[u], id)) top.push(v[u], id);
+            }
         } else {
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
@@ -367,7 +409,8 @@ template <int SP, int F, int K2>
 __global__ __launch_bounds__(256) void knn32_screen_kernel(const float *__restrict__ f32, uint64_t cap,
                                                            uint64_t n_end, const float *__restrict__ q32,
                                                            uint32_t nq, uint32_t chunk_len, float w0, float w1,
-                                                           float *__restrict__ pd, uint32_t *__restrict__ pi) {
+                                                           int nlinks, float *__restrict__ pd,
+                                                           uint32_t *__restrict__ pi) {
     constexpr int FS = Geo<SP, F>::FS;
     __shared__ __attribute__((aligned(16))) float tile[kTile * FS];
     const uint32_t qs = blockIdx.x * kTile + threadIdx.x;
@@ -383,8 +426,8 @@ __global__ __launch_bounds__(256) void knn32_screen_kernel(const float *__restri
     for (uint64_t base = c0; base < c1; base += kTile) {
         stage_row<SP, FS>(tile, threadIdx.x, f32, cap, base + threadIdx.x);
         __syncthreads();
-        screen_tile<SP, FS, K2, kTile>(tile, qf, w0, w0sq, w1, [&](int j) { return (uint32_t)(base + j); }, top,
-                                       ctau);
+        screen_tile<SP, FS, K2, kTile>(tile, qf, w0, w0sq, w1, nlinks, [&](int j) { return (uint32_t)(base + j); },
+                                       top, ctau);
         __syncthreads();
     }
     if (qs >= nq) return;
@@ -758,6 +801,105 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         }
 }
 
+// ---- wave scan (KinematicChain) --------------------------------------------------------------
+// The chain metric has no box bound worth culling with, so every (query, state) pair is
+// evaluated; a thread-per-query list of PRM*'s k = 41 (ConnectionStrategy.h:147) plus margin
+// does not fit in registers, so the layout of the group walk is used instead: a wave serves
+// kWaveGroup consecutive queries, lane l holds state l of the current 64-state tile (joint
+// positions, chain_positions), and query g's K2-list lives across the wave (lane j = entry j).
+// The store is split in chunks along grid.y; the certificate merges the chunk lists.
+constexpr int kWaveGroup = 8;
+
+__device__ __forceinline__ float chain_dist32(const float *x, const float *q, int NM, float link, int nlinks) {
+    float acc = 0.f;
+    for (int i = 0; i < NM; ++i) {
+        if (i < nlinks) {
+            const float dx = x[i] - q[i], dy = x[NM + i] - q[NM + i];
+            acc += __builtin_amdgcn_sqrtf(fmaf(dy, dy, dx * dx));
+        }
+    }
+    return acc * link;
+}
+
+template <int F, int K2, int G>
+__global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__restrict__ f32, uint64_t cap,
+                                                             uint64_t n_end, const float *__restrict__ q32,
+                                                             uint32_t nq, uint32_t chunk_len, float link, int nlinks,
+                                                             float *__restrict__ pd, uint32_t *__restrict__ pi) {
+    constexpr int NM = F / 2;
+    static_assert(K2 <= 64, "lists are spread over one wave");
+    __shared__ __attribute__((aligned(16))) float qrow[G * F];
+    const int lane = threadIdx.x;
+    const uint32_t g0 = blockIdx.x * G;
+    for (int t = lane; t < G * F; t += 64) {
+        const uint32_t qi = g0 + t / F;
+        qrow[t] = qi < nq ? q32[(size_t)qi * F + t % F] : __builtin_nanf("");
+    }
+    __syncthreads();
+    uint32_t qoff = 0;  // re-read the wave-uniform query rows from LDS per tile (see knn32_group_kernel)
+    float Ld[G];
+    uint32_t Li[G];
+    float td[G];
+    uint32_t ti[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        Ld[g] = __builtin_inff();
+        Li[g] = kNoId;
+        td[g] = g0 + g < nq ? __builtin_inff() : -__builtin_inff();
+        ti[g] = kNoId;
+    }
+    auto offer = [&](int g, float d, uint32_t id) {
+        uint64_t bm = __ballot(d < td[g]);
+        while (bm) {
+            const int l = __builtin_ctzll(bm);
+            bm &= bm - 1;
+            const float cd = readlane_f(d, l);
+            const uint32_t ci = readlane_u(id, l);
+            if (cd < td[g] || (cd == td[g] && ci < ti[g])) {
+                const float pv = shr1_f(Ld[g], -__builtin_inff());
+                const uint32_t pv_i = shr1_u(Li[g], 0u);
+                const bool lt_cur = cd < Ld[g] || (cd == Ld[g] && ci < Li[g]);
+                const bool lt_prev = lane > 0 && (cd < pv || (cd == pv && ci < pv_i));
+                const float nd = lt_prev ? pv : (lt_cur ? cd : Ld[g]);
+                const uint32_t ni = lt_prev ? pv_i : (lt_cur ? ci : Li[g]);
+                Ld[g] = nd;
+                Li[g] = ni;
+                td[g] = readlane_f(Ld[g], K2 - 1);
+                ti[g] = readlane_u(Li[g], K2 - 1);
+            }
+        }
+    };
+    const uint64_t c0 = (uint64_t)blockIdx.y * chunk_len;
+    const uint64_t c1 = min(c0 + chunk_len, n_end);
+    float x[F], xn[F];
+    if (c0 < c1) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) x[f] = f32[(uint64_t)f * cap + c0 + lane];
+    }
+    for (uint64_t base = c0; base < c1; base += 64) {
+        const bool more = base + 64 < c1;
+        if (more) {  // prefetch the next tile while this one is scanned
+#pragma unroll
+            for (int f = 0; f < F; ++f) xn[f] = f32[(uint64_t)f * cap + base + 64 + lane];
+        }
+        const uint32_t id = (uint32_t)(base + lane);
+        asm volatile("" : "+s"(qoff));
+#pragma unroll
+        for (int g = 0; g < G; ++g) offer(g, chain_dist32(x, &qrow[qoff + g * F], NM, link, nlinks), id);
+        if (more) {
+#pragma unroll
+            for (int f = 0; f < F; ++f) x[f] = xn[f];
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+        if (g0 + g < nq && lane < K2) {
+            const size_t o = ((size_t)blockIdx.y * nq + g0 + g) * K2 + lane;
+            pd[o] = Ld[g];
+            pi[o] = Li[g];
+        }
+}
+
 template <int SP>
 __device__ __forceinline__ double screen_error(const DevSpace &sp, double B, double L) {
     double e = 0.0;
@@ -766,6 +908,12 @@ __device__ __forceinline__ double screen_error(const DevSpace &sp, double B, dou
             sp.w1 * (1.1 * sqrt(12.0 * kU) + 2e-6 + 4.5e-5);
     } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
         e = 1.1 * sqrt(12.0 * kU) + 2e-6 + 4.5e-5;
+    } else if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+        // |P_i| <= i: rounding the positions and differencing them costs <= 4 u i per
+        // coordinate, each term <= 14.2 u i, so the terms together <= 7.1 u n (n + 1); the n
+        // additions and the final link product cost <= (n + 1) u of the sum
+        const double n = (double)sp.dim;
+        e = sp.link * 8.0 * kU * n * (n + 1.0) + (n + 2.0) * kU * L;
     } else {
         e = 6.0 * sqrt((double)sp.dim) * kU * B + 6.0 * kU * L;
     }
@@ -807,13 +955,13 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(const float *__restric
             double sv[F];
 #pragma unroll
             for (int f = 0; f < F; ++f) sv[f] = feat64[(uint64_t)f * cap + id];
-            ex.offer(feat_dist<SP, F, 0>(sv, qv, sp), id);  // the reference formula, fp64
+            ex.offer(feat_dist<SP, F, SP == OMPL_GPU_SPACE_KCHAIN ? F / 2 : 0>(sv, qv, sp), id);  // fp64, reference order
         }
     }
     bool ok = true;
     if (t.i[K2 - 1] != kNoId) {  // the list is full: prove that no excluded element can enter
         double B = absmax;
-        const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_SO3 ? 0 : F);
+        const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_REALVECTOR ? F : 0);
         for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qv[c]));
         const double L = (double)t.d[K2 - 1];
         double dk = ex.d[K - 1];
@@ -1018,6 +1166,15 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
         return p;
     }
     const uint64_t tiles = std::max<uint64_t>(n_end / kTile, 1);
+    if (sp.kind == OMPL_GPU_SPACE_KCHAIN) {  // wave scan: ~8 waves per SIMD
+        const uint64_t groups = (nq + kWaveGroup - 1) / kWaveGroup;
+        const uint64_t target = (uint64_t)num_cus * 32;
+        const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>((target + groups - 1) / groups, tiles));
+        const uint64_t per = (tiles + S - 1) / S;
+        p.chunk_len = (uint32_t)(per * kTile);
+        p.chunks = (uint32_t)((n_end + p.chunk_len - 1) / p.chunk_len);
+        return p;
+    }
     const uint64_t qblocks = (nq + kTile - 1) / kTile;
     const uint64_t target = (uint64_t)num_cus * 8;
     uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>((target + qblocks - 1) / qblocks, tiles));
@@ -1081,7 +1238,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     e = hipMemsetAsync(fail, 0, 4, st);
     if (e != hipSuccess) return e;
     bool walked = false;
-    if constexpr (SP != OMPL_GPU_SPACE_SO3) {  // SO3 has no group walk (cull_supported)
+    if constexpr (SP == OMPL_GPU_SPACE_SE3 || SP == OMPL_GPU_SPACE_REALVECTOR) {  // cull_supported
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, kGroup, false, 1, true>), dim3((nq + kGroup - 1) / kGroup),
@@ -1093,10 +1250,18 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         }
     }
     if (p.cull && !walked) return hipErrorInvalidValue;
+    if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+        timer_begin(st, "knn32_wave_scan_kernel");
+        hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup>), dim3((nq + kWaveGroup - 1) / kWaveGroup, p.chunks),
+                           dim3(64), 0, st, f32, cap, n_end, q32, nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
+        timer_end(st);
+        walked = true;
+    }
     if (!walked) {
         timer_begin(st, "knn32_screen_kernel");
+        const float w0 = SP == OMPL_GPU_SPACE_KCHAIN ? (float)sp.link : (float)sp.w0;
         hipLaunchKernelGGL((knn32_screen_kernel<SP, F, K2>), dim3((nq + kTile - 1) / kTile, p.chunks), dim3(kTile), 0,
-                           st, f32, cap, n_end, q32, nq, p.chunk_len, (float)sp.w0, (float)sp.w1, pd, pi);
+                           st, f32, cap, n_end, q32, nq, p.chunk_len, w0, (float)sp.w1, sp.dim, pd, pi);
         timer_end(st);
     }
     hipLaunchKernelGGL((knn_certify_kernel<SP, F, K2, K>), dim3((nq + 255) / 256), b256, 0, st, pd, pi, p.chunks, nq,
@@ -1115,6 +1280,11 @@ hipError_t run_fast_k(const DevSpace &sp, const FastPlan &p, const FastLayout &L
     case 32:
         if constexpr (K2 >= 32)
             return run_fast<SP, F, K2, 32>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
+        break;
+    case 64:
+        if constexpr (K2 >= 64 && SP == OMPL_GPU_SPACE_KCHAIN)  // PRM* k = 41 (ConnectionStrategy.h:147)
+            return run_fast<SP, F, K2, 64>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
+        break;
     }
     return hipErrorInvalidValue;
 }
@@ -1277,6 +1447,7 @@ hipError_t build_sorted(const float *f32, uint64_t cap, uint32_t n, const FastBo
 OMPL_AMD_FAST_DECL(fast_se3)
 OMPL_AMD_FAST_DECL(fast_so3)
 OMPL_AMD_FAST_DECL(fast_rv)
+OMPL_AMD_FAST_DECL(fast_chain)
 
 // common body of the per-space entry points
 template <int SP, int F>

@@ -292,3 +292,25 @@ def test_fast_path_fallback_when_certificate_fails(gpu):
     assert screened == 300 and fallbacks > 0
     oi, od = _oracle_ext(sp, data, q, 10)
     assert_knn_parity(ids, d, oi, od, 10)
+
+
+@pytest.mark.parametrize("k", [10, 41])
+def test_chain_screen_is_used_and_exact(gpu, k):
+    """KinematicChain: the fp32 joint-position screen + fp64 certificate (PRM*'s k = 41,
+    ConnectionStrategy.h:147) returns the oracle's neighbours bit for bit."""
+    rng = np.random.default_rng(33)
+    sp = SPACES["chain12"]()
+    data, q = W.uniform_chain(rng, 40000, 12), W.uniform_chain(rng, 300, 12)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    ids, d, cnt = nn.nearestKBatch(q, k)
+    screened, fallbacks = nn.stats()
+    assert screened == 300 and fallbacks < 30 and (cnt == k).all()
+    oi, od, _ = O.knn(sp, data, q[:40], k)
+    np.testing.assert_array_equal(d[:40], od)
+    np.testing.assert_array_equal(ids[:40].astype(np.int64), oi.astype(np.int64))
+    gone = rng.choice(40000, 5000, replace=False)
+    for i in gone[:50]:
+        nn.remove(int(i))
+    ids2, _, _ = nn.nearestKBatch(q, k)
+    assert not np.isin(ids2.astype(np.int64), gone[:50]).any()
