@@ -9,11 +9,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "cpp", "plugin_test.cpp")
+MV_SRC = os.path.join(ROOT, "tests", "cpp", "mv_plugin_test.cpp")
 REF_SRC = "/root/reference/src"
 
 
-def _build(out, extra):
-    cmd = ["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "include"), *extra, SRC, "-o", out,
+def _build(out, extra, src=SRC):
+    cmd = ["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "include"), *extra, src, "-o", out,
            "-L", os.path.join(ROOT, "ompl_amd", "lib"), "-L", os.path.join(ROOT, "oracle"), "-lompl_gpu", "-loracle",
            f"-Wl,-rpath,{os.path.join(ROOT, 'ompl_amd', 'lib')}", f"-Wl,-rpath,{os.path.join(ROOT, 'oracle')}"]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -38,3 +39,16 @@ def test_plugin_runs_on_gpu(tmp_path, gpu):
     exe = _build(str(tmp_path / "plugin_run"), [])
     r = subprocess.run([exe, "run"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "PLUGIN OK" in r.stdout, r.stdout + r.stderr
+
+
+def test_motion_validator_plugin_compiles_standalone(tmp_path):
+    exe = _build(str(tmp_path / "mv_sa"), [], MV_SRC)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0 and "MV PLUGIN COMPILED" in r.stdout
+
+
+@pytest.mark.gpu
+def test_motion_validator_plugin_runs_on_gpu(tmp_path, gpu):
+    exe = _build(str(tmp_path / "mv_run"), [], MV_SRC)
+    r = subprocess.run([exe, "run"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "MV PLUGIN OK" in r.stdout, r.stdout + r.stderr
