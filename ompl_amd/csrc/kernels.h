@@ -73,7 +73,8 @@ struct FastBounds {
 constexpr int kCullTile = 64;
 constexpr int kSuperTiles = 32;
 // queries per wave in the group walk.  Measured on MI355X (SE3, 10^6 states, 10^5 queries,
-// k=10): G=8 3.9 % of the tiles fetched / 4.4 ms, G=4 2.8 % / 3.5 ms, G=2 1.9 % / 3.2 ms —
+// k=10): G=8 3.9 % of the tiles fetched / 4.4 ms, G=4 2.8 % / 3.5 ms, G=2 1.9 % / 3.2 ms (packed
+// two-query math at G=2: 3.7 ms) —
 // the walk is a chain of dependent memory round trips per wave, so more, narrower waves win
 constexpr int kGroup = 2;
 struct SortedStore {
