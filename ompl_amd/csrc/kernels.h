@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "device_space.h"
+#include "kd_order.h"
 
 namespace ompl_amd {
 
@@ -65,11 +66,12 @@ struct FastBounds {
     float absmax;                       // max |coordinate| stored (error bound of the fp32 screen)
 };
 
-// Spatially sorted fp32 copy of the store for the group walk (SE3 and R^n): states in
-// Morton order over the key coordinates, 64-state tiles (one state per lane) and 32-tile
-// super-tiles with axis-aligned boxes over every coordinate of the metric (SE3: the
-// translation and the sign-canonical quaternion, plus the largest quaternion norm excess,
-// so the box yields a lower bound of the full SE3 distance).
+// Spatially sorted fp32 copy of the store for the group walk (SE3 and R^n): states in k-d
+// leaf order (kd_order.cpp: median splits along the widest coordinate), 64-state tiles (one
+// state per lane, one k-d leaf) and 32-tile super-tiles (subtrees) with axis-aligned boxes over
+// every coordinate of the metric (SE3: the translation and the sign-canonical quaternion,
+// plus the largest quaternion norm excess, so the box yields a lower bound of the full SE3
+// distance).
 constexpr int kCullTile = 64;
 constexpr int kSuperTiles = 32;
 // queries per wave in the group walk.  Measured on MI355X (SE3, 10^6 states, 10^5 queries,
@@ -82,8 +84,10 @@ struct SortedStore {
     uint32_t *ids = nullptr;     // [n_pad] original id of each sorted slot (kNoId = padding)
     float *tbox = nullptr;       // [ntiles][box_w] lo.., hi.. (, eta, pad)
     float *sbox = nullptr;       // [nsuper][box_w]
-    uint32_t *tkey0 = nullptr;   // [ntiles] Morton key of each tile's first state
-    uint32_t n = 0, n_pad = 0, ntiles = 0, nsuper = 0;
+    uint32_t *tkey0 = nullptr;   // [ntiles] key of each tile = its index (queries' keys are home tiles)
+    KdNode *nodes = nullptr;     // internal k-d nodes, pre-order (kd_order.h)
+    uint32_t n = 0, n_pad = 0, ntiles = 0, nsuper = 0, nnodes = 0;
+    uint32_t kd_tiles = 0;       // leaves of the k-d tree: the tiles holding live states (removed ones follow)
     size_t bytes = 0;
     // optional device counters (owned by the caller), kNN walk: [0] tiles fetched, [1] tiles
     // a brute-force walk of the same query groups would have fetched, [2] (tile, query) pairs

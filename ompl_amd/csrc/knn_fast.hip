@@ -30,7 +30,7 @@ bool cull_supported(const DevSpace &sp) {
 }
 
 void free_sorted_store(SortedStore *s) {
-    for (void *x : {(void *)s->rows, (void *)s->ids, (void *)s->tbox, (void *)s->sbox, (void *)s->tkey0})
+    for (void *x : {(void *)s->rows, (void *)s->ids, (void *)s->tbox, (void *)s->sbox, (void *)s->tkey0, (void *)s->nodes})
         if (x) (void)hipFree(x);
     *s = SortedStore{};
 }

@@ -111,9 +111,27 @@ __device__ __forceinline__ void chain_positions(const double *feat, float *o) {
 }
 
 // ---- queries: fp32 rows, keys, order ---------------------------------------------------
+// home leaf of coordinates c (the box coordinates of Geo::NB) in the k-d tree of the sorted store
+__device__ __forceinline__ uint32_t kd_home_tile(const float *c, const KdNode *__restrict__ nodes, uint32_t ntiles) {
+    uint32_t node = 0, t0 = 0, tiles = ntiles;
+    for (int depth = 0; tiles > 1 && depth < 40; ++depth) {
+        const KdNode nd = nodes[node];
+        if (c[nd.dim] < nd.split) {
+            tiles = nd.left_tiles;
+            node = node + 1;
+        } else {
+            t0 += nd.left_tiles;
+            tiles -= nd.left_tiles;
+            node = nd.right;
+        }
+    }
+    return t0;
+}
+
 template <int SP, int F>
 __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, FastBounds b, float *__restrict__ q32u,
-                                  uint32_t *__restrict__ keys, uint32_t *__restrict__ idx) {
+                                  uint32_t *__restrict__ keys, uint32_t *__restrict__ idx,
+                                  const KdNode *__restrict__ nodes, uint32_t ntiles) {
     constexpr int FS = Geo<SP, F>::FS;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nq) return;
@@ -139,6 +157,17 @@ __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, Fa
     for (int f = 0; f < FS; ++f) q32u[(size_t)i * FS + f] = o[f];
     if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
         keys[i] = 0u;  // no spatial order for the chain metric (no culled walk)
+    } else if (nodes && ntiles > 1) {
+        // order by home leaf: the box coordinates, quaternion sign-canonical as in the store
+        float c[Geo<SP, F>::NB];
+        if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+            const float sg = x[6] < 0.f ? -1.f : 1.f;
+            c[0] = x[0]; c[1] = x[1]; c[2] = x[2];
+            c[3] = sg * x[3]; c[4] = sg * x[4]; c[5] = sg * x[5]; c[6] = sg * x[6];
+        } else {
+            for (int d = 0; d < Geo<SP, F>::NB; ++d) c[d] = o[d];
+        }
+        keys[i] = kd_home_tile(c, nodes, ntiles);
     } else {
         float c[kKeyDims];
         key_coords<SP>(x, c, b.nkey);
@@ -157,21 +186,6 @@ __global__ void query_gather_kernel(const float *__restrict__ q32u, const uint32
 }
 
 // ---- sorted store (culled screen) ----------------------------------------------------------
-template <int SP, int F>
-__global__ void tree_key_kernel(const float *__restrict__ f32, uint64_t cap, uint32_t n, FastBounds b,
-                                uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    constexpr int R = Geo<SP, F>::R;
-    float x[R > kKeyDims ? R : kKeyDims + 1];
-    const int D = SP == OMPL_GPU_SPACE_SE3 ? 7 : b.nkey;
-    for (int d = 0; d < D; ++d) x[d] = f32[(uint64_t)d * cap + i];
-    float c[kKeyDims];
-    key_coords<SP>(x, c, b.nkey);
-    keys[i] = b.nkey > 0 ? morton_key(c, b) : (x[0] == x[0] ? 0u : 0xFFFFFFFFu);
-    ids[i] = i;
-}
-
 template <int SP, int F>
 __global__ void tree_gather_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ ids_sorted,
                                    uint32_t n, uint32_t n_pad, float *__restrict__ rows, uint32_t *__restrict__ ids) {
@@ -233,7 +247,9 @@ __global__ void tile_box_kernel(const float *__restrict__ rows, uint32_t n_pad, 
         o[2 * NB] = eta * 1.00001f;
         o[2 * NB + 1] = 0.f;
     }
-    tkey0[t] = t * kCullTile < n ? keys_sorted[t * kCullTile] : 0xFFFFFFFFu;
+    tkey0[t] = t;  // queries carry their home leaf as key (kd_home_tile)
+    (void)keys_sorted;
+    (void)n;
 }
 
 template <int SP, int F>
@@ -1230,7 +1246,8 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     uint32_t *pi = (uint32_t *)(ws + L.pi);
     uint32_t *fail = (uint32_t *)(ws + L.fail);
     const dim3 b256(256);
-    hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys, idx);
+    hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys, idx,
+                       (p.cull && ss) ? ss->nodes : nullptr, (p.cull && ss) ? ss->kd_tiles : 0u);
     size_t cb = L.cub_bytes;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + L.cub, cb, keys, keys2, idx, perm, (int)nq, 0, 32, st);
     if (e != hipSuccess) return e;
@@ -1357,7 +1374,7 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
     hipError_t e;
     if (phase == 0) {
         hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys,
-                           idx);
+                           idx, ss->nodes, ss->kd_tiles);
         size_t cb = L.cub_bytes;
         if ((e = hipcub::DeviceRadixSort::SortPairs(ws + L.cub, cb, keys, keys2, idx, perm, (int)nq, 0, 32, st)) !=
             hipSuccess)
@@ -1390,43 +1407,59 @@ hipError_t build_sorted(const float *f32, uint64_t cap, uint32_t n, const FastBo
     s->ntiles = std::max<uint32_t>(1, (n + kCullTile - 1) / kCullTile);
     s->n_pad = s->ntiles * kCullTile;
     s->nsuper = (s->ntiles + kSuperTiles - 1) / kSuperTiles;
-    uint32_t *keys = nullptr, *ids0 = nullptr, *keys_s = nullptr, *ids_s = nullptr;
-    void *tmp = nullptr;
-    size_t tb = 0;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, keys_s, ids0, ids_s, (int)n, 0, 32, st);
+    (void)b;
+    uint32_t *ids_s = nullptr;
+    hipError_t e = hipSuccess;
     auto done = [&](hipError_t r) {
-        for (void *x : {(void *)keys, (void *)ids0, (void *)keys_s, (void *)ids_s, tmp})
-            if (x) (void)hipFree(x);
+        if (ids_s) (void)hipFree(ids_s);
         if (r != hipSuccess) free_sorted_store(s);
         return r;
     };
-    if (e != hipSuccess) return done(e);
-    if ((e = hipMalloc(&keys, 4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&ids0, 4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&keys_s, 4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return done(e);
+    // k-d leaf order on the host (kd_order.cpp) over the box coordinates, SE3 quaternions
+    // sign-canonical as the sorted rows store them
+    std::vector<float> hx((size_t)R * std::max<uint32_t>(n, 1));
+    if (n) {
+        if ((e = hipMemcpy2DAsync(hx.data(), 4ull * n, f32, 4ull * cap, 4ull * n, R, hipMemcpyDeviceToHost, st)) !=
+            hipSuccess)
+            return done(e);
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);
+        if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+            for (uint32_t i = 0; i < n; ++i)
+                if (hx[6ull * n + i] < 0.f)
+                    for (int r = 3; r < 7; ++r) hx[(size_t)r * n + i] = -hx[(size_t)r * n + i];
+        }
+    }
+    std::vector<uint32_t> perm;
+    std::vector<KdNode> nodes;
+    kd_tile_order(hx.data(), n, n, Geo<SP, F>::NB, kCullTile, perm, nodes);
+    s->nnodes = (uint32_t)nodes.size();
+    {
+        uint32_t live = 0;
+        for (uint32_t i = 0; i < n; ++i) live += hx[i] == hx[i] ? 1u : 0u;
+        s->kd_tiles = (live + kCullTile - 1) / kCullTile;
+    }
     if ((e = hipMalloc(&ids_s, 4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&tmp, std::max<size_t>(tb, 1))) != hipSuccess) return done(e);
+    if ((e = hipMalloc(&s->nodes, sizeof(KdNode) * std::max<size_t>(nodes.size(), 1))) != hipSuccess) return done(e);
     if ((e = hipMalloc(&s->rows, 4ull * R * s->n_pad)) != hipSuccess) return done(e);
     if ((e = hipMalloc(&s->ids, 4ull * s->n_pad)) != hipSuccess) return done(e);
     if ((e = hipMalloc(&s->tbox, 4ull * BW * s->ntiles)) != hipSuccess) return done(e);
     if ((e = hipMalloc(&s->sbox, 4ull * BW * s->nsuper)) != hipSuccess) return done(e);
     if ((e = hipMalloc(&s->tkey0, 4ull * s->ntiles)) != hipSuccess) return done(e);
-    s->bytes = 4ull * R * s->n_pad + 4ull * s->n_pad + 4ull * BW * (s->ntiles + s->nsuper) + 4ull * s->ntiles;
-    if (n) {
-        hipLaunchKernelGGL((tree_key_kernel<SP, F>), dim3((n + 255) / 256), dim3(256), 0, st, f32, cap, n, b, keys,
-                           ids0);
-        if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_s, ids0, ids_s, (int)n, 0, 32, st)) !=
-            hipSuccess)
-            return done(e);
-    }
+    s->bytes = 4ull * R * s->n_pad + 4ull * s->n_pad + 4ull * BW * (s->ntiles + s->nsuper) + 4ull * s->ntiles +
+               sizeof(KdNode) * nodes.size();
+    if (n && (e = hipMemcpyAsync(ids_s, perm.data(), 4ull * n, hipMemcpyHostToDevice, st)) != hipSuccess)
+        return done(e);
+    if (!nodes.empty() && (e = hipMemcpyAsync(s->nodes, nodes.data(), sizeof(KdNode) * nodes.size(),
+                                              hipMemcpyHostToDevice, st)) != hipSuccess)
+        return done(e);
     hipLaunchKernelGGL((tree_gather_kernel<SP, F>), dim3((s->n_pad + 255) / 256), dim3(256), 0, st, f32, cap, ids_s,
                        n, s->n_pad, s->rows, s->ids);
     hipLaunchKernelGGL((tile_box_kernel<SP, F>), dim3((s->ntiles + 255) / 256), dim3(256), 0, st, s->rows, s->n_pad,
-                       s->ntiles, keys_s, n, s->tbox, s->tkey0);
+                       s->ntiles, (const uint32_t *)nullptr, n, s->tbox, s->tkey0);
     hipLaunchKernelGGL((super_box_kernel<SP, F>), dim3((s->nsuper + 255) / 256), dim3(256), 0, st, s->tbox,
                        s->ntiles, s->nsuper, s->sbox);
     if ((e = hipGetLastError()) != hipSuccess) return done(e);
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);  // temporaries freed below
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);  // host vectors / temporaries released below
     return done(hipSuccess);
 }
 
