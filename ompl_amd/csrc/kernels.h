@@ -74,11 +74,13 @@ struct FastBounds {
 // distance).
 constexpr int kCullTile = 64;
 constexpr int kSuperTiles = 32;
-// queries per wave in the group walk.  Measured on MI355X (SE3, 10^6 states, 10^5 queries,
-// k=10): G=8 3.9 % of the tiles fetched / 4.4 ms, G=4 2.8 % / 3.5 ms, G=2 1.9 % / 3.2 ms (packed
-// two-query math at G=2: 3.7 ms) —
-// the walk is a chain of dependent memory round trips per wave, so more, narrower waves win
-constexpr int kGroup = 2;
+// queries per wave in the group walk.  Measured on MI355X (k=10, 10^5 queries, k-d tiles):
+// SE3 10^6 states G=2 2.09 ms, G=4 2.18 ms; R^6 10^5 states G=2 2.20 ms, G=4 1.50 ms.  (With
+// Morton-run tiles, SE3: G=8 4.4 ms, G=4 3.5 ms, G=2 3.2 ms; packed two-query math 3.7 ms.)
+// The walk is a chain of dependent memory round trips per wave, so narrower waves win where
+// the walk is long (SE3, 10^6 states), wider ones where the store is small and L2-resident.
+template <int SP>
+constexpr int group_queries() { return SP == OMPL_GPU_SPACE_SE3 ? 2 : 4; }
 struct SortedStore {
     float *rows = nullptr;       // [rows32][n_pad] (SE3 quaternions sign-canonical: w >= 0)
     uint32_t *ids = nullptr;     // [n_pad] original id of each sorted slot (kNoId = padding)

@@ -1258,7 +1258,8 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     if constexpr (SP == OMPL_GPU_SPACE_SE3 || SP == OMPL_GPU_SPACE_REALVECTOR) {  // cull_supported
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
-            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, kGroup, false, 1, true>), dim3((nq + kGroup - 1) / kGroup),
+            constexpr int G = group_queries<SP>();
+            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, false, 1, true>), dim3((nq + G - 1) / G),
                                dim3(64), 0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox,
                                ss->nsuper, ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi,
                                ss->counters);
@@ -1321,7 +1322,7 @@ hipError_t run_fast_space(const DevSpace &sp, const FastPlan &p, const FastLayou
 // radius workspace: query order + fp32 rows (as the kNN walk), per-query counts (nq + 1,
 // the last one zero) and the offsets their exclusive scan gives (nq + 2: [nq] = total,
 // [nq + 1] = longest segment)
-constexpr int kRadiusGroup = 2;
+constexpr int kRadiusGroup = 4;  // 10^7-state radius pass: G=2 2.37 ms, G=4 2.27 ms (tiles shared by more queries)
 
 struct RadiusLayout {
     size_t keys, keys2, idx, perm, cub, q32u, q32, counts, off, scan, red, total;
