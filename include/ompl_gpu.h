@@ -169,6 +169,10 @@ ompl_gpu_status ompl_gpu_nn_knn_device(ompl_gpu_nn *h, const double *d_queries, 
  * *screened counts queries that took the screen, *fallbacks those re-run exactly. */
 ompl_gpu_status ompl_gpu_nn_set_exact(ompl_gpu_nn *h, int exact_only);
 ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint64_t *fallbacks);
+/* Of those *fallbacks: *full counts the queries whose bounded exact re-run (one pass over the
+ * store for all uncertified queries, keeping d <= the certificate's exact k-th distance)
+ * exceeded its candidate cap and took the full exact scan. */
+ompl_gpu_status ompl_gpu_nn_rerun_stats(const ompl_gpu_nn *h, uint64_t *full);
 /* Group walk: 64-state tiles fetched, summed over query groups, vs the tiles a full scan
  * by the same groups would have touched; *query_tiles counts (tile, query) scans, i.e.
  * 64 distance evaluations each.  Any output may be NULL. */

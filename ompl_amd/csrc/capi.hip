@@ -99,7 +99,7 @@ struct ompl_gpu_nn {
     std::vector<uint8_t> removed;
     std::mutex mu;
     DevBuf q, out_d, out_i, ws, ws2, stage, counts, offsets, qoff, ids, dists, sorted_ids, sorted_d, tmp, fb_q, fb_d,
-        fb_i;
+        fb_i, fb_c, fb_cd, fb_ci;
     DevBuf rrt_n, rrt_pd, rrt_pi;  // device RRT growth: live size, per-block partial minima
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
@@ -112,7 +112,7 @@ struct ompl_gpu_nn {
     DevBuf cull_counter;      // SortedStore::counters: kNN walk [tiles fetched, tiles of a brute-force
                               // walk, (tile, query) pairs scanned], radius walk [tiles, pairs] (device)
     bool fast = true;        // OMPL_GPU_EXACT_ONLY=1 forces the exact fp64 scan
-    uint64_t fast_queries = 0, fast_fallbacks = 0;
+    uint64_t fast_queries = 0, fast_fallbacks = 0, fast_overflows = 0;  // overflows: bounded re-run exceeded its cap
     // profiling of the dominant scan kernel (HIP events on the launch stream)
     bool profile = false;
     std::vector<KernelTimer> pending;
@@ -477,8 +477,23 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
         h->fast_queries += nq;
         h->fast_fallbacks += nfail;
         if (nfail == 0) return OMPL_GPU_OK;
-        // exact fp64 re-run of the uncertified queries, then scatter into the outputs
+        // exact fp64 re-run of the uncertified queries: a bounded pass for all of them at once
+        // (knn_bounded_kernel), the full exact path for any that overflow its candidate cap
         const int F = h->g.F;
+        if (nfail <= kBoundedMaxQ) {
+            HIP_OR_FAIL(h->fb_c.ensure(sizeof(uint32_t) * (2 * nfail + 1)));
+            HIP_OR_FAIL(h->fb_cd.ensure(sizeof(double) * nfail * kBoundedCap));
+            HIP_OR_FAIL(h->fb_ci.ensure(sizeof(uint32_t) * nfail * kBoundedCap));
+            uint32_t *cnt = (uint32_t *)h->fb_c.p;
+            HIP_OR_FAIL(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (nfail + 1), h->stream));
+            HIP_OR_FAIL(launch_knn_bounded(h->sp, h->g, h->feat, h->cap, n_end, d_qf, d_fail_list, nfail, k, d_dist,
+                                           d_ids, cnt, (double *)h->fb_cd.p, (uint32_t *)h->fb_ci.p, h->stream));
+            HIP_OR_FAIL(hipMemcpyAsync(&nfail, cnt + nfail, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+            d_fail_list = cnt + nfail + 1;
+            HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+            h->fast_overflows += nfail;
+            if (nfail == 0) return OMPL_GPU_OK;
+        }
         HIP_OR_FAIL(h->fb_q.ensure(sizeof(double) * nfail * F));
         HIP_OR_FAIL(h->fb_d.ensure(sizeof(double) * nfail * k));
         HIP_OR_FAIL(h->fb_i.ensure(sizeof(uint32_t) * nfail * k));
@@ -859,6 +874,12 @@ ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
     if (screened) *screened = h->fast_queries;
     if (fallbacks) *fallbacks = h->fast_fallbacks;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_rerun_stats(const ompl_gpu_nn *h, uint64_t *full) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    if (full) *full = h->fast_overflows;
     return OMPL_GPU_OK;
 }
 

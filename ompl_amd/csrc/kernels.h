@@ -127,6 +127,18 @@ hipError_t launch_knn_large(const DevSpace &sp, const FeatGeom &g, const double 
                             hipStream_t st);
 hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t first, uint64_t n, float *feat32,
                           hipStream_t st);
+// bounded exact re-run of the fast path's uncertified queries list[0..nlist) (nlist <=
+// kBoundedMaxQ): od / oi hold the certificate's exact lists (row q = query q, k entries),
+// whose k-th distance bounds the answer; the exact top-k overwrites them.  counts (device,
+// nlist + 1 + nlist words, zeroed by the caller) returns at [nlist] the number of queries
+// that need the full exact path and at [nlist + 1 ..] their indices.  cand_d / cand_i hold
+// nlist * kBoundedCap entries.
+constexpr uint32_t kBoundedCap = 1024;
+constexpr uint32_t kBoundedMaxQ = 512;
+hipError_t launch_knn_bounded(const DevSpace &sp, const FeatGeom &g, const double *feat, uint64_t cap,
+                              uint64_t n_end, const double *qf, const uint32_t *list, uint32_t nlist, uint32_t k,
+                              double *od, uint32_t *oi, uint32_t *counts, double *cand_d, uint32_t *cand_i,
+                              hipStream_t st);
 // gather rows q = list[i] of an AoS [*][F] fp64 array into dst[i]; scatter results back
 hipError_t launch_gather_rows(const double *src, int F, const uint32_t *list, uint32_t n, double *dst, hipStream_t st);
 hipError_t launch_scatter_results(const double *d, const uint32_t *ids, uint32_t k, const uint32_t *list, uint32_t n,

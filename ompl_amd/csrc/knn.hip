@@ -180,6 +180,109 @@ __global__ __launch_bounds__(256) void knn_stream_merge_kernel(const double *__r
 }
 
 // ---------------------------------------------------------------------------------
+// bounded exact re-run of the fast path's uncertified queries.  The certificate already
+// wrote, for query q, the exact k-th distance b_q among its screened candidates; those k
+// candidates are stored states, so the true k nearest all have d <= b_q.  One pass over
+// the store therefore keeps every state with exact d <= b_q (few per query) and a rank
+// sort of that set yields the exact (distance, id) top-k — the same answer as the full
+// stream re-run, at one read of the store for all failed queries together instead of one
+// per query.  A query with more than kBoundedCap such states is reported as overflowing
+// and re-run by the full exact path.
+template <int SP, int F, int NMAX, int ITEMS>
+__global__ __launch_bounds__(256) void knn_bounded_kernel(const double *__restrict__ feat, uint64_t cap,
+                                                          uint64_t n_end, const double *__restrict__ qfeat,
+                                                          const uint32_t *__restrict__ list, uint32_t nlist,
+                                                          const double *__restrict__ out_d, uint32_t out_k,
+                                                          DevSpace sp, uint32_t *__restrict__ counts,
+                                                          double *__restrict__ cand_d, uint32_t *__restrict__ cand_i) {
+    const uint64_t base = (uint64_t)blockIdx.x * (256 * ITEMS) + threadIdx.x;
+    double sf[ITEMS][F];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint64_t g = base + (uint64_t)it * 256;
+#pragma unroll
+        for (int f = 0; f < F; ++f) sf[it][f] = g < n_end ? feat[(uint64_t)f * cap + g] : __builtin_nan("");
+    }
+    for (uint32_t j = 0; j < nlist; ++j) {
+        const uint32_t q = list[j];
+        const double b = out_d[(size_t)q * out_k + out_k - 1];
+        double qv[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) qv[f] = qfeat[(size_t)q * F + f];
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it) {
+            double d;
+            if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+                // as knn_stream_kernel: the translation term alone bounds the distance below
+                const double a = sp.w0 * l2_dist(sf[it], qv, 3);
+                if (!(a <= b)) continue;
+                d = 0.0;
+                d += a;
+                d += sp.w1 * so3_arc(sf[it] + 3, qv + 3);
+            } else {
+                d = feat_dist<SP, F, NMAX>(sf[it], qv, sp);
+            }
+            if (d <= b) {  // NaN (unused / removed slot) never passes
+                const uint32_t slot = atomicAdd(&counts[j], 1u);
+                if (slot < kBoundedCap) {
+                    cand_d[(size_t)j * kBoundedCap + slot] = d;
+                    cand_i[(size_t)j * kBoundedCap + slot] = (uint32_t)(base + (uint64_t)it * 256);
+                }
+            }
+        }
+    }
+}
+
+// block per re-run query: rank-sort its candidates by (distance, id) in LDS and write the
+// first out_k into the query's output row; too many (or, impossibly, too few) candidates
+// put the query on the overflow list (counts[nlist] = its length, list from counts + nlist + 1)
+__global__ __launch_bounds__(256) void knn_bounded_select_kernel(const uint32_t *__restrict__ list, uint32_t nlist,
+                                                                 uint32_t *__restrict__ counts,
+                                                                 const double *__restrict__ cand_d,
+                                                                 const uint32_t *__restrict__ cand_i, uint32_t out_k,
+                                                                 double *__restrict__ out_d,
+                                                                 uint32_t *__restrict__ out_i) {
+    __shared__ double sd[kBoundedCap];
+    __shared__ uint32_t si[kBoundedCap];
+    const uint32_t j = blockIdx.x, q = list[j];
+    const uint32_t c = counts[j];
+    if (c > kBoundedCap || c < out_k) {
+        if (threadIdx.x == 0) counts[nlist + 1 + atomicAdd(&counts[nlist], 1u)] = q;
+        return;
+    }
+    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
+        sd[e] = cand_d[(size_t)j * kBoundedCap + e];
+        si[e] = cand_i[(size_t)j * kBoundedCap + e];
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
+        const double d = sd[e];
+        const uint32_t id = si[e];
+        uint32_t rank = 0;
+        for (uint32_t m = 0; m < c; ++m) rank += (sd[m] < d || (sd[m] == d && si[m] < id)) ? 1u : 0u;
+        if (rank < out_k) {
+            out_d[(size_t)q * out_k + rank] = d;
+            out_i[(size_t)q * out_k + rank] = id;
+        }
+    }
+}
+
+template <int SP, int F, int NMAX>
+hipError_t run_knn_bounded(const DevSpace &sp, const double *feat, uint64_t cap, uint64_t n_end, const double *qf,
+                           const uint32_t *list, uint32_t nlist, uint32_t k, double *od, uint32_t *oi,
+                           uint32_t *counts, double *cand_d, uint32_t *cand_i, hipStream_t st) {
+    constexpr int ITEMS = F <= 8 ? 4 : 1;
+    const uint64_t blocks = (n_end + 256 * ITEMS - 1) / (256 * ITEMS);
+    timer_begin(st, "knn_bounded_kernel");
+    hipLaunchKernelGGL((knn_bounded_kernel<SP, F, NMAX, ITEMS>), dim3((uint32_t)blocks), dim3(256), 0, st, feat, cap,
+                       n_end, qf, list, nlist, od, k, sp, counts, cand_d, cand_i);
+    timer_end(st);
+    hipLaunchKernelGGL(knn_bounded_select_kernel, dim3(nlist), dim3(256), 0, st, list, nlist, counts, cand_d, cand_i,
+                       k, od, oi);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
 // radius search.  Hits are written per (query, chunk) segment in ascending id order
 // so that a stable sort by distance yields (distance, id) order.
 template <int SP, int F, int NMAX, bool FILL>
@@ -567,6 +670,16 @@ hipError_t launch_knn(const DevSpace &sp, const FeatGeom &g, const double *feat,
     if (p.K == 0) return hipErrorInvalidValue;
     if (knn_workspace_bytes(sp, g, nq, k, n_end, num_cus) > ws_bytes) return hipErrorInvalidValue;
     OMPL_AMD_SPACE_DISPATCH(run_knn, sp, p, feat, cap, n_end, qf, nq, k, od, oi, ws, st)
+}
+
+hipError_t launch_knn_bounded(const DevSpace &sp, const FeatGeom &g, const double *feat, uint64_t cap,
+                              uint64_t n_end, const double *qf, const uint32_t *list, uint32_t nlist, uint32_t k,
+                              double *od, uint32_t *oi, uint32_t *counts, double *cand_d, uint32_t *cand_i,
+                              hipStream_t st) {
+    if (nlist == 0 || k == 0) return hipSuccess;
+    if (nlist > kBoundedMaxQ) return hipErrorInvalidValue;
+    OMPL_AMD_SPACE_DISPATCH(run_knn_bounded, sp, feat, cap, n_end, qf, list, nlist, k, od, oi, counts, cand_d, cand_i,
+                            st)
 }
 
 RadiusPlan radius_plan(uint32_t nq, uint64_t n_end, int num_cus) {

@@ -138,6 +138,13 @@ class NearestNeighborsGPU:
         abi.check(abi.lib.ompl_gpu_nn_stats(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
+    def rerun_stats(self) -> int:
+        """Re-run queries whose bounded exact pass overflowed its candidate cap and took the
+        full exact scan (a subset of stats()[1])."""
+        a = C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_nn_rerun_stats(self._h, C.byref(a)))
+        return a.value
+
     def cull_stats(self) -> tuple[int, int, int]:
         """(64-state tiles the culled screen fetched, tiles a full scan would have fetched,
         (tile, query) pairs scanned — 64 distance evaluations each)."""

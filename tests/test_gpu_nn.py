@@ -294,6 +294,51 @@ def test_fast_path_fallback_when_certificate_fails(gpu):
     assert_knn_parity(ids, d, oi, od, 10)
 
 
+def test_bounded_rerun_se3_near_rotations(gpu):
+    """SE(3) states whose rotations differ by < 1e-3 rad: the screen's rotation error bound
+    (fp32 acos near 1) fails certificates; the bounded exact re-run (one store pass keeping
+    d <= the certificate's exact k-th distance) must return the oracle's lists."""
+    rng = np.random.default_rng(36)
+    sp = SE3StateSpace()
+    n = 40000
+    v = rng.normal(0, 1e-3, (n, 3))
+    quat = np.column_stack([v, np.ones(n)])
+    quat /= np.linalg.norm(quat, axis=1, keepdims=True)
+    data = np.column_stack([rng.uniform(0, 1, (n, 3)) * 0.02, quat])
+    q = data[rng.choice(n, 200, replace=False)].copy()
+    q[:, :3] += rng.normal(0, 1e-4, (200, 3))
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    ids, d, _ = nn.nearestKBatch(q, 10)
+    screened, fallbacks = nn.stats()
+    assert screened == 200 and fallbacks > 0
+    assert nn.rerun_stats() < fallbacks  # most took the bounded pass
+    oi, od = _oracle_ext(sp, data, q, 10)
+    assert_knn_parity(ids, d, oi, od, 10)
+
+
+def test_bounded_rerun_overflow_takes_full_path(gpu):
+    """2,000 identical copies of one state: every query next to it has more than the bounded
+    re-run's candidate cap (1,024) at d <= its k-th distance, so the full exact scan answers."""
+    rng = np.random.default_rng(37)
+    sp = SE3StateSpace()
+    base = W.uniform_se3(rng, 30000)
+    dup = np.repeat(base[:1], 2000, axis=0)
+    data = np.concatenate([base[1:15000], dup, base[15000:]])
+    q = np.repeat(base[:1], 8, axis=0)
+    q[:, :3] += rng.normal(0, 1e-6, (8, 3))
+    q = np.concatenate([q, W.uniform_se3(rng, 120)])
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    ids, d, _ = nn.nearestKBatch(q, 10)
+    screened, fallbacks = nn.stats()
+    assert screened == len(q) and fallbacks >= 8 and nn.rerun_stats() >= 8
+    oi, od = _oracle_ext(sp, data, q, 10)
+    assert_knn_parity(ids, d, oi, od, 10)
+    # the duplicates' tie class is resolved by insertion id, as on the exact path
+    np.testing.assert_array_equal(ids[:8].astype(np.int64), np.tile(np.arange(14999, 15009), (8, 1)))
+
+
 @pytest.mark.parametrize("k", [10, 41])
 def test_chain_screen_is_used_and_exact(gpu, k):
     """KinematicChain: the fp32 joint-position screen + fp64 certificate (PRM*'s k = 41,
