@@ -413,6 +413,7 @@ static ompl_gpu_status ensure_sorted(ompl_gpu_nn *h) {
     h->sorted_bounds = current_bounds(h);
     HIP_OR_FAIL(build_sorted_store(h->sp, h->g, h->feat32, h->cap, (uint32_t)h->n_total, h->sorted_bounds, &h->sorted,
                                    h->stream));
+    HIP_OR_FAIL(build_sorted_rows64(h->g, h->feat, h->cap, &h->sorted, h->stream));
     h->sorted_dirty = false;
     if (!h->cull_counter.p) {
         HIP_OR_FAIL(h->cull_counter.ensure(kCullCounters * sizeof(unsigned long long)));

@@ -88,6 +88,9 @@ struct SortedStore {
     float *sbox = nullptr;       // [nsuper][box_w]
     uint32_t *tkey0 = nullptr;   // [ntiles] key of each tile = its index (queries' keys are home tiles)
     KdNode *nodes = nullptr;     // internal k-d nodes, pre-order (kd_order.h)
+    double *rows64 = nullptr;    // [n_pad][fa] fp64 features in sorted order (AoS: one 64 B row per
+                                 // SE3 state), read by the certificate; padding rows are NaN
+    int fa = 0;                  // fp64 row width: F rounded up to a multiple of 4
     uint32_t n = 0, n_pad = 0, ntiles = 0, nsuper = 0, nnodes = 0;
     uint32_t kd_tiles = 0;       // leaves of the k-d tree: the tiles holding live states (removed ones follow)
     size_t bytes = 0;
@@ -101,6 +104,8 @@ bool cull_supported(const DevSpace &sp);
 hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, uint64_t cap, uint32_t n,
                               const FastBounds &b, SortedStore *s, hipStream_t st);
 void free_sorted_store(SortedStore *s);
+// fp64 AoS rows of the sorted copy (s->rows64), gathered from the SoA fp64 store by s->ids
+hipError_t build_sorted_rows64(const FeatGeom &g, const double *feat64, uint64_t cap, SortedStore *s, hipStream_t st);
 
 int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq);  // screening list size, 0 = not eligible
 int fp32_rows(const DevSpace &sp, const FeatGeom &g);     // rows of the fp32 SoA copy

@@ -30,9 +30,36 @@ bool cull_supported(const DevSpace &sp) {
 }
 
 void free_sorted_store(SortedStore *s) {
-    for (void *x : {(void *)s->rows, (void *)s->ids, (void *)s->tbox, (void *)s->sbox, (void *)s->tkey0, (void *)s->nodes})
+    for (void *x : {(void *)s->rows, (void *)s->ids, (void *)s->tbox, (void *)s->sbox, (void *)s->tkey0, (void *)s->nodes,
+                    (void *)s->rows64})
         if (x) (void)hipFree(x);
     *s = SortedStore{};
+}
+
+namespace {
+__global__ void rows64_gather_kernel(const double *__restrict__ f64, uint64_t cap, int F, int FA,
+                                     const uint32_t *__restrict__ ids, uint32_t n_pad, double *__restrict__ rows64) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread per (slot, column)
+    if (t >= (uint64_t)n_pad * FA) return;
+    const uint32_t p = (uint32_t)(t / FA);
+    const int f = (int)(t % FA);
+    const uint32_t id = ids[p];
+    rows64[t] = f >= F ? 0.0 : (id == kNoId ? __builtin_nan("") : f64[(uint64_t)f * cap + id]);
+}
+}  // namespace
+
+hipError_t build_sorted_rows64(const FeatGeom &g, const double *feat64, uint64_t cap, SortedStore *s, hipStream_t st) {
+    if (s->rows64) (void)hipFree(s->rows64);
+    s->rows64 = nullptr;
+    s->fa = (g.F + 3) & ~3;
+    const uint64_t total = (uint64_t)s->n_pad * s->fa;
+    hipError_t e = hipMalloc(&s->rows64, 8ull * std::max<uint64_t>(total, 1));
+    if (e != hipSuccess) return e;
+    s->bytes += 8ull * total;
+    if (total)
+        hipLaunchKernelGGL(rows64_gather_kernel, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, st, feat64, cap,
+                           g.F, s->fa, s->ids, s->n_pad, s->rows64);
+    return hipGetLastError();
 }
 
 hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, uint64_t cap, uint32_t n,

@@ -666,7 +666,8 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         const uint64_t p = (uint64_t)t * kCullTile + lane;
 #pragma unroll
         for (int r = 0; r < R; ++r) x[r] = rows[(uint64_t)r * n_pad + p];
-        id = ids[p];
+        id = (uint32_t)p;  // lists hold sorted positions; the certificate maps them to ids
+        (void)ids;
     };
     // scan tile tin (index inside its super-tile) against every query whose own box bound
     // lb (held by lane tin + 32 * (g / GH)) is still below its threshold: the tile was
@@ -995,6 +996,86 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(const float *__restric
     if (!ok) fail_list[atomicAdd(fail_count, 1u)] = q;
 }
 
+// The same certificate with one lane per candidate (single screening list per query, the
+// group walk's output): K2 lanes of a wave serve one query, each recomputes its candidate's
+// exact distance (the K2 gathers of a query are in flight together instead of one thread
+// issuing them in turn), ranks it by (distance, id) against its K2 - 1 neighbours with
+// cross-lane reads, and writes itself at its rank if the rank is below out_k.  The proof
+// is the same expression as knn_certify_kernel's on the same values.
+template <int SP, int F, int K2>
+__global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__restrict__ pd,
+                                                               const uint32_t *__restrict__ pi, uint32_t nq,
+                                                               const uint32_t *__restrict__ perm,
+                                                               const double *__restrict__ feat64, uint64_t cap,
+                                                               const uint32_t *__restrict__ pos_ids,
+                                                               const double *__restrict__ rows64,
+                                                               const double *__restrict__ qf64, DevSpace sp,
+                                                               float absmax, double *__restrict__ out_d,
+                                                               uint32_t *__restrict__ out_i, uint32_t out_k,
+                                                               uint32_t *__restrict__ fail_count,
+                                                               uint32_t *__restrict__ fail_list) {
+    static_assert(K2 == 16 || K2 == 32 || K2 == 64, "lanes per query");
+    constexpr int QPB = 256 / K2;
+    const uint32_t qs = blockIdx.x * QPB + threadIdx.x / K2;
+    const int j = (int)(threadIdx.x % K2);
+    const int gbase = (int)(threadIdx.x & 63) - j;  // wave lane of this query's entry 0
+    const bool live = qs < nq;                      // uniform over the query's lanes
+    const float d32 = live ? pd[(size_t)qs * K2 + j] : __builtin_inff();
+    const uint32_t e = live ? pi[(size_t)qs * K2 + j] : kNoId;  // id, or sorted position (rows64)
+    const uint32_t q = live ? perm[qs] : 0u;
+    double qv[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qv[f] = live ? qf64[(size_t)q * F + f] : 0.0;
+    double d = __builtin_inf();
+    uint32_t id = kNoId;
+    if (e != kNoId) {
+        double sv[F];
+        if (rows64) {  // the group walk's lists: one contiguous fp64 row per candidate
+            constexpr int FA = (F + 3) & ~3;
+            id = pos_ids[e];
+            const double2 *r2 = reinterpret_cast<const double2 *>(rows64 + (size_t)e * FA);
+#pragma unroll
+            for (int c = 0; c < FA / 2; ++c) {
+                const double2 v = r2[c];
+                if (2 * c < F) sv[2 * c] = v.x;
+                if (2 * c + 1 < F) sv[2 * c + 1] = v.y;
+            }
+        } else {
+            id = e;
+#pragma unroll
+            for (int f = 0; f < F; ++f) sv[f] = feat64[(uint64_t)f * cap + id];
+        }
+        d = feat_dist<SP, F, SP == OMPL_GPU_SPACE_KCHAIN ? F / 2 : 0>(sv, qv, sp);  // fp64, reference order
+    }
+    uint32_t rank = 0;
+#pragma unroll 4
+    for (int m = 0; m < K2; ++m) {
+        const double dm = __shfl(d, gbase + m);
+        const uint32_t im = (uint32_t)__shfl((int)id, gbase + m);
+        rank += (dm < d || (dm == d && (im < id || (im == id && m < j)))) ? 1u : 0u;
+    }
+    // exact k-th distance = the largest of the first out_k ranks
+    double dk = rank < out_k ? d : -__builtin_inf();
+#pragma unroll
+    for (int o = K2 / 2; o > 0; o >>= 1) dk = fmax(dk, __shfl_xor(dk, o));
+    const bool full = (uint32_t)__shfl((int)id, gbase + K2 - 1) != kNoId;
+    const float L32 = __shfl(d32, gbase + K2 - 1);
+    bool ok = true;
+    if (full) {  // prove that no element outside the list can enter (knn_certify_kernel)
+        double B = absmax;
+        const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_REALVECTOR ? F : 0);
+        for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qv[c]));
+        const double L = (double)L32;
+        ok = dk + screen_error<SP>(sp, B, L) < L * (1.0 - 8.0 * kU);
+    }
+    if (!live) return;
+    if (rank < out_k) {
+        out_d[(size_t)q * out_k + rank] = d;
+        out_i[(size_t)q * out_k + rank] = id;
+    }
+    if (j == 0 && !ok) fail_list[atomicAdd(fail_count, 1u)] = q;
+}
+
 // ---- culled radius search (SE3, R^n) ------------------------------------------------------
 // nearestR (NearestNeighborsGNAT.h:236-245; Linear :135-142: d <= r inclusive, ascending).
 // The bound is fixed, so no step of the walk waits on an earlier result: a wave serves G
@@ -1009,7 +1090,7 @@ template <int SP, int F, int G, bool FILL>
 __global__ __launch_bounds__(64) void radius32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ q32,
-    const uint32_t *__restrict__ perm, uint32_t nq, const double *__restrict__ feat64, uint64_t cap,
+    const uint32_t *__restrict__ perm, uint32_t nq, const double *__restrict__ rows64,
     const double *__restrict__ qf64, DevSpace sp, float absmax, double r, uint64_t *__restrict__ counts,
     const uint64_t *__restrict__ offsets, uint32_t *__restrict__ out_i, double *__restrict__ out_d,
     unsigned long long *__restrict__ counters) {
@@ -1107,10 +1188,16 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
                     ++qscans;
                     bool hit = state_dist32<SP, F>(x, &qrow[g * FS], w0, w1) <= thr[g];  // NaN never hits
                     double dd = 0.0;
-                    if (hit) {
+                    if (hit) {  // exact decision from the sorted fp64 row (coalesced over the tile)
+                        constexpr int FA = (F + 3) & ~3;
                         double sv[F];
+                        const double2 *r2 = reinterpret_cast<const double2 *>(rows64 + p * FA);
 #pragma unroll
-                        for (int f = 0; f < F; ++f) sv[f] = feat64[(uint64_t)f * cap + id];
+                        for (int c = 0; c < FA / 2; ++c) {
+                            const double2 v = r2[c];
+                            if (2 * c < F) sv[2 * c] = v.x;
+                            if (2 * c + 1 < F) sv[2 * c + 1] = v.y;
+                        }
                         dd = feat_dist<SP, F, 0>(sv, qv[g], sp);
                         hit = dd <= r;
                     }
@@ -1282,8 +1369,19 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
                            st, f32, cap, n_end, q32, nq, p.chunk_len, w0, (float)sp.w1, sp.dim, pd, pi);
         timer_end(st);
     }
-    hipLaunchKernelGGL((knn_certify_kernel<SP, F, K2, K>), dim3((nq + 255) / 256), b256, 0, st, pd, pi, p.chunks, nq,
-                       perm, f64, cap, qf64, sp, b.absmax, od, oi, k, fail, fail + 1);
+    if (p.chunks == 1) {
+        constexpr uint32_t QPB = 256 / K2;
+        // the group walk's lists hold positions in the sorted store (rows64 / ids map them)
+        const bool pos = walked && p.cull;
+        if (pos && !ss->rows64) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((knn_certify_wave_kernel<SP, F, K2>), dim3((nq + QPB - 1) / QPB), b256, 0, st, pd, pi, nq,
+                           perm, f64, cap, pos ? ss->ids : nullptr, pos ? ss->rows64 : nullptr, qf64, sp, b.absmax,
+                           od, oi, k, fail, fail + 1);
+    } else {
+        if (p.cull) return hipErrorInvalidValue;  // position lists need the wave certificate
+        hipLaunchKernelGGL((knn_certify_kernel<SP, F, K2, K>), dim3((nq + 255) / 256), b256, 0, st, pd, pi, p.chunks,
+                           nq, perm, f64, cap, qf64, sp, b.absmax, od, oi, k, fail, fail + 1);
+    }
     return hipGetLastError();
 }
 
@@ -1372,6 +1470,9 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
     float *q32u = (float *)(ws + L.q32u), *q32 = (float *)(ws + L.q32);
     uint64_t *counts = (uint64_t *)(ws + L.counts), *offs = (uint64_t *)(ws + L.off);
     const dim3 grid((nq + kRadiusGroup - 1) / kRadiusGroup), b64(64), b256(256);
+    if (!ss->rows64) return hipErrorInvalidValue;
+    (void)f64;
+    (void)cap;
     hipError_t e;
     if (phase == 0) {
         hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys,
@@ -1383,7 +1484,7 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
         hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
         if ((e = hipMemsetAsync(counts + nq, 0, 8, st)) != hipSuccess) return e;
         hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, false>), grid, b64, 0, st, ss->rows, ss->n_pad,
-                           ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, f64, cap, qf64, sp,
+                           ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64, sp,
                            b.absmax, r, counts, nullptr, nullptr, nullptr, nullptr);
         size_t sb = L.scan_bytes, rb = L.red_bytes;
         if ((e = hipcub::DeviceScan::ExclusiveSum(ws + L.scan, sb, counts, offs, (int)nq + 1, st)) != hipSuccess)
@@ -1393,7 +1494,7 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
     }
     timer_begin(st, "radius32_group_kernel");
     hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, true>), grid, b64, 0, st, ss->rows, ss->n_pad,
-                       ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, f64, cap, qf64, sp,
+                       ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64, sp,
                        b.absmax, r, nullptr, offs, out_i, out_d, ss->counters);
     timer_end(st);
     return hipGetLastError();
