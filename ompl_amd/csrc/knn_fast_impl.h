@@ -37,6 +37,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "feat_dist.h"
 #include "kernels.h"
@@ -583,13 +584,59 @@ __device__ __forceinline__ uint32_t fold_tiles(uint64_t m) {  // lanes t and t+3
     return (uint32_t)(m | (m >> 32));
 }
 
+// (distance, id) order of the wave lists
+__device__ __forceinline__ bool lex_less32(float a, uint32_t ia, float b, uint32_t ib) {
+    return a < b || (a == b && ia < ib);
+}
+// one compare-exchange stage of a wave-wide bitonic network: partner lane ^ j, this lane
+// keeps the smaller pair iff `keep_min`
+__device__ __forceinline__ void bitonic_step(float &d, uint32_t &i, int j, bool keep_min) {
+    const float od = __shfl_xor(d, j);
+    const uint32_t oi = (uint32_t)__shfl_xor((int)i, j);
+    const bool other_less = lex_less32(od, oi, d, i);
+    if (other_less == keep_min) {
+        d = od;
+        i = oi;
+    }
+}
+// Merge the wave's candidates (d, i) (non-candidates hold (+inf, kNoId)) into the sorted
+// 64-entry list (Ld, Li) (lane j = entry j): sort the candidates ascending (bitonic, 21
+// stages), reverse them against the list, keep the lane-wise minimum — the 64 smallest of
+// the union, as a bitonic sequence — and sort that (6 stages).  Costs ~27 shuffle stages,
+// against one list shift per candidate for the one-by-one insertion; used when many lanes
+// pass at once (the first tiles of a walk).
+__device__ __forceinline__ void wave_merge_sorted(float &Ld, uint32_t &Li, float d, uint32_t i, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) bitonic_step(d, i, j, ((lane & j) == 0) == ((lane & k) == 0));
+    const float rd = __shfl(d, 63 - lane);
+    const uint32_t ri = (uint32_t)__shfl((int)i, 63 - lane);
+    if (lex_less32(rd, ri, Ld, Li)) {
+        Ld = rd;
+        Li = ri;
+    }
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) bitonic_step(Ld, Li, j, (lane & j) == 0);
+}
+// candidates in one ballot above which the bulk merge is used (OMPL_GPU_BULK overrides, for
+// measurements; 64 = never)
+inline int bulk_threshold(int sp) {
+    static const int env = [] {
+        const char *e = std::getenv("OMPL_GPU_BULK");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (env >= 0) return env;
+    return sp == OMPL_GPU_SPACE_SE3 ? 32 : 8;  // measured: SE3 2.24 / 2.09 / 2.07 / 2.05 ms at 64 / 8 / 16 / 32; R^6 1.60 / 1.12 / 1.13 / 1.21
+}
+
 template <int SP, int F, int K2, int G, bool PK, int MINW, bool QS>
 __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
     const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
     uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi,
-    unsigned long long *__restrict__ counters) {
+    unsigned long long *__restrict__ counters, int bulk) {
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
     constexpr int GH = G / 2;
     static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
@@ -678,6 +725,13 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     // element still has a screened distance >= the final K2-th distance)
     auto offer = [&](int g, float d, uint32_t id) {
             uint64_t bm = __ballot(d < td[g]);
+            if (__popcll(bm) > bulk) {  // many at once: sort-merge (same top K2)
+                const bool c = d < td[g];
+                wave_merge_sorted(Ld[g], Li[g], c ? d : __builtin_inff(), c ? id : kNoId, lane);
+                td[g] = readlane_f(Ld[g], K2 - 1);
+                ti[g] = readlane_u(Li[g], K2 - 1);
+                return;
+            }
             while (bm) {
                 const int l = __builtin_ctzll(bm);
                 bm &= bm - 1;
@@ -1349,7 +1403,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, false, 1, true>), dim3((nq + G - 1) / G),
                                dim3(64), 0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox,
                                ss->nsuper, ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi,
-                               ss->counters);
+                               ss->counters, bulk_threshold(SP));
             timer_end(st);
             walked = true;
         }
