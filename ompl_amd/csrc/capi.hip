@@ -99,7 +99,9 @@ struct ompl_gpu_nn {
     std::vector<uint8_t> removed;
     std::mutex mu;
     DevBuf q, out_d, out_i, ws, ws2, stage, counts, offsets, qoff, ids, dists, sorted_ids, sorted_d, tmp, fb_q, fb_d,
-        fb_i, fb_c, fb_cd, fb_ci;
+        fb_i, fb_c, fb_cd, fb_ci, slab_i, slab_d;
+    uint32_t radius_slab = 64;      // per-query slab of the one-pass radius walk (adapts upward)
+    uint64_t radius_one_pass = 0;   // radius calls answered by the one-pass walk
     DevBuf rrt_n, rrt_pd, rrt_pi;  // device RRT growth: live size, per-block partial minima
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
@@ -593,8 +595,19 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
         HIP_OR_FAIL(h->ws.ensure(radius_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq)));
         uint64_t *d_off = nullptr;
-        HIP_OR_FAIL(launch_radius_fast(h->sp, h->g, h->feat, h->cap, &h->sorted, d_qf, (uint32_t)nq, r, b, h->ws.p,
-                                       h->ws.bytes, 0, &d_off, nullptr, nullptr, h->stream));
+        // one walk: hits go to a fixed slab per query (the slab size adapts to the longest
+        // segment seen); only if some query overflows its slab does a second (fill) walk run
+        uint32_t slab = h->radius_slab;
+        while (slab > 16 && (uint64_t)nq * slab > (1ull << 27)) slab >>= 1;
+        b.slab = slab;
+        HIP_OR_FAIL(h->slab_i.ensure(sizeof(uint32_t) * nq * slab));
+        HIP_OR_FAIL(h->slab_d.ensure(sizeof(double) * nq * slab));
+        {
+            ProfileScope prof(h);
+            HIP_OR_FAIL(launch_radius_fast(h->sp, h->g, h->feat, h->cap, &h->sorted, d_qf, (uint32_t)nq, r, b,
+                                           h->ws.p, h->ws.bytes, 2, &d_off, (uint32_t *)h->slab_i.p,
+                                           (double *)h->slab_d.p, h->stream));
+        }
         uint64_t tm[2] = {0, 0};  // total, longest segment
         HIP_OR_FAIL(hipMemcpyAsync(tm, d_off + nq, sizeof(tm), hipMemcpyDeviceToHost, h->stream));
         HIP_OR_FAIL(hipMemcpyAsync(d_qoff, d_off, sizeof(uint64_t) * (nq + 1), hipMemcpyDeviceToDevice, h->stream));
@@ -603,17 +616,29 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
         if (tm[0] == 0) return OMPL_GPU_OK;
         if (tm[0] > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "radius result above 2^31 entries");
         const uint64_t tot = tm[0];
+        if (tm[1] <= slab) {  // every segment is complete in its slab: sort into the CSR result
+            h->radius_one_pass += 1;
+            HIP_OR_FAIL(h->sorted_ids.ensure(sizeof(uint32_t) * tot));
+            HIP_OR_FAIL(h->sorted_d.ensure(sizeof(double) * tot));
+            uint32_t *si = (uint32_t *)h->sorted_ids.p;
+            double *sd = (double *)h->sorted_d.p;
+            HIP_OR_FAIL(launch_segment_rank_sort(d_qoff, (const uint32_t *)h->slab_i.p, (const double *)h->slab_d.p,
+                                                 (uint32_t)nq, si, sd, h->stream, slab));
+            *res_i = si;
+            *res_d = sd;
+            return OMPL_GPU_OK;
+        }
+        uint32_t grow = 16;
+        while (grow < tm[1] && grow < kRankSortMax) grow <<= 1;
+        h->radius_slab = grow;  // the next call's slab holds this call's longest segment
         HIP_OR_FAIL(h->ids.ensure(sizeof(uint32_t) * tot));
         HIP_OR_FAIL(h->dists.ensure(sizeof(double) * tot));
         HIP_OR_FAIL(h->sorted_ids.ensure(sizeof(uint32_t) * tot));
         HIP_OR_FAIL(h->sorted_d.ensure(sizeof(double) * tot));
         uint32_t *ui = (uint32_t *)h->ids.p, *si = (uint32_t *)h->sorted_ids.p;
         double *ud = (double *)h->dists.p, *sd = (double *)h->sorted_d.p;
-        {
-            ProfileScope prof(h);
-            HIP_OR_FAIL(launch_radius_fast(h->sp, h->g, h->feat, h->cap, &h->sorted, d_qf, (uint32_t)nq, r, b, h->ws.p,
-                                           h->ws.bytes, 1, &d_off, ui, ud, h->stream));
-        }
+        HIP_OR_FAIL(launch_radius_fast(h->sp, h->g, h->feat, h->cap, &h->sorted, d_qf, (uint32_t)nq, r, b, h->ws.p,
+                                       h->ws.bytes, 1, &d_off, ui, ud, h->stream));
         if (tm[1] <= kRankSortMax) {
             HIP_OR_FAIL(launch_segment_rank_sort(d_qoff, ui, ud, (uint32_t)nq, si, sd, h->stream));
             *res_i = si;

@@ -64,6 +64,7 @@ struct FastBounds {
     float lo[kKeyDims], inv[kKeyDims];  // key box (inv = 1 / extent) of the first nkey key coordinates
     int nkey;                           // SE3: 6 (translation + canonical quaternion xyz); R^n: min(n, 6); SO3: 0
     float absmax;                       // max |coordinate| stored (error bound of the fp32 screen)
+    uint32_t slab = 0;                  // radius phase 2: hits kept per query (slab capacity)
 };
 
 // Spatially sorted fp32 copy of the store for the group walk (SE3 and R^n): states in k-d
@@ -154,15 +155,18 @@ size_t radius_fast_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32
 // phase 0: queries ordered on the Morton curve and their hits counted; *d_offsets (device,
 // inside ws) then holds nq + 2 entries: the exclusive offsets [0, nq] (so [nq] = total) and
 // the longest segment at [nq + 1].  phase 1 (same ws, same queries): every hit's (id, fp64
-// distance) written into its query's segment, in walk order.
+// distance) written into its query's segment, in walk order.  phase 2 (one pass): like
+// phase 0, and the first b.slab hits of query q are written to out_i / out_d [q * b.slab ..]
+// in walk order; if the longest segment fits in the slab, no phase 1 is needed.
 hipError_t launch_radius_fast(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap,
                               const SortedStore *sorted, const double *qfeat64, uint32_t nq, double r,
                               const FastBounds &b, void *ws, size_t ws_bytes, int phase, uint64_t **d_offsets,
                               uint32_t *out_i, double *out_d, hipStream_t st);
 // sort every CSR segment (at most kRankSortMax long) by (distance, id): rank placement in LDS
 constexpr uint32_t kRankSortMax = 1024;
+// in_stride != 0: segment q is read from [q * in_stride, ...) (a radius slab) instead of offsets[q]
 hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_i, const double *in_d, uint32_t nq,
-                                    uint32_t *out_i, double *out_d, hipStream_t st);
+                                    uint32_t *out_i, double *out_d, hipStream_t st, uint32_t in_stride = 0);
 // motion endpoints of neighbour results: edge e pairs query q with stored state ids[e]
 // (CSR offsets, or offsets == nullptr and e = q * stride + j)
 hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,

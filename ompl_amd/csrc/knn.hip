@@ -433,16 +433,17 @@ __global__ __launch_bounds__(64) void segment_rank_sort_kernel(const uint64_t *_
                                                                const uint32_t *__restrict__ in_i,
                                                                const double *__restrict__ in_d,
                                                                uint32_t *__restrict__ out_i,
-                                                               double *__restrict__ out_d) {
+                                                               double *__restrict__ out_d, uint32_t in_stride) {
     __shared__ double sd[kRankSortMax];
     __shared__ uint32_t si[kRankSortMax];
     const uint32_t q = blockIdx.x;
     const uint64_t b = off[q];
     const uint32_t L = (uint32_t)(off[q + 1] - b);
     if (L > kRankSortMax) return;  // the caller sorts with radix passes instead
+    const uint64_t ib = in_stride ? (uint64_t)q * in_stride : b;
     for (uint32_t j = threadIdx.x; j < L; j += blockDim.x) {
-        sd[j] = in_d[b + j];
-        si[j] = in_i[b + j];
+        sd[j] = in_d[ib + j];
+        si[j] = in_i[ib + j];
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < L; j += blockDim.x) {
@@ -726,9 +727,10 @@ hipError_t launch_store_soa(const double *aos, uint32_t n, int width, double *so
 }
 
 hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_i, const double *in_d, uint32_t nq,
-                                    uint32_t *out_i, double *out_d, hipStream_t st) {
+                                    uint32_t *out_i, double *out_d, hipStream_t st, uint32_t in_stride) {
     if (nq == 0) return hipSuccess;
-    hipLaunchKernelGGL(segment_rank_sort_kernel, dim3(nq), dim3(64), 0, st, offsets, in_i, in_d, out_i, out_d);
+    hipLaunchKernelGGL(segment_rank_sort_kernel, dim3(nq), dim3(64), 0, st, offsets, in_i, in_d, out_i, out_d,
+                       in_stride);
     return hipGetLastError();
 }
 

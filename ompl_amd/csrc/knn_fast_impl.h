@@ -1140,16 +1140,19 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
 // kept element is then decided by its exact fp64 distance in the reference's operation
 // order.  FILL = false counts the hits of each query, FILL = true writes (id, d) into the
 // query's CSR segment in tile order; the caller sorts each segment by (distance, id).
-template <int SP, int F, int G, bool FILL>
+// MODE 2 (SLAB) counts like MODE 0 and also writes the first `slab` hits of each query to its
+// fixed-size slab, so that one walk suffices when no query has more hits than that.
+template <int SP, int F, int G, int MODE>
 __global__ __launch_bounds__(64) void radius32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ q32,
     const uint32_t *__restrict__ perm, uint32_t nq, const double *__restrict__ rows64,
     const double *__restrict__ qf64, DevSpace sp, float absmax, double r, uint64_t *__restrict__ counts,
     const uint64_t *__restrict__ offsets, uint32_t *__restrict__ out_i, double *__restrict__ out_d,
-    unsigned long long *__restrict__ counters) {
+    unsigned long long *__restrict__ counters, uint32_t slab) {
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
     constexpr int GH = G / 2;
+    constexpr bool FILL = MODE == 1, SLAB = MODE == 2;
     static_assert(G % 2 == 0, "radius walk shape");
     __shared__ __attribute__((aligned(16))) float qrow[G * FS];
     const int lane = threadIdx.x;
@@ -1261,6 +1264,13 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
                         out_i[pos] = id;
                         out_d[pos] = dd;
                     }
+                    if (SLAB && hit) {
+                        const uint64_t j = cnt[g] + (uint64_t)__popcll(bm & lt);
+                        if (j < slab) {
+                            out_i[(uint64_t)qo[g] * slab + j] = id;
+                            out_d[(uint64_t)qo[g] * slab + j] = dd;
+                        }
+                    }
                     cur[g] += (uint64_t)__popcll(bm);
                     cnt[g] += (uint64_t)__popcll(bm);
                 }
@@ -1272,7 +1282,8 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
 #pragma unroll
             for (int g = 0; g < G; ++g)
                 if (g0 + g < nq) counts[qo[g]] = cnt[g];
-        } else if (counters) {
+        }
+        if (MODE != 0 && counters) {
             atomicAdd(&counters[3], (unsigned long long)visited);  // tiles fetched by the radius walk
             atomicAdd(&counters[4], (unsigned long long)qscans);   // (tile, query) pairs scanned
         }
@@ -1528,7 +1539,8 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
     (void)f64;
     (void)cap;
     hipError_t e;
-    if (phase == 0) {
+    if (phase == 2 && (b.slab == 0 || !out_i || !out_d)) return hipErrorInvalidValue;
+    if (phase == 0 || phase == 2) {
         hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys,
                            idx, ss->nodes, ss->kd_tiles);
         size_t cb = L.cub_bytes;
@@ -1537,9 +1549,17 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
             return e;
         hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
         if ((e = hipMemsetAsync(counts + nq, 0, 8, st)) != hipSuccess) return e;
-        hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, false>), grid, b64, 0, st, ss->rows, ss->n_pad,
-                           ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64, sp,
-                           b.absmax, r, counts, nullptr, nullptr, nullptr, nullptr);
+        if (phase == 2) {
+            timer_begin(st, "radius32_group_kernel");
+            hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 2>), grid, b64, 0, st, ss->rows, ss->n_pad,
+                               ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64,
+                               sp, b.absmax, r, counts, nullptr, out_i, out_d, ss->counters, b.slab);
+            timer_end(st);
+        } else {
+            hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 0>), grid, b64, 0, st, ss->rows, ss->n_pad,
+                               ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64,
+                               sp, b.absmax, r, counts, nullptr, nullptr, nullptr, nullptr, 0u);
+        }
         size_t sb = L.scan_bytes, rb = L.red_bytes;
         if ((e = hipcub::DeviceScan::ExclusiveSum(ws + L.scan, sb, counts, offs, (int)nq + 1, st)) != hipSuccess)
             return e;
@@ -1547,9 +1567,9 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
         return hipGetLastError();
     }
     timer_begin(st, "radius32_group_kernel");
-    hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, true>), grid, b64, 0, st, ss->rows, ss->n_pad,
+    hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 1>), grid, b64, 0, st, ss->rows, ss->n_pad,
                        ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64, sp,
-                       b.absmax, r, nullptr, offs, out_i, out_d, ss->counters);
+                       b.absmax, r, nullptr, offs, out_i, out_d, ss->counters, 0u);
     timer_end(st);
     return hipGetLastError();
 }

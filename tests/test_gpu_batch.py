@@ -52,6 +52,10 @@ def test_radius_culled_vs_oracle(gpu, name, mode):
         off = _check_radius(nn, sp, data, q, r)
         if r == 0.0:
             assert (np.diff(off)[:5] >= 1).all()
+    # the largest radius again: its longest segment overflowed the one-pass walk's first slab
+    # (64 hits) above, so this call runs the single walk with the grown slab
+    assert np.diff(off).max() > 64
+    _check_radius(nn, sp, data, q, radii[-1])
     if mode == 0:
         tiles, pairs = nn.radius_cull_stats()
         assert 0 < tiles <= pairs
