@@ -110,6 +110,8 @@ struct ompl_gpu_nn {
     SortedStore sorted;
     FastBounds sorted_bounds{};
     bool sorted_dirty = true;
+    DevBuf raw_aos;         // [n_total][da] fp64 raw states by id (edge endpoints), rebuilt lazily
+    bool aos_dirty = true;
     bool cull = true;         // ompl_gpu_nn_set_exact(h, 2) disables the culled screen
     DevBuf cull_counter;      // SortedStore::counters: kNN walk [tiles fetched, tiles of a brute-force
                               // walk, (tile, query) pairs scanned], radius walk [tiles, pairs] (device)
@@ -329,6 +331,7 @@ ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, 
     // screening bounds (knn_fast.hip): key box of the first <= 6 coordinates, max |coordinate|
     const int nb = tracked_dims(h->sp);
     h->sorted_dirty = true;
+    h->aos_dirty = true;
     const int na = h->sp.kind == OMPL_GPU_SPACE_SE3 ? 3 : (h->sp.kind == OMPL_GPU_SPACE_SO3 ? 0 : dim);
     for (size_t i = 0; i < n; ++i) {
         const double *s = states + i * dim;
@@ -360,6 +363,7 @@ ompl_gpu_status ompl_gpu_nn_remove(ompl_gpu_nn *h, uint64_t id) {
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     h->removed[id] = 1;
     h->sorted_dirty = true;
+    h->aos_dirty = true;
     h->n_live--;
     return OMPL_GPU_OK;
 }
@@ -378,6 +382,7 @@ ompl_gpu_status ompl_gpu_nn_clear(ompl_gpu_nn *h) {
     h->n_total = h->n_live = 0;
     h->absmax = 0.0;
     h->sorted_dirty = true;
+    h->aos_dirty = true;
     h->removed.clear();
     return OMPL_GPU_OK;
 }
@@ -811,8 +816,16 @@ ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries
     if (m == 0) return OMPL_GPU_OK;
     if (nq == 0 || nq > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_INVALID_ARG, "query count out of range");
     HIP_OR_FAIL(hipSetDevice(h->device));
+    // endpoints are gathered by random id: one contiguous row per state instead of one cache
+    // line per coordinate of the SoA store
+    const int da = (h->sp.dim + 1) & ~1;
+    if (h->aos_dirty && h->n_total) {
+        HIP_OR_FAIL(h->raw_aos.ensure(sizeof(double) * h->n_total * da));
+        HIP_OR_FAIL(launch_aos_rows(h->raw, h->cap, h->sp.dim, da, h->n_total, (double *)h->raw_aos.p, h->stream));
+        h->aos_dirty = false;
+    }
     HIP_OR_FAIL(launch_edges(h->sp, h->raw, h->cap, d_queries, (uint32_t)nq, d_offsets, d_ids, stride, m, from_query,
-                             d_from, d_to, h->stream));
+                             d_from, d_to, h->stream, h->n_total ? (const double *)h->raw_aos.p : nullptr, da));
     return OMPL_GPU_OK;
 }
 
@@ -1138,6 +1151,7 @@ ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const 
     h->n_total = n1;
     h->removed.resize(h->n_total, 0);
     h->sorted_dirty = true;
+    h->aos_dirty = true;
     return OMPL_GPU_OK;
 }
 

@@ -169,9 +169,11 @@ hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_
                                     uint32_t *out_i, double *out_d, hipStream_t st, uint32_t in_stride = 0);
 // motion endpoints of neighbour results: edge e pairs query q with stored state ids[e]
 // (CSR offsets, or offsets == nullptr and e = q * stride + j)
+// aos (optional): [n][da] copy of the raw states (launch_aos_rows), read instead of the SoA store
 hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
                         const uint64_t *offsets, const uint32_t *ids, uint32_t stride, uint64_t m, int from_query,
-                        double *from, double *to, hipStream_t st);
+                        double *from, double *to, hipStream_t st, const double *aos = nullptr, int da = 0);
+hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uint64_t n, double *aos, hipStream_t st);
 // ---- RRT growth on device (rrt.hip) -------------------------------------------------------
 size_t rrt_part_entries(uint64_t n_max);
 hipError_t launch_rrt_grow(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck, const FeatGeom &g,

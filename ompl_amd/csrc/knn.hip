@@ -463,7 +463,7 @@ __global__ __launch_bounds__(64) void segment_rank_sort_kernel(const uint64_t *_
 __global__ void edges_kernel(DevSpace sp, const double *__restrict__ raw, uint64_t cap, const double *__restrict__ q,
                              uint32_t nq, const uint64_t *__restrict__ off, const uint32_t *__restrict__ ids,
                              uint32_t stride, uint64_t m, int from_query, double *__restrict__ from,
-                             double *__restrict__ to) {
+                             double *__restrict__ to, const double *__restrict__ aos, int da) {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= m) return;
     uint32_t qi;
@@ -487,7 +487,7 @@ __global__ void edges_kernel(DevSpace sp, const double *__restrict__ raw, uint64
     for (int c = 0; c < dim; ++c) {
         const double qv = q[(size_t)qi * dim + c];
         qd[c] = qv;
-        nd[c] = id == kNoId ? qv : raw[(uint64_t)c * cap + id];
+        nd[c] = id == kNoId ? qv : (aos ? aos[(uint64_t)id * da + c] : raw[(uint64_t)c * cap + id]);
     }
 }
 
@@ -736,10 +736,26 @@ hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_
 
 hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
                         const uint64_t *offsets, const uint32_t *ids, uint32_t stride, uint64_t m, int from_query,
-                        double *from, double *to, hipStream_t st) {
+                        double *from, double *to, hipStream_t st, const double *aos, int da) {
     if (m == 0) return hipSuccess;
     hipLaunchKernelGGL(edges_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, sp, raw, cap, q, nq, offsets,
-                       ids, stride, m, from_query, from, to);
+                       ids, stride, m, from_query, from, to, aos, da);
+    return hipGetLastError();
+}
+
+__global__ void aos_rows_kernel(const double *__restrict__ soa, uint64_t cap, int dim, int da, uint64_t n,
+                                double *__restrict__ aos) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread per (state, column)
+    if (t >= n * da) return;
+    const uint64_t i = t / da;
+    const int c = (int)(t % da);
+    aos[t] = c < dim ? soa[(uint64_t)c * cap + i] : 0.0;
+}
+
+hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uint64_t n, double *aos, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(aos_rows_kernel, dim3((unsigned)((n * da + 255) / 256)), dim3(256), 0, st, soa, cap, dim, da, n,
+                       aos);
     return hipGetLastError();
 }
 
