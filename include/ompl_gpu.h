@@ -234,6 +234,14 @@ ompl_gpu_status ompl_gpu_mv_reset_counters(ompl_gpu_mv *h);
 ompl_gpu_status ompl_gpu_mv_state_checks(ompl_gpu_mv *h, uint64_t *checks);
 /* isValid per state (host AoS). */
 ompl_gpu_status ompl_gpu_svc_check(ompl_gpu_mv *h, const double *states, size_t m, uint8_t *valid);
+/* SpaceInformation::getMotionStates(s1, s2, states, count, endpoints, alloc = true)
+ * (src/ompl/base/src/SpaceInformation.cpp:201-275) for m motions: out = [m][per][dim] with
+ * per = count + (endpoints ? 2 : 0) = the function's return value — [s1], the states at
+ * j / (count + 1) for j in [1, count], [s2].  Host AoS / device-resident variants. */
+ompl_gpu_status ompl_gpu_mv_motion_states(ompl_gpu_mv *h, const double *s1, const double *s2, size_t m,
+                                          uint32_t count, int endpoints, double *out);
+ompl_gpu_status ompl_gpu_mv_motion_states_device(ompl_gpu_mv *h, const double *d_s1, const double *d_s2, size_t m,
+                                                 uint32_t count, int endpoints, double *d_out);
 
 /* ---- RRT growth on device ----------------------------------------------------
  * The RRT loop (RRT.cpp:128-192) without its goal test, for ns samples in order: nearest

@@ -102,6 +102,8 @@ SIGNATURES = {
     "ompl_gpu_mv_reset_counters": (C.c_int, [_P]),
     "ompl_gpu_mv_state_checks": (C.c_int, [_P, _U64]),
     "ompl_gpu_svc_check": (C.c_int, [_P, _D, C.c_size_t, _U8]),
+    "ompl_gpu_mv_motion_states": (C.c_int, [_P, _D, _D, C.c_size_t, C.c_uint32, C.c_int, _D]),
+    "ompl_gpu_mv_motion_states_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_uint32, C.c_int, _P]),
 }
 
 

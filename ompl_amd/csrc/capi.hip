@@ -187,7 +187,7 @@ struct ompl_gpu_mv {
     double *ck_data = nullptr;
     unsigned long long *counters = nullptr;  // valid, invalid, isValid calls
     std::mutex mu;
-    DevBuf s1, s2, valid, nd, fi;
+    DevBuf s1, s2, valid, nd, fi, ms;
 };
 
 extern "C" {
@@ -1096,6 +1096,41 @@ ompl_gpu_status ompl_gpu_svc_check(ompl_gpu_mv *h, const double *states, size_t 
     HIP_OR_FAIL(hipMemcpyAsync(h->s1.p, states, sb, hipMemcpyHostToDevice, h->stream));
     HIP_OR_FAIL(launch_state_valid(h->sp, h->ck, (const double *)h->s1.p, (uint32_t)m, (uint8_t *)h->valid.p, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(valid, h->valid.p, m, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_motion_states_device(ompl_gpu_mv *h, const double *d_s1, const double *d_s2, size_t m,
+                                                 uint32_t count, int endpoints, double *d_out) {
+    const uint64_t per = motion_states_per(count, endpoints);
+    if (!h || (m && per && (!d_s1 || !d_s2 || !d_out))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if ((uint64_t)m * per > 0xFFFFFFFFull || m > 0xFFFFFFFFull)
+        return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many motion states in one call");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (m == 0 || per == 0) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(launch_motion_states(h->sp, d_s1, d_s2, (uint32_t)m, count, endpoints ? 1 : 0, d_out, h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_motion_states(ompl_gpu_mv *h, const double *s1, const double *s2, size_t m,
+                                          uint32_t count, int endpoints, double *out) {
+    const uint64_t per = motion_states_per(count, endpoints);
+    if (!h || (m && per && (!s1 || !s2 || !out))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if ((uint64_t)m * per > 0xFFFFFFFFull || m > 0xFFFFFFFFull)
+        return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many motion states in one call");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (m == 0 || per == 0) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    const size_t sb = sizeof(double) * m * h->sp.dim, ob = sb * per;
+    HIP_OR_FAIL(h->s1.ensure(sb));
+    HIP_OR_FAIL(h->s2.ensure(sb));
+    HIP_OR_FAIL(h->ms.ensure(ob));
+    HIP_OR_FAIL(hipMemcpyAsync(h->s1.p, s1, sb, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(h->s2.p, s2, sb, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(launch_motion_states(h->sp, (const double *)h->s1.p, (const double *)h->s2.p, (uint32_t)m, count,
+                                     endpoints ? 1 : 0, (double *)h->ms.p, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(out, h->ms.p, ob, hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     return OMPL_GPU_OK;
 }

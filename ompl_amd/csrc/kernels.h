@@ -213,5 +213,9 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
                          hipStream_t st);
 hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const double *s, uint32_t m, uint8_t *valid,
                               hipStream_t st);
+// getMotionStates: states per motion (SpaceInformation.cpp:201-275 with alloc = true)
+inline uint32_t motion_states_per(uint32_t count, int endpoints) { return count + (endpoints ? 2u : 0u); }
+hipError_t launch_motion_states(const DevSpace &sp, const double *s1, const double *s2, uint32_t m, uint32_t count,
+                                int endpoints, double *out, hipStream_t st);
 
 }  // namespace ompl_amd

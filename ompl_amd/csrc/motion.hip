@@ -130,6 +130,44 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
     return hipGetLastError();
 }
 
+// SpaceInformation::getMotionStates (SpaceInformation.cpp:201-275, alloc = true): thread per
+// (motion, output slot); slot k of a motion is s1 (k = 0 with endpoints), s2 (last slot with
+// endpoints), else the interior sample j = k (+1 without endpoints) at t = j / (count + 1)
+__global__ __launch_bounds__(256) void motion_states_kernel(DevSpace sp, const double *__restrict__ s1,
+                                                            const double *__restrict__ s2, uint32_t m, uint32_t count,
+                                                            int endpoints, uint32_t per, double *__restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)m * per) return;
+    const uint32_t e = (uint32_t)(t / per), k = (uint32_t)(t % per);
+    const int dim = sp.dim;
+    double *o = out + t * dim;
+    const double *a = s1 + (size_t)e * dim, *b = s2 + (size_t)e * dim;
+    if (endpoints && k == 0) {
+        for (int c = 0; c < dim; ++c) o[c] = a[c];
+        return;
+    }
+    if (endpoints && k == per - 1) {
+        for (int c = 0; c < dim; ++c) o[c] = b[c];
+        return;
+    }
+    const uint32_t j = endpoints ? k : k + 1;
+    double x[kChainMaxLinks], y[kChainMaxLinks], r[kChainMaxLinks];
+    load_state(a, dim, x);
+    load_state(b, dim, y);
+    interpolate(sp, x, y, (double)j / (double)(count + 1), r);
+    for (int c = 0; c < dim; ++c) o[c] = r[c];
+}
+
+hipError_t launch_motion_states(const DevSpace &sp, const double *s1, const double *s2, uint32_t m, uint32_t count,
+                                int endpoints, double *out, hipStream_t st) {
+    const uint32_t per = motion_states_per(count, endpoints);
+    const uint64_t n = (uint64_t)m * per;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(motion_states_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sp, s1, s2, m, count,
+                       endpoints, per, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const double *s, uint32_t m, uint8_t *valid,
                               hipStream_t st) {
     if (m == 0) return hipSuccess;

@@ -86,6 +86,21 @@ class DiscreteMotionValidatorGPU:
         abi.check(abi.lib.ompl_gpu_svc_check(self._h, abi.dptr(s), s.shape[0], out.ctypes.data_as(abi._U8)))
         return out.astype(bool)
 
+    def getMotionStates(self, s1, s2, count: int, endpoints: bool = True) -> np.ndarray:
+        """SpaceInformation::getMotionStates (SpaceInformation.cpp:201-275, alloc = true) for a
+        batch of motions: [m, count + (2 if endpoints else 0), dim]."""
+        a = abi.as_states(s1, self.dim)
+        b = abi.as_states(s2, self.dim)
+        if a.shape != b.shape:
+            raise ValueError("s1 and s2 must have the same shape")
+        if count < 0:
+            raise ValueError("count must be >= 0")
+        per = count + (2 if endpoints else 0)
+        out = np.zeros((a.shape[0], per, self.dim))
+        abi.check(abi.lib.ompl_gpu_mv_motion_states(self._h, abi.dptr(a), abi.dptr(b), a.shape[0], int(count),
+                                                    int(bool(endpoints)), abi.dptr(out)))
+        return out
+
     # device-resident
     def set_stream(self, stream_ptr: int | None) -> None:
         abi.check(abi.lib.ompl_gpu_mv_set_stream(self._h, C.c_void_p(stream_ptr or 0)))

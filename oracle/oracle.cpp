@@ -201,6 +201,36 @@ double oracle_distance(const ompl_gpu_space *sp, const double *a, const double *
     return std::numeric_limits<double>::quiet_NaN();
 }
 
+// SpaceInformation::getMotionStates with alloc = true — SpaceInformation.cpp:201-275: count
+// is raised by one to the number of segments; fewer than 2 segments yield only the
+// endpoints (when asked for); otherwise [s1], interpolate(j / segments) for j in
+// [1, segments - 1], [s2]
+uint32_t oracle_motion_states(const ompl_gpu_space *sp, const double *s1, const double *s2, size_t m,
+                              uint32_t count, int endpoints, double *out) {
+    const uint32_t segs = count + 1;
+    const uint32_t per = segs < 2 ? (endpoints ? 2u : 0u) : segs + (endpoints ? 1u : 0u) - (endpoints ? 0u : 1u);
+    const int dim = sp->dim;
+    for (size_t e = 0; e < m; ++e) {
+        const double *a = s1 + e * dim, *b = s2 + e * dim;
+        double *o = out + e * per * dim;
+        uint32_t added = 0;
+        if (endpoints && per > 0) {
+            std::copy(a, a + dim, o);
+            ++added;
+        }
+        if (segs >= 2)
+            for (uint32_t j = 1; j < segs && added < per; ++j) {
+                oracle_interpolate(sp, a, b, (double)j / (double)segs, o + (size_t)added * dim);
+                ++added;
+            }
+        if (added < per && endpoints) {
+            std::copy(b, b + dim, o + (size_t)added * dim);
+            ++added;
+        }
+    }
+    return per;
+}
+
 // CompoundStateSpace::interpolate — StateSpace.cpp:1109-1116
 void oracle_interpolate(const ompl_gpu_space *sp, const double *from, const double *to, double t, double *out) {
     switch (sp->kind) {

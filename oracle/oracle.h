@@ -39,6 +39,10 @@ double oracle_distance(const ompl_gpu_space *sp, const double *a, const double *
 void oracle_interpolate(const ompl_gpu_space *sp, const double *from, const double *to, double t,
                         double *out);
 uint32_t oracle_valid_segment_count(const ompl_gpu_space *sp, const double *a, const double *b);
+/* SpaceInformation::getMotionStates(s1, s2, states, count, endpoints, alloc = true) for m
+ * motions; out = [m][count + (endpoints ? 2 : 0)][dim]; returns the states per motion. */
+uint32_t oracle_motion_states(const ompl_gpu_space *sp, const double *s1, const double *s2, size_t m,
+                              uint32_t count, int endpoints, double *out);
 
 /* ---- validity + motion -------------------------------------------------- */
 int oracle_is_valid(const ompl_gpu_space *sp, const ompl_gpu_checker *ck, const double *s);

@@ -28,6 +28,7 @@ _ORACLE_SIGS = {
     "oracle_distance": (C.c_double, [_SP, _D, _D]),
     "oracle_interpolate": (None, [_SP, _D, _D, C.c_double, _D]),
     "oracle_valid_segment_count": (C.c_uint32, [_SP, _D, _D]),
+    "oracle_motion_states": (C.c_uint32, [_SP, _D, _D, C.c_size_t, C.c_uint32, C.c_int, _D]),
     "oracle_is_valid": (C.c_int, [_SP, _CK, _D]),
     "oracle_check_motions": (C.c_uint64, [_SP, _CK, _D, _D, C.c_size_t, _U8, _I32, _I32]),
     "oracle_check_motions_mt": (C.c_uint64, [_SP, _CK, _D, _D, C.c_size_t, _U8, C.c_int]),
@@ -75,6 +76,18 @@ def interpolate(sp, a, b, t) -> np.ndarray:
     a, b = _arr(a), _arr(b)
     o = np.empty(sp.dim)
     lib.oracle_interpolate(C.byref(s), abi.dptr(a), abi.dptr(b), float(t), abi.dptr(o))
+    return o
+
+
+def motion_states(sp, s1, s2, count, endpoints=True) -> np.ndarray:
+    """getMotionStates for each motion: [m, count + (2 if endpoints else 0), dim]."""
+    s = sp.to_abi()
+    a, b = abi.as_states(s1, sp.dim), abi.as_states(s2, sp.dim)
+    per = count + (2 if endpoints else 0)
+    o = np.zeros((a.shape[0], per, sp.dim))
+    got = lib.oracle_motion_states(C.byref(s), abi.dptr(a), abi.dptr(b), a.shape[0], count, int(endpoints),
+                                   abi.dptr(o))
+    assert got == per
     return o
 
 

@@ -91,3 +91,31 @@ def test_state_validity_random(gpu):
     x = W.uniform_chain(rng, 50000, 12)
     mv = DiscreteMotionValidatorGPU(sp, ck, gpu)
     np.testing.assert_array_equal(mv.isValid(x), O.is_valid(sp, ck, x))
+
+
+@pytest.mark.parametrize("name", ["se3", "so3", "r6", "chain12"])
+@pytest.mark.parametrize("count,endpoints", [(0, True), (0, False), (1, True), (7, False), (12, True)])
+def test_get_motion_states(gpu, name, count, endpoints):
+    """SpaceInformation::getMotionStates (SpaceInformation.cpp:201-275, alloc = true) on the
+    device against the oracle: same number of states, endpoints copied, interior samples at
+    j / (count + 1).  R^n and the chain (arithmetic only) are bit-identical; SO3 / SE3 slerp
+    differs from glibc only through sin / acos (a few ulps)."""
+    from ompl_amd.spaces import SO3StateSpace
+    rng = np.random.default_rng(91)
+    sp = {"se3": SE3StateSpace, "so3": SO3StateSpace, "r6": lambda: RealVectorStateSpace(6),
+          "chain12": lambda: KinematicChainSpace(12, 1.0 / 12)}[name]()
+    sample = {"se3": lambda n: W.uniform_se3(rng, n), "so3": lambda n: W.uniform_quat(rng, n),
+              "r6": lambda n: W.uniform_rv(rng, n, 6), "chain12": lambda n: W.uniform_chain(rng, n, 12)}[name]
+    a, b = sample(300), sample(300)
+    a[:3] = b[:3]  # zero-length motions
+    mv = DiscreteMotionValidatorGPU(sp, AllValidChecker(), gpu)
+    got = mv.getMotionStates(a, b, count, endpoints)
+    want = O.motion_states(sp, a, b, count, endpoints)
+    assert got.shape == want.shape == (300, count + (2 if endpoints else 0), sp.dim)
+    if name in ("r6", "chain12"):
+        np.testing.assert_array_equal(got, want)
+    else:
+        np.testing.assert_allclose(got, want, rtol=0, atol=4e-15)
+    if endpoints:
+        np.testing.assert_array_equal(got[:, 0], a)
+        np.testing.assert_array_equal(got[:, -1], b)
