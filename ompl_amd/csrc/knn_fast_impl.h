@@ -784,6 +784,20 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             hi = mid;
     }
     const uint32_t s0 = (lo > 0 ? lo - 1 : 0) / kSuperTiles;
+    // scan the middle query's home tile (its k-d leaf) first, for every query of the group:
+    // the thresholds start near the final K2-th distances, so the box tests that follow
+    // exclude more tiles; the home tile is then dropped from its super-tile's mask
+    const uint32_t th = min(key, ntiles - 1);
+    {
+        float x[R];
+        uint32_t id;
+        load_state(th, x, id);
+        float lbh[GH];
+#pragma unroll
+        for (int j = 0; j < GH; ++j) lbh[j] = -__builtin_inff();
+        scan_state(x, id, 0, lbh);
+        ++visited;
+    }
     // visit order: s0 - 1, s0, s0 + 1 (the group's neighbourhood, which sets the thresholds),
     // then every other super-tile in curve order whose box passes, 64 box tests at a time
     uint32_t base = s0 > 0 ? s0 - 1 : 0;
@@ -825,6 +839,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     while (s >= 0) {
         float lb[GH];
         uint32_t m = tile_mask(bx, lb);
+        if ((uint32_t)s == th / kSuperTiles) m &= ~(1u << (th % kSuperTiles));  // scanned first
         const int sn = next_super();
         float x[R], xn[R];
         uint32_t id = kNoId, idn = kNoId;
