@@ -627,7 +627,7 @@ inline int bulk_threshold(int sp) {
         return e ? std::atoi(e) : -1;
     }();
     if (env >= 0) return env;
-    return sp == OMPL_GPU_SPACE_SE3 ? 32 : 8;  // measured: SE3 2.24 / 2.09 / 2.07 / 2.05 ms at 64 / 8 / 16 / 32; R^6 1.60 / 1.12 / 1.13 / 1.21
+    return 8;  // measured (G = 4): SE3 1.58 / 1.42 / 1.41 ms at 64 / 8 / 32; R^6 1.60 / 1.12 / 1.13 / 1.21 at 64 / 8 / 16 / 32
 }
 
 template <int SP, int F, int K2, int G, bool PK, int MINW, bool QS>
@@ -1426,10 +1426,26 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             constexpr int G = group_queries<SP>();
-            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, false, 1, true>), dim3((nq + G - 1) / G),
-                               dim3(64), 0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox,
-                               ss->nsuper, ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi,
-                               ss->counters, bulk_threshold(SP));
+            static const int genv = [] {
+                const char *e = std::getenv("OMPL_GPU_GROUP");  // measurements only
+                return e ? std::atoi(e) : 0;
+            }();
+            if (genv == 8) {
+                hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, 8, false, 1, true>), dim3((nq + 7) / 8), dim3(64),
+                                   0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
+                                   ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters,
+                                   bulk_threshold(SP));
+            } else if (genv == 2) {
+                hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, 2, false, 1, true>), dim3((nq + 1) / 2), dim3(64),
+                                   0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
+                                   ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters,
+                                   bulk_threshold(SP));
+            } else {
+                hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, false, 1, true>), dim3((nq + G - 1) / G),
+                                   dim3(64), 0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox,
+                                   ss->nsuper, ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi,
+                                   ss->counters, bulk_threshold(SP));
+            }
             timer_end(st);
             walked = true;
         }
