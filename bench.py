@@ -395,7 +395,7 @@ class Runner:
             dt = "f32" if kern_name.startswith("knn32") else "f64"
             what = f"{nq} x {n} (query, state) pairs per launch x {flop} flop (SURVEY §8d), brute force"
         achieved = pairs * flop / (kern_ms * 1e-3) / 1e12
-        return {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
+        return {"bound": "valu", "achieved": achieved, "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
                 "frac": achieved / PEAK_TFLOPS[dt], "traffic": traffic["bytes"] if traffic else None,
                 "kernel": kern_name, "kernel_ms": kern_ms,
                 "algorithmic": what + f"; {dt} VALU peak (compute-bound on VALU, no MFMA)",

@@ -412,6 +412,9 @@ ompl_gpu_status ompl_gpu_nn_get_states(ompl_gpu_nn *h, uint64_t first, size_t n,
 
 static uint64_t n_end_of(const ompl_gpu_nn *h) { return (h->n_total + kTile - 1) / kTile * kTile; }
 
+// the fp32 screens need coordinates far from fp32 overflow (kernels.h kScreenMaxAbs); NaN fails
+static bool screen_safe(const ompl_gpu_nn *h) { return h->absmax < kScreenMaxAbs; }
+
 constexpr int kCullCounters = 5;
 
 // (re)build the Morton-sorted fp32 copy the culled walks read, if adds or removes made it stale
@@ -433,9 +436,10 @@ static ompl_gpu_status ensure_sorted(ompl_gpu_nn *h) {
 // knn on device-resident features (queries already converted); caller holds the lock
 static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, size_t nq, uint32_t k, uint32_t *d_ids,
                                            double *d_dist) {
-    const bool large = k > 32 && large_k_supported(h->sp) && (h->fast || k > (uint32_t)kMaxK);
+    const bool large = k > 32 && large_k_supported(h->sp) && (h->fast || k > (uint32_t)kMaxK) && screen_safe(h);
     if (k > (uint32_t)kMaxK && !large)
-        return fail(OMPL_GPU_ERR_UNSUPPORTED, "k above 64 is not supported for this state space");
+        return fail(OMPL_GPU_ERR_UNSUPPORTED, screen_safe(h) ? "k above 64 is not supported for this state space"
+                                                             : "k above 64 needs stored coordinates below 1e18");
     const uint64_t n_end = n_end_of(h);
     if (n_end == 0) {
         // empty structure: every entry is (inf, none)
@@ -464,7 +468,7 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
                                      size_t(4) << 30, h->num_cus, h->stream));
         return OMPL_GPU_OK;
     }
-    if (h->fast && fast_k2(h->sp, k, (uint32_t)nq) > 0) {
+    if (h->fast && screen_safe(h) && fast_k2(h->sp, k, (uint32_t)nq) > 0) {
         // fp32 screen + fp64 certificate (knn_fast.hip); uncertified queries re-run exactly
         const bool cull = h->cull && cull_supported(h->sp);
         if (cull) {
@@ -473,6 +477,7 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
         }
         FastBounds b = cull ? h->sorted_bounds : current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
+        b.n_live = (uint32_t)h->n_live;
         const size_t wsb = knn_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus, cull);
         HIP_OR_FAIL(h->ws.ensure(wsb));
         uint32_t *d_fail_count = nullptr, *d_fail_list = nullptr;
@@ -592,7 +597,7 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
         HIP_OR_FAIL(hipMemsetAsync(d_qoff, 0, sizeof(uint64_t) * (nq + 1), h->stream));
         return OMPL_GPU_OK;
     }
-    if (h->fast && h->cull && cull_supported(h->sp) && nq <= 0x7FFFFFFFull) {
+    if (h->fast && h->cull && cull_supported(h->sp) && nq <= 0x7FFFFFFFull && screen_safe(h) && r < kScreenMaxAbs) {
         // culled walk over the Morton-sorted copy (knn_fast_impl.h)
         ompl_gpu_status s = ensure_sorted(h);
         if (s != OMPL_GPU_OK) return s;
@@ -848,6 +853,7 @@ ompl_gpu_status ompl_gpu_nn_knn_device(ompl_gpu_nn *h, const double *d_queries, 
     if (!h || (nq && (!d_queries || !d_ids || !d_dist))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
     std::lock_guard<std::mutex> lk(h->mu);
     if (nq == 0 || k == 0) return OMPL_GPU_OK;
+    if (nq > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many queries in one call");
     HIP_OR_FAIL(hipSetDevice(h->device));
     const double *qf = nullptr;
     ompl_gpu_status s = device_query_features(h, d_queries, nq, &qf);
@@ -1102,6 +1108,7 @@ ompl_gpu_status ompl_gpu_svc_check(ompl_gpu_mv *h, const double *states, size_t 
 
 ompl_gpu_status ompl_gpu_mv_motion_states_device(ompl_gpu_mv *h, const double *d_s1, const double *d_s2, size_t m,
                                                  uint32_t count, int endpoints, double *d_out) {
+    if (count > 0xFFFFFFFDu) return fail(OMPL_GPU_ERR_INVALID_ARG, "count above UINT32_MAX - 2");
     const uint64_t per = motion_states_per(count, endpoints);
     if (!h || (m && per && (!d_s1 || !d_s2 || !d_out))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
     if ((uint64_t)m * per > 0xFFFFFFFFull || m > 0xFFFFFFFFull)
@@ -1115,6 +1122,7 @@ ompl_gpu_status ompl_gpu_mv_motion_states_device(ompl_gpu_mv *h, const double *d
 
 ompl_gpu_status ompl_gpu_mv_motion_states(ompl_gpu_mv *h, const double *s1, const double *s2, size_t m,
                                           uint32_t count, int endpoints, double *out) {
+    if (count > 0xFFFFFFFDu) return fail(OMPL_GPU_ERR_INVALID_ARG, "count above UINT32_MAX - 2");
     const uint64_t per = motion_states_per(count, endpoints);
     if (!h || (m && per && (!s1 || !s2 || !out))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
     if ((uint64_t)m * per > 0xFFFFFFFFull || m > 0xFFFFFFFFull)

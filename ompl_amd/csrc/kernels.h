@@ -65,7 +65,11 @@ struct FastBounds {
     int nkey;                           // SE3: 6 (translation + canonical quaternion xyz); R^n: min(n, 6); SO3: 0
     float absmax;                       // max |coordinate| stored (error bound of the fp32 screen)
     uint32_t slab = 0;                  // radius phase 2: hits kept per query (slab capacity)
+    uint32_t n_live = 0;                // live stored states: a screening list that is not full must hold them all
 };
+// The fp32 screens assume coordinates far from fp32 overflow: with |x| < kScreenMaxAbs every
+// squared fp32 distance is finite (the C ABI takes the exact fp64 path otherwise).
+constexpr double kScreenMaxAbs = 1e18;
 
 // Spatially sorted fp32 copy of the store for the group walk (SE3 and R^n): states in k-d
 // leaf order (kd_order.cpp: median splits along the widest coordinate), 64-state tiles (one
@@ -214,7 +218,8 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
 hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const double *s, uint32_t m, uint8_t *valid,
                               hipStream_t st);
 // getMotionStates: states per motion (SpaceInformation.cpp:201-275 with alloc = true)
-inline uint32_t motion_states_per(uint32_t count, int endpoints) { return count + (endpoints ? 2u : 0u); }
+// in 64 bits: count near UINT32_MAX must not wrap (the C ABI rejects count > UINT32_MAX - 2)
+inline uint64_t motion_states_per(uint32_t count, int endpoints) { return (uint64_t)count + (endpoints ? 2u : 0u); }
 hipError_t launch_motion_states(const DevSpace &sp, const double *s1, const double *s2, uint32_t m, uint32_t count,
                                 int endpoints, double *out, hipStream_t st);
 

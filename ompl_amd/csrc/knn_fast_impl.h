@@ -619,16 +619,9 @@ __device__ __forceinline__ void wave_merge_sorted(float &Ld, uint32_t &Li, float
 #pragma unroll
     for (int j = 32; j > 0; j >>= 1) bitonic_step(Ld, Li, j, (lane & j) == 0);
 }
-// candidates in one ballot above which the bulk merge is used (OMPL_GPU_BULK overrides, for
-// measurements; 64 = never)
-inline int bulk_threshold(int sp) {
-    static const int env = [] {
-        const char *e = std::getenv("OMPL_GPU_BULK");
-        return e ? std::atoi(e) : -1;
-    }();
-    if (env >= 0) return env;
-    return 8;  // measured (G = 4): SE3 1.58 / 1.42 / 1.41 ms at 64 / 8 / 32; R^6 1.60 / 1.12 / 1.13 / 1.21 at 64 / 8 / 16 / 32
-}
+// candidates in one ballot above which the bulk merge is used.  Measured (G = 4): SE3 1.58 /
+// 1.42 / 1.41 ms at 64 / 8 / 32; R^6 1.60 / 1.12 / 1.13 / 1.21 ms at 64 / 8 / 16 / 32
+constexpr int kBulkThreshold = 8;
 
 template <int SP, int F, int K2, int G, bool PK, int MINW, bool QS>
 __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
@@ -986,6 +979,12 @@ __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__rest
         }
 }
 
+// Underflow: a square below FLT_MIN (flushed or subnormal) is off by at most FLT_MIN in
+// absolute terms, so a screened distance sqrt(sum of D squares) is off by at most
+// sqrt(D * FLT_MIN) ~ 1e-19 — negligible at any usual scale, but the relative terms above
+// vanish for stores whose coordinates are all tiny.
+constexpr double kFltMin = 1.1754943508222875e-38;
+
 template <int SP>
 __device__ __forceinline__ double screen_error(const DevSpace &sp, double B, double L) {
     double e = 0.0;
@@ -999,10 +998,12 @@ __device__ __forceinline__ double screen_error(const DevSpace &sp, double B, dou
         // coordinate, each term <= 14.2 u i, so the terms together <= 7.1 u n (n + 1); the n
         // additions and the final link product cost <= (n + 1) u of the sum
         const double n = (double)sp.dim;
-        e = sp.link * 8.0 * kU * n * (n + 1.0) + (n + 2.0) * kU * L;
+        e = sp.link * 8.0 * kU * n * (n + 1.0) + (n + 2.0) * kU * L + sp.link * n * sqrt(2.0 * kFltMin);
     } else {
         e = 6.0 * sqrt((double)sp.dim) * kU * B + 6.0 * kU * L;
     }
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) e += sp.w0 * sqrt(3.0 * kFltMin);
+    if constexpr (SP == OMPL_GPU_SPACE_REALVECTOR) e += sqrt(16.0 * kFltMin);
     return 2.0 * e;
 }
 
@@ -1011,7 +1012,7 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(const float *__restric
                                                           uint32_t S, uint32_t nq, const uint32_t *__restrict__ perm,
                                                           const double *__restrict__ feat64, uint64_t cap,
                                                           const double *__restrict__ qf64, DevSpace sp,
-                                                          float absmax, double *__restrict__ out_d,
+                                                          float absmax, uint32_t n_live, double *__restrict__ out_d,
                                                           uint32_t *__restrict__ out_i, uint32_t out_k,
                                                           uint32_t *__restrict__ fail_count,
                                                           uint32_t *__restrict__ fail_list) {
@@ -1055,6 +1056,11 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(const float *__restric
         for (int j = 0; j < K; ++j)
             if (j == (int)out_k - 1) dk = ex.d[j];
         ok = dk + screen_error<SP>(sp, B, L) < L * (1.0 - 8.0 * kU);
+    } else {  // a list that is not full must hold every live state (an overflowed d32 is never admitted)
+        uint32_t held = 0;
+#pragma unroll
+        for (int j = 0; j < K2; ++j) held += t.i[j] != kNoId ? 1u : 0u;
+        ok = held >= n_live;
     }
 #pragma unroll
     for (int j = 0; j < K; ++j)
@@ -1079,7 +1085,8 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
                                                                const uint32_t *__restrict__ pos_ids,
                                                                const double *__restrict__ rows64,
                                                                const double *__restrict__ qf64, DevSpace sp,
-                                                               float absmax, double *__restrict__ out_d,
+                                                               float absmax, uint32_t n_live,
+                                                               double *__restrict__ out_d,
                                                                uint32_t *__restrict__ out_i, uint32_t out_k,
                                                                uint32_t *__restrict__ fail_count,
                                                                uint32_t *__restrict__ fail_list) {
@@ -1129,7 +1136,10 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
     for (int o = K2 / 2; o > 0; o >>= 1) dk = fmax(dk, __shfl_xor(dk, o));
     const bool full = (uint32_t)__shfl((int)id, gbase + K2 - 1) != kNoId;
     const float L32 = __shfl(d32, gbase + K2 - 1);
-    bool ok = true;
+    // entries this query's list holds (its K2 lanes of the wave)
+    const uint64_t gmask = K2 == 64 ? ~0ull : (((1ull << K2) - 1ull) << gbase);
+    const uint32_t held = (uint32_t)__popcll(__ballot(id != kNoId) & gmask);
+    bool ok = full || held >= n_live;  // not full: it must hold every live state
     if (full) {  // prove that no element outside the list can enter (knn_certify_kernel)
         double B = absmax;
         const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_REALVECTOR ? F : 0);
@@ -1426,26 +1436,10 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             constexpr int G = group_queries<SP>();
-            static const int genv = [] {
-                const char *e = std::getenv("OMPL_GPU_GROUP");  // measurements only
-                return e ? std::atoi(e) : 0;
-            }();
-            if (genv == 8) {
-                hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, 8, false, 1, true>), dim3((nq + 7) / 8), dim3(64),
-                                   0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
-                                   ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters,
-                                   bulk_threshold(SP));
-            } else if (genv == 2) {
-                hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, 2, false, 1, true>), dim3((nq + 1) / 2), dim3(64),
-                                   0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
-                                   ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters,
-                                   bulk_threshold(SP));
-            } else {
-                hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, false, 1, true>), dim3((nq + G - 1) / G),
-                                   dim3(64), 0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox,
-                                   ss->nsuper, ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi,
-                                   ss->counters, bulk_threshold(SP));
-            }
+            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, false, 1, true>), dim3((nq + G - 1) / G), dim3(64),
+                               0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
+                               ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters,
+                               kBulkThreshold);
             timer_end(st);
             walked = true;
         }
@@ -1472,11 +1466,11 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (pos && !ss->rows64) return hipErrorInvalidValue;
         hipLaunchKernelGGL((knn_certify_wave_kernel<SP, F, K2>), dim3((nq + QPB - 1) / QPB), b256, 0, st, pd, pi, nq,
                            perm, f64, cap, pos ? ss->ids : nullptr, pos ? ss->rows64 : nullptr, qf64, sp, b.absmax,
-                           od, oi, k, fail, fail + 1);
+                           b.n_live, od, oi, k, fail, fail + 1);
     } else {
         if (p.cull) return hipErrorInvalidValue;  // position lists need the wave certificate
         hipLaunchKernelGGL((knn_certify_kernel<SP, F, K2, K>), dim3((nq + 255) / 256), b256, 0, st, pd, pi, p.chunks,
-                           nq, perm, f64, cap, qf64, sp, b.absmax, od, oi, k, fail, fail + 1);
+                           nq, perm, f64, cap, qf64, sp, b.absmax, b.n_live, od, oi, k, fail, fail + 1);
     }
     return hipGetLastError();
 }

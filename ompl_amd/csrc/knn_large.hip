@@ -143,6 +143,7 @@ __device__ __forceinline__ double screen_err(const DevSpace &sp, double B, doubl
         e = 1.1 * sqrt(12.0 * kU) + 1e-6 + 4.5e-5;
     else
         e = 6.0 * sqrt((double)sp.dim) * kU * B + 6.0 * kU * L;
+    e += sqrt(16.0 * 1.1754943508222875e-38);  // underflow of the squares (knn_fast_impl.h screen_error)
     return 2.0 * e;
 }
 

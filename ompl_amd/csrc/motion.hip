@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void motion_states_kernel(DevSpace sp, const d
 
 hipError_t launch_motion_states(const DevSpace &sp, const double *s1, const double *s2, uint32_t m, uint32_t count,
                                 int endpoints, double *out, hipStream_t st) {
-    const uint32_t per = motion_states_per(count, endpoints);
+    const uint32_t per = (uint32_t)motion_states_per(count, endpoints);  // count <= UINT32_MAX - 2 (capi)
     const uint64_t n = (uint64_t)m * per;
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(motion_states_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sp, s1, s2, m, count,

@@ -119,3 +119,18 @@ def test_get_motion_states(gpu, name, count, endpoints):
     if endpoints:
         np.testing.assert_array_equal(got[:, 0], a)
         np.testing.assert_array_equal(got[:, -1], b)
+
+
+def test_motion_states_count_limit(gpu):
+    """count near UINT32_MAX: the states-per-motion arithmetic must not wrap (the call is
+    rejected with OMPL_GPU_ERR_INVALID_ARG instead of returning OK with nothing written)."""
+    import ctypes as C
+
+    from ompl_amd import abi
+    sp = RealVectorStateSpace(2)
+    mv = DiscreteMotionValidatorGPU(sp, AllValidChecker(), gpu)
+    a = np.zeros((1, 2))
+    out = np.zeros(8)
+    for count in (0xFFFFFFFE, 0xFFFFFFFF):
+        st = abi.lib.ompl_gpu_mv_motion_states(mv._h, abi.dptr(a), abi.dptr(a), 1, count, 1, abi.dptr(out))
+        assert st == abi.ERR_INVALID_ARG

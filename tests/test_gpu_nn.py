@@ -359,3 +359,26 @@ def test_chain_screen_is_used_and_exact(gpu, k):
         nn.remove(int(i))
     ids2, _, _ = nn.nearestKBatch(q, k)
     assert not np.isin(ids2.astype(np.int64), gone[:50]).any()
+
+
+@pytest.mark.parametrize("scale", [1e20, 1e-25])
+def test_extreme_coordinates(gpu, path, scale):
+    """Coordinates near fp32 overflow (1e20: squared fp32 distances overflow to inf) or far
+    below fp32 precision (1e-25: squares underflow): the screens must not drop neighbours —
+    the result equals the reference formula bit for bit (R^n uses only exact IEEE ops)."""
+    rng = np.random.default_rng(41)
+    sp = RealVectorStateSpace(4)
+    data, q = W.uniform_rv(rng, 5000, 4) * scale, W.uniform_rv(rng, 100, 4) * scale
+    nn = make_nn(sp, gpu, path)
+    nn.add(data)
+    for k in (1, 10):
+        ids, d, cnt = nn.nearestKBatch(q, k)
+        oi, od, _ = O.knn(sp, data, q, k)
+        assert (cnt == k).all()
+        np.testing.assert_array_equal(d, od)
+        np.testing.assert_array_equal(ids.astype(np.int64), oi.astype(np.int64))
+    r = float(np.median(od[:, 9]))
+    off, rid, rd = nn.nearestRBatch(q, r)
+    ooff, oids, _ = O.radius(sp, data, q, r)
+    np.testing.assert_array_equal(off, ooff)
+    np.testing.assert_array_equal(rid.astype(np.int64), oids.astype(np.int64))
