@@ -8,6 +8,8 @@
 // here, signature for signature, so the plugin compiles and runs on its own.
 #pragma once
 
+#include "ompl_surface_rng.h"  // ompl::RNG (one per NN instance, as GNAT's GreedyKCenters::rng_)
+
 #ifdef OMPL_AMD_WITH_OMPL
 #include <ompl/datastructures/NearestNeighbors.h>
 #include <ompl/util/Exception.h>

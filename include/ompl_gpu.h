@@ -26,6 +26,14 @@
  *   ompl_gpu_mv_counters   MotionValidator::getValidMotionCount/getInvalidMotionCount
  *                          src/ompl/base/MotionValidator.h:102-139
  *   ompl_gpu_svc_check     StateValidityChecker::isValid         src/ompl/base/StateValidityChecker.h:111
+ *   ompl_gpu_svc_check_host  the same predicate on the host CPU (single-state isValid)
+ *   ompl_gpu_nn_distance_host  StateSpace::distance of the handle's space on the host
+ *                          (NearestNeighbors::setDistanceFunction verify mode, NearestNeighbors.h:58-61)
+ *   ompl_gpu_rng_*         RNG::setSeed / getSeed                src/ompl/util/src/RandomNumbers.cpp:208-216
+ *   ompl_gpu_sampler_*     StateSpace::allocStateSampler + StateSampler::sampleUniform
+ *                          src/ompl/base/src/StateSpace.cpp:800-806, :1118-1128,
+ *                          base/src/StateSampler.cpp:47-52, spaces/src/RealVectorStateSpace.cpp:45-53,
+ *                          spaces/src/SO3StateSpace.cpp:99-102
  *   ompl_gpu_steer_device  the RRT extend step (nearest -> interpolate to range)
  *                          src/ompl/geometric/planners/rrt/src/RRT.cpp:137-146
  *   ompl_gpu_rrt_grow_device  the RRT loop itself                 RRT.cpp:128-192
@@ -157,6 +165,10 @@ ompl_gpu_status ompl_gpu_nn_nearest(ompl_gpu_nn *h, const double *queries, size_
  * offsets has nq+1 entries. */
 ompl_gpu_status ompl_gpu_nn_radius(ompl_gpu_nn *h, const double *queries, size_t nq, double r,
                                    uint64_t **ids, double **dists, uint64_t *offsets);
+/* The handle's metric on the host: out[i] = distance(a[i], b[i]) for m pairs of AoS states, in
+ * the reference's operation order (host libm). */
+ompl_gpu_status ompl_gpu_nn_distance_host(const ompl_gpu_nn *h, const double *a, const double *b, size_t m,
+                                          double *out);
 /* Device-resident variants: all pointers are device memory, the call is
  * asynchronous on the handle's stream.  queries are AoS fp64; ids are uint32
  * (0xFFFFFFFF = no result); dist fp64. */
@@ -232,8 +244,15 @@ ompl_gpu_status ompl_gpu_mv_counters(ompl_gpu_mv *h, uint64_t *valid, uint64_t *
 ompl_gpu_status ompl_gpu_mv_reset_counters(ompl_gpu_mv *h);
 /* total isValid() evaluations the bisection variant made (the reference's work). */
 ompl_gpu_status ompl_gpu_mv_state_checks(ompl_gpu_mv *h, uint64_t *checks);
-/* isValid per state (host AoS). */
+/* isValid per state (host AoS, evaluated on the device). */
 ompl_gpu_status ompl_gpu_svc_check(ompl_gpu_mv *h, const double *states, size_t m, uint8_t *valid);
+/* the same predicate evaluated on the host CPU, from the same source as the device code
+ * (bit-identical wherever the predicate calls no libm function; the KCHAIN checker's cos / sin
+ * are glibc's here, the device math library's there).  For single-state isValid calls, where a
+ * device round trip costs more than the predicate. */
+ompl_gpu_status ompl_gpu_svc_check_host(ompl_gpu_mv *h, const double *states, size_t m, uint8_t *valid);
+/* device-resident batch: d_states AoS fp64, d_valid one byte per state; asynchronous. */
+ompl_gpu_status ompl_gpu_svc_check_device(ompl_gpu_mv *h, const double *d_states, size_t m, uint8_t *d_valid);
 /* SpaceInformation::getMotionStates(s1, s2, states, count, endpoints, alloc = true)
  * (src/ompl/base/src/SpaceInformation.cpp:201-275) for m motions: out = [m][per][dim] with
  * per = count + (endpoints ? 2 : 0) = the function's return value — [s1], the states at
@@ -255,6 +274,30 @@ ompl_gpu_status ompl_gpu_mv_motion_states_device(ompl_gpu_mv *h, const double *d
  * synchronous on return. */
 ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
                                          double max_distance, uint32_t *d_nearest, uint32_t *d_added);
+
+/* ---- the reference's input streams (host) ------------------------------------
+ * ompl::RNG restated on the same standard-library engines (std::ranlux24_base seed generator,
+ * std::mt19937 + std::uniform_real_distribution per RNG, RandomNumbers.cpp:53-279).
+ * ompl_gpu_rng_set_seed = RNG::setSeed (call before any RNG is constructed for deterministic
+ * streams); every sampler created afterwards draws its RNG seeds from that generator in the
+ * reference's construction order. */
+void ompl_gpu_rng_set_seed(uint32_t seed);
+uint32_t ompl_gpu_rng_get_seed(void);
+uint64_t ompl_gpu_rng_seeds_drawn(void); /* seeds handed out so far (observability) */
+/* n x RNG(local_seed).uniformReal(low, high): an explicitly seeded RNG (RandomNumbers.cpp:225-228),
+ * which draws nothing from the seed generator */
+ompl_gpu_status ompl_gpu_rng_uniform_real(uint32_t local_seed, size_t n, double low, double high, double *out);
+typedef struct ompl_gpu_sampler ompl_gpu_sampler;
+/* allocStateSampler of the space: SE3 = CompoundStateSampler + R^3 + SO3 samplers (3 seeds),
+ * R^n / KCHAIN one RealVectorStateSampler, SO3 one SO3StateSampler.  low / high: bounds of the
+ * R^n part (dim reals; SE3: 3), NULL = [0, 1] (KCHAIN: [-pi, pi], KinematicChain.h:87-100). */
+ompl_gpu_status ompl_gpu_sampler_create(ompl_gpu_sampler **out, const ompl_gpu_space *space, const double *low,
+                                        const double *high);
+ompl_gpu_status ompl_gpu_sampler_destroy(ompl_gpu_sampler *s);
+/* n successive sampleUniform calls, AoS rows (copyToReals order) */
+ompl_gpu_status ompl_gpu_sampler_sample_uniform(ompl_gpu_sampler *s, size_t n, double *out);
+/* local seeds of the sampler's RNGs in construction order (at most 3) */
+ompl_gpu_status ompl_gpu_sampler_local_seeds(const ompl_gpu_sampler *s, uint32_t *seeds, int *count);
 
 #ifdef __cplusplus
 }

@@ -102,6 +102,17 @@ SIGNATURES = {
     "ompl_gpu_mv_reset_counters": (C.c_int, [_P]),
     "ompl_gpu_mv_state_checks": (C.c_int, [_P, _U64]),
     "ompl_gpu_svc_check": (C.c_int, [_P, _D, C.c_size_t, _U8]),
+    "ompl_gpu_svc_check_host": (C.c_int, [_P, _D, C.c_size_t, _U8]),
+    "ompl_gpu_svc_check_device": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "ompl_gpu_nn_distance_host": (C.c_int, [_P, _D, _D, C.c_size_t, _D]),
+    "ompl_gpu_rng_set_seed": (None, [C.c_uint32]),
+    "ompl_gpu_rng_get_seed": (C.c_uint32, []),
+    "ompl_gpu_rng_seeds_drawn": (C.c_uint64, []),
+    "ompl_gpu_rng_uniform_real": (C.c_int, [C.c_uint32, C.c_size_t, C.c_double, C.c_double, _D]),
+    "ompl_gpu_sampler_create": (C.c_int, [C.POINTER(_P), C.POINTER(SpaceStruct), _D, _D]),
+    "ompl_gpu_sampler_destroy": (C.c_int, [_P]),
+    "ompl_gpu_sampler_sample_uniform": (C.c_int, [_P, C.c_size_t, _D]),
+    "ompl_gpu_sampler_local_seeds": (C.c_int, [_P, _U32, C.POINTER(C.c_int)]),
     "ompl_gpu_mv_motion_states": (C.c_int, [_P, _D, _D, C.c_size_t, C.c_uint32, C.c_int, _D]),
     "ompl_gpu_mv_motion_states_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_uint32, C.c_int, _P]),
 }

@@ -127,6 +127,7 @@ struct ompl_gpu_nn {
 
 namespace ompl_amd {
 thread_local KernelTimer *g_kernel_timer = nullptr;
+void set_last_error(const char *msg) { g_last_error = msg; }  // sampler.cpp
 }
 
 namespace {
@@ -185,6 +186,7 @@ struct ompl_gpu_mv {
     FeatGeom g{};
     DevChecker ck{};
     double *ck_data = nullptr;
+    std::vector<double> ck_host;  // host copy of the checker data (ompl_gpu_svc_check_host)
     unsigned long long *counters = nullptr;  // valid, invalid, isValid calls
     std::mutex mu;
     DevBuf s1, s2, valid, nd, fi, ms;
@@ -394,6 +396,14 @@ ompl_gpu_status ompl_gpu_nn_size(const ompl_gpu_nn *h, size_t *live, size_t *tot
     return OMPL_GPU_OK;
 }
 
+ompl_gpu_status ompl_gpu_nn_distance_host(const ompl_gpu_nn *h, const double *a, const double *b, size_t m,
+                                          double *out) {
+    if (!h || (m && (!a || !b || !out))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    const int dim = h->sp.dim;
+    for (size_t i = 0; i < m; ++i) out[i] = raw_distance(h->sp, a + i * dim, b + i * dim);
+    return OMPL_GPU_OK;
+}
+
 ompl_gpu_status ompl_gpu_nn_get_states(ompl_gpu_nn *h, uint64_t first, size_t n, double *out) {
     if (!h || (n && !out)) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -501,8 +511,9 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
             HIP_OR_FAIL(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (nfail + 1), h->stream));
             HIP_OR_FAIL(launch_knn_bounded(h->sp, h->g, h->feat, h->cap, n_end, d_qf, d_fail_list, nfail, k, d_dist,
                                            d_ids, cnt, (double *)h->fb_cd.p, (uint32_t *)h->fb_ci.p, h->stream));
-            HIP_OR_FAIL(hipMemcpyAsync(&nfail, cnt + nfail, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
-            d_fail_list = cnt + nfail + 1;
+            const uint32_t nlist = nfail;  // the copy below overwrites nfail with the overflow count
+            d_fail_list = cnt + nlist + 1;
+            HIP_OR_FAIL(hipMemcpyAsync(&nfail, cnt + nlist, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
             HIP_OR_FAIL(hipStreamSynchronize(h->stream));
             h->fast_overflows += nfail;
             if (nfail == 0) return OMPL_GPU_OK;
@@ -986,6 +997,7 @@ ompl_gpu_status ompl_gpu_mv_create(ompl_gpu_mv **out, const ompl_gpu_space *spac
         if (e == hipSuccess)
             e = hipMemcpy(h->ck_data, checker->data, sizeof(double) * per * h->ck.count, hipMemcpyHostToDevice);
         h->ck.data = h->ck_data;
+        h->ck_host.assign(checker->data, checker->data + per * h->ck.count);
     }
     if (e != hipSuccess) {
         ompl_gpu_mv_destroy(h);
@@ -1103,6 +1115,25 @@ ompl_gpu_status ompl_gpu_svc_check(ompl_gpu_mv *h, const double *states, size_t 
     HIP_OR_FAIL(launch_state_valid(h->sp, h->ck, (const double *)h->s1.p, (uint32_t)m, (uint8_t *)h->valid.p, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(valid, h->valid.p, m, hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_svc_check_host(ompl_gpu_mv *h, const double *states, size_t m, uint8_t *valid) {
+    if (!h || (m && (!states || !valid))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    DevChecker ck = h->ck;
+    ck.data = h->ck_host.empty() ? nullptr : h->ck_host.data();
+    const int dim = h->sp.dim;
+    for (size_t i = 0; i < m; ++i) valid[i] = is_valid(h->sp, ck, states + i * dim) ? 1 : 0;
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_svc_check_device(ompl_gpu_mv *h, const double *d_states, size_t m, uint8_t *d_valid) {
+    if (!h || (m && (!d_states || !d_valid))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (m > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many states in one call");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (m == 0) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(launch_state_valid(h->sp, h->ck, d_states, (uint32_t)m, d_valid, h->stream));
     return OMPL_GPU_OK;
 }
 

@@ -1,5 +1,9 @@
 // device_space.h — device restatement of the reference's state-space leaves in
-// IEEE fp64 with the reference's operation order.  This translation unit is
+// IEEE fp64 with the reference's operation order.  Every function is __host__ __device__:
+// the library's host side runs the same code (StateValidityCheckerGPU's single-state isValid,
+// the distance the NN plugin's verify mode compares against), so host and device agree bit for
+// bit wherever no libm call is involved (the device math library may differ from glibc by an
+// ulp in cos / sin / acos).  This translation unit is
 // compiled with -ffp-contract=off: no multiply-add is fused, matching the
 // reference x86-64 build (CMakeModules/CompilerSettings.cmake:8, no -march).
 //
@@ -45,7 +49,7 @@ __host__ __device__ inline int feature_count(int kind, int dim) {
     return kind == OMPL_GPU_SPACE_KCHAIN ? 2 * dim : dim;
 }
 
-__device__ __forceinline__ double l2_dist(const double *a, const double *b, int n) {
+__host__ __device__ __forceinline__ double l2_dist(const double *a, const double *b, int n) {
     double acc = 0.0;
     for (int i = 0; i < n; ++i) {
         double diff = a[i] - b[i];
@@ -54,7 +58,7 @@ __device__ __forceinline__ double l2_dist(const double *a, const double *b, int 
     return sqrt(acc);
 }
 
-__device__ __forceinline__ double so3_arc(const double *p, const double *q) {
+__host__ __device__ __forceinline__ double so3_arc(const double *p, const double *q) {
     double dq = fabs(p[0] * q[0] + p[1] * q[1] + p[2] * q[2] + p[3] * q[3]);
     if (dq > 1.0 - kQuatNormErr) return 0.0;
     return acos(dq);
@@ -62,7 +66,7 @@ __device__ __forceinline__ double so3_arc(const double *p, const double *q) {
 
 // chain distance from precomputed cumulative cos/sin features (cs[0..n) = cos, cs[n..2n) = sin)
 template <int NMAX>
-__device__ __forceinline__ double chain_dist_feat(const double *a, const double *b, int n, double link) {
+__host__ __device__ __forceinline__ double chain_dist_feat(const double *a, const double *b, int n, double link) {
     double dx = 0., dy = 0., dist = 0.;
 #pragma unroll
     for (int i = 0; i < NMAX; ++i) {
@@ -76,7 +80,7 @@ __device__ __forceinline__ double chain_dist_feat(const double *a, const double 
 }
 
 // raw-angle chain distance (motion validator: validSegmentCount on raw states)
-__device__ __forceinline__ double chain_dist_raw(const double *a, const double *b, int n, double link) {
+__host__ __device__ __forceinline__ double chain_dist_raw(const double *a, const double *b, int n, double link) {
     double th1 = 0., th2 = 0., dx = 0., dy = 0., dist = 0.;
     for (int i = 0; i < n; ++i) {
         th1 += a[i];
@@ -88,7 +92,7 @@ __device__ __forceinline__ double chain_dist_raw(const double *a, const double *
     return dist * link;
 }
 
-__device__ __forceinline__ double se3_dist(const double *a, const double *b, double w0, double w1) {
+__host__ __device__ __forceinline__ double se3_dist(const double *a, const double *b, double w0, double w1) {
     double dist = 0.0;
     dist += w0 * l2_dist(a, b, 3);
     dist += w1 * so3_arc(a + 3, b + 3);
@@ -96,7 +100,7 @@ __device__ __forceinline__ double se3_dist(const double *a, const double *b, dou
 }
 
 // distance on raw AoS states (dim reals)
-__device__ inline double raw_distance(const DevSpace &sp, const double *a, const double *b) {
+__host__ __device__ inline double raw_distance(const DevSpace &sp, const double *a, const double *b) {
     switch (sp.kind) {
     case OMPL_GPU_SPACE_REALVECTOR: return l2_dist(a, b, sp.dim);
     case OMPL_GPU_SPACE_SO3: return so3_arc(a, b);
@@ -105,11 +109,11 @@ __device__ inline double raw_distance(const DevSpace &sp, const double *a, const
     }
 }
 
-__device__ __forceinline__ uint32_t seg_count(double d, double lvs, uint32_t f) {
+__host__ __device__ __forceinline__ uint32_t seg_count(double d, double lvs, uint32_t f) {
     return f * (uint32_t)ceil(d / lvs);
 }
 
-__device__ inline uint32_t valid_segment_count(const DevSpace &sp, const double *a, const double *b) {
+__host__ __device__ inline uint32_t valid_segment_count(const DevSpace &sp, const double *a, const double *b) {
     switch (sp.kind) {
     case OMPL_GPU_SPACE_REALVECTOR: return seg_count(l2_dist(a, b, sp.dim), sp.lvs0, sp.f0);
     case OMPL_GPU_SPACE_SO3: return seg_count(so3_arc(a, b), sp.lvs0, sp.f0);
@@ -125,11 +129,11 @@ __device__ inline uint32_t valid_segment_count(const DevSpace &sp, const double 
     }
 }
 
-__device__ __forceinline__ void lerp(const double *f, const double *t_, double t, double *o, int n) {
+__host__ __device__ __forceinline__ void lerp(const double *f, const double *t_, double t, double *o, int n) {
     for (int i = 0; i < n; ++i) o[i] = f[i] + (t_[i] - f[i]) * t;
 }
 
-__device__ inline void slerp(const double *f, const double *to, double t, double *o) {
+__host__ __device__ inline void slerp(const double *f, const double *to, double t, double *o) {
     double theta = so3_arc(f, to);
     if (theta > kDblEps) {
         double d = 1.0 / sin(theta);
@@ -146,7 +150,7 @@ __device__ inline void slerp(const double *f, const double *to, double t, double
     }
 }
 
-__device__ inline void chain_interp(const double *f, const double *to, double t, double *o, int n) {
+__host__ __device__ inline void chain_interp(const double *f, const double *to, double t, double *o, int n) {
     for (int i = 0; i < n; ++i) {
         double diff = to[i] - f[i];
         if (fabs(diff) <= kPi) {
@@ -168,7 +172,7 @@ __device__ inline void chain_interp(const double *f, const double *to, double t,
 
 // interpolate; rot=false skips the SO3 part of SE3 when the validity checker only
 // reads the translation (its output is then unused: the result bit is unchanged).
-__device__ inline void interpolate(const DevSpace &sp, const double *f, const double *to, double t, double *o,
+__host__ __device__ inline void interpolate(const DevSpace &sp, const double *f, const double *to, double t, double *o,
                                    bool rot = true) {
     switch (sp.kind) {
     case OMPL_GPU_SPACE_REALVECTOR: lerp(f, to, t, o, sp.dim); break;
@@ -191,7 +195,7 @@ struct DevChecker {
     const double *data;  // device copy
 };
 
-__device__ __forceinline__ bool hypercube_valid(const double *s, int ndim, double edge) {
+__host__ __device__ __forceinline__ bool hypercube_valid(const double *s, int ndim, double edge) {
     bool found = false;
     for (int i = ndim - 1; i >= 0; i--) {
         if (!found) {
@@ -203,7 +207,7 @@ __device__ __forceinline__ bool hypercube_valid(const double *s, int ndim, doubl
     return true;
 }
 
-__device__ __forceinline__ bool spheres_valid(const double *s, const double *c, int count) {
+__host__ __device__ __forceinline__ bool spheres_valid(const double *s, const double *c, int count) {
     for (int i = 0; i < count; ++i) {
         double dx = c[4 * i + 0] - s[0];
         double dy = c[4 * i + 1] - s[1];
@@ -213,7 +217,7 @@ __device__ __forceinline__ bool spheres_valid(const double *s, const double *c, 
     return true;
 }
 
-__device__ __forceinline__ bool circles_valid(const double *s, const double *c, int count) {
+__host__ __device__ __forceinline__ bool circles_valid(const double *s, const double *c, int count) {
     for (int i = 0; i < count; ++i) {
         double dx = c[3 * i + 0] - s[0];
         double dy = c[3 * i + 1] - s[1];
@@ -222,7 +226,7 @@ __device__ __forceinline__ bool circles_valid(const double *s, const double *c, 
     return true;
 }
 
-__device__ __forceinline__ bool seg_intersect(double a0x, double a0y, double a1x, double a1y, double b0x, double b0y,
+__host__ __device__ __forceinline__ bool seg_intersect(double a0x, double a0y, double a1x, double a1y, double b0x, double b0y,
                                               double b1x, double b1y) {
     double s10_x = a1x - a0x;
     double s10_y = a1y - a0y;
@@ -244,7 +248,7 @@ __device__ __forceinline__ bool seg_intersect(double a0x, double a0y, double a1x
 
 constexpr int kChainMaxLinks = 32;
 
-__device__ inline bool chain_valid(const double *s, int n, double link, const double *env, int nenv) {
+__host__ __device__ inline bool chain_valid(const double *s, int n, double link, const double *env, int nenv) {
     double px[kChainMaxLinks + 2], py[kChainMaxLinks + 2];  // segment i = (p[i], p[i+1])
     double theta = 0., x = 0., y = 0.;
     px[0] = 0.;
@@ -272,7 +276,7 @@ __device__ inline bool chain_valid(const double *s, int n, double link, const do
     return true;
 }
 
-__device__ inline bool is_valid(const DevSpace &sp, const DevChecker &ck, const double *s) {
+__host__ __device__ inline bool is_valid(const DevSpace &sp, const DevChecker &ck, const double *s) {
     switch (ck.kind) {
     case OMPL_GPU_CHECK_ALL_VALID: return true;
     case OMPL_GPU_CHECK_HYPERCUBE: return hypercube_valid(s, ck.ndim, ck.edge);

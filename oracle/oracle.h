@@ -82,6 +82,16 @@ uint64_t oracle_gnat_radius_count(const oracle_gnat *g, const double *q, size_t 
 uint64_t oracle_check_motions_mt(const ompl_gpu_space *sp, const ompl_gpu_checker *ck, const double *s1,
                                  const double *s2, size_t m, uint8_t *valid, int nthreads);
 
+/* ---- the reference's input streams (oracle/rng.cpp) ------------------- */
+uint32_t oracle_mt19937_10000th(void);
+uint32_t oracle_ranlux24_base_10000th(void);
+/* the first n RNG() seeds after RNG::setSeed(seed) */
+void oracle_seed_stream(uint32_t seed, size_t n, uint32_t *out);
+/* n sampleUniform() of the space's default sampler whose RNGs have the given local seeds
+ * (SE3: compound, R^3, SO3; SO3: one; R^n / KCHAIN: one); low/high: bounds of the R^n part */
+void oracle_sample_uniform(const ompl_gpu_space *sp, const uint32_t *local_seeds, const double *low,
+                           const double *high, size_t n, double *out);
+
 #ifdef __cplusplus
 }
 #endif

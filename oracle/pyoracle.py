@@ -41,6 +41,10 @@ _ORACLE_SIGS = {
     "oracle_gnat_size": (C.c_size_t, [C.c_void_p]),
     "oracle_gnat_knn": (None, [C.c_void_p, _D, C.c_size_t, C.c_uint32, _U32, _D, _U32, C.c_int]),
     "oracle_gnat_radius_count": (C.c_uint64, [C.c_void_p, _D, C.c_size_t, C.c_double, _U64, C.c_int]),
+    "oracle_mt19937_10000th": (C.c_uint32, []),
+    "oracle_ranlux24_base_10000th": (C.c_uint32, []),
+    "oracle_seed_stream": (None, [C.c_uint32, C.c_size_t, _U32]),
+    "oracle_sample_uniform": (None, [_SP, _U32, _D, _D, C.c_size_t, _D]),
 }
 _REF_SIGS = {
     "ref_linear_knn": (C.c_int, [_SP, _D, C.c_size_t, _D, C.c_size_t, C.c_uint32, _U32, _D, _U32]),
@@ -151,6 +155,25 @@ def radius(sp, data, queries, r):
     lib.oracle_radius(C.byref(s), abi.dptr(d), d.shape[0], abi.dptr(q), nq, float(r), off.ctypes.data_as(_U64),
                       ids.ctypes.data_as(_U32), abi.dptr(dist), cnt.ctypes.data_as(_U64))
     return off, ids[:tot], dist[:tot]
+
+
+def seed_stream(seed, n):
+    """The first n RNG() seeds after RNG::setSeed(seed)."""
+    out = np.zeros(n, np.uint32)
+    lib.oracle_seed_stream(int(seed), int(n), out.ctypes.data_as(_U32))
+    return out
+
+
+def sample_uniform(sp, local_seeds, n, low=None, high=None):
+    """n sampleUniform() of the space's default sampler with the given RNG local seeds."""
+    s = sp.to_abi()
+    seeds = np.ascontiguousarray(local_seeds, dtype=np.uint32)
+    lo = _arr(low if low is not None else getattr(sp, "low", [0.0]))
+    hi = _arr(high if high is not None else getattr(sp, "high", [1.0]))
+    out = np.zeros((int(n), sp.dim))
+    lib.oracle_sample_uniform(C.byref(s), seeds.ctypes.data_as(_U32), abi.dptr(lo), abi.dptr(hi), int(n),
+                              abi.dptr(out))
+    return out
 
 
 class Gnat:

@@ -10,6 +10,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "cpp", "plugin_test.cpp")
 MV_SRC = os.path.join(ROOT, "tests", "cpp", "mv_plugin_test.cpp")
+BOUNDARY_SRC = os.path.join(ROOT, "tests", "cpp", "boundary_test.cpp")
 REF_SRC = "/root/reference/src"
 
 
@@ -52,3 +53,22 @@ def test_motion_validator_plugin_runs_on_gpu(tmp_path, gpu):
     exe = _build(str(tmp_path / "mv_run"), [], MV_SRC)
     r = subprocess.run([exe, "run"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "MV PLUGIN OK" in r.stdout, r.stdout + r.stderr
+
+
+def test_boundary_compiles_and_rng_streams(tmp_path):
+    """Standalone ompl::RNG: the seed stream after RNG::setSeed(42) and the uniformReal stream
+    equal the oracle's restatement (CPU only)."""
+    exe = _build(str(tmp_path / "boundary_sa"), [], BOUNDARY_SRC)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0 and "BOUNDARY COMPILED" in r.stdout, r.stdout + r.stderr
+    r = subprocess.run([exe, "rng"], capture_output=True, text=True)
+    assert r.returncode == 0 and "BOUNDARY RNG OK" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_boundary_runs_on_gpu(tmp_path, gpu):
+    """One RNG seed per NearestNeighborsGPU, setDistanceFunction verification, the
+    StateValidityChecker plugin (host == device == oracle) and the SelfConfig hook."""
+    exe = _build(str(tmp_path / "boundary_run"), [], BOUNDARY_SRC)
+    r = subprocess.run([exe, "run"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "BOUNDARY OK" in r.stdout, r.stdout + r.stderr
