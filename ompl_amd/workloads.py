@@ -1,13 +1,16 @@
-"""Synthetic inputs of the BASELINE.json configurations (numpy, seeded).
+"""Synthetic inputs of the BASELINE.json configurations.
 
-Samplers restate the reference's distributions (not its bit streams — parity is
-defined on identical inputs, which the tests feed to both sides):
+reference_states() draws from the reference's own streams (ompl_amd.sampling: RNG::setSeed, then
+one allocStateSampler() per array in order, RandomNumbers.cpp:53-279, StateSpace.cpp:800-806,
+:1118-1128) — what the bench and the golden fixtures use.  The numpy samplers below restate the
+same distributions with numpy's generator, for tests whose inputs only need to be arbitrary
+(parity is defined on identical inputs, which the tests feed to both sides):
   uniform R^n in bounds          RealVectorStateSampler::sampleUniform (RealVectorStateSpace.cpp:45-53)
   uniform SO3, Shoemake          RNG::quaternion (util/src/RandomNumbers.cpp:263-279)
   SE3 = uniform R^3 x SO3        CompoundStateSampler::sampleUniform (base/src/StateSampler.cpp:47-52)
 Environments:
   createHornEnvironment(d, eps)  demos/KinematicChain.h:279-315
-  sphere field                   32 spheres, r = 0.1, seed 7
+  sphere field                   32 spheres, r = 0.1, centres from RNG(7)
 """
 from __future__ import annotations
 
@@ -60,8 +63,41 @@ def horn_environment(d: int, eps: float) -> np.ndarray:
 
 
 def sphere_field(count: int = 32, radius: float = 0.1, seed: int = 7, low=0.0, high=1.0):
-    rng = np.random.default_rng(seed)
-    return rng.uniform(low, high, size=(count, 3)), np.full(count, radius)
+    """count sphere centres = 3 * count successive RNG(seed).uniformReal(low, high) draws."""
+    from . import sampling
+
+    c = sampling.rng_uniform(seed, 3 * count, low, high).reshape(count, 3)
+    return np.ascontiguousarray(c), np.full(count, radius)
+
+
+def reference_states(space, counts, seed: int = 42):
+    """RNG::setSeed(seed); then for each n in counts: sampler = space.allocStateSampler(),
+    n x sampler.sampleUniform().  Returns one array per count."""
+    from . import sampling
+
+    sampling.set_seed(seed)
+    out = []
+    for n in counts:
+        out.append(sampling.StateSampler(space).sample_uniform(int(n)))
+    return out
+
+
+def reference_valid_states(space, n: int, is_valid, seed: int = 42, chunk: int = 1_000_000, sampler=None):
+    """The first n valid states of one sampler's uniform stream — what the reference's
+    UniformValidStateSampler yields in order (rejection, ValidStateSampler attempts), since an
+    invalid draw is simply followed by the next one.  Pass `sampler` to continue a stream."""
+    from . import sampling
+
+    if sampler is None:
+        sampling.set_seed(seed)
+        sampler = sampling.StateSampler(space)
+    parts, have = [], 0
+    while have < n:
+        x = sampler.sample_uniform(chunk)
+        x = x[np.asarray(is_valid(x), dtype=bool)]
+        parts.append(x[: n - have])
+        have += len(parts[-1])
+    return np.ascontiguousarray(np.concatenate(parts)), sampler
 
 
 def rrt_star_k(n: int, d: int) -> int:
