@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--single-query-reps", type=int, default=200, help="RRT-style one-query scans (0 = skip)")
     ap.add_argument("--rrt-iters", type=int, default=2000, help="device RRT iterations after the bench (0 = skip)")
+    ap.add_argument("--rrt-star-queries", type=int, default=1000,
+                    help="cfg3: batch of RRT* neighbourhood queries at k = 6,169 (0 = skip)")
     a = ap.parse_args()
     t, q, k = DEFAULTS[a.workload]
     a.tree = t if a.tree is None else a.tree
@@ -90,19 +92,31 @@ def parse():
     return a
 
 
-def _valid_states(mv, sampler, rng, n, chunk=1_000_000):
-    """n valid states by rejection (the roadmap / sample sets of PRM* and BIT* hold only valid
-    states: PRM.cpp:356-378, ImplicitGraph.cpp:981), the predicate evaluated on the device."""
-    out, have = [], 0
-    while have < n:
-        x = sampler(rng, chunk)
-        x = x[mv.isValid(x)]
-        out.append(x[: n - have])
-        have += len(out[-1])
-    return np.ascontiguousarray(np.concatenate(out))
+def reference_inputs(sp, n_tree, nq, rank, valid=None):
+    """The reference's input streams: RNG::setSeed(42), then a tree sampler and a query sampler
+    (space->allocStateSampler() twice, RandomNumbers.cpp:53-279, StateSpace.cpp:800-806).  The
+    tree is identical on every rank; rank r takes queries [r*nq, (r+1)*nq) of the query stream.
+    With `valid`, only valid states are kept, in stream order (UniformValidStateSampler)."""
+    from ompl_amd import sampling as S
+    from ompl_amd import workloads as W
+
+    S.set_seed(42)
+    ts, qs = S.StateSampler(sp), S.StateSampler(sp)
+    need = nq * (rank + 1)
+    if valid is None:
+        return ts.sample_uniform(n_tree), np.ascontiguousarray(qs.sample_uniform(need)[rank * nq:])
+    tree, _ = W.reference_valid_states(sp, n_tree, valid, sampler=ts, chunk=min(2_000_000, max(4 * n_tree, 4096)))
+    q, _ = W.reference_valid_states(sp, need, valid, sampler=qs, chunk=min(2_000_000, max(4 * need, 4096)))
+    return tree, np.ascontiguousarray(q[rank * nq:])
 
 
-def _gnat_knn_rate(sp, tree, queries, k, budget_s):
+CPU_THREADS = 8  # SURVEY §8d protocol: 1 core and all 8 cores of the reference container
+
+
+def _gnat_knn_rate(sp, tree, queries, k, budget_s, nthreads):
+    """GNAT restatement (oracle/gnat.cpp, reference defaults) over the tree: queries/s of
+    nearestK on `nthreads` threads (const queries on one structure, like the reference's
+    thread-safe GNAT), on as many queries as fit the budget.  Build time reported apart."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
 
@@ -110,64 +124,73 @@ def _gnat_knn_rate(sp, tree, queries, k, budget_s):
     t0 = time.perf_counter()
     g.add(tree)
     build_s = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    g.knn(queries[:200], k)
-    per = (time.perf_counter() - t0) / 200
-    nq = int(min(len(queries), max(200, 0.6 * budget_s / max(per, 1e-9))))
-    t0 = time.perf_counter()
-    ids, d, _ = g.knn(queries[:nq], k)
-    return nq, nq / (time.perf_counter() - t0), build_s, ids, d
+    out = {"build_s": build_s}
+    for nt in (1, nthreads):
+        t0 = time.perf_counter()
+        g.knn(queries[:200 * nt], k, nt)
+        per = (time.perf_counter() - t0) / (200 * nt)
+        nq = int(min(len(queries), max(200 * nt, 0.3 * budget_s / max(per, 1e-9))))
+        t0 = time.perf_counter()
+        ids, d, _ = g.knn(queries[:nq], k, nt)
+        out[nt] = (nq, nq / (time.perf_counter() - t0), ids, d)
+    return out
 
 
-def _motion_rate(sp, ck, s1, s2, budget_s):
+def _motion_rate(sp, ck, s1, s2, budget_s, nthreads):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
 
     t0 = time.perf_counter()
-    O.check_motions_mt(sp, ck, s1, s2, 1)
+    O.check_motions_mt(sp, ck, s1, s2, nthreads)
     t = time.perf_counter() - t0
     reps = 1
     if t < budget_s:
         reps = int(max(1, budget_s / max(t, 1e-9)))
         t0 = time.perf_counter()
         for _ in range(reps):
-            O.check_motions_mt(sp, ck, s1, s2, 1)
+            O.check_motions_mt(sp, ck, s1, s2, nthreads)
         t = (time.perf_counter() - t0) / reps
     return len(s1) / t, reps
 
 
-def cpu_baseline(workload, sp, ck, tree, rng, k, budget_s, radius=None):
-    """The oracle restatement, 1 thread, on a bounded sample of the same workload on this host:
-    GNAT (oracle/gnat.cpp, reference defaults) where building it over the tree is affordable
-    (cfg2, cfg3), else the Linear brute force (cfg4: 10^6 chain states, cfg5: 10^7 SE(3)
-    samples) — a slower CPU path than the reference's GNAT, said so in `sample`."""
+def cpu_baseline(workload, sp, ck, tree, queries, k, budget_s, radius=None):
+    """The oracle restatement on a bounded sample of the same workload (the run's own queries) on
+    this host, on 1 thread and on CPU_THREADS threads: GNAT (oracle/gnat.cpp,
+    reference defaults) where building it over the tree is affordable (cfg2, cfg3), else the
+    Linear brute force (cfg4: 10^6 chain states, cfg5: 10^7 SE(3) samples) — a slower CPU path
+    than the reference's GNAT, said so in `sample`.  `value` is the all-threads figure."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
 
-    from ompl_amd import workloads as W
-
+    T = CPU_THREADS
     if workload in ("cfg3", "cfg2"):
-        q = W.uniform_se3(rng, 20000) if workload == "cfg3" else W.uniform_rv(rng, 20000, 6)
-        nq, qps, build_s, ids, d = _gnat_knn_rate(sp, tree, q, k, budget_s)
+        r = _gnat_knn_rate(sp, tree, queries, k, budget_s, T)
+        (nq1, qps1, ids, d), (nqT, qpsT, _, _) = r[1], r[T]
         if workload == "cfg2":
-            return {"value": qps, "unit": "NN queries/s", "cores": 1, "kind": "port",
+            return {"value": qpsT, "unit": "NN queries/s", "cores": T, "kind": "port",
                     "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same 10^5-state "
-                               f"R^6 store: {nq} nearestK(k={k}) queries; index build {build_s:.2f} s excluded"),
-                    "nn_queries_per_s": qps}
+                               f"R^6 store, the run's own queries: {nqT} nearestK(k={k}) on {T} threads "
+                               f"(const queries on one structure); index build {r['build_s']:.2f} s excluded"),
+                    "single_thread": {"value": qps1, "queries": nq1}, "nn_queries_per_s": qpsT}
         maxd = 0.2 * sp.getMaximumExtent()
         s1 = tree[ids[:, 0].astype(np.int64)]
-        s2 = np.empty_like(q[:nq])
-        for i in range(nq):  # steering is not timed on the CPU side (favours the CPU)
+        q = queries[:nq1]
+        s2 = np.empty_like(q)
+        for i in range(nq1):  # steering is not timed on the CPU side (favours the CPU)
             s2[i] = O.interpolate(sp, s1[i], q[i], maxd / d[i, 0]) if d[i, 0] > maxd else q[i]
-        mps, reps = _motion_rate(sp, ck, s1, s2, 0.3 * budget_s)
-        return {"value": 2.0 / (1.0 / qps + 1.0 / mps), "unit": UNIT, "cores": 1, "kind": "port",
+        mps1, _ = _motion_rate(sp, ck, s1, s2, 0.15 * budget_s, 1)
+        mpsT, reps = _motion_rate(sp, ck, s1, s2, 0.15 * budget_s, T)
+        comb = lambda a, b: 2.0 / (1.0 / a + 1.0 / b)  # noqa: E731  (one query + one motion check per sample)
+        return {"value": comb(qpsT, mpsT), "unit": UNIT, "cores": T, "kind": "port",
                 "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same 10^6-state "
-                           f"SE(3) tree: {nq} nearestK(k={k}) queries, then {nq} checkMotion(nearest, steered) x{reps} "
-                           f"with the oracle DiscreteMotionValidator; index build {build_s:.2f} s excluded"),
-                "nn_queries_per_s": qps, "motion_checks_per_s": mps}
+                           f"SE(3) tree and the run's own samples: {nqT} nearestK(k={k}) queries, then {nq1} "
+                           f"checkMotion(nearest, steered) x{reps} with the oracle DiscreteMotionValidator, on {T} "
+                           f"threads; index build {r['build_s']:.2f} s excluded"),
+                "single_thread": {"value": comb(qps1, mps1), "nn_queries_per_s": qps1, "motion_checks_per_s": mps1},
+                "nn_queries_per_s": qpsT, "motion_checks_per_s": mpsT, "gnat_build_s": r["build_s"]}
     # brute force over 10^6 chain / 10^7 SE(3) states: time a few queries
     dim = sp.dim
-    q = (W.uniform_chain(rng, 64, 12) if workload == "cfg4" else W.uniform_se3(rng, 64))
+    q = queries[:64]
     t0 = time.perf_counter()
     if workload == "cfg4":
         O.knn(sp, tree, q[:1], k)
@@ -185,7 +208,7 @@ def cpu_baseline(workload, sp, ck, tree, rng, k, budget_s, radius=None):
         s1 = np.repeat(q[:nq], np.diff(off).astype(np.int64), axis=0)  # checkMotion(vertex, sample)
         s2 = tree[ids.astype(np.int64)]
     t_nn = time.perf_counter() - t0
-    mps, reps = _motion_rate(sp, ck, s1.reshape(-1, dim), s2.reshape(-1, dim), 0.3 * budget_s)
+    mps, reps = _motion_rate(sp, ck, s1.reshape(-1, dim), s2.reshape(-1, dim), 0.3 * budget_s, 1)
     m = len(s1)
     t_mv = m / mps
     what = (f"nearestK(k={k})" if workload == "cfg4" else f"nearestR(r={radius:.4f})")
@@ -223,6 +246,60 @@ def single_query_scan(torch, nn, dev, reps, n_tree):
                          "note": "the 56 MB store is Infinity-Cache resident across back-to-back scans"}}
 
 
+def _timed(torch, stream, fn, reps):
+    """mean ms of fn() over reps, HIP events on the library's stream"""
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fn()
+    torch.cuda.synchronize()
+    ev[0].record(stream)
+    for _ in range(reps):
+        fn()
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps
+
+
+def sphere_variant(torch, run, local, reps=5):
+    """SURVEY §8d M2's 32-sphere field (r = 0.1, centres from RNG(7)) on the same (nearest,
+    steered) edges as the timed step, for realistic early-exit rates: the hypercube passage of
+    the headline rejects most motions at their first isValid(s2)."""
+    from ompl_amd import DiscreteMotionValidatorGPU
+    from ompl_amd import workloads as W
+    from ompl_amd.checkers import SpheresChecker
+
+    c, r = W.sphere_field(32, 0.1, 7)
+    mv = DiscreteMotionValidatorGPU(run.sp, SpheresChecker(c, r), local)
+    mv.set_stream(run.stream.cuda_stream)
+    valid = torch.empty(run.m, dtype=torch.uint8, device=run.dev)
+    c0 = mv.stateChecks()
+    ms = _timed(torch, run.stream, lambda: mv.check_device(run.s_from.data_ptr(), run.s_to.data_ptr(), run.m,
+                                                           valid.data_ptr()), reps)
+    checks = (mv.stateChecks() - c0) / (reps + 1)
+    return {"checker": "32 spheres r=0.1, centres RNG(7)", "motion_checks_per_s": run.m / (ms * 1e-3),
+            "ms_per_batch": ms, "edges": run.m, "valid_fraction": float(valid.float().mean().item()),
+            "isValid_calls_per_edge": checks / run.m}
+
+
+def rrt_star_knn(torch, run, n_tree, nq=1000, reps=3):
+    """M2(iii): RRT*'s neighbourhood query k = ceil(k_rrt ln(n+1)) = 6,169 at n = 10^6
+    (RRTstar.cpp:603-618, :1147-1159) for a batch of the run's samples, through the large-k path
+    (knn_large.hip: fp32 histogram threshold + exact fp64 candidates + segmented sort)."""
+    from ompl_amd import workloads as W
+
+    k = W.rrt_star_k(n_tree, 6)
+    nq = min(nq, run.nq)
+    ids = torch.empty((nq, k), dtype=torch.int32, device=run.dev)
+    dd = torch.empty((nq, k), dtype=torch.float64, device=run.dev)
+    q = run.queries.data_ptr()
+    ms0, n0, _ = run.nn.kernel_time()
+    ms = _timed(torch, run.stream, lambda: run.nn.knn_device(q, nq, k, ids.data_ptr(), dd.data_ptr()), reps)
+    ms1, n1, name = run.nn.kernel_time()
+    kern_ms = (ms1 - ms0) / max(n1 - n0, 1)
+    assert bool((dd[:, 1:] >= dd[:, :-1]).all().item()), "large-k lists must be sorted"
+    return {"k": k, "queries": nq, "queries_per_s": nq / (ms * 1e-3), "ms_per_batch": ms, "kernel": name,
+            "kernel_ms": kern_ms, "pairs_per_batch": float(nq) * n_tree}
+
+
 def rrt_device(torch, nn, mv, sp, dev, iters):
     """The RRT loop itself (RRT.cpp:128-192 without the goal test), `iters` dependent iterations
     queued on the device with no host round trip (ompl_gpu_rrt_grow_device).  Grows the tree,
@@ -255,15 +332,12 @@ class Runner:
         self.args, self.torch, self.dev = args, torch, dev
         wl, nq, k = args.workload, args.queries, args.k
         self.radius = None
-        qrng = np.random.default_rng(1000 + rank)                       # samples sharded by rank
         if wl == "cfg3":
             self.sp, self.ck = SE3StateSpace(0.0, 1.0), HypercubeChecker(3, 0.1)
-            self.tree = W.uniform_se3(np.random.default_rng(42), args.tree)   # identical on every rank
-            q = W.uniform_se3(qrng, nq)
+            self.tree, q = reference_inputs(self.sp, args.tree, nq, rank)
         elif wl == "cfg2":
             self.sp, self.ck = RealVectorStateSpace(6), HypercubeChecker(6, 0.1)
-            self.tree = W.uniform_rv(np.random.default_rng(42), args.tree, 6)
-            q = W.uniform_rv(qrng, nq, 6)
+            self.tree, q = reference_inputs(self.sp, args.tree, nq, rank)
         elif wl == "cfg4":
             self.sp = KinematicChainSpace(12, 1.0 / 12)                   # KinematicChainBenchmark.cpp:48-49
             self.ck = KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))
@@ -278,13 +352,9 @@ class Runner:
         elif wl == "cfg5":
             self.k = 0
         self.mv = DiscreteMotionValidatorGPU(self.sp, self.ck, local)
-        if wl == "cfg4":
-            self.tree = _valid_states(self.mv, lambda g, n: W.uniform_chain(g, n, 12), np.random.default_rng(42),
-                                      args.tree)
-            q = _valid_states(self.mv, lambda g, n: W.uniform_chain(g, n, 12), qrng, nq, chunk=max(4 * nq, 4096))
-        elif wl == "cfg5":
-            self.tree = _valid_states(self.mv, W.uniform_se3, np.random.default_rng(42), args.tree, chunk=2_000_000)
-            q = _valid_states(self.mv, W.uniform_se3, qrng, nq, chunk=2 * nq)
+        if wl in ("cfg4", "cfg5"):  # roadmap / sample sets hold valid states (PRM.cpp:356-378, ImplicitGraph.cpp:981)
+            self.tree, q = reference_inputs(self.sp, args.tree, nq, rank, valid=self.mv.isValid)
+        self.q_host = q
         self.nq = nq
         self.queries = torch.from_numpy(q).to(dev)
         self.nn = NearestNeighborsGPU(self.sp, local)
@@ -408,19 +478,64 @@ class Runner:
         return {"kq": k[2], "rq": r[1]}
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N fresh child processes of this script, one
+    per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set (the same environment
+    torch.distributed.run provides).  The parent never imports torch nor touches a GPU; it waits
+    for the children and exits with the first failure's code (the others are stopped)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            if p.poll() is not None:
+                live.remove(p)
+                if p.returncode != 0 and rc == 0:
+                    rc = p.returncode
+                    for q in live:
+                        q.terminate()
+    sys.exit(rc)
+
+
 def main():
     args = parse()
-    import torch
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        spawn_ranks(args.gpus)  # does not return
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    visible = torch.cuda.device_count()  # counts devices without initialising them
+    if local >= visible:
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local} but only {visible} GPU(s) are visible "
+                         f"(--gpus {args.gpus})")
     dist = None
     torch.cuda.set_device(local)
+    rccl_ranks = 1
     if world > 1:
         import torch.distributed as dist
 
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        one = torch.ones(1, device=torch.device("cuda", local))
+        dist.all_reduce(one)  # ranks as RCCL counts them
+        rccl_ranks = int(one.item())
+        if rccl_ranks != world:
+            raise SystemExit(f"bench.py: RCCL reports {rccl_ranks} ranks, expected {world}")
 
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(dev)  # a real (non-null) stream shared by torch events and the library
@@ -464,13 +579,16 @@ def main():
     total_units = float(u.item())
     valid_frac = float(run.valid[: max(run.m, 1)].float().mean().item()) if args.workload != "cfg2" else None
 
-    single = rrt = None
+    single = rrt = spheres = rrt_star = None
+    if rank == 0 and args.workload == "cfg3":
+        spheres = sphere_variant(torch, run, local)
+        if args.rrt_star_queries > 0:
+            rrt_star = rrt_star_knn(torch, run, args.tree, args.rrt_star_queries)
     if rank == 0 and args.workload == "cfg3" and args.single_query_reps > 0:
         single = single_query_scan(torch, run.nn, dev, args.single_query_reps, args.tree)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.workload, run.sp, run.ck, run.tree, np.random.default_rng(7), run.k,
-                           args.cpu_seconds, run.radius)
+        cpu = cpu_baseline(args.workload, run.sp, run.ck, run.tree, run.q_host, run.k, args.cpu_seconds, run.radius)
     if rank == 0 and args.workload == "cfg3" and args.rrt_iters > 0:
         rrt = rrt_device(torch, run.nn, run.mv, run.sp, dev, args.rrt_iters)
 
@@ -482,6 +600,7 @@ def main():
             "value": total_units / elapsed,
             "unit": unit,
             "n_gpus": world,
+            "rccl_ranks": rccl_ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
@@ -489,7 +608,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32 screen + f64 certify" if screen else "f64",
-            "data": "synthetic (seeded uniform states; tree seed 42, queries seed 1000+rank)",
+            "data": ("synthetic: the reference's RNG streams — RNG::setSeed(42), then a tree sampler and a query "
+                     "sampler (allocStateSampler x2); rank r takes queries [r*Q, (r+1)*Q)"),
             "config": run.config(world),
             "nn_queries_per_s": run.nq * world / (nn_ms * 1e-3),
             "phase_ms": {"nn": nn_ms, "steer_or_edges": edge_ms, "motion": mv_ms},
@@ -500,6 +620,10 @@ def main():
         if args.workload != "cfg2":
             line["motion_checks_per_s"] = run.m * world / (mv_ms * 1e-3)
             line["motion_valid_fraction"] = valid_frac
+        if spheres:
+            line["motion_spheres"] = spheres
+        if rrt_star:
+            line["rrt_star_knn"] = rrt_star
         if single:
             line["single_query"] = single
         if rrt:
