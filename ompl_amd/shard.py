@@ -8,7 +8,11 @@ Tree-sharded mode (for state sets beyond one GPU's HBM): each rank holds a conti
 slice of the ids, answers every query on its slice, and the per-rank top-k candidate
 lists are exchanged with one all_gather over RCCL (xGMI) and merged on every rank.
 RCCL's built-in reductions cannot merge top-k lists, so the exchange is an all_gather
-of Q*k*(8+8) bytes per rank followed by a local (distance, id) merge.
+of Q*k*(8+8) bytes per rank followed by a local (distance, id) merge.  Radius results are
+variable-size: a count all_gather, then padded payload all_gathers (allgather_radius).
+
+Growing sets (BIT* batches, PRM* causal prefixes): each rank contributes its part of a batch
+of new states and allgather_states gives every replica the whole batch in rank order.
 """
 from __future__ import annotations
 
@@ -44,3 +48,62 @@ def allgather_merge(d_local: torch.Tensor, ids_global: torch.Tensor, k: int, gro
     dist.all_gather(ds, d_local.contiguous(), group=group)
     dist.all_gather(ii, ids_global.contiguous(), group=group)
     return merge_topk(torch.cat(ds, dim=1), torch.cat(ii, dim=1), k)
+
+
+def _allgather_varlen(x: torch.Tensor, group=None):
+    """All-gather a tensor whose leading dimension differs per rank: one all_gather of the
+    counts, then one of the payload padded to the largest count (RCCL's all_gather needs equal
+    shapes).  Returns (list of per-rank tensors, counts)."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    counts = [int(c.item()) for c in ns]
+    m = max(counts) if counts else 0
+    pad = torch.zeros((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    pad[: x.shape[0]] = x
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return [p[:c] for p, c in zip(parts, counts)], counts
+
+
+def allgather_states(local: torch.Tensor, group=None) -> torch.Tensor:
+    """New states of one batch, contributed by every rank (each samples / validity-filters its
+    part: BIT*'s batch of samples, ImplicitGraph.cpp:924-1000; PRM*'s milestones of a causal
+    prefix, PRM.cpp:562-596), gathered in rank order on every rank, so that every replica of the
+    tree appends the same states in the same order and ids agree across ranks."""
+    parts, _ = _allgather_varlen(local.contiguous(), group)
+    return torch.cat(parts, dim=0)
+
+
+def merge_csr(offsets: list, ids: list, dists: list):
+    """Per-rank radius results for the same queries (CSR: offsets [Q+1], global ids, distances)
+    -> one CSR whose segments hold the union sorted by (distance, id), the order
+    NearestNeighborsGNAT::nearestR / Linear report (NearestNeighborsGNAT.h:236-245)."""
+    nq = offsets[0].numel() - 1
+    seg_d, seg_i, seg_q = [], [], []
+    for off, ii, dd in zip(offsets, ids, dists):
+        cnt = off[1:] - off[:-1]
+        seg_q.append(torch.repeat_interleave(torch.arange(nq, dtype=torch.int64, device=off.device), cnt))
+        seg_i.append(ii.to(torch.int64))
+        seg_d.append(dd)
+    q, i, d = torch.cat(seg_q), torch.cat(seg_i), torch.cat(seg_d)
+    o = torch.argsort(i, stable=True)           # id, then distance, then query: lexicographic
+    o = o[torch.argsort(d[o], stable=True)]
+    o = o[torch.argsort(q[o], stable=True)]
+    counts = torch.bincount(q, minlength=nq)
+    out_off = torch.zeros(nq + 1, dtype=torch.int64, device=q.device)
+    out_off[1:] = torch.cumsum(counts, 0)
+    return out_off, i[o], d[o]
+
+
+def allgather_radius(offsets: torch.Tensor, ids_global: torch.Tensor, dists: torch.Tensor, group=None):
+    """Tree-sharded nearestR (SURVEY §8e "Radius search"): every rank answers the same queries
+    on its slice of the states; the variable-size CSR results are exchanged as a count
+    all_gather followed by padded payload all_gathers, and merged on every rank."""
+    offs, _ = _allgather_varlen(offsets.to(torch.int64).contiguous(), group)
+    ii, _ = _allgather_varlen(ids_global.to(torch.int64).contiguous(), group)
+    dd, _ = _allgather_varlen(dists.contiguous(), group)
+    return merge_csr(offs, ii, dd)

@@ -1,6 +1,9 @@
-"""World-size-2 gloo tests (CPU) of the multi-GPU decomposition: query sharding covers
-every query exactly once, and the tree-sharded all_gather + merge reproduces the
-single-process top-k exactly (ids and distances, ties by id)."""
+"""Multi-rank tests of the multi-GPU decomposition over gloo (world size 2 and 3, CPU): query
+sharding covers every query exactly once; the tree-sharded all_gather + merge reproduces the
+single-process top-k exactly (ids and distances, ties by id); the radius CSR exchange (count
+all_gather + padded payload) reproduces nearestR; the per-batch state gather delivers every
+rank's new states to every replica in rank order.  test_sharded_hip_path_world2 runs the same
+with the HIP kernels answering each shard; test_bench_spawn_plumbing covers `bench.py --gpus N`."""
 import os
 import socket
 
@@ -92,3 +95,113 @@ def test_merge_topk_orders_by_distance_then_id():
     i = torch.tensor([[4, 9, 2, -1]])
     md, mi = merge_topk(d, i, 3)
     assert mi.tolist() == [[2, 9, 4]] and md.tolist() == [[0.1, 0.1, 0.5]]
+
+
+def _exchange_worker(rank, world, port, result_dir, use_gpu):
+    """Tree-sharded kNN + nearestR and the per-batch state gather on `world` gloo ranks.  With
+    use_gpu every rank answers its shard with the HIP path (NearestNeighborsGPU on cuda:0; the
+    collectives run on CPU tensors over gloo); without it, with the oracle."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import pyoracle as O
+
+    from ompl_amd import workloads as W
+    from ompl_amd.shard import allgather_radius, allgather_states
+    from ompl_amd.spaces import SE3StateSpace
+
+    sp = SE3StateSpace()
+    data, q = W.reference_states(sp, (6000, 40), seed=42)
+    data[4001] = data[17]  # a tie across shards
+    lo, hi = shard_bounds(len(data), rank, world)
+    r = 0.45
+    if use_gpu:
+        from ompl_amd import NearestNeighborsGPU
+
+        nn = NearestNeighborsGPU(sp, 0)
+        nn.add(data[lo:hi])
+        li, ld, _ = nn.nearestKBatch(q, 12)
+        li = np.where(np.isinf(ld), -1, li.astype(np.int64))  # missing entries: (inf, NO_ID)
+        off, ri, rd = nn.nearestRBatch(q, r)
+    else:
+        li, ld, _ = O.knn(sp, data[lo:hi], q, 12)
+        li = np.where(li == 0xFFFFFFFF, -1, li.astype(np.int64))
+        off, ri, rd = O.radius(sp, data[lo:hi], q, r)
+    gid = torch.from_numpy(np.where(li >= 0, li + lo, -1))
+    d, i = allgather_merge(torch.from_numpy(ld), gid, 12)
+    goff, gi, gd = allgather_radius(torch.from_numpy(off.astype(np.int64)),
+                                    torch.from_numpy(ri.astype(np.int64) + lo), torch.from_numpy(rd))
+    # a batch of new states: rank r contributes r + 3 of them; every rank gets all, rank order
+    mine = torch.full((rank + 3, 7), float(rank), dtype=torch.float64)
+    batch = allgather_states(mine)
+    np.savez(os.path.join(result_dir, f"x{rank}.npz"), d=d.numpy(), i=i.numpy(), off=goff.numpy(), ri=gi.numpy(),
+             rd=gd.numpy(), batch=batch.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _check_exchange(tmp_path, world):
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import pyoracle as O
+
+    from ompl_amd import workloads as W
+    from ompl_amd.spaces import SE3StateSpace
+
+    sp = SE3StateSpace()
+    data, q = W.reference_states(sp, (6000, 40), seed=42)
+    data[4001] = data[17]
+    oi, od, _ = O.knn(sp, data, q, 12)
+    ooff, oid, ord_ = O.radius(sp, data, q, 0.45)
+    for r in range(world):
+        z = np.load(tmp_path / f"x{r}.npz")
+        np.testing.assert_array_equal(z["i"], oi.astype(np.int64))
+        np.testing.assert_allclose(z["d"], od, rtol=0, atol=4e-16)
+        np.testing.assert_array_equal(z["off"], ooff.astype(np.int64))
+        np.testing.assert_array_equal(z["ri"], oid.astype(np.int64))
+        np.testing.assert_allclose(z["rd"], ord_, rtol=0, atol=4e-16)
+        b = z["batch"]
+        assert b.shape == (sum(k + 3 for k in range(world)), 7)
+        np.testing.assert_array_equal(b[:, 0], np.concatenate([np.full(k + 3, float(k)) for k in range(world)]))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_radius_and_state_exchange_gloo(tmp_path, world):
+    port = _free_port()
+    mp.start_processes(_exchange_worker, args=(world, port, str(tmp_path), False), nprocs=world, join=True,
+                       start_method="spawn")
+    _check_exchange(tmp_path, world)
+
+
+@pytest.mark.gpu
+def test_sharded_hip_path_world2(tmp_path, gpu):
+    """The same decomposition with each rank's shard answered by the HIP kernels (two ranks
+    sharing the box's one GPU, collectives over gloo)."""
+    port = _free_port()
+    mp.start_processes(_exchange_worker, args=(2, port, str(tmp_path), True), nprocs=2, join=True,
+                       start_method="spawn")
+    _check_exchange(tmp_path, 2)
+
+
+def test_bench_spawn_plumbing():
+    """`bench.py --gpus 2` without a launcher starts one child per rank with RANK / LOCAL_RANK /
+    WORLD_SIZE set; with no GPU visible each rank fails loudly and so does the parent.  A
+    WORLD_SIZE that disagrees with --gpus is refused before any GPU work."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = "-1"  # no GPU even where one exists
+    env["CUDA_VISIBLE_DEVICES"] = "-1"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "rank 0 needs GPU 0" in r.stderr or "rank 1 needs GPU 1" in r.stderr, r.stderr[-2000:]
+    env["WORLD_SIZE"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "--gpus 4 but WORLD_SIZE=2" in r.stderr
