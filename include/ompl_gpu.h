@@ -185,6 +185,9 @@ ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint
  * store for all uncertified queries, keeping d <= the certificate's exact k-th distance)
  * exceeded its candidate cap and took the full exact scan. */
 ompl_gpu_status ompl_gpu_nn_rerun_stats(const ompl_gpu_nn *h, uint64_t *full);
+/* The culled walks' sorted copy: device k-d builds and tail appends (states added since the
+ * last build placed along the Morton curve without a rebuild) performed so far. */
+ompl_gpu_status ompl_gpu_nn_index_stats(const ompl_gpu_nn *h, uint64_t *builds, uint64_t *appends);
 /* Group walk: 64-state tiles fetched, summed over query groups, vs the tiles a full scan
  * by the same groups would have touched; *query_tiles counts (tile, query) scans, i.e.
  * 64 distance evaluations each.  Any output may be NULL. */

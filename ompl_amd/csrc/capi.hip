@@ -94,6 +94,7 @@ struct ompl_gpu_nn {
     double *feat = nullptr;  // [F][cap]
     double *raw = nullptr;   // [dim][cap] (KCHAIN) or == feat
     float *feat32 = nullptr; // [rows32][cap] fp32 copy for the screening scan (knn_fast.hip)
+    uint8_t *live = nullptr; // [cap] 1 = stored and not removed (the device k-d build's input)
     int rows32 = 0;
     uint64_t cap = 0, n_total = 0, n_live = 0;
     std::vector<uint8_t> removed;
@@ -106,17 +107,19 @@ struct ompl_gpu_nn {
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
     double lo[kKeyDims] = {0}, hi[kKeyDims] = {0}, absmax = 0.0;
-    // Morton-sorted fp32 copy for the culled screen (rebuilt lazily after add/remove)
+    // k-d sorted fp32 copy for the culled walks: built on the device, states added later go to
+    // its Morton-ordered tail, removals are tombstoned in place (kernels.h SortedStore)
     SortedStore sorted;
-    FastBounds sorted_bounds{};
-    bool sorted_dirty = true;
-    DevBuf raw_aos;         // [n_total][da] fp64 raw states by id (edge endpoints), rebuilt lazily
-    bool aos_dirty = true;
+    DevBuf raw_aos;         // [n_total][da] fp64 raw states by id (edge endpoints), appended lazily
+    uint64_t aos_n = 0;     // ids [0, aos_n) converted
+    uint64_t sorted_builds = 0, sorted_appends = 0;  // device k-d builds / tail appends
     bool cull = true;         // ompl_gpu_nn_set_exact(h, 2) disables the culled screen
     DevBuf cull_counter;      // SortedStore::counters: kNN walk [tiles fetched, tiles of a brute-force
                               // walk, (tile, query) pairs scanned], radius walk [tiles, pairs] (device)
     bool fast = true;        // OMPL_GPU_EXACT_ONLY=1 forces the exact fp64 scan
-    uint64_t fast_queries = 0, fast_fallbacks = 0, fast_overflows = 0;  // overflows: bounded re-run exceeded its cap
+    uint64_t fast_queries = 0;
+    DevBuf stats_dev;         // device counters: [0] queries re-run exactly, [1] of those, full scans
+    bool stats_init = false;
     // profiling of the dominant scan kernel (HIP events on the launch stream)
     bool profile = false;
     std::vector<KernelTimer> pending;
@@ -245,6 +248,7 @@ ompl_gpu_status ompl_gpu_nn_destroy(ompl_gpu_nn *h) {
     if (h->raw && h->raw != h->feat) (void)hipFree(h->raw);
     if (h->feat) (void)hipFree(h->feat);
     if (h->feat32) (void)hipFree(h->feat32);
+    if (h->live) (void)hipFree(h->live);
     free_sorted_store(&h->sorted);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
@@ -281,6 +285,10 @@ static ompl_gpu_status grow(ompl_gpu_nn *h, uint64_t need) {
             HIP_OR_FAIL(hipMemcpy2DAsync(n32, nc * sizeof(float), h->feat32, h->cap * sizeof(float),
                                          h->n_total * sizeof(float), h->rows32, hipMemcpyDeviceToDevice, h->stream));
     }
+    uint8_t *nl = nullptr;
+    HIP_OR_FAIL(hipMalloc(&nl, nc));
+    HIP_OR_FAIL(hipMemsetAsync(nl, 0, nc, h->stream));
+    if (h->n_total) HIP_OR_FAIL(hipMemcpyAsync(nl, h->live, h->n_total, hipMemcpyDeviceToDevice, h->stream));
     HIP_OR_FAIL(hipMalloc(&nf, sizeof(double) * F * nc));
     HIP_OR_FAIL(hipMemsetAsync(nf, 0xFF, sizeof(double) * F * nc, h->stream));  // all-ones = NaN
     if (sep_raw) {
@@ -299,6 +307,8 @@ static ompl_gpu_status grow(ompl_gpu_nn *h, uint64_t need) {
     if (h->raw && h->raw != h->feat) (void)hipFree(h->raw);
     if (h->feat) (void)hipFree(h->feat);
     if (h->feat32) (void)hipFree(h->feat32);
+    if (h->live) (void)hipFree(h->live);
+    h->live = nl;
     h->feat = nf;
     h->feat32 = n32;
     h->raw = sep_raw ? nr : nf;
@@ -330,10 +340,10 @@ ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, 
         HIP_OR_FAIL(launch_store_soa(sr, (uint32_t)n, dim, h->raw, h->cap, h->n_total, h->stream));
     }
     if (h->rows32) HIP_OR_FAIL(launch_rows32(h->sp, h->g, h->feat, h->cap, h->n_total, n, h->feat32, h->stream));
-    // screening bounds (knn_fast.hip): key box of the first <= 6 coordinates, max |coordinate|
+    HIP_OR_FAIL(hipMemsetAsync(h->live + h->n_total, 1, n, h->stream));
+    // screening bounds (knn_fast.hip): key box of the first <= 6 coordinates, max |coordinate|;
+    // the sorted copy picks the new ids up in its tail at the next query (ensure_sorted)
     const int nb = tracked_dims(h->sp);
-    h->sorted_dirty = true;
-    h->aos_dirty = true;
     const int na = h->sp.kind == OMPL_GPU_SPACE_SE3 ? 3 : (h->sp.kind == OMPL_GPU_SPACE_SO3 ? 0 : dim);
     for (size_t i = 0; i < n; ++i) {
         const double *s = states + i * dim;
@@ -362,10 +372,10 @@ ompl_gpu_status ompl_gpu_nn_remove(ompl_gpu_nn *h, uint64_t id) {
     const float nanf = __builtin_nanf("");
     if (h->rows32)
         HIP_OR_FAIL(hipMemcpyAsync(h->feat32 + id, &nanf, sizeof(float), hipMemcpyHostToDevice, h->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    HIP_OR_FAIL(hipMemsetAsync(h->live + id, 0, 1, h->stream));
+    HIP_OR_FAIL(tombstone_sorted_store(&h->sorted, id, h->stream));  // the sorted copy, in place
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));                     // the host NaNs are stack values
     h->removed[id] = 1;
-    h->sorted_dirty = true;
-    h->aos_dirty = true;
     h->n_live--;
     return OMPL_GPU_OK;
 }
@@ -379,12 +389,13 @@ ompl_gpu_status ompl_gpu_nn_clear(ompl_gpu_nn *h) {
         if (h->raw != h->feat)
             HIP_OR_FAIL(hipMemsetAsync(h->raw, 0xFF, sizeof(double) * h->sp.dim * h->cap, h->stream));
         if (h->rows32) HIP_OR_FAIL(hipMemsetAsync(h->feat32, 0xFF, sizeof(float) * h->rows32 * h->cap, h->stream));
+        HIP_OR_FAIL(hipMemsetAsync(h->live, 0, h->cap, h->stream));
         HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     }
     h->n_total = h->n_live = 0;
     h->absmax = 0.0;
-    h->sorted_dirty = true;
-    h->aos_dirty = true;
+    h->sorted.built = false;  // keeps its allocations
+    h->aos_n = 0;
     h->removed.clear();
     return OMPL_GPU_OK;
 }
@@ -427,19 +438,29 @@ static bool screen_safe(const ompl_gpu_nn *h) { return h->absmax < kScreenMaxAbs
 
 constexpr int kCullCounters = 5;
 
-// (re)build the Morton-sorted fp32 copy the culled walks read, if adds or removes made it stale
+// bring the sorted copy the culled walks read up to date, on the handle's stream with no host
+// round trip: a full device build when there is none (or too many tombstones / a full tail),
+// else the states added since the last call go to its tail
 static ompl_gpu_status ensure_sorted(ompl_gpu_nn *h) {
-    if (!h->sorted_dirty && h->sorted.n == h->n_total) return OMPL_GPU_OK;
-    h->sorted_bounds = current_bounds(h);
-    HIP_OR_FAIL(build_sorted_store(h->sp, h->g, h->feat32, h->cap, (uint32_t)h->n_total, h->sorted_bounds, &h->sorted,
-                                   h->stream));
-    HIP_OR_FAIL(build_sorted_rows64(h->g, h->feat, h->cap, &h->sorted, h->stream));
-    h->sorted_dirty = false;
+    SortedStore &s = h->sorted;
+    bool rebuild = !s.built || s.removed * 4 > (uint64_t)s.main_live + 256;
+    if (!rebuild && h->n_total > s.covered) {
+        bool fits = false;
+        HIP_OR_FAIL(append_sorted_store(h->sp, h->g, h->feat32, h->feat, h->cap, h->n_total, current_bounds(h), &s,
+                                        h->stream, &fits));
+        rebuild = !fits;
+        if (fits) h->sorted_appends++;
+    }
+    if (rebuild) {
+        HIP_OR_FAIL(build_sorted_store(h->sp, h->g, h->feat32, h->feat, h->cap, h->n_total, (uint32_t)h->n_live, h->live,
+                                       &s, h->stream));
+        h->sorted_builds++;
+    }
     if (!h->cull_counter.p) {
         HIP_OR_FAIL(h->cull_counter.ensure(kCullCounters * sizeof(unsigned long long)));
         HIP_OR_FAIL(hipMemsetAsync(h->cull_counter.p, 0, kCullCounters * sizeof(unsigned long long), h->stream));
     }
-    h->sorted.counters = (unsigned long long *)h->cull_counter.p;
+    s.counters = (unsigned long long *)h->cull_counter.p;
     return OMPL_GPU_OK;
 }
 
@@ -485,7 +506,7 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
             ompl_gpu_status s = ensure_sorted(h);
             if (s != OMPL_GPU_OK) return s;
         }
-        FastBounds b = cull ? h->sorted_bounds : current_bounds(h);
+        FastBounds b = current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
         b.n_live = (uint32_t)h->n_live;
         const size_t wsb = knn_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus, cull);
@@ -494,40 +515,24 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
         HIP_OR_FAIL(launch_knn_fast(h->sp, h->g, h->feat, h->feat32, h->cap, n_end, cull ? &h->sorted : nullptr, d_qf,
                                     (uint32_t)nq, k, b, d_dist, d_ids, h->ws.p, h->ws.bytes, h->num_cus, h->stream,
                                     &d_fail_count, &d_fail_list));
-        uint32_t nfail = 0;
-        HIP_OR_FAIL(hipMemcpyAsync(&nfail, d_fail_count, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
-        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+        // exact re-run of the uncertified queries, decided on the device: the bounded pass (one
+        // store read for all of them), a full scan for any that overflow its candidate cap
+        HIP_OR_FAIL(h->fb_c.ensure(sizeof(uint32_t) * (kBoundedMaxQ + 1 + nq)));
+        HIP_OR_FAIL(h->fb_cd.ensure(sizeof(double) * kBoundedMaxQ * kBoundedCap));
+        HIP_OR_FAIL(h->fb_ci.ensure(sizeof(uint32_t) * kBoundedMaxQ * kBoundedCap));
+        uint32_t *cnt = (uint32_t *)h->fb_c.p;
+        HIP_OR_FAIL(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (kBoundedMaxQ + 1), h->stream));
+        HIP_OR_FAIL(launch_knn_bounded(h->sp, h->g, h->feat, h->cap, n_end, d_qf, d_fail_list, d_fail_count, k, d_dist,
+                                       d_ids, cnt, (double *)h->fb_cd.p, (uint32_t *)h->fb_ci.p, h->num_cus,
+                                       h->stream));
         h->fast_queries += nq;
-        h->fast_fallbacks += nfail;
-        if (nfail == 0) return OMPL_GPU_OK;
-        // exact fp64 re-run of the uncertified queries: a bounded pass for all of them at once
-        // (knn_bounded_kernel), the full exact path for any that overflow its candidate cap
-        const int F = h->g.F;
-        if (nfail <= kBoundedMaxQ) {
-            HIP_OR_FAIL(h->fb_c.ensure(sizeof(uint32_t) * (2 * nfail + 1)));
-            HIP_OR_FAIL(h->fb_cd.ensure(sizeof(double) * nfail * kBoundedCap));
-            HIP_OR_FAIL(h->fb_ci.ensure(sizeof(uint32_t) * nfail * kBoundedCap));
-            uint32_t *cnt = (uint32_t *)h->fb_c.p;
-            HIP_OR_FAIL(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (nfail + 1), h->stream));
-            HIP_OR_FAIL(launch_knn_bounded(h->sp, h->g, h->feat, h->cap, n_end, d_qf, d_fail_list, nfail, k, d_dist,
-                                           d_ids, cnt, (double *)h->fb_cd.p, (uint32_t *)h->fb_ci.p, h->stream));
-            const uint32_t nlist = nfail;  // the copy below overwrites nfail with the overflow count
-            d_fail_list = cnt + nlist + 1;
-            HIP_OR_FAIL(hipMemcpyAsync(&nfail, cnt + nlist, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
-            HIP_OR_FAIL(hipStreamSynchronize(h->stream));
-            h->fast_overflows += nfail;
-            if (nfail == 0) return OMPL_GPU_OK;
+        HIP_OR_FAIL(h->stats_dev.ensure(2 * sizeof(unsigned long long)));
+        if (!h->stats_init) {
+            HIP_OR_FAIL(hipMemsetAsync(h->stats_dev.p, 0, 2 * sizeof(unsigned long long), h->stream));
+            h->stats_init = true;
         }
-        HIP_OR_FAIL(h->fb_q.ensure(sizeof(double) * nfail * F));
-        HIP_OR_FAIL(h->fb_d.ensure(sizeof(double) * nfail * k));
-        HIP_OR_FAIL(h->fb_i.ensure(sizeof(uint32_t) * nfail * k));
-        HIP_OR_FAIL(launch_gather_rows(d_qf, F, d_fail_list, nfail, (double *)h->fb_q.p, h->stream));
-        HIP_OR_FAIL(h->ws2.ensure(knn_workspace_bytes(h->sp, h->g, nfail, k, n_end, h->num_cus)));
-        HIP_OR_FAIL(launch_knn(h->sp, h->g, h->feat, h->cap, n_end, (const double *)h->fb_q.p, nfail, k,
-                               (double *)h->fb_d.p, (uint32_t *)h->fb_i.p, h->ws2.p, h->ws2.bytes, h->num_cus,
-                               h->stream));
-        HIP_OR_FAIL(launch_scatter_results((const double *)h->fb_d.p, (const uint32_t *)h->fb_i.p, k, d_fail_list,
-                                           nfail, d_dist, d_ids, h->stream));
+        HIP_OR_FAIL(launch_count_add(d_fail_count, cnt + kBoundedMaxQ, (unsigned long long *)h->stats_dev.p,
+                                     h->stream));
         return OMPL_GPU_OK;
     }
     const size_t wsb = knn_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus);
@@ -612,7 +617,7 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
         // culled walk over the Morton-sorted copy (knn_fast_impl.h)
         ompl_gpu_status s = ensure_sorted(h);
         if (s != OMPL_GPU_OK) return s;
-        FastBounds b = h->sorted_bounds;
+        FastBounds b = current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
         HIP_OR_FAIL(h->ws.ensure(radius_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq)));
         uint64_t *d_off = nullptr;
@@ -835,10 +840,20 @@ ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries
     // endpoints are gathered by random id: one contiguous row per state instead of one cache
     // line per coordinate of the SoA store
     const int da = (h->sp.dim + 1) & ~1;
-    if (h->aos_dirty && h->n_total) {
-        HIP_OR_FAIL(h->raw_aos.ensure(sizeof(double) * h->n_total * da));
-        HIP_OR_FAIL(launch_aos_rows(h->raw, h->cap, h->sp.dim, da, h->n_total, (double *)h->raw_aos.p, h->stream));
-        h->aos_dirty = false;
+    if (h->aos_n < h->n_total) {  // rows of the ids added since the last call (ids never move)
+        if (h->raw_aos.bytes < sizeof(double) * h->n_total * da) {
+            DevBuf nb;
+            HIP_OR_FAIL(nb.ensure(sizeof(double) * std::max<uint64_t>(h->cap, h->n_total) * da));
+            if (h->aos_n)
+                HIP_OR_FAIL(hipMemcpyAsync(nb.p, h->raw_aos.p, sizeof(double) * h->aos_n * da, hipMemcpyDeviceToDevice,
+                                           h->stream));
+            std::swap(h->raw_aos.p, nb.p);
+            std::swap(h->raw_aos.bytes, nb.bytes);
+            HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // nb (the old buffer) is freed on return
+        }
+        HIP_OR_FAIL(launch_aos_rows(h->raw, h->cap, h->sp.dim, da, h->aos_n, h->n_total - h->aos_n,
+                                    (double *)h->raw_aos.p, h->stream));
+        h->aos_n = h->n_total;
     }
     HIP_OR_FAIL(launch_edges(h->sp, h->raw, h->cap, d_queries, (uint32_t)nq, d_offsets, d_ids, stride, m, from_query,
                              d_from, d_to, h->stream, h->n_total ? (const double *)h->raw_aos.p : nullptr, da));
@@ -926,16 +941,41 @@ ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, 
     return OMPL_GPU_OK;
 }
 
+// the re-run counters live on the device (the query path never waits for them): read them here
+static ompl_gpu_status read_stats(const ompl_gpu_nn *ch, unsigned long long *c) {
+    ompl_gpu_nn *h = const_cast<ompl_gpu_nn *>(ch);
+    std::lock_guard<std::mutex> lk(h->mu);
+    c[0] = c[1] = 0;
+    if (!h->stats_init) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(hipMemcpyAsync(c, h->stats_dev.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
 ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint64_t *fallbacks) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    unsigned long long c[2];
+    ompl_gpu_status s = read_stats(h, c);
+    if (s != OMPL_GPU_OK) return s;
     if (screened) *screened = h->fast_queries;
-    if (fallbacks) *fallbacks = h->fast_fallbacks;
+    if (fallbacks) *fallbacks = c[0];
     return OMPL_GPU_OK;
 }
 
 ompl_gpu_status ompl_gpu_nn_rerun_stats(const ompl_gpu_nn *h, uint64_t *full) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
-    if (full) *full = h->fast_overflows;
+    unsigned long long c[2];
+    ompl_gpu_status s = read_stats(h, c);
+    if (s != OMPL_GPU_OK) return s;
+    if (full) *full = c[1];
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_index_stats(const ompl_gpu_nn *h, uint64_t *builds, uint64_t *appends) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    if (builds) *builds = h->sorted_builds;
+    if (appends) *appends = h->sorted_appends;
     return OMPL_GPU_OK;
 }
 
@@ -1221,11 +1261,10 @@ ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const 
     uint64_t n1 = n0;
     HIP_OR_FAIL(hipMemcpyAsync(&n1, h->rrt_n.p, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (n1 > n0) HIP_OR_FAIL(hipMemsetAsync(h->live + n0, 1, n1 - n0, h->stream));
     h->n_live += n1 - n0;
     h->n_total = n1;
     h->removed.resize(h->n_total, 0);
-    h->sorted_dirty = true;
-    h->aos_dirty = true;
     return OMPL_GPU_OK;
 }
 

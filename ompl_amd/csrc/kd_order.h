@@ -1,10 +1,9 @@
-// kd_order.h — k-d leaf order of the sorted store (kd_order.cpp, host) and its node record,
-// which the device walks to find a query's home leaf (knn_fast_impl.h).
+// kd_order.h — the node record of the sorted store's k-d tree (built on the device,
+// knn_fast_impl.h build_sorted), which the device walks to find a query's home leaf.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
 
-#include <vector>
 
 namespace ompl_amd {
 
@@ -18,10 +17,5 @@ struct KdNode {
     uint32_t left_tiles;
     uint32_t right;
 };
-
-// x: rows [dims][stride] of n states.  perm: the states in leaf order (leaves of `tile`
-// states; removed states, NaN in row 0, last); nodes: the internal nodes, pre-order.
-void kd_tile_order(const float *x, size_t stride, uint32_t n, int dims, uint32_t tile, std::vector<uint32_t> &perm,
-                   std::vector<KdNode> &nodes);
 
 }  // namespace ompl_amd

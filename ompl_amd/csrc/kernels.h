@@ -89,15 +89,27 @@ constexpr int group_queries() { return SP == OMPL_GPU_SPACE_SE3 ? 4 : 8; }  // m
 struct SortedStore {
     float *rows = nullptr;       // [rows32][n_pad] (SE3 quaternions sign-canonical: w >= 0)
     uint32_t *ids = nullptr;     // [n_pad] original id of each sorted slot (kNoId = padding)
-    float *tbox = nullptr;       // [ntiles][box_w] lo.., hi.. (, eta, pad)
-    float *sbox = nullptr;       // [nsuper][box_w]
-    uint32_t *tkey0 = nullptr;   // [ntiles] key of each tile = its index (queries' keys are home tiles)
-    KdNode *nodes = nullptr;     // internal k-d nodes, pre-order (kd_order.h)
+    float *tbox = nullptr;       // [tiles][box_w] lo.., hi.. (, eta, pad)
+    float *sbox = nullptr;       // [supers][box_w]
+    uint32_t *tkey0 = nullptr;   // [tiles] key of each tile = its index (queries' keys are home tiles)
+    KdNode *nodes = nullptr;     // internal k-d nodes of the main tiles, pre-order (kd_order.h)
     double *rows64 = nullptr;    // [n_pad][fa] fp64 features in sorted order (AoS: one 64 B row per
                                  // SE3 state), read by the certificate; padding rows are NaN
+    uint32_t *inv = nullptr;     // [cap_inv] sorted position of each id (kNoId: not placed)
     int fa = 0;                  // fp64 row width: F rounded up to a multiple of 4
     uint32_t n = 0, n_pad = 0, ntiles = 0, nsuper = 0, nnodes = 0;
-    uint32_t kd_tiles = 0;       // leaves of the k-d tree: the tiles holding live states (removed ones follow)
+    uint32_t kd_tiles = 0;       // main tiles (leaves of the k-d tree, built on the device)
+    // incremental state: the main k-d tiles hold the live ids of [0, main_covered) at the build;
+    // states added since then are re-tiled along the Morton curve in the tail region, tiles
+    // [tail_t0, tail_t0 + tail_cap_tiles) (tail_t0 a super-tile boundary); removals write a NaN
+    // into the state's sorted row (inv) — boxes stay conservative — until a quarter of the
+    // main states are gone, which triggers a rebuild
+    bool built = false;
+    uint32_t main_live = 0, tail_t0 = 0, tail_cap_tiles = 0;
+    uint64_t main_covered = 0, covered = 0, removed = 0;
+    size_t cap_pos = 0, cap_nodes = 0, cap_inv = 0;  // allocated positions / nodes / inv entries
+    void *scratch = nullptr;     // build / append workspace (grow-only)
+    size_t scratch_bytes = 0;
     size_t bytes = 0;
     // optional device counters (owned by the caller), kNN walk: [0] tiles fetched, [1] tiles
     // a brute-force walk of the same query groups would have fetched, [2] (tile, query) pairs
@@ -105,12 +117,18 @@ struct SortedStore {
     unsigned long long *counters = nullptr;
 };
 bool cull_supported(const DevSpace &sp);
-// (re)build the sorted copy of ids [0, n) from the fp32 store; allocates into *s
-hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, uint64_t cap, uint32_t n,
-                              const FastBounds &b, SortedStore *s, hipStream_t st);
+// full device build of the sorted copy over the live ids of [0, n_total) (live[id] != 0, n_live
+// of them); asynchronous on st
+hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, const double *feat64,
+                              uint64_t cap, uint64_t n_total, uint32_t n_live, const uint8_t *live, SortedStore *s,
+                              hipStream_t st);
+// place ids [s->main_covered, n_total) in the tail region; *fits = false when they do not fit (rebuild)
+hipError_t append_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, const double *feat64,
+                               uint64_t cap, uint64_t n_total, const FastBounds &b, SortedStore *s, hipStream_t st,
+                               bool *fits);
+// removal of a placed id: its sorted fp32 row 0 becomes NaN
+hipError_t tombstone_sorted_store(SortedStore *s, uint64_t id, hipStream_t st);
 void free_sorted_store(SortedStore *s);
-// fp64 AoS rows of the sorted copy (s->rows64), gathered from the SoA fp64 store by s->ids
-hipError_t build_sorted_rows64(const FeatGeom &g, const double *feat64, uint64_t cap, SortedStore *s, hipStream_t st);
 
 int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq);  // screening list size, 0 = not eligible
 int fp32_rows(const DevSpace &sp, const FeatGeom &g);     // rows of the fp32 SoA copy
@@ -137,18 +155,22 @@ hipError_t launch_knn_large(const DevSpace &sp, const FeatGeom &g, const double 
                             hipStream_t st);
 hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t first, uint64_t n, float *feat32,
                           hipStream_t st);
-// bounded exact re-run of the fast path's uncertified queries list[0..nlist) (nlist <=
-// kBoundedMaxQ): od / oi hold the certificate's exact lists (row q = query q, k entries),
-// whose k-th distance bounds the answer; the exact top-k overwrites them.  counts (device,
-// nlist + 1 + nlist words, zeroed by the caller) returns at [nlist] the number of queries
-// that need the full exact path and at [nlist + 1 ..] their indices.  cand_d / cand_i hold
-// nlist * kBoundedCap entries.
+// exact re-run of the fast path's uncertified queries, with no host round trip: list[0..*d_nlist)
+// (device count).  The first kBoundedMaxQ take the bounded pass: od / oi hold the certificate's
+// exact lists (row q = query q, k entries), whose k-th distance bounds the answer, and the exact
+// top-k overwrites them; queries with more than kBoundedCap candidates (and list entries past
+// kBoundedMaxQ) take a full exact scan.  counts (device, kBoundedMaxQ + 1 + nq words, the first
+// kBoundedMaxQ + 1 zeroed by the caller) returns at [kBoundedMaxQ] the number of full scans and
+// at [kBoundedMaxQ + 1 ..] their query indices.  cand_d / cand_i hold kBoundedMaxQ * kBoundedCap
+// entries.
 constexpr uint32_t kBoundedCap = 1024;
 constexpr uint32_t kBoundedMaxQ = 512;
 hipError_t launch_knn_bounded(const DevSpace &sp, const FeatGeom &g, const double *feat, uint64_t cap,
-                              uint64_t n_end, const double *qf, const uint32_t *list, uint32_t nlist, uint32_t k,
-                              double *od, uint32_t *oi, uint32_t *counts, double *cand_d, uint32_t *cand_i,
-                              hipStream_t st);
+                              uint64_t n_end, const double *qf, const uint32_t *list, const uint32_t *d_nlist,
+                              uint32_t k, double *od, uint32_t *oi, uint32_t *counts, double *cand_d,
+                              uint32_t *cand_i, int num_cus, hipStream_t st);
+// acc[0] += *a; acc[1] += *b (device-side statistics, one thread)
+hipError_t launch_count_add(const uint32_t *a, const uint32_t *b, unsigned long long *acc, hipStream_t st);
 // gather rows q = list[i] of an AoS [*][F] fp64 array into dst[i]; scatter results back
 hipError_t launch_gather_rows(const double *src, int F, const uint32_t *list, uint32_t n, double *dst, hipStream_t st);
 hipError_t launch_scatter_results(const double *d, const uint32_t *ids, uint32_t k, const uint32_t *list, uint32_t n,
@@ -177,7 +199,9 @@ hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_
 hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
                         const uint64_t *offsets, const uint32_t *ids, uint32_t stride, uint64_t m, int from_query,
                         double *from, double *to, hipStream_t st, const double *aos = nullptr, int da = 0);
-hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uint64_t n, double *aos, hipStream_t st);
+// rows of ids [first, first + n) of the SoA store into aos[id][da]
+hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uint64_t first, uint64_t n, double *aos,
+                           hipStream_t st);
 // ---- RRT growth on device (rrt.hip) -------------------------------------------------------
 size_t rrt_part_entries(uint64_t n_max);
 hipError_t launch_rrt_grow(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck, const FeatGeom &g,

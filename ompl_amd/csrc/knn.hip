@@ -186,15 +186,19 @@ __global__ __launch_bounds__(256) void knn_stream_merge_kernel(const double *__r
 // the store therefore keeps every state with exact d <= b_q (few per query) and a rank
 // sort of that set yields the exact (distance, id) top-k — the same answer as the full
 // stream re-run, at one read of the store for all failed queries together instead of one
-// per query.  A query with more than kBoundedCap such states is reported as overflowing
-// and re-run by the full exact path.
+// per query.  A query with more than kBoundedCap such states overflows to the full scan.
+// The list length is read on the device (no host round trip): the kernels are launched
+// with fixed grids and return at once when nothing failed.
 template <int SP, int F, int NMAX, int ITEMS>
 __global__ __launch_bounds__(256) void knn_bounded_kernel(const double *__restrict__ feat, uint64_t cap,
                                                           uint64_t n_end, const double *__restrict__ qfeat,
-                                                          const uint32_t *__restrict__ list, uint32_t nlist,
+                                                          const uint32_t *__restrict__ list,
+                                                          const uint32_t *__restrict__ nlist_ptr,
                                                           const double *__restrict__ out_d, uint32_t out_k,
                                                           DevSpace sp, uint32_t *__restrict__ counts,
                                                           double *__restrict__ cand_d, uint32_t *__restrict__ cand_i) {
+    const uint32_t nlist = min(*nlist_ptr, kBoundedMaxQ);
+    if (nlist == 0) return;
     const uint64_t base = (uint64_t)blockIdx.x * (256 * ITEMS) + threadIdx.x;
     double sf[ITEMS][F];
 #pragma unroll
@@ -233,10 +237,12 @@ __global__ __launch_bounds__(256) void knn_bounded_kernel(const double *__restri
     }
 }
 
-// block per re-run query: rank-sort its candidates by (distance, id) in LDS and write the
-// first out_k into the query's output row; too many (or, impossibly, too few) candidates
-// put the query on the overflow list (counts[nlist] = its length, list from counts + nlist + 1)
-__global__ __launch_bounds__(256) void knn_bounded_select_kernel(const uint32_t *__restrict__ list, uint32_t nlist,
+// block j < nlist: rank-sort query list[j]'s candidates by (distance, id) in LDS and write the
+// first out_k into its output row; too many (or, impossibly, too few) candidates put the query
+// on the overflow list (counts[kBoundedMaxQ] = its length, entries from counts + kBoundedMaxQ + 1).
+// The last block moves list entries beyond kBoundedMaxQ (not re-run here) to the overflow list.
+__global__ __launch_bounds__(256) void knn_bounded_select_kernel(const uint32_t *__restrict__ list,
+                                                                 const uint32_t *__restrict__ nlist_ptr,
                                                                  uint32_t *__restrict__ counts,
                                                                  const double *__restrict__ cand_d,
                                                                  const uint32_t *__restrict__ cand_i, uint32_t out_k,
@@ -244,10 +250,18 @@ __global__ __launch_bounds__(256) void knn_bounded_select_kernel(const uint32_t 
                                                                  uint32_t *__restrict__ out_i) {
     __shared__ double sd[kBoundedCap];
     __shared__ uint32_t si[kBoundedCap];
-    const uint32_t j = blockIdx.x, q = list[j];
+    const uint32_t total = *nlist_ptr, nlist = min(total, kBoundedMaxQ);
+    uint32_t *ov_count = counts + kBoundedMaxQ, *ov_list = counts + kBoundedMaxQ + 1;
+    if (blockIdx.x == kBoundedMaxQ) {  // excess list entries: straight to the full scan
+        for (uint32_t e = kBoundedMaxQ + threadIdx.x; e < total; e += blockDim.x) ov_list[atomicAdd(ov_count, 1u)] = list[e];
+        return;
+    }
+    const uint32_t j = blockIdx.x;
+    if (j >= nlist) return;
+    const uint32_t q = list[j];
     const uint32_t c = counts[j];
     if (c > kBoundedCap || c < out_k) {
-        if (threadIdx.x == 0) counts[nlist + 1 + atomicAdd(&counts[nlist], 1u)] = q;
+        if (threadIdx.x == 0) ov_list[atomicAdd(ov_count, 1u)] = q;
         return;
     }
     for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
@@ -267,18 +281,70 @@ __global__ __launch_bounds__(256) void knn_bounded_select_kernel(const uint32_t 
     }
 }
 
+// full exact scan of the overflow list: persistent blocks, block b answers overflow entries
+// b, b + gridDim.x, ...; each block scans the whole store for its query (per-thread register
+// top-K, block selection) — the rare path (more than kBoundedCap states within the bound).
+template <int SP, int F, int NMAX, int K>
+__global__ __launch_bounds__(256) void knn_full_list_kernel(const double *__restrict__ feat, uint64_t cap,
+                                                            uint64_t n_end, const double *__restrict__ qfeat,
+                                                            const uint32_t *__restrict__ count_ptr,
+                                                            const uint32_t *__restrict__ list, DevSpace sp,
+                                                            uint32_t out_k, double *__restrict__ out_d,
+                                                            uint32_t *__restrict__ out_i) {
+    __shared__ double lds_d[4 * K];
+    __shared__ uint32_t lds_i[4 * K];
+    const uint32_t count = *count_ptr;
+    for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
+        const uint32_t q = list[e];
+        double qf[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) qf[f] = qfeat[(size_t)q * F + f];
+        TopK<K> top;
+        top.init();
+        for (uint64_t i = threadIdx.x; i < n_end; i += blockDim.x) {
+            double sf[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) sf[f] = feat[(uint64_t)f * cap + i];
+            top.offer(feat_dist<SP, F, NMAX>(sf, qf, sp), (uint32_t)i);
+        }
+        double rd;
+        uint32_t ri;
+        block_select<K>(top, lds_d, lds_i, rd, ri);
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (wave == 0 && lane < (int)out_k) {
+            out_d[(size_t)q * out_k + lane] = rd;
+            out_i[(size_t)q * out_k + lane] = ri;
+        }
+        __syncthreads();  // lds reuse by the next entry
+    }
+}
+
 template <int SP, int F, int NMAX>
 hipError_t run_knn_bounded(const DevSpace &sp, const double *feat, uint64_t cap, uint64_t n_end, const double *qf,
-                           const uint32_t *list, uint32_t nlist, uint32_t k, double *od, uint32_t *oi,
-                           uint32_t *counts, double *cand_d, uint32_t *cand_i, hipStream_t st) {
+                           const uint32_t *list, const uint32_t *d_nlist, uint32_t k, double *od, uint32_t *oi,
+                           uint32_t *counts, double *cand_d, uint32_t *cand_i, int num_cus, hipStream_t st) {
     constexpr int ITEMS = F <= 8 ? 4 : 1;
     const uint64_t blocks = (n_end + 256 * ITEMS - 1) / (256 * ITEMS);
-    timer_begin(st, "knn_bounded_kernel");
     hipLaunchKernelGGL((knn_bounded_kernel<SP, F, NMAX, ITEMS>), dim3((uint32_t)blocks), dim3(256), 0, st, feat, cap,
-                       n_end, qf, list, nlist, od, k, sp, counts, cand_d, cand_i);
-    timer_end(st);
-    hipLaunchKernelGGL(knn_bounded_select_kernel, dim3(nlist), dim3(256), 0, st, list, nlist, counts, cand_d, cand_i,
-                       k, od, oi);
+                       n_end, qf, list, d_nlist, od, k, sp, counts, cand_d, cand_i);
+    hipLaunchKernelGGL(knn_bounded_select_kernel, dim3(kBoundedMaxQ + 1), dim3(256), 0, st, list, d_nlist, counts,
+                       cand_d, cand_i, k, od, oi);
+    const uint32_t *ov_count = counts + kBoundedMaxQ, *ov_list = counts + kBoundedMaxQ + 1;
+    const dim3 grid((unsigned)std::max(num_cus, 1));
+    switch (k_bucket(k)) {
+#define OMPL_AMD_FULL(KK)                                                                                       \
+    case KK:                                                                                                   \
+        hipLaunchKernelGGL((knn_full_list_kernel<SP, F, NMAX, KK>), grid, dim3(256), 0, st, feat, cap, n_end, qf, \
+                           ov_count, ov_list, sp, k, od, oi);                                                  \
+        break;
+        OMPL_AMD_FULL(1)
+        OMPL_AMD_FULL(4)
+        OMPL_AMD_FULL(16)
+        OMPL_AMD_FULL(32)
+        OMPL_AMD_FULL(64)
+#undef OMPL_AMD_FULL
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -674,13 +740,12 @@ hipError_t launch_knn(const DevSpace &sp, const FeatGeom &g, const double *feat,
 }
 
 hipError_t launch_knn_bounded(const DevSpace &sp, const FeatGeom &g, const double *feat, uint64_t cap,
-                              uint64_t n_end, const double *qf, const uint32_t *list, uint32_t nlist, uint32_t k,
-                              double *od, uint32_t *oi, uint32_t *counts, double *cand_d, uint32_t *cand_i,
-                              hipStream_t st) {
-    if (nlist == 0 || k == 0) return hipSuccess;
-    if (nlist > kBoundedMaxQ) return hipErrorInvalidValue;
-    OMPL_AMD_SPACE_DISPATCH(run_knn_bounded, sp, feat, cap, n_end, qf, list, nlist, k, od, oi, counts, cand_d, cand_i,
-                            st)
+                              uint64_t n_end, const double *qf, const uint32_t *list, const uint32_t *d_nlist,
+                              uint32_t k, double *od, uint32_t *oi, uint32_t *counts, double *cand_d,
+                              uint32_t *cand_i, int num_cus, hipStream_t st) {
+    if (k == 0) return hipSuccess;
+    OMPL_AMD_SPACE_DISPATCH(run_knn_bounded, sp, feat, cap, n_end, qf, list, d_nlist, k, od, oi, counts, cand_d, cand_i,
+                            num_cus, st)
 }
 
 RadiusPlan radius_plan(uint32_t nq, uint64_t n_end, int num_cus) {
@@ -743,19 +808,20 @@ hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, con
     return hipGetLastError();
 }
 
-__global__ void aos_rows_kernel(const double *__restrict__ soa, uint64_t cap, int dim, int da, uint64_t n,
-                                double *__restrict__ aos) {
+__global__ void aos_rows_kernel(const double *__restrict__ soa, uint64_t cap, int dim, int da, uint64_t first,
+                                uint64_t n, double *__restrict__ aos) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread per (state, column)
     if (t >= n * da) return;
-    const uint64_t i = t / da;
+    const uint64_t i = first + t / da;
     const int c = (int)(t % da);
-    aos[t] = c < dim ? soa[(uint64_t)c * cap + i] : 0.0;
+    aos[i * da + c] = c < dim ? soa[(uint64_t)c * cap + i] : 0.0;
 }
 
-hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uint64_t n, double *aos, hipStream_t st) {
+hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uint64_t first, uint64_t n, double *aos,
+                           hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(aos_rows_kernel, dim3((unsigned)((n * da + 255) / 256)), dim3(256), 0, st, soa, cap, dim, da, n,
-                       aos);
+    hipLaunchKernelGGL(aos_rows_kernel, dim3((unsigned)((n * da + 255) / 256)), dim3(256), 0, st, soa, cap, dim, da,
+                       first, n, aos);
     return hipGetLastError();
 }
 

@@ -31,43 +31,43 @@ bool cull_supported(const DevSpace &sp) {
 
 void free_sorted_store(SortedStore *s) {
     for (void *x : {(void *)s->rows, (void *)s->ids, (void *)s->tbox, (void *)s->sbox, (void *)s->tkey0, (void *)s->nodes,
-                    (void *)s->rows64})
+                    (void *)s->rows64, (void *)s->inv, s->scratch})
         if (x) (void)hipFree(x);
     *s = SortedStore{};
 }
 
 namespace {
-__global__ void rows64_gather_kernel(const double *__restrict__ f64, uint64_t cap, int F, int FA,
-                                     const uint32_t *__restrict__ ids, uint32_t n_pad, double *__restrict__ rows64) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread per (slot, column)
-    if (t >= (uint64_t)n_pad * FA) return;
-    const uint32_t p = (uint32_t)(t / FA);
-    const int f = (int)(t % FA);
-    const uint32_t id = ids[p];
-    rows64[t] = f >= F ? 0.0 : (id == kNoId ? __builtin_nan("") : f64[(uint64_t)f * cap + id]);
+__global__ void tombstone_kernel(const uint32_t *__restrict__ inv, uint64_t id, float *__restrict__ rows) {
+    const uint32_t p = inv[id];
+    if (p != kNoId) rows[p] = __builtin_nanf("");  // row 0 of the fp32 copy: every distance is NaN
 }
 }  // namespace
 
-hipError_t build_sorted_rows64(const FeatGeom &g, const double *feat64, uint64_t cap, SortedStore *s, hipStream_t st) {
-    if (s->rows64) (void)hipFree(s->rows64);
-    s->rows64 = nullptr;
-    s->fa = (g.F + 3) & ~3;
-    const uint64_t total = (uint64_t)s->n_pad * s->fa;
-    hipError_t e = hipMalloc(&s->rows64, 8ull * std::max<uint64_t>(total, 1));
-    if (e != hipSuccess) return e;
-    s->bytes += 8ull * total;
-    if (total)
-        hipLaunchKernelGGL(rows64_gather_kernel, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, st, feat64, cap,
-                           g.F, s->fa, s->ids, s->n_pad, s->rows64);
+hipError_t tombstone_sorted_store(SortedStore *s, uint64_t id, hipStream_t st) {
+    if (!s->built || id >= s->covered || id >= s->cap_inv) return hipSuccess;
+    hipLaunchKernelGGL(tombstone_kernel, dim3(1), dim3(1), 0, st, s->inv, id, s->rows);
+    s->removed += 1;
     return hipGetLastError();
 }
 
-hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, uint64_t cap, uint32_t n,
-                              const FastBounds &b, SortedStore *s, hipStream_t st) {
+hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, const double *feat64,
+                              uint64_t cap, uint64_t n_total, uint32_t n_live, const uint8_t *live, SortedStore *s,
+                              hipStream_t st) {
     switch (sp.kind) {
-    case OMPL_GPU_SPACE_SE3: return fast_se3_build(g, feat32, cap, n, b, s, st);
-    case OMPL_GPU_SPACE_REALVECTOR: return fast_rv_build(g, feat32, cap, n, b, s, st);
+    case OMPL_GPU_SPACE_SE3: return fast_se3_build(g, feat32, feat64, cap, n_total, n_live, live, s, st);
+    case OMPL_GPU_SPACE_REALVECTOR: return fast_rv_build(g, feat32, feat64, cap, n_total, n_live, live, s, st);
     }
+    return hipErrorInvalidValue;
+}
+
+hipError_t append_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, const double *feat64,
+                               uint64_t cap, uint64_t n_total, const FastBounds &b, SortedStore *s, hipStream_t st,
+                               bool *fits) {
+    switch (sp.kind) {
+    case OMPL_GPU_SPACE_SE3: return fast_se3_append(g, feat32, feat64, cap, n_total, b, s, st, fits);
+    case OMPL_GPU_SPACE_REALVECTOR: return fast_rv_append(g, feat32, feat64, cap, n_total, b, s, st, fits);
+    }
+    *fits = false;
     return hipErrorInvalidValue;
 }
 
@@ -124,6 +124,19 @@ hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t
     const uint64_t t = n * rows;
     hipLaunchKernelGGL(to_fp32_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, feat64, cap, rows, first,
                        n, feat32);
+    return hipGetLastError();
+}
+
+namespace {
+__global__ void count_add_kernel(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b,
+                                 unsigned long long *__restrict__ acc) {
+    acc[0] += *a;
+    acc[1] += *b;
+}
+}  // namespace
+
+hipError_t launch_count_add(const uint32_t *a, const uint32_t *b, unsigned long long *acc, hipStream_t st) {
+    hipLaunchKernelGGL(count_add_kernel, dim3(1), dim3(1), 0, st, a, b, acc);
     return hipGetLastError();
 }
 

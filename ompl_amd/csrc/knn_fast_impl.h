@@ -1599,69 +1599,523 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
     return hipGetLastError();
 }
 
-template <int SP, int F>
-hipError_t build_sorted(const float *f32, uint64_t cap, uint32_t n, const FastBounds &b, SortedStore *s,
-                        hipStream_t st) {
-    constexpr int R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
-    free_sorted_store(s);
-    s->n = n;
-    s->ntiles = std::max<uint32_t>(1, (n + kCullTile - 1) / kCullTile);
-    s->n_pad = s->ntiles * kCullTile;
-    s->nsuper = (s->ntiles + kSuperTiles - 1) / kSuperTiles;
-    (void)b;
-    uint32_t *ids_s = nullptr;
-    hipError_t e = hipSuccess;
-    auto done = [&](hipError_t r) {
-        if (ids_s) (void)hipFree(ids_s);
-        if (r != hipSuccess) free_sorted_store(s);
-        return r;
-    };
-    // k-d leaf order on the host (kd_order.cpp) over the box coordinates, SE3 quaternions
-    // sign-canonical as the sorted rows store them
-    std::vector<float> hx((size_t)R * std::max<uint32_t>(n, 1));
-    if (n) {
-        if ((e = hipMemcpy2DAsync(hx.data(), 4ull * n, f32, 4ull * cap, 4ull * n, R, hipMemcpyDeviceToHost, st)) !=
-            hipSuccess)
-            return done(e);
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);
-        if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-            for (uint32_t i = 0; i < n; ++i)
-                if (hx[6ull * n + i] < 0.f)
-                    for (int r = 3; r < 7; ++r) hx[(size_t)r * n + i] = -hx[(size_t)r * n + i];
+// ---- device k-d build of the sorted store (no host round trip) -------------------------------
+// The tree shape depends only on the number of live states: a node of T tiles splits into
+// floor(T/2) (left) and T - floor(T/2) tiles, down to one-tile leaves (the left part holds
+// exactly floor(T/2) full tiles, so only the last leaf is partial).  A node is identified at
+// level L by the L bits of its path; its tile range follows from the path, its pre-order index
+// too (left child = index + 1, right child = index + floor(T/2)).  Per level, every node picks
+// the widest coordinate of its box and its states are sorted by (node, coordinate) — one radix
+// sort of (tile-range start << 32 | ordered coordinate) keys for all nodes of the level — which
+// puts the floor(T/2) * 64 smallest on the left: the host median split (std::nth_element) of
+// round 1, as one sort per level on the device.
+struct KdNodeRef {
+    uint32_t t0, T, pidx;
+    bool valid;
+};
+
+__device__ __forceinline__ KdNodeRef kd_node_at(uint32_t ntiles, int level, uint32_t path) {
+    KdNodeRef r{0u, ntiles, 0u, true};
+    for (int b = level - 1; b >= 0; --b) {
+        if (r.T <= 1) {
+            r.valid = false;
+            return r;
+        }
+        const uint32_t tl = r.T >> 1;
+        if ((path >> b) & 1u) {
+            r.pidx += tl;
+            r.t0 += tl;
+            r.T -= tl;
+        } else {
+            r.pidx += 1;
+            r.T = tl;
         }
     }
-    std::vector<uint32_t> perm;
-    std::vector<KdNode> nodes;
-    kd_tile_order(hx.data(), n, n, Geo<SP, F>::NB, kCullTile, perm, nodes);
-    s->nnodes = (uint32_t)nodes.size();
-    {
-        uint32_t live = 0;
-        for (uint32_t i = 0; i < n; ++i) live += hx[i] == hx[i] ? 1u : 0u;
-        s->kd_tiles = (live + kCullTile - 1) / kCullTile;
+    return r;
+}
+
+// box coordinate d of state id (SE3: translation, then the sign-canonical quaternion w >= 0)
+template <int SP, int F>
+__device__ __forceinline__ float kd_coord(const float *__restrict__ f32, uint64_t cap, uint32_t id, int d) {
+    float v = f32[(uint64_t)d * cap + id];
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        if (d >= 3 && f32[6ull * cap + id] < 0.f) v = -v;
     }
-    if ((e = hipMalloc(&ids_s, 4ull * std::max<uint32_t>(n, 1))) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->nodes, sizeof(KdNode) * std::max<size_t>(nodes.size(), 1))) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->rows, 4ull * R * s->n_pad)) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->ids, 4ull * s->n_pad)) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->tbox, 4ull * BW * s->ntiles)) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->sbox, 4ull * BW * s->nsuper)) != hipSuccess) return done(e);
-    if ((e = hipMalloc(&s->tkey0, 4ull * s->ntiles)) != hipSuccess) return done(e);
-    s->bytes = 4ull * R * s->n_pad + 4ull * s->n_pad + 4ull * BW * (s->ntiles + s->nsuper) + 4ull * s->ntiles +
-               sizeof(KdNode) * nodes.size();
-    if (n && (e = hipMemcpyAsync(ids_s, perm.data(), 4ull * n, hipMemcpyHostToDevice, st)) != hipSuccess)
-        return done(e);
-    if (!nodes.empty() && (e = hipMemcpyAsync(s->nodes, nodes.data(), sizeof(KdNode) * nodes.size(),
-                                              hipMemcpyHostToDevice, st)) != hipSuccess)
-        return done(e);
-    hipLaunchKernelGGL((tree_gather_kernel<SP, F>), dim3((s->n_pad + 255) / 256), dim3(256), 0, st, f32, cap, ids_s,
-                       n, s->n_pad, s->rows, s->ids);
-    hipLaunchKernelGGL((tile_box_kernel<SP, F>), dim3((s->ntiles + 255) / 256), dim3(256), 0, st, s->rows, s->n_pad,
-                       s->ntiles, (const uint32_t *)nullptr, n, s->tbox, s->tkey0);
-    hipLaunchKernelGGL((super_box_kernel<SP, F>), dim3((s->nsuper + 255) / 256), dim3(256), 0, st, s->tbox,
-                       s->ntiles, s->nsuper, s->sbox);
-    if ((e = hipGetLastError()) != hipSuccess) return done(e);
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);  // host vectors / temporaries released below
-    return done(hipSuccess);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t ordered_bits(float v) {  // monotone float -> uint32 (NaN last)
+    if (!(v == v)) return 0xFFFFFFFFu;
+    const uint32_t u = __float_as_uint(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ void kd_live_flags_kernel(const uint8_t *__restrict__ live, uint64_t n, uint8_t *__restrict__ flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flags[i] = live[i];
+}
+
+// level boxes of the tiles of the current order: box of positions [t * 64, t * 64 + 64) ∩ [0, n)
+template <int SP, int F>
+__global__ void kd_tile_boxes_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ perm,
+                                     uint32_t n, uint32_t ntiles, float *__restrict__ tb) {
+    constexpr int NB = Geo<SP, F>::NB;
+    const uint32_t t = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= ntiles) return;
+    const uint32_t p = t * kCullTile + lane;
+    const bool in = p < n;
+    const uint32_t id = in ? perm[p] : 0u;
+#pragma unroll
+    for (int d = 0; d < NB; ++d) {
+        float lo = in ? kd_coord<SP, F>(f32, cap, id, d) : __builtin_inff();
+        float hi = in ? lo : -__builtin_inff();
+        if (!(lo == lo)) {
+            lo = __builtin_inff();
+            hi = -__builtin_inff();
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            lo = fminf(lo, __shfl_xor(lo, o));
+            hi = fmaxf(hi, __shfl_xor(hi, o));
+        }
+        if (lane == 0) {
+            tb[(size_t)t * 2 * NB + d] = lo;
+            tb[(size_t)t * 2 * NB + NB + d] = hi;
+        }
+    }
+}
+
+// one block per node of the level: widest box coordinate -> ndim[path]
+template <int SP, int F>
+__global__ __launch_bounds__(256) void kd_node_dim_kernel(const float *__restrict__ tb, uint32_t ntiles, int level,
+                                                          uint32_t *__restrict__ ndim) {
+    constexpr int NB = Geo<SP, F>::NB;
+    __shared__ float slo[NB][256], shi[NB][256];
+    const KdNodeRef nd = kd_node_at(ntiles, level, blockIdx.x);
+    if (!nd.valid || nd.T <= 1) return;
+    float lo[NB], hi[NB];
+#pragma unroll
+    for (int d = 0; d < NB; ++d) {
+        lo[d] = __builtin_inff();
+        hi[d] = -__builtin_inff();
+    }
+    for (uint32_t t = nd.t0 + threadIdx.x; t < nd.t0 + nd.T; t += blockDim.x)
+#pragma unroll
+        for (int d = 0; d < NB; ++d) {
+            lo[d] = fminf(lo[d], tb[(size_t)t * 2 * NB + d]);
+            hi[d] = fmaxf(hi[d], tb[(size_t)t * 2 * NB + NB + d]);
+        }
+#pragma unroll
+    for (int d = 0; d < NB; ++d) {
+        slo[d][threadIdx.x] = lo[d];
+        shi[d][threadIdx.x] = hi[d];
+    }
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w)
+#pragma unroll
+            for (int d = 0; d < NB; ++d) {
+                slo[d][threadIdx.x] = fminf(slo[d][threadIdx.x], slo[d][threadIdx.x + w]);
+                shi[d][threadIdx.x] = fmaxf(shi[d][threadIdx.x], shi[d][threadIdx.x + w]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int bd = 0;
+        float be = -1.f;
+        for (int d = 0; d < NB; ++d) {
+            const float e = shi[d][0] - slo[d][0];
+            if (e > be) {  // first widest, as the host build
+                be = e;
+                bd = d;
+            }
+        }
+        ndim[blockIdx.x] = (uint32_t)bd;
+    }
+}
+
+// sort key of position p at this level: (start tile of its node << 32) | ordered coordinate
+// (0 once its node is a leaf, which keeps leaves in place under the stable sort)
+template <int SP, int F>
+__global__ void kd_keys_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ perm,
+                               uint32_t n, uint32_t ntiles, int level, const uint32_t *__restrict__ ndim,
+                               uint64_t *__restrict__ keys) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t t = p / kCullTile;
+    uint32_t t0 = 0, T = ntiles, path = 0;
+    int l = 0;
+    for (; l < level && T > 1; ++l) {
+        const uint32_t tl = T >> 1;
+        const uint32_t right = t >= t0 + tl ? 1u : 0u;
+        path = (path << 1) | right;
+        if (right) {
+            t0 += tl;
+            T -= tl;
+        } else {
+            T = tl;
+        }
+    }
+    uint32_t low = 0;
+    if (l == level && T > 1) low = ordered_bits(kd_coord<SP, F>(f32, cap, perm[p], (int)ndim[path]));
+    keys[p] = ((uint64_t)t0 << 32) | low;
+}
+
+// node records of the level (pre-order): split = first coordinate of the right part
+template <int SP, int F>
+__global__ void kd_split_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ perm,
+                                uint32_t n, uint32_t ntiles, int level, const uint32_t *__restrict__ ndim,
+                                KdNode *__restrict__ nodes) {
+    const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;
+    if (level < 31 && path >= (1u << level)) return;
+    const KdNodeRef nd = kd_node_at(ntiles, level, path);
+    if (!nd.valid || nd.T <= 1) return;
+    const uint32_t tl = nd.T >> 1;
+    const uint32_t pos = (nd.t0 + tl) * kCullTile;
+    const int d = (int)ndim[path];
+    const float split = pos < n ? kd_coord<SP, F>(f32, cap, perm[pos], d) : __builtin_inff();
+    nodes[nd.pidx] = KdNode{(uint32_t)d, split, tl, nd.pidx + tl};
+}
+
+// rows / ids of positions [p0, p1): ids from src (index p - p0) for p - p0 < cnt, else padding
+template <int SP, int F>
+__global__ void sorted_gather_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ src,
+                                     uint32_t cnt, uint32_t p0, uint32_t p1, uint32_t n_pad, float *__restrict__ rows,
+                                     uint32_t *__restrict__ ids, uint32_t *__restrict__ inv) {
+    constexpr int R = Geo<SP, F>::R;
+    const uint32_t p = p0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= p1) return;
+    if (p - p0 < cnt) {
+        const uint32_t id = src[p - p0];
+        float x[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r] = f32[(uint64_t)r * cap + id];
+        if constexpr (SP == OMPL_GPU_SPACE_SE3) {  // |dot| is sign-invariant: store w >= 0
+            if (x[6] < 0.f)
+#pragma unroll
+                for (int r = 3; r < 7; ++r) x[r] = -x[r];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = x[r];
+        ids[p] = id;
+        inv[id] = p;
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = __builtin_nanf("");
+        ids[p] = kNoId;
+    }
+}
+
+template <int SP, int F>
+__global__ void tail_keys_kernel(const float *__restrict__ f32, uint64_t cap, uint64_t first, uint32_t n, FastBounds b,
+                                 uint32_t *__restrict__ keys, uint32_t *__restrict__ idx) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t id = (uint32_t)(first + i);
+    constexpr int R = Geo<SP, F>::R;
+    float x[R > kKeyDims + 1 ? R : kKeyDims + 1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = f32[(uint64_t)r * cap + id];
+    float c[kKeyDims];
+    key_coords<SP>(x, c, b.nkey);
+    keys[i] = morton_key(c, b);
+    idx[i] = id;
+}
+
+__global__ void iota_kernel(uint32_t *__restrict__ a, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = i;
+}
+
+__global__ void rows64_range_kernel(const double *__restrict__ f64, uint64_t cap, int F, int FA,
+                                    const uint32_t *__restrict__ ids, uint32_t p0, uint32_t p1,
+                                    double *__restrict__ rows64) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (slot, column)
+    const uint64_t p = p0 + t / FA;
+    if (p >= p1) return;
+    const int f = (int)(t % FA);
+    const uint32_t id = ids[p];
+    rows64[p * FA + f] = f >= F ? 0.0 : (id == kNoId ? __builtin_nan("") : f64[(uint64_t)f * cap + id]);
+}
+
+template <int SP, int F>
+__global__ void tile_box_range_kernel(const float *__restrict__ rows, uint32_t n_pad, uint32_t t0, uint32_t t1,
+                                      float *__restrict__ tbox) {
+    constexpr int NB = Geo<SP, F>::NB, BW = Geo<SP, F>::BW;
+    const uint32_t t = t0 + blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= t1) return;
+    const uint32_t p = t * kCullTile + lane;
+    float x[NB];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) x[c] = rows[(size_t)c * n_pad + p];
+    const bool ok = x[0] == x[0];  // padding / removed
+    float eta = 0.f;
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        if (ok) {
+            float n2 = x[3] * x[3];
+            n2 = fmaf(x[4], x[4], n2);
+            n2 = fmaf(x[5], x[5], n2);
+            n2 = fmaf(x[6], x[6], n2);
+            eta = fmaxf(n2 - 1.f, 0.f);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) eta = fmaxf(eta, __shfl_xor(eta, o));
+    }
+    float *o = tbox + (size_t)t * BW;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+        float lo = ok ? x[c] : __builtin_inff(), hi = ok ? x[c] : -__builtin_inff();
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1) {
+            lo = fminf(lo, __shfl_xor(lo, s));
+            hi = fmaxf(hi, __shfl_xor(hi, s));
+        }
+        if (lane == 0) {
+            o[c] = lo;
+            o[NB + c] = hi;
+        }
+    }
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        if (lane == 0) {
+            o[2 * NB] = eta * 1.00001f;
+            o[2 * NB + 1] = 0.f;
+        }
+    }
+}
+
+template <int SP, int F>
+__global__ void super_box_range_kernel(const float *__restrict__ tbox, uint32_t ntiles, uint32_t s0, uint32_t s1,
+                                       float *__restrict__ sbox) {
+    constexpr int NB = Geo<SP, F>::NB, BW = Geo<SP, F>::BW;
+    const uint32_t sI = s0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (sI >= s1) return;
+    const uint32_t t0 = sI * kSuperTiles, t1 = min((sI + 1) * kSuperTiles, ntiles);
+    for (int c = 0; c < NB; ++c) {
+        float lo = __builtin_inff(), hi = -__builtin_inff();
+        for (uint32_t t = t0; t < t1; ++t) {
+            lo = fminf(lo, tbox[(size_t)t * BW + c]);
+            hi = fmaxf(hi, tbox[(size_t)t * BW + NB + c]);
+        }
+        sbox[(size_t)sI * BW + c] = lo;
+        sbox[(size_t)sI * BW + NB + c] = hi;
+    }
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        float eta = 0.f;
+        for (uint32_t t = t0; t < t1; ++t) eta = fmaxf(eta, tbox[(size_t)t * BW + 2 * NB]);
+        sbox[(size_t)sI * BW + 2 * NB] = eta;
+        sbox[(size_t)sI * BW + 2 * NB + 1] = 0.f;
+    }
+}
+
+inline hipError_t scratch_ensure(SortedStore *s, size_t bytes) {
+    if (bytes <= s->scratch_bytes) return hipSuccess;
+    if (s->scratch) (void)hipFree(s->scratch);
+    s->scratch = nullptr;
+    s->scratch_bytes = 0;
+    const size_t nb = std::max(bytes, (size_t)1 << 20);
+    hipError_t e = hipMalloc(&s->scratch, nb);
+    if (e == hipSuccess) s->scratch_bytes = nb;
+    return e;
+}
+
+template <typename T>
+inline hipError_t grow_array(T **p, size_t &have, size_t need) {
+    if (need <= have && *p) return hipSuccess;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    have = 0;
+    hipError_t e = hipMalloc((void **)p, sizeof(T) * std::max<size_t>(need, 1));
+    if (e == hipSuccess) have = need;
+    return e;
+}
+
+// (re)allocate the store's arrays for `pad_tiles` tiles (grow-only: no free / realloc in the
+// steady state, so builds and tail appends stay asynchronous)
+template <int SP, int F>
+hipError_t sorted_alloc(SortedStore *s, uint32_t pad_tiles, uint32_t max_nodes, uint64_t inv_cap, int fa,
+                        hipStream_t st) {
+    constexpr int R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
+    const size_t n_pad = (size_t)pad_tiles * kCullTile;
+    const uint32_t nsup = (pad_tiles + kSuperTiles - 1) / kSuperTiles;
+    hipError_t e;
+    if (n_pad > s->cap_pos) {  // rows are laid out with stride n_pad: reallocate all row arrays together
+        size_t dummy = 0;
+        if ((e = grow_array(&s->rows, dummy, (size_t)R * n_pad)) != hipSuccess) return e;
+        dummy = 0;
+        if ((e = grow_array(&s->ids, dummy, n_pad)) != hipSuccess) return e;
+        dummy = 0;
+        if ((e = grow_array(&s->rows64, dummy, n_pad * (size_t)fa)) != hipSuccess) return e;
+        dummy = 0;
+        if ((e = grow_array(&s->tbox, dummy, (size_t)pad_tiles * BW)) != hipSuccess) return e;
+        dummy = 0;
+        if ((e = grow_array(&s->sbox, dummy, (size_t)nsup * BW)) != hipSuccess) return e;
+        dummy = 0;
+        if ((e = grow_array(&s->tkey0, dummy, (size_t)pad_tiles)) != hipSuccess) return e;
+        s->cap_pos = n_pad;
+        hipLaunchKernelGGL(iota_kernel, dim3((pad_tiles + 255) / 256), dim3(256), 0, st, s->tkey0, pad_tiles);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    s->n_pad = (uint32_t)s->cap_pos;
+    s->fa = fa;
+    if ((e = grow_array(&s->nodes, s->cap_nodes, std::max<uint32_t>(max_nodes, 1))) != hipSuccess) return e;
+    if ((e = grow_array(&s->inv, s->cap_inv, inv_cap)) != hipSuccess) return e;
+    s->bytes = s->cap_pos * (4ull * R + 4 + 8ull * fa) + (s->cap_pos / kCullTile) * (4ull * BW + 4) +
+               ((s->cap_pos / kCullTile + kSuperTiles - 1) / kSuperTiles) * 4ull * BW + s->cap_nodes * sizeof(KdNode) +
+               s->cap_inv * 4ull;
+    return hipSuccess;
+}
+
+// Full build over ids [0, n_total) whose live flag is set (n_live of them), on `st`, no sync.
+template <int SP, int F>
+hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint64_t n_total, uint32_t n_live,
+                        const uint8_t *live, SortedStore *s, hipStream_t st) {
+    constexpr int NB = Geo<SP, F>::NB;
+    const int fa = (F + 3) & ~3;
+    const uint32_t main_tiles = std::max<uint32_t>(1, (n_live + kCullTile - 1) / kCullTile);
+    const uint32_t main_sup_tiles = (main_tiles + kSuperTiles - 1) / kSuperTiles * kSuperTiles;
+    const uint32_t tail_tiles = (std::max<uint32_t>(64, main_tiles / 8) + kSuperTiles - 1) / kSuperTiles * kSuperTiles;
+    hipError_t e;
+    if ((e = sorted_alloc<SP, F>(s, main_sup_tiles + tail_tiles, main_tiles, std::max<uint64_t>(cap, n_total), fa,
+                                 st)) != hipSuccess)
+        return e;
+    // scratch: flags | perm x2 | keys x2 | tile boxes | node dims | selected count | cub temp
+    const size_t n = std::max<uint64_t>(n_total, 1);
+    int depth = 0;
+    while ((1u << depth) < main_tiles) ++depth;
+    int tbits = 1;
+    while ((1u << tbits) <= main_tiles) ++tbits;
+    size_t cub_sel = 0, cub_sort = 0;
+    hipcub::CountingInputIterator<uint32_t> count_it(0);
+    (void)hipcub::DeviceSelect::Flagged(nullptr, cub_sel, count_it, (const uint8_t *)nullptr, (uint32_t *)nullptr,
+                                        (uint32_t *)nullptr, (int)n);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_sort, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                             (uint32_t *)nullptr, (uint32_t *)nullptr, (int)std::max<uint32_t>(n_live, 1),
+                                             0, 32 + tbits);
+    size_t off = 0;
+    auto take = [&](size_t b) {
+        const size_t o = off;
+        off += align_up(b);
+        return o;
+    };
+    const size_t o_flags = take(n), o_p0 = take(4 * n), o_p1 = take(4 * n), o_k0 = take(8 * n), o_k1 = take(8 * n),
+                 o_tb = take(4ull * main_tiles * 2 * NB), o_nd = take(4ull * main_tiles + 4), o_cnt = take(8),
+                 o_cub = take(std::max(cub_sel, cub_sort));
+    if ((e = scratch_ensure(s, off)) != hipSuccess) return e;
+    char *w = (char *)s->scratch;
+    uint8_t *flags = (uint8_t *)(w + o_flags);
+    uint32_t *perm = (uint32_t *)(w + o_p0), *perm2 = (uint32_t *)(w + o_p1);
+    uint64_t *keys = (uint64_t *)(w + o_k0), *keys2 = (uint64_t *)(w + o_k1);
+    float *tb = (float *)(w + o_tb);
+    uint32_t *ndim = (uint32_t *)(w + o_nd), *nsel = (uint32_t *)(w + o_cnt);
+    const dim3 b256(256);
+    hipLaunchKernelGGL(kd_live_flags_kernel, dim3((unsigned)((n_total + 255) / 256)), b256, 0, st, live, n_total, flags);
+    size_t cb = std::max(cub_sel, cub_sort);
+    if ((e = hipcub::DeviceSelect::Flagged(w + o_cub, cb, count_it, flags, perm, nsel, (int)n_total, st)) != hipSuccess)
+        return e;
+    for (int level = 0; level < depth; ++level) {
+        hipLaunchKernelGGL((kd_tile_boxes_kernel<SP, F>), dim3((main_tiles + 3) / 4), b256, 0, st, f32, cap, perm,
+                           n_live, main_tiles, tb);
+        hipLaunchKernelGGL((kd_node_dim_kernel<SP, F>), dim3(1u << level), b256, 0, st, tb, main_tiles, level, ndim);
+        hipLaunchKernelGGL((kd_keys_kernel<SP, F>), dim3((n_live + 255) / 256), b256, 0, st, f32, cap, perm, n_live,
+                           main_tiles, level, ndim, keys);
+        cb = std::max(cub_sel, cub_sort);
+        if ((e = hipcub::DeviceRadixSort::SortPairs(w + o_cub, cb, keys, keys2, perm, perm2, (int)n_live, 0, 32 + tbits,
+                                                    st)) != hipSuccess)
+            return e;
+        std::swap(perm, perm2);
+        hipLaunchKernelGGL((kd_split_kernel<SP, F>), dim3(((1u << level) + 255) / 256), b256, 0, st, f32, cap, perm,
+                           n_live, main_tiles, level, ndim, s->nodes);
+    }
+    if ((e = hipMemsetAsync(s->inv, 0xFF, 4ull * s->cap_inv, st)) != hipSuccess) return e;
+    const uint32_t p_end = (main_sup_tiles + tail_tiles) * kCullTile;  // padding: gap and tail region NaN
+    hipLaunchKernelGGL((sorted_gather_kernel<SP, F>), dim3((p_end + 255) / 256), b256, 0, st, f32, cap, perm, n_live,
+                       0u, p_end, s->n_pad, s->rows, s->ids, s->inv);
+    hipLaunchKernelGGL((tile_box_range_kernel<SP, F>), dim3((main_sup_tiles + 3) / 4), b256, 0, st, s->rows, s->n_pad,
+                       0u, main_sup_tiles, s->tbox);
+    const uint32_t nsup = main_sup_tiles / kSuperTiles;
+    hipLaunchKernelGGL((super_box_range_kernel<SP, F>), dim3((nsup + 255) / 256), b256, 0, st, s->tbox, main_sup_tiles,
+                       0u, nsup, s->sbox);
+    const uint64_t c64 = (uint64_t)main_sup_tiles * kCullTile * fa;
+    hipLaunchKernelGGL(rows64_range_kernel, dim3((unsigned)((c64 + 255) / 256)), b256, 0, st, f64, cap, F, fa, s->ids,
+                       0u, main_sup_tiles * kCullTile, s->rows64);
+    s->kd_tiles = main_tiles;
+    s->nnodes = main_tiles - 1;
+    s->main_live = n_live;
+    s->tail_t0 = main_sup_tiles;
+    s->tail_cap_tiles = tail_tiles;
+    s->ntiles = main_sup_tiles;
+    s->nsuper = nsup;
+    s->n = n_live;
+    s->covered = n_total;
+    s->main_covered = n_total;
+    s->removed = 0;
+    s->built = true;
+    return hipGetLastError();
+}
+
+// Tail append: ids [main_covered, n_total) (states added since the build) re-tiled along the
+// Morton curve in the tail region (tiles from tail_t0, a super-tile boundary), with their
+// boxes; false in *fits when they exceed the tail region (the caller rebuilds).
+template <int SP, int F>
+hipError_t append_sorted(const float *f32, const double *f64, uint64_t cap, uint64_t n_total, const FastBounds &b,
+                         SortedStore *s, hipStream_t st, bool *fits) {
+    const uint64_t n_tail64 = n_total - s->main_covered;
+    *fits = s->built && n_tail64 <= (uint64_t)s->tail_cap_tiles * kCullTile;
+    if (!*fits) return hipSuccess;
+    hipError_t e;
+    if (n_total > s->cap_inv) {  // the store grew past the id map: grow it, keeping the placed ids
+        uint32_t *ninv = nullptr;
+        const size_t ncap = std::max<size_t>(2 * s->cap_inv, n_total);
+        if ((e = hipMalloc(&ninv, 4ull * ncap)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(ninv, 0xFF, 4ull * ncap, st)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(ninv, s->inv, 4ull * s->cap_inv, hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;  // before the old map is freed
+        (void)hipFree(s->inv);
+        s->inv = ninv;
+        s->cap_inv = ncap;
+    }
+    const uint32_t n_tail = (uint32_t)n_tail64;
+    if (n_tail == 0) return hipSuccess;
+    size_t cub = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                             (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n_tail, 0, 32);
+    size_t off = 0;
+    auto take = [&](size_t bb) {
+        const size_t o = off;
+        off += align_up(bb);
+        return o;
+    };
+    const size_t o_k0 = take(4ull * n_tail), o_k1 = take(4ull * n_tail), o_i0 = take(4ull * n_tail),
+                 o_i1 = take(4ull * n_tail), o_cub = take(cub);
+    if ((e = scratch_ensure(s, off)) != hipSuccess) return e;
+    char *w = (char *)s->scratch;
+    uint32_t *k0 = (uint32_t *)(w + o_k0), *k1 = (uint32_t *)(w + o_k1);
+    uint32_t *i0 = (uint32_t *)(w + o_i0), *i1 = (uint32_t *)(w + o_i1);
+    const dim3 b256(256);
+    hipLaunchKernelGGL((tail_keys_kernel<SP, F>), dim3((n_tail + 255) / 256), b256, 0, st, f32, cap, s->main_covered,
+                       n_tail, b, k0, i0);
+    if ((e = hipcub::DeviceRadixSort::SortPairs(w + o_cub, cub, k0, k1, i0, i1, (int)n_tail, 0, 32, st)) != hipSuccess)
+        return e;
+    const uint32_t tiles = (n_tail + kCullTile - 1) / kCullTile;
+    const uint32_t p0 = s->tail_t0 * kCullTile, p1 = p0 + tiles * kCullTile;
+    hipLaunchKernelGGL((sorted_gather_kernel<SP, F>), dim3((p1 - p0 + 255) / 256), b256, 0, st, f32, cap, i1, n_tail,
+                       p0, p1, s->n_pad, s->rows, s->ids, s->inv);
+    const uint32_t t1 = s->tail_t0 + tiles;
+    hipLaunchKernelGGL((tile_box_range_kernel<SP, F>), dim3((tiles + 3) / 4), b256, 0, st, s->rows, s->n_pad,
+                       s->tail_t0, t1, s->tbox);
+    const uint32_t s0 = s->tail_t0 / kSuperTiles, s1 = (t1 + kSuperTiles - 1) / kSuperTiles;
+    hipLaunchKernelGGL((super_box_range_kernel<SP, F>), dim3((s1 - s0 + 255) / 256), b256, 0, st, s->tbox, t1, s0, s1,
+                       s->sbox);
+    const uint64_t c64 = (uint64_t)(p1 - p0) * s->fa;
+    hipLaunchKernelGGL(rows64_range_kernel, dim3((unsigned)((c64 + 255) / 256)), b256, 0, st, f64, cap, F, s->fa,
+                       s->ids, p0, p1, s->rows64);
+    s->ntiles = t1;
+    s->nsuper = s1;
+    s->n = p1;
+    s->covered = n_total;
+    return hipGetLastError();
 }
 
 }  // namespace
@@ -1672,8 +2126,10 @@ hipError_t build_sorted(const float *f32, uint64_t cap, uint32_t n, const FastBo
                     uint64_t cap, uint64_t n_end, const SortedStore *sorted, const double *qfeat64, uint32_t nq, \
                     uint32_t k, const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes,  \
                     int num_cus, hipStream_t st, uint32_t **fail_count, uint32_t **fail_list);                  \
-    hipError_t NAME##_build(const FeatGeom &g, const float *feat32, uint64_t cap, uint32_t n, const FastBounds &b, \
-                            SortedStore *s, hipStream_t st);                                                   \
+    hipError_t NAME##_build(const FeatGeom &g, const float *feat32, const double *feat64, uint64_t cap,          \
+                            uint64_t n_total, uint32_t n_live, const uint8_t *live, SortedStore *s, hipStream_t st); \
+    hipError_t NAME##_append(const FeatGeom &g, const float *feat32, const double *feat64, uint64_t cap,         \
+                             uint64_t n_total, const FastBounds &b, SortedStore *s, hipStream_t st, bool *fits);  \
     hipError_t NAME##_radius(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap,          \
                              const SortedStore *sorted, const double *qfeat64, uint32_t nq, double r,          \
                              const FastBounds &b, void *ws, size_t ws_bytes, int phase, uint64_t **d_offsets,  \

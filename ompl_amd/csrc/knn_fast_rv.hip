@@ -17,11 +17,18 @@ hipError_t fast_rv(const DevSpace &sp, const FeatGeom &g, const double *feat64, 
 #undef OMPL_AMD_RV
 }
 
-hipError_t fast_rv_build(const FeatGeom &g, const float *feat32, uint64_t cap, uint32_t n, const FastBounds &b,
-                         SortedStore *s, hipStream_t st) {
-    if (g.F == 4) return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 4>(feat32, cap, n, b, s, st);
-    if (g.F == 8) return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 8>(feat32, cap, n, b, s, st);
-    return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 16>(feat32, cap, n, b, s, st);
+hipError_t fast_rv_build(const FeatGeom &g, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_total,
+                         uint32_t n_live, const uint8_t *live, SortedStore *s, hipStream_t st) {
+    if (g.F == 4) return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 4>(feat32, feat64, cap, n_total, n_live, live, s, st);
+    if (g.F == 8) return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 8>(feat32, feat64, cap, n_total, n_live, live, s, st);
+    return build_sorted<OMPL_GPU_SPACE_REALVECTOR, 16>(feat32, feat64, cap, n_total, n_live, live, s, st);
+}
+
+hipError_t fast_rv_append(const FeatGeom &g, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_total,
+                          const FastBounds &b, SortedStore *s, hipStream_t st, bool *fits) {
+    if (g.F == 4) return append_sorted<OMPL_GPU_SPACE_REALVECTOR, 4>(feat32, feat64, cap, n_total, b, s, st, fits);
+    if (g.F == 8) return append_sorted<OMPL_GPU_SPACE_REALVECTOR, 8>(feat32, feat64, cap, n_total, b, s, st, fits);
+    return append_sorted<OMPL_GPU_SPACE_REALVECTOR, 16>(feat32, feat64, cap, n_total, b, s, st, fits);
 }
 
 hipError_t fast_rv_radius(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap,

@@ -11,9 +11,14 @@ hipError_t fast_se3(const DevSpace &sp, const FeatGeom &g, const double *feat64,
                                              out_i, ws, ws_bytes, num_cus, st, fail_count, fail_list);
 }
 
-hipError_t fast_se3_build(const FeatGeom &, const float *feat32, uint64_t cap, uint32_t n, const FastBounds &b,
-                          SortedStore *s, hipStream_t st) {
-    return build_sorted<OMPL_GPU_SPACE_SE3, 7>(feat32, cap, n, b, s, st);
+hipError_t fast_se3_build(const FeatGeom &, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_total,
+                          uint32_t n_live, const uint8_t *live, SortedStore *s, hipStream_t st) {
+    return build_sorted<OMPL_GPU_SPACE_SE3, 7>(feat32, feat64, cap, n_total, n_live, live, s, st);
+}
+
+hipError_t fast_se3_append(const FeatGeom &, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_total,
+                           const FastBounds &b, SortedStore *s, hipStream_t st, bool *fits) {
+    return append_sorted<OMPL_GPU_SPACE_SE3, 7>(feat32, feat64, cap, n_total, b, s, st, fits);
 }
 
 hipError_t fast_se3_radius(const DevSpace &sp, const FeatGeom &g, const double *feat64, uint64_t cap,

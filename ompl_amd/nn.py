@@ -145,6 +145,12 @@ class NearestNeighborsGPU:
         abi.check(abi.lib.ompl_gpu_nn_rerun_stats(self._h, C.byref(a)))
         return a.value
 
+    def index_stats(self) -> tuple[int, int]:
+        """(device k-d builds of the sorted copy, tail appends that avoided a rebuild)."""
+        a, b = C.c_uint64(0), C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_nn_index_stats(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def cull_stats(self) -> tuple[int, int, int]:
         """(64-state tiles the culled screen fetched, tiles a full scan would have fetched,
         (tile, query) pairs scanned — 64 distance evaluations each)."""

@@ -102,6 +102,7 @@ def test_radius_device_api_and_edges(gpu):
     fr = torch.empty((tot, 7), dtype=torch.float64, device=dev)
     to = torch.empty_like(fr)
     nn.edges_device(dq.data_ptr(), 400, off.data_ptr(), ids.data_ptr(), 0, tot, True, fr.data_ptr(), to.data_ptr())
+    nn.sync()
     seg = np.repeat(np.arange(400), np.diff(ooff).astype(np.int64))
     np.testing.assert_array_equal(fr.cpu().numpy(), q[seg])
     np.testing.assert_array_equal(to.cpu().numpy(), data[oids.astype(np.int64)])
@@ -113,6 +114,7 @@ def test_radius_device_api_and_edges(gpu):
     fr2 = torch.empty((400 * k, 7), dtype=torch.float64, device=dev)
     to2 = torch.empty_like(fr2)
     nn.edges_device(dq.data_ptr(), 400, None, ki.data_ptr(), k, 400 * k, False, fr2.data_ptr(), to2.data_ptr())
+    nn.sync()  # the device-resident calls are asynchronous on the handle's stream
     kin = ki.cpu().numpy().astype(np.int64).reshape(-1)
     np.testing.assert_array_equal(fr2.cpu().numpy(), data[kin])
     np.testing.assert_array_equal(to2.cpu().numpy(), np.repeat(q, k, axis=0))
