@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--single-query-reps", type=int, default=200, help="RRT-style one-query scans (0 = skip)")
     ap.add_argument("--rrt-iters", type=int, default=2000, help="device RRT iterations after the bench (0 = skip)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the extra measurements (index maintenance, sphere checker, RRT* k) after the timed steps")
     ap.add_argument("--rrt-star-queries", type=int, default=1000,
                     help="cfg3: batch of RRT* neighbourhood queries at k = 6,169 (0 = skip)")
     a = ap.parse_args()
@@ -298,6 +300,47 @@ def rrt_star_knn(torch, run, n_tree, nq=1000, reps=3):
     assert bool((dd[:, 1:] >= dd[:, :-1]).all().item()), "large-k lists must be sorted"
     return {"k": k, "queries": nq, "queries_per_s": nq / (ms * 1e-3), "ms_per_batch": ms, "kernel": name,
             "kernel_ms": kern_ms, "pairs_per_batch": float(nq) * n_tree}
+
+
+def index_maintenance(torch, run, local, batches=10, batch=100, nq=1000):
+    """The culled index kept current on the device: a full k-d build of a fresh
+    structure over the tree, then a BIT*-style loop — add a batch of new samples (host upload,
+    ImplicitGraph.cpp:682-692 addToSamples), place them in the index's tail, answer a batch of
+    queries — timed with HIP events on the library's stream."""
+    from ompl_amd import NearestNeighborsGPU
+    from ompl_amd import sampling as S
+
+    nn = NearestNeighborsGPU(run.sp, local)
+    nn.add(run.tree)
+    nn.set_stream(run.stream.cuda_stream)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(run.stream)
+    nn.build_index()
+    ev[1].record(run.stream)
+    torch.cuda.synchronize()
+    build_ms = ev[0].elapsed_time(ev[1])
+    new = S.StateSampler(run.sp).sample_uniform(batches * batch)
+    ids = torch.empty((nq, run.k), dtype=torch.int32, device=run.dev)
+    dd = torch.empty((nq, run.k), dtype=torch.float64, device=run.dev)
+    q = run.queries.data_ptr()
+    t_app = t_q = 0.0
+    for b in range(batches):
+        nn.add(new[b * batch:(b + 1) * batch])
+        ev[0].record(run.stream)
+        nn.build_index()
+        ev[1].record(run.stream)
+        nn.knn_device(q, nq, run.k, ids.data_ptr(), dd.data_ptr())
+        e2 = torch.cuda.Event(enable_timing=True)
+        e2.record(run.stream)
+        torch.cuda.synchronize()
+        t_app += ev[0].elapsed_time(ev[1])
+        t_q += ev[1].elapsed_time(e2)
+    builds, appends = nn.index_stats()
+    return {"states": len(run.tree), "full_build_ms": build_ms, "append_ms_per_batch": t_app / batches,
+            "batch_states": batch, "query_ms_per_batch": t_q / batches, "queries_per_batch": nq,
+            "builds": builds, "appends": appends,
+            "note": "device k-d build (one radix sort per level); appends place new states in a Morton tail"}
 
 
 def rrt_device(torch, nn, mv, sp, dev, iters):
@@ -579,8 +622,10 @@ def main():
     total_units = float(u.item())
     valid_frac = float(run.valid[: max(run.m, 1)].float().mean().item()) if args.workload != "cfg2" else None
 
-    single = rrt = spheres = rrt_star = None
-    if rank == 0 and args.workload == "cfg3":
+    single = rrt = spheres = rrt_star = index = None
+    if rank == 0 and args.workload in ("cfg3", "cfg2") and not args.no_extras:
+        index = index_maintenance(torch, run, local)
+    if rank == 0 and args.workload == "cfg3" and not args.no_extras:
         spheres = sphere_variant(torch, run, local)
         if args.rrt_star_queries > 0:
             rrt_star = rrt_star_knn(torch, run, args.tree, args.rrt_star_queries)
@@ -620,6 +665,8 @@ def main():
         if args.workload != "cfg2":
             line["motion_checks_per_s"] = run.m * world / (mv_ms * 1e-3)
             line["motion_valid_fraction"] = valid_frac
+        if index:
+            line["index"] = index
         if spheres:
             line["motion_spheres"] = spheres
         if rrt_star:

@@ -185,6 +185,10 @@ ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint
  * store for all uncertified queries, keeping d <= the certificate's exact k-th distance)
  * exceeded its candidate cap and took the full exact scan. */
 ompl_gpu_status ompl_gpu_nn_rerun_stats(const ompl_gpu_nn *h, uint64_t *full);
+/* Bring the culled walks' sorted copy up to date now (a device k-d build, or placing the states
+ * added since the last call in its tail) instead of at the next batched query; asynchronous on
+ * the handle's stream.  No-op for spaces without a culled walk (SO3, KCHAIN). */
+ompl_gpu_status ompl_gpu_nn_build_index(ompl_gpu_nn *h);
 /* The culled walks' sorted copy: device k-d builds and tail appends (states added since the
  * last build placed along the Morton curve without a rebuild) performed so far. */
 ompl_gpu_status ompl_gpu_nn_index_stats(const ompl_gpu_nn *h, uint64_t *builds, uint64_t *appends);

@@ -85,6 +85,7 @@ SIGNATURES = {
     "ompl_gpu_nn_stats": (C.c_int, [_P, _U64, _U64]),
     "ompl_gpu_nn_rerun_stats": (C.c_int, [_P, _U64]),
     "ompl_gpu_nn_index_stats": (C.c_int, [_P, _U64, _U64]),
+    "ompl_gpu_nn_build_index": (C.c_int, [_P]),
     "ompl_gpu_nn_profile": (C.c_int, [_P, C.c_int]),
     "ompl_gpu_nn_cull_stats": (C.c_int, [_P, _U64, _U64, _U64]),
     "ompl_gpu_nn_kernel_time": (C.c_int, [_P, _D, _U64, C.POINTER(C.c_char_p)]),

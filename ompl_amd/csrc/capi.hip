@@ -972,6 +972,14 @@ ompl_gpu_status ompl_gpu_nn_rerun_stats(const ompl_gpu_nn *h, uint64_t *full) {
     return OMPL_GPU_OK;
 }
 
+ompl_gpu_status ompl_gpu_nn_build_index(ompl_gpu_nn *h) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!cull_supported(h->sp) || h->n_total == 0) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    return ensure_sorted(h);
+}
+
 ompl_gpu_status ompl_gpu_nn_index_stats(const ompl_gpu_nn *h, uint64_t *builds, uint64_t *appends) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
     if (builds) *builds = h->sorted_builds;

@@ -145,6 +145,10 @@ class NearestNeighborsGPU:
         abi.check(abi.lib.ompl_gpu_nn_rerun_stats(self._h, C.byref(a)))
         return a.value
 
+    def build_index(self) -> None:
+        """Bring the culled walks' sorted copy up to date now (asynchronous on the handle's stream)."""
+        abi.check(abi.lib.ompl_gpu_nn_build_index(self._h))
+
     def index_stats(self) -> tuple[int, int]:
         """(device k-d builds of the sorted copy, tail appends that avoided a rebuild)."""
         a, b = C.c_uint64(0), C.c_uint64(0)
