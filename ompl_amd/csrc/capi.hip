@@ -107,6 +107,7 @@ struct ompl_gpu_nn {
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
     double lo[kKeyDims] = {0}, hi[kKeyDims] = {0}, absmax = 0.0;
+    double qeta = 0.0;  // SE3: largest |norm^2 - 1| of the stored quaternions (fp32 screen error bound)
     // k-d sorted fp32 copy for the culled walks: built on the device, states added later go to
     // its Morton-ordered tail, removals are tombstoned in place (kernels.h SortedStore)
     SortedStore sorted;
@@ -157,6 +158,7 @@ FastBounds current_bounds(const ompl_gpu_nn *h) {
         b.inv[c] = 0.5f;
     }
     b.absmax = (float)h->absmax;
+    b.qeta = (float)h->qeta * 1.01f;
     return b;
 }
 // arms g_kernel_timer for the scope of one query call when the handle profiles
@@ -353,6 +355,11 @@ ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, 
             h->hi[c] = std::max(h->hi[c], s[c]);
         }
         for (int c = 0; c < na; ++c) h->absmax = std::max(h->absmax, std::fabs(s[c]));
+        if (h->sp.kind == OMPL_GPU_SPACE_SE3) {
+            const double n2 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5] + s[6] * s[6];
+            const double eta = std::fabs(n2 - 1.0);
+            h->qeta = (eta == eta) ? std::max(h->qeta, eta) : 1.0;  // NaN: no fp32 screen
+        }
     }
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // host staging buffers are reused
     h->n_total += n;
@@ -394,6 +401,7 @@ ompl_gpu_status ompl_gpu_nn_clear(ompl_gpu_nn *h) {
     }
     h->n_total = h->n_live = 0;
     h->absmax = 0.0;
+    h->qeta = 0.0;
     h->sorted.built = false;  // keeps its allocations
     h->aos_n = 0;
     h->removed.clear();
@@ -434,9 +442,16 @@ ompl_gpu_status ompl_gpu_nn_get_states(ompl_gpu_nn *h, uint64_t first, size_t n,
 static uint64_t n_end_of(const ompl_gpu_nn *h) { return (h->n_total + kTile - 1) / kTile * kTile; }
 
 // the fp32 screens need coordinates far from fp32 overflow (kernels.h kScreenMaxAbs); NaN fails
-static bool screen_safe(const ompl_gpu_nn *h) { return h->absmax < kScreenMaxAbs; }
+static bool screen_safe(const ompl_gpu_nn *h) {
+    // SE3 quaternions far from unit norm would make the chord screen's error bound useless
+    return h->absmax < kScreenMaxAbs && !(h->qeta > 1e-4);
+}
 
+#ifdef OMPL_AMD_PROBE
+constexpr int kCullCounters = 10;  // + walk event counters of the probe build (tools/probe)
+#else
 constexpr int kCullCounters = 5;
+#endif
 
 // bring the sorted copy the culled walks read up to date, on the handle's stream with no host
 // round trip: a full device build when there is none (or too many tombstones / a full tail),
@@ -860,6 +875,20 @@ ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries
     return OMPL_GPU_OK;
 }
 
+#ifdef OMPL_AMD_PROBE
+// probe build only: the raw walk counters
+extern "C" ompl_gpu_status ompl_gpu_probe_counters(ompl_gpu_nn *h, uint64_t *out, int n) {
+    std::lock_guard<std::mutex> lk(h->mu);
+    unsigned long long c[kCullCounters] = {};
+    if (h->cull_counter.p) {
+        HIP_OR_FAIL(hipMemcpyAsync(c, h->cull_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    }
+    for (int i = 0; i < n && i < kCullCounters; ++i) out[i] = c[i];
+    return OMPL_GPU_OK;
+}
+#endif
+
 ompl_gpu_status ompl_gpu_nn_radius_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *query_tiles) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
@@ -1263,6 +1292,8 @@ ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const 
         }
         for (int c = 0; c < na; ++c) h->absmax = std::max(h->absmax, std::fabs(x[c]));
     }
+    // appended states are slerp interpolations of unit quaternions (fp64): a conservative excess
+    if (h->sp.kind == OMPL_GPU_SPACE_SE3) h->qeta = std::max(h->qeta, 1e-12);
     HIP_OR_FAIL(launch_rrt_grow(h->sp, mv->sp, mv->ck, h->g, h->feat, h->feat32, h->rows32, h->cap, n0,
                                 (uint64_t *)h->rrt_n.p, d_samples, (uint32_t)ns, max_distance, (double *)h->rrt_pd.p,
                                 (uint32_t *)h->rrt_pi.p, d_nearest, d_added, mv->counters, h->stream));

@@ -66,6 +66,7 @@ struct FastBounds {
     float absmax;                       // max |coordinate| stored (error bound of the fp32 screen)
     uint32_t slab = 0;                  // radius phase 2: hits kept per query (slab capacity)
     uint32_t n_live = 0;                // live stored states: a screening list that is not full must hold them all
+    float qeta = 0.f;                   // SE3: largest |norm^2 - 1| of the stored quaternions (screen_error)
 };
 // The fp32 screens assume coordinates far from fp32 overflow: with |x| < kScreenMaxAbs every
 // squared fp32 distance is finite (the C ABI takes the exact fp64 path otherwise).

@@ -26,9 +26,15 @@
 //
 // Error bound e (u = 2^-24, B = max |coordinate|, D = dims, L as above), doubled for slack:
 //   translation / R^n : 6 sqrt(D) u B + 6 u L   (fp32 conversion + sum of squares + sqrt)
-//   rotation          : 1.1 sqrt(2 * 6u) + 1e-6 + 4.5e-5
-//                       (|dot32 - dot| <= 6u; acos is 1/2-Hoelder near 1; the reference
-//                        returns 0 for dot > 1 - 1e-9, SO3StateSpace.cpp:258-260)
+//   SE3 rotation      : the screen measures the rotation by the chord, theta = 2 asin(c / 2),
+//                       c = min(|p - q|, |p + q|), which is well conditioned near theta = 0
+//                       (acos(|p.q|) in fp32 is not: its error there is sqrt(12 u) ~ 1e-3).  For
+//                       unit quaternions 2 asin(c / 2) = acos(|p.q|) exactly; with norms
+//                       |p|^2 = 1 + eta_p, |q|^2 = 1 + eta_q the two differ by at most
+//                       2.25 sqrt(|eta_p + eta_q| / 2) (acos is 1/2-Hoelder with constant pi/sqrt 2);
+//                       + 4.5e-5 (the reference returns 0 for |dot| > 1 - 1e-9,
+//                       SO3StateSpace.cpp:258-260) + 2e-6 (fp32 evaluation, acos01's 2e-8)
+//   SO3 rotation      : 1.1 sqrt(2 * 6u) + 1e-6 + 4.5e-5 (the chunked screen keeps acos(|dot|))
 #pragma once
 // Included by one translation unit per space (knn_fast_{se3,so3,rv}.hip) so that the
 // template instantiations compile in parallel; knn_fast.hip holds the dispatch.
@@ -292,6 +298,23 @@ __device__ __forceinline__ float acos01(float x) {
     return __builtin_amdgcn_sqrtf(1.f - x) * p;
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+__device__ __forceinline__ float chord_angle(const float *p, const float *q) {
+    f2 a = f2{p[0], p[0]} + f2{-q[0], q[0]};
+    f2 c2 = a * a;
+    a = f2{p[1], p[1]} + f2{-q[1], q[1]};
+    c2 = pk_fma(a, a, c2);
+    a = f2{p[2], p[2]} + f2{-q[2], q[2]};
+    c2 = pk_fma(a, a, c2);
+    a = f2{p[3], p[3]} + f2{-q[3], q[3]};
+    c2 = pk_fma(a, a, c2);
+    const float h = 0.5f * __builtin_amdgcn_sqrtf(fminf(c2.x, c2.y));  // c / 2 in [0, 0.7072]
+    return fmaf(-2.f, acos01(h), 3.14159265358979f);                    // 2 asin(c / 2)
+}
+
 // Rotation pre-reject threshold: an element with |dot| <= cos(tau/w1 + 1e-5) has
 // acos(|dot|) > tau/w1 even after every fp32 error, hence distance > tau: skip it without
 // the square root and the arc cosine.  ctau < 0 rejects nothing.
@@ -324,21 +347,12 @@ __device__ __forceinline__ void screen_tile(const float *tile, const float *qf, 
             }
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
-                if (v[u] * w0sq < top.tau2) {
+                if (v[u] * w0sq < top.tau2) {  // the translation term alone loses: skip the rotation
                     const float4 r = t4[(j0 + u) * 2 + 1];
-                    float dot = r.x * qf[4];
-                    dot = fmaf(r.y, qf[5], dot);
-                    dot = fmaf(r.z, qf[6], dot);
-                    dot = fmaf(r.w, qf[7], dot);
-                    const float c = abs1(dot);
-                    if (c > ctau) {
-                        const float d = w0 * __builtin_amdgcn_sqrtf(v[u]) + w1 * acos01(c);
-                        const uint32_t id = id_of(j0 + u);
-                        if (top.admits(d, id)) {
-                            top.push(d, id);
-                            ctau = rot_threshold(top.d[K2 - 1], w1);
-                        }
-                    }
+                    const float p[4] = {r.x, r.y, r.z, r.w};
+                    const float d = w0 * __builtin_amdgcn_sqrtf(v[u]) + w1 * chord_angle(p, qf + 4);
+                    const uint32_t id = id_of(j0 + u);
+                    if (top.admits(d, id)) top.push(d, id);
                 }
             }
         } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
@@ -474,8 +488,8 @@ __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w
             const float g = fmaxf(fmaxf(bx[c] - q[c], q[c] - bx[NB + c]), 0.f);
             tg = fmaf(g, g, tg);
         }
-        // rotation: acos|<q,p>| >= chord min(|q - p|, |q + p|) for unit quaternions; a norm
-        // excess eta of either side lowers the chord^2 bound by at most eta_q + eta_p
+        // rotation: the screened 2 asin(c / 2) >= c = min(|p - q|, |p + q|) >= the distance
+        // from q or from -q to the box (state_dist32)
         float rp = 0.f, rm = 0.f;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -485,8 +499,7 @@ __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w
             rp = fmaf(gp, gp, rp);
             rm = fmaf(gm, gm, rm);
         }
-        const float r2 = fminf(rp, rm) - (bx[2 * NB] + q[3]);
-        return w0 * __builtin_amdgcn_sqrtf(tg) + w1 * __builtin_amdgcn_sqrtf(fmaxf(r2, 0.f));
+        return w0 * __builtin_amdgcn_sqrtf(tg) + w1 * __builtin_amdgcn_sqrtf(fminf(rp, rm));
     } else {
         float acc = 0.f;
 #pragma unroll
@@ -498,8 +511,10 @@ __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w
     }
 }
 
-// fp32 screened distance of a lane's state x (R stored coordinates) to query row q; the
-// operation sequence is screen_tile's, so screen_error bounds it too
+// fp32 screened distance of a lane's state x (R stored coordinates) to query row q.  SE3:
+// translation as the reference, rotation by the chord (error bound in the header):
+// theta = 2 asin(c / 2) = pi - 2 acos(c / 2), c^2 = min(|p - q|^2, |p + q|^2), both sums on
+// packed fp32 (one v_pk_add / v_pk_fma per component gives both)
 template <int SP, int F>
 __device__ __forceinline__ float state_dist32(const float *x, const float *q, float w0, float w1) {
     if constexpr (SP == OMPL_GPU_SPACE_SE3) {
@@ -507,11 +522,7 @@ __device__ __forceinline__ float state_dist32(const float *x, const float *q, fl
         float t = dx * dx;
         t = fmaf(dy, dy, t);
         t = fmaf(dz, dz, t);
-        float dot = x[3] * q[4];
-        dot = fmaf(x[4], q[5], dot);
-        dot = fmaf(x[5], q[6], dot);
-        dot = fmaf(x[6], q[7], dot);
-        return w0 * __builtin_amdgcn_sqrtf(t) + w1 * acos01(abs1(dot));
+        return w0 * __builtin_amdgcn_sqrtf(t) + w1 * chord_angle(x + 3, q + 4);
     } else {
         float acc = 0.f;
 #pragma unroll
@@ -520,50 +531,6 @@ __device__ __forceinline__ float state_dist32(const float *x, const float *q, fl
             acc = fmaf(diff, diff, acc);
         }
         return __builtin_amdgcn_sqrtf(acc);
-    }
-}
-
-// the same distance for two queries a, b at once on packed fp32 (v_pk_fma / v_pk_mul /
-// v_pk_add: two IEEE operations per instruction, identical roundings to state_dist32)
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-
-template <int SP, int F>
-__device__ __forceinline__ f2 state_dist32x2(const float *x, const float *qa, const float *qb, float w0, float w1) {
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        const f2 dx = f2{x[0], x[0]} - f2{qa[0], qb[0]};
-        const f2 dy = f2{x[1], x[1]} - f2{qa[1], qb[1]};
-        const f2 dz = f2{x[2], x[2]} - f2{qa[2], qb[2]};
-        f2 t = dx * dx;
-        t = pk_fma(dy, dy, t);
-        t = pk_fma(dz, dz, t);
-        f2 dot = f2{x[3], x[3]} * f2{qa[4], qb[4]};
-        dot = pk_fma(f2{x[4], x[4]}, f2{qa[5], qb[5]}, dot);
-        dot = pk_fma(f2{x[5], x[5]}, f2{qa[6], qb[6]}, dot);
-        dot = pk_fma(f2{x[6], x[6]}, f2{qa[7], qb[7]}, dot);
-        const f2 c = f2{abs1(dot.x), abs1(dot.y)};
-        // acos01 on both lanes of c
-        f2 p = f2{-0.0012624911f, -0.0012624911f};
-        p = pk_fma(p, c, f2{0.0066700901f, 0.0066700901f});
-        p = pk_fma(p, c, f2{-0.0170881256f, -0.0170881256f});
-        p = pk_fma(p, c, f2{0.0308918810f, 0.0308918810f});
-        p = pk_fma(p, c, f2{-0.0501743046f, -0.0501743046f});
-        p = pk_fma(p, c, f2{0.0889789874f, 0.0889789874f});
-        p = pk_fma(p, c, f2{-0.2145988016f, -0.2145988016f});
-        p = pk_fma(p, c, f2{1.5707963050f, 1.5707963050f});
-        const f2 om = f2{1.f, 1.f} - c;
-        const f2 ac = f2{__builtin_amdgcn_sqrtf(om.x), __builtin_amdgcn_sqrtf(om.y)} * p;
-        const f2 st = f2{__builtin_amdgcn_sqrtf(t.x), __builtin_amdgcn_sqrtf(t.y)};
-        return f2{w0, w0} * st + f2{w1, w1} * ac;
-    } else {
-        f2 acc = f2{0.f, 0.f};
-#pragma unroll
-        for (int f = 0; f < F; ++f) {
-            const f2 diff = f2{x[f], x[f]} - f2{qa[f], qb[f]};
-            acc = pk_fma(diff, diff, acc);
-        }
-        return f2{__builtin_amdgcn_sqrtf(acc.x), __builtin_amdgcn_sqrtf(acc.y)};
     }
 }
 
@@ -623,13 +590,15 @@ __device__ __forceinline__ void wave_merge_sorted(float &Ld, uint32_t &Li, float
 // 1.42 / 1.41 ms at 64 / 8 / 32; R^6 1.60 / 1.12 / 1.13 / 1.21 ms at 64 / 8 / 16 / 32
 constexpr int kBulkThreshold = 8;
 
-template <int SP, int F, int K2, int G, bool PK, int MINW, bool QS>
+// K2: lanes per query in the output (16 / 32 / 64); k2 <= K2: the list length the walk keeps
+// (the certificate's margin: k + 2 for the culled spaces, whose screen error is small)
+template <int SP, int F, int K2, int G, int MINW, bool QS>
 __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
     const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
     uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi,
-    unsigned long long *__restrict__ counters, int bulk) {
+    unsigned long long *__restrict__ counters, int bulk, int k2) {
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
     constexpr int GH = G / 2;
     static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
@@ -669,6 +638,9 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         ti[g] = kNoId;
     }
     uint32_t visited = 0, qscans = 0;  // tiles fetched; (tile, query) scans
+#ifdef OMPL_AMD_PROBE
+    uint32_t pr_offers = 0, pr_bulk = 0, pr_ins = 0, pr_supers = 0, pr_rounds = 0;
+#endif
 
     // tiles of super-tile s some query may still need; lb[j]: this lane's bound for tile
     // (lane & 31) and query half * GH + j
@@ -694,6 +666,9 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     // lb[j]: this lane's bound for its tile and query half * GH + j
     auto tile_mask = [&](const float (&bx)[BW], float (&lb)[GH]) -> uint32_t {
         relaunder();
+#ifdef OMPL_AMD_PROBE
+        ++pr_supers;
+#endif
         bool need = false;
 #pragma unroll
         for (int j = 0; j < GH; ++j) {
@@ -718,11 +693,17 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     // element still has a screened distance >= the final K2-th distance)
     auto offer = [&](int g, float d, uint32_t id) {
             uint64_t bm = __ballot(d < td[g]);
+#ifdef OMPL_AMD_PROBE
+            ++pr_offers;
+#endif
             if (__popcll(bm) > bulk) {  // many at once: sort-merge (same top K2)
+#ifdef OMPL_AMD_PROBE
+                ++pr_bulk;
+#endif
                 const bool c = d < td[g];
                 wave_merge_sorted(Ld[g], Li[g], c ? d : __builtin_inff(), c ? id : kNoId, lane);
-                td[g] = readlane_f(Ld[g], K2 - 1);
-                ti[g] = readlane_u(Li[g], K2 - 1);
+                td[g] = readlane_f(Ld[g], k2 - 1);
+                ti[g] = readlane_u(Li[g], k2 - 1);
                 return;
             }
             while (bm) {
@@ -731,6 +712,9 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
                 const float cd = readlane_f(d, l);
                 const uint32_t ci = readlane_u(id, l);
                 if (cd < td[g] || (cd == td[g] && ci < ti[g])) {
+#ifdef OMPL_AMD_PROBE
+                    ++pr_ins;
+#endif
                     const float pv = shr1_f(Ld[g], -__builtin_inff());
                     const uint32_t pv_i = shr1_u(Li[g], 0u);
                     const bool lt_cur = cd < Ld[g] || (cd == Ld[g] && ci < Li[g]);
@@ -739,31 +723,18 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
                     const uint32_t ni = lt_prev ? pv_i : (lt_cur ? ci : Li[g]);
                     Ld[g] = nd;
                     Li[g] = ni;
-                    td[g] = readlane_f(Ld[g], K2 - 1);
-                    ti[g] = readlane_u(Li[g], K2 - 1);
+                    td[g] = readlane_f(Ld[g], k2 - 1);
+                    ti[g] = readlane_u(Li[g], k2 - 1);
                 }
             }
     };
     auto scan_state = [&](const float (&x)[R], uint32_t id, int tin, const float (&lb)[GH]) {
         relaunder();
-        if constexpr (!PK) {
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                if (!(readlane_f(lb[g % GH], tin + (g < GH ? 0 : 32)) < td[g])) continue;
-                ++qscans;
-                offer(g, state_dist32<SP, F>(x, qscan(g), w0, w1), id);
-            }
-            return;
-        }
-#pragma unroll
-        for (int g = 0; g < G; g += 2) {
-            const bool na = readlane_f(lb[g % GH], tin + (g < GH ? 0 : 32)) < td[g];
-            const bool nb = readlane_f(lb[(g + 1) % GH], tin + (g + 1 < GH ? 0 : 32)) < td[g + 1];
-            if (!(na || nb)) continue;
-            const f2 d = state_dist32x2<SP, F>(x, qscan(g), qscan(g + 1), w0, w1);
-            qscans += (uint32_t)na + (uint32_t)nb;
-            if (na) offer(g, d.x, id);
-            if (nb) offer(g + 1, d.y, id);
+        for (int g = 0; g < G; ++g) {
+            if (!(readlane_f(lb[g % GH], tin + (g < GH ? 0 : 32)) < td[g])) continue;
+            ++qscans;
+            offer(g, state_dist32<SP, F>(x, qscan(g), w0, w1), id);
         }
     };
     // start at the super-tile holding the group's middle query on the Morton curve
@@ -800,6 +771,9 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         while (!sm) {
             if (sb >= nsuper) return -1;
             relaunder();
+#ifdef OMPL_AMD_PROBE
+            ++pr_rounds;
+#endif
             const uint32_t s = sb + lane;
             bool need = false;
             if (s < nsuper && (s + 1 < s0 || s > s0 + 1)) {
@@ -870,13 +844,20 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         atomicAdd(&counters[0], (unsigned long long)visited);  // tiles scanned
         atomicAdd(&counters[1], (unsigned long long)ntiles);   // tiles of a brute-force walk
         atomicAdd(&counters[2], (unsigned long long)qscans);   // (tile, query) pairs scanned
+#ifdef OMPL_AMD_PROBE
+        atomicAdd(&counters[5], (unsigned long long)pr_offers);
+        atomicAdd(&counters[6], (unsigned long long)pr_bulk);
+        atomicAdd(&counters[7], (unsigned long long)pr_ins);
+        atomicAdd(&counters[8], (unsigned long long)pr_supers);
+        atomicAdd(&counters[9], (unsigned long long)pr_rounds);
+#endif
     }
 #pragma unroll
     for (int g = 0; g < G; ++g)
         if (g0 + g < nq && lane < K2) {
             const size_t o = (size_t)(g0 + g) * K2 + lane;
-            pd[o] = Ld[g];
-            pi[o] = Li[g];
+            pd[o] = lane < k2 ? Ld[g] : __builtin_inff();
+            pi[o] = lane < k2 ? Li[g] : kNoId;
         }
 }
 
@@ -985,12 +966,13 @@ __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__rest
 // vanish for stores whose coordinates are all tiny.
 constexpr double kFltMin = 1.1754943508222875e-38;
 
+// eta: |norm^2 - 1| of the stored quaternions (largest) plus the query's (SE3)
 template <int SP>
-__device__ __forceinline__ double screen_error(const DevSpace &sp, double B, double L) {
+__device__ __forceinline__ double screen_error(const DevSpace &sp, double B, double L, double eta = 0.0) {
     double e = 0.0;
     if constexpr (SP == OMPL_GPU_SPACE_SE3) {
         e = sp.w0 * (6.0 * 1.7320508075688772 * kU * B) + 6.0 * kU * L +
-            sp.w1 * (1.1 * sqrt(12.0 * kU) + 2e-6 + 4.5e-5);
+            sp.w1 * (2.25 * sqrt(0.5 * eta + 1e-15) + 2e-6 + 4.5e-5);
     } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
         e = 1.1 * sqrt(12.0 * kU) + 2e-6 + 4.5e-5;
     } else if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
@@ -1007,12 +989,23 @@ __device__ __forceinline__ double screen_error(const DevSpace &sp, double B, dou
     return 2.0 * e;
 }
 
+// |norm^2 - 1| of an SE3 query's quaternion (fp64), for screen_error
+template <int SP>
+__device__ __forceinline__ double query_eta(const double *qv) {
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        const double n = qv[3] * qv[3] + qv[4] * qv[4] + qv[5] * qv[5] + qv[6] * qv[6];
+        return fabs(n - 1.0);
+    }
+    return 0.0;
+}
+
 template <int SP, int F, int K2, int K>
 __global__ __launch_bounds__(256) void knn_certify_kernel(const float *__restrict__ pd, const uint32_t *__restrict__ pi,
                                                           uint32_t S, uint32_t nq, const uint32_t *__restrict__ perm,
                                                           const double *__restrict__ feat64, uint64_t cap,
                                                           const double *__restrict__ qf64, DevSpace sp,
-                                                          float absmax, uint32_t n_live, double *__restrict__ out_d,
+                                                          float absmax, float qeta, uint32_t n_live,
+                                                          double *__restrict__ out_d,
                                                           uint32_t *__restrict__ out_i, uint32_t out_k,
                                                           uint32_t *__restrict__ fail_count,
                                                           uint32_t *__restrict__ fail_list) {
@@ -1055,7 +1048,7 @@ __global__ __launch_bounds__(256) void knn_certify_kernel(const float *__restric
 #pragma unroll
         for (int j = 0; j < K; ++j)
             if (j == (int)out_k - 1) dk = ex.d[j];
-        ok = dk + screen_error<SP>(sp, B, L) < L * (1.0 - 8.0 * kU);
+        ok = dk + screen_error<SP>(sp, B, L, (double)qeta + query_eta<SP>(qv)) < L * (1.0 - 8.0 * kU);
     } else {  // a list that is not full must hold every live state (an overflowed d32 is never admitted)
         uint32_t held = 0;
 #pragma unroll
@@ -1085,8 +1078,8 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
                                                                const uint32_t *__restrict__ pos_ids,
                                                                const double *__restrict__ rows64,
                                                                const double *__restrict__ qf64, DevSpace sp,
-                                                               float absmax, uint32_t n_live,
-                                                               double *__restrict__ out_d,
+                                                               float absmax, float qeta, uint32_t n_live,
+                                                               uint32_t k2, double *__restrict__ out_d,
                                                                uint32_t *__restrict__ out_i, uint32_t out_k,
                                                                uint32_t *__restrict__ fail_count,
                                                                uint32_t *__restrict__ fail_list) {
@@ -1134,10 +1127,12 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
     double dk = rank < out_k ? d : -__builtin_inf();
 #pragma unroll
     for (int o = K2 / 2; o > 0; o >>= 1) dk = fmax(dk, __shfl_xor(dk, o));
-    const bool full = (uint32_t)__shfl((int)id, gbase + K2 - 1) != kNoId;
-    const float L32 = __shfl(d32, gbase + K2 - 1);
+    // the walk's list holds k2 <= K2 entries (the rest of the K2 lanes are empty)
+    const bool full = (uint32_t)__shfl((int)id, gbase + (int)k2 - 1) != kNoId;
+    const float L32 = __shfl(d32, gbase + (int)k2 - 1);
     // entries this query's list holds (its K2 lanes of the wave)
-    const uint64_t gmask = K2 == 64 ? ~0ull : (((1ull << K2) - 1ull) << gbase);
+    uint64_t gmask = ~0ull;
+    if constexpr (K2 < 64) gmask = ((1ull << K2) - 1ull) << gbase;
     const uint32_t held = (uint32_t)__popcll(__ballot(id != kNoId) & gmask);
     bool ok = full || held >= n_live;  // not full: it must hold every live state
     if (full) {  // prove that no element outside the list can enter (knn_certify_kernel)
@@ -1145,7 +1140,7 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
         const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_REALVECTOR ? F : 0);
         for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qv[c]));
         const double L = (double)L32;
-        ok = dk + screen_error<SP>(sp, B, L) < L * (1.0 - 8.0 * kU);
+        ok = dk + screen_error<SP>(sp, B, L, (double)qeta + query_eta<SP>(qv)) < L * (1.0 - 8.0 * kU);
     }
     if (!live) return;
     if (rank < out_k) {
@@ -1172,7 +1167,7 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ q32,
     const uint32_t *__restrict__ perm, uint32_t nq, const double *__restrict__ rows64,
-    const double *__restrict__ qf64, DevSpace sp, float absmax, double r, uint64_t *__restrict__ counts,
+    const double *__restrict__ qf64, DevSpace sp, float absmax, float qeta, double r, uint64_t *__restrict__ counts,
     const uint64_t *__restrict__ offsets, uint32_t *__restrict__ out_i, double *__restrict__ out_d,
     unsigned long long *__restrict__ counters, uint32_t slab) {
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
@@ -1206,7 +1201,7 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
         const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : F;
         for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qv[g][c]));
         // every element with d <= r has d32 <= r + e; rounding to fp32 is covered by the 16 u
-        const double t = (r + screen_error<SP>(sp, B, r)) * (1.0 + 16.0 * kU);
+        const double t = (r + screen_error<SP>(sp, B, r, (double)qeta + query_eta<SP>(qv[g]))) * (1.0 + 16.0 * kU);
         thr[g] = live ? (float)t : -__builtin_inff();
         cur[g] = (FILL && live) ? offsets[qo[g]] : 0ull;
     }
@@ -1343,7 +1338,8 @@ __global__ void scatter_results_kernel(const double *__restrict__ d, const uint3
 
 // ---- host orchestration -----------------------------------------------------------------
 struct FastPlan {
-    int K2, K;
+    int K2, K;   // K2: lanes / slots per query list (16 / 32 / 64); K: the certificate's k bucket
+    int k2;      // entries the walk keeps (<= K2): k + 2 for the culled walks, K2 otherwise
     bool cull;
     uint32_t chunks, chunk_len;
 };
@@ -1352,8 +1348,13 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
     FastPlan p{};
     p.K2 = fast_k2(sp, k, nq);
     p.K = k_bucket(k);
+    p.k2 = p.K2;
     p.cull = cull;
-    if (cull) {  // group walk: one list per query
+    if (cull) {  // group walk: one list per query, k + 2 entries in the smallest slot bucket
+        p.k2 = (int)k + 2;
+        int lanes = k_bucket(k + 2);
+        if (lanes < 16) lanes = 16;
+        if (p.K2 > 0 && lanes <= p.K2) p.K2 = lanes;
         p.chunks = 1;
         p.chunk_len = 0;
         return p;
@@ -1436,10 +1437,10 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             constexpr int G = group_queries<SP>();
-            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, false, 1, true>), dim3((nq + G - 1) / G), dim3(64),
-                               0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
-                               ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters,
-                               kBulkThreshold);
+            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
+                               ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0,
+                               q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, kBulkThreshold,
+                               p.k2);
             timer_end(st);
             walked = true;
         }
@@ -1466,11 +1467,11 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (pos && !ss->rows64) return hipErrorInvalidValue;
         hipLaunchKernelGGL((knn_certify_wave_kernel<SP, F, K2>), dim3((nq + QPB - 1) / QPB), b256, 0, st, pd, pi, nq,
                            perm, f64, cap, pos ? ss->ids : nullptr, pos ? ss->rows64 : nullptr, qf64, sp, b.absmax,
-                           b.n_live, od, oi, k, fail, fail + 1);
+                           b.qeta, b.n_live, (uint32_t)p.k2, od, oi, k, fail, fail + 1);
     } else {
         if (p.cull) return hipErrorInvalidValue;  // position lists need the wave certificate
         hipLaunchKernelGGL((knn_certify_kernel<SP, F, K2, K>), dim3((nq + 255) / 256), b256, 0, st, pd, pi, p.chunks,
-                           nq, perm, f64, cap, qf64, sp, b.absmax, b.n_live, od, oi, k, fail, fail + 1);
+                           nq, perm, f64, cap, qf64, sp, b.absmax, b.qeta, b.n_live, od, oi, k, fail, fail + 1);
     }
     return hipGetLastError();
 }
@@ -1578,12 +1579,12 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
             timer_begin(st, "radius32_group_kernel");
             hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 2>), grid, b64, 0, st, ss->rows, ss->n_pad,
                                ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64,
-                               sp, b.absmax, r, counts, nullptr, out_i, out_d, ss->counters, b.slab);
+                               sp, b.absmax, b.qeta, r, counts, nullptr, out_i, out_d, ss->counters, b.slab);
             timer_end(st);
         } else {
             hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 0>), grid, b64, 0, st, ss->rows, ss->n_pad,
                                ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64,
-                               sp, b.absmax, r, counts, nullptr, nullptr, nullptr, nullptr, 0u);
+                               sp, b.absmax, b.qeta, r, counts, nullptr, nullptr, nullptr, nullptr, 0u);
         }
         size_t sb = L.scan_bytes, rb = L.red_bytes;
         if ((e = hipcub::DeviceScan::ExclusiveSum(ws + L.scan, sb, counts, offs, (int)nq + 1, st)) != hipSuccess)
@@ -1594,7 +1595,7 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
     timer_begin(st, "radius32_group_kernel");
     hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 1>), grid, b64, 0, st, ss->rows, ss->n_pad,
                        ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64, sp,
-                       b.absmax, r, nullptr, offs, out_i, out_d, ss->counters, 0u);
+                       b.absmax, b.qeta, r, nullptr, offs, out_i, out_d, ss->counters, 0u);
     timer_end(st);
     return hipGetLastError();
 }

@@ -62,21 +62,26 @@ def test_clustered_and_duplicate_states(gpu):
 
 
 def test_se3_quaternion_signs_and_norms(gpu):
-    """The group walk stores sign-canonical quaternions and bounds the rotation part by the
-    chord to the box, corrected for norm excess: stored and query quaternions with w < 0 and
-    norms away from 1 must not lose a neighbour."""
+    """The group walk stores sign-canonical quaternions and screens the rotation by the chord,
+    whose error bound grows with the quaternions' norm excess: stored and query quaternions
+    with w < 0 and norms a hair away from 1 keep the culled walk and lose no neighbour; norms
+    far from 1 (3 %) make the bound useless, and the exact path answers instead."""
     rng = np.random.default_rng(64)
     sp = SE3StateSpace()
-    data = W.uniform_se3(rng, 60000)
-    data[:, 3:] *= rng.choice([-1.0, 1.0], size=(60000, 1)) * rng.uniform(0.97, 1.03, size=(60000, 1))
-    q = W.uniform_se3(rng, 700)
-    q[:, 3:] *= rng.choice([-1.0, 1.0], size=(700, 1)) * rng.uniform(0.97, 1.03, size=(700, 1))
-    nn = NearestNeighborsGPU(sp, gpu)
-    nn.add(data)
-    _check(nn, sp, data, np.arange(len(data)), q, 10)
-    scanned, total, qtiles = nn.cull_stats()
-    assert 0 < scanned <= total
-    assert scanned <= qtiles <= 8 * scanned  # each fetched tile is scanned by 1..G queries
+    for spread, culled in ((1e-9, True), (0.03, False)):
+        data = W.uniform_se3(rng, 60000)
+        data[:, 3:] *= rng.choice([-1.0, 1.0], size=(60000, 1)) * rng.uniform(1 - spread, 1 + spread, (60000, 1))
+        q = W.uniform_se3(rng, 700)
+        q[:, 3:] *= rng.choice([-1.0, 1.0], size=(700, 1)) * rng.uniform(1 - spread, 1 + spread, (700, 1))
+        nn = NearestNeighborsGPU(sp, gpu)
+        nn.add(data)
+        _check(nn, sp, data, np.arange(len(data)), q, 10)
+        scanned, total, qtiles = nn.cull_stats()
+        if culled:
+            assert 0 < scanned <= total
+            assert scanned <= qtiles <= 8 * scanned  # each fetched tile is scanned by 1..G queries
+        else:
+            assert scanned == 0
 
 
 def test_group_tail_and_small_batches(gpu):
