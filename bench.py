@@ -13,9 +13,11 @@ no collective in the data path).
 
 The other configurations are measured with --workload (same JSON line, same unit):
     cfg2  R^6, 10^5 states, batched nearestK(k=10)                       (configs[1], M1)
-    cfg4  PRM* milestone batch in the KinematicChain R^12 space: 10^6 valid roadmap
-          vertices, per step B new valid milestones -> nearestK(k = 41, KStarStrategy)
-          + checkMotion(neighbour, milestone) for every edge          (configs[3], M3)
+    cfg4  PRM* roadmap construction in the KinematicChain R^12 space, causal: a 10^6-vertex
+          valid roadmap, then per step the next B valid milestones, each connected to its
+          k_i = ceil((e + e/12) ln(i + 1)) nearest among ALL earlier vertices (the roadmap and
+          the batch's earlier milestones) + checkMotion(neighbour, milestone) per edge, then
+          inserted (PRM.cpp:562-596)                                     (configs[3], M3)
     cfg5  BIT* batch on SE(3): 10^7 valid samples, per step 10^5 vertices -> nearestR
           (r = 0.1528, ImplicitGraph.cpp:1372-1381) + checkMotion(vertex, sample) for every
           edge, 32-sphere checker                                     (configs[4], M4)
@@ -384,7 +386,9 @@ class Runner:
         elif wl == "cfg4":
             self.sp = KinematicChainSpace(12, 1.0 / 12)                   # KinematicChainBenchmark.cpp:48-49
             self.ck = KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))
-            self.k = k or W.prm_star_k(args.tree + 1, 12)                # KStarStrategy, n counts the milestone
+            self.kc = math.e + math.e / 12.0                              # KStarStrategy (ConnectionStrategy.h:141)
+            last = args.tree + nq * (args.warmup + args.steps) * int(os.environ.get("WORLD_SIZE", "1"))
+            self.k = int(math.ceil(self.kc * math.log(last)))           # k_cap: the largest k_i of the run
         else:
             self.sp = SE3StateSpace(0.0, 1.0)
             c, r = W.sphere_field(32, 0.1, 7)
@@ -395,8 +399,18 @@ class Runner:
         elif wl == "cfg5":
             self.k = 0
         self.mv = DiscreteMotionValidatorGPU(self.sp, self.ck, local)
-        if wl in ("cfg4", "cfg5"):  # roadmap / sample sets hold valid states (PRM.cpp:356-378, ImplicitGraph.cpp:981)
+        if wl == "cfg5":  # sample sets hold valid states (ImplicitGraph.cpp:981)
             self.tree, q = reference_inputs(self.sp, args.tree, nq, rank, valid=self.mv.isValid)
+        elif wl == "cfg4":  # roadmap + the milestones of every step: valid states (PRM.cpp:356-378)
+            # one causal batch per step holds world * nq milestones of the query stream; every rank
+            # inserts the whole batch (replicas stay identical) and computes the neighbours and edges
+            # of its slice [rank * nq, (rank + 1) * nq) — no collective in the data path
+            nsteps, world = args.warmup + args.steps, int(os.environ.get("WORLD_SIZE", "1"))
+            self.tree, q = reference_inputs(self.sp, args.tree, nq * world * nsteps, 0, valid=self.mv.isValid)
+            self.milestones = [q[i * nq * world:(i + 1) * nq * world] for i in range(nsteps)]
+            self.slice = (rank * nq, (rank + 1) * nq)
+            self.step_i = 0
+            self.n_mid = args.tree + nq * world * (args.warmup + args.steps / 2.0)  # mean store size, timed steps
         self.q_host = q
         self.nq = nq
         self.queries = torch.from_numpy(q).to(dev)
@@ -409,6 +423,9 @@ class Runner:
         if wl in ("cfg3", "cfg2", "cfg4"):
             self.ids = torch.empty((nq, self.k), dtype=torch.int32, device=dev)
             self.dd = torch.empty((nq, self.k), dtype=torch.float64, device=dev)
+        if wl == "cfg4":
+            self.cnt = torch.empty(nq, dtype=torch.int32, device=dev)
+            self.evalid = torch.empty((nq, self.k), dtype=torch.uint8, device=dev)
         m = nq * self.k if wl == "cfg4" else nq
         if wl == "cfg5":
             self.off = torch.empty(nq + 1, dtype=torch.int64, device=dev)
@@ -424,6 +441,17 @@ class Runner:
 
     def step(self, e=None):
         a, nn, mv, q = self.args, self.nn, self.mv, self.queries.data_ptr()
+        if a.workload == "cfg4":  # one causal PRM* batch (synchronous: its kNN, scan, edges, insert)
+            if e:
+                e[0].record(self.stream)
+            batch = self.milestones[self.step_i]
+            self.step_i += 1
+            self.m = nn.prm_add_milestones_device(mv, batch, self.kc, self.k, self.ids.data_ptr(),
+                                                  self.cnt.data_ptr(), self.evalid.data_ptr(), *self.slice)
+            if e:
+                for j in (1, 2, 3):
+                    e[j].record(self.stream)
+            return
         if e:
             e[0].record(self.stream)
         if a.workload == "cfg5":
@@ -477,10 +505,13 @@ class Runner:
             base.update(workload="configs[1]: R^6 RealVectorStateSpace, batched nearestK(k=10)", k=self.k,
                         state_space="R^6 [0,1]^6")
         elif a.workload == "cfg4":
-            base.update(workload="configs[3]: PRM* milestone batch, KinematicChain R^12 (horn environment) — "
-                                 "nearestK(k = ceil((e + e/12) ln n)) + checkMotion(neighbour, milestone) per edge",
-                        k=self.k, state_space="KinematicChain 12 links, linkLength 1/12",
-                        edges_per_step=self.m, note="roadmap vertices and milestones are valid states (rejection)")
+            base.update(workload="configs[3]: PRM* roadmap construction, causal batches, KinematicChain R^12 (horn "
+                                 "environment) — milestone i: nearestK(k_i = ceil((e + e/12) ln(i+1))) over every "
+                                 "earlier vertex + checkMotion(neighbour, milestone) per edge + insert",
+                        k_max=self.k, state_space="KinematicChain 12 links, linkLength 1/12",
+                        edges_last_step=self.m,
+                        note=("roadmap vertices and milestones are valid states (rejection); the batch's "
+                              "milestones are uploaded from the host inside each step (~1 MB, <0.1% of the step)"))
         else:
             base.update(workload="configs[4]: BIT* batch on SE(3) — nearestR(r = 1.1 r_RGG (ln n / n)^(1/6)) + "
                                  "checkMotion(vertex, sample) per edge, 32 spheres r=0.1",
@@ -489,7 +520,8 @@ class Runner:
         return base
 
     def roofline(self, kern_ms, kern_name, before, after, launches):
-        wl, nq, n = self.args.workload, self.nq, self.args.tree
+        wl, nq = self.args.workload, self.nq
+        n = getattr(self, "n_mid", self.args.tree)
         traffic = pmc_traffic(wl, kern_name)
         if kern_name == "radius32_group_kernel":
             pairs = (after["rq"] - before["rq"]) * 64 / launches
@@ -620,7 +652,14 @@ def main():
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
     elapsed, nn_ms, edge_ms, mv_ms, kern_ms = t.tolist()
     total_units = float(u.item())
-    valid_frac = float(run.valid[: max(run.m, 1)].float().mean().item()) if args.workload != "cfg2" else None
+    if args.workload == "cfg4":  # edge validity of the last batch: row r holds cnt[r] edges
+        cols = torch.arange(run.k, device=dev).unsqueeze(0)
+        live = cols < run.cnt.unsqueeze(1)
+        valid_frac = float(run.evalid[live].float().mean().item()) if bool(live.any()) else None
+    elif args.workload != "cfg2":
+        valid_frac = float(run.valid[: max(run.m, 1)].float().mean().item())
+    else:
+        valid_frac = None
 
     single = rrt = spheres = rrt_star = index = None
     if rank == 0 and args.workload in ("cfg3", "cfg2") and not args.no_extras:
@@ -662,7 +701,12 @@ def main():
             "roofline": run.roofline(kern_ms, kern_name, c0, c1, max(args.steps, 1)),
             "cpu_baseline": cpu,
         }
-        if args.workload != "cfg2":
+        if args.workload == "cfg4":  # one synchronous call per step: kNN, causal scan, edges and insert together
+            line["phase_ms"] = {"prm_batch": nn_ms}
+            line["edges_checked_per_s"] = run.m * world / (nn_ms * 1e-3)
+            line["motion_valid_fraction"] = valid_frac
+            line["roadmap_vertices"] = run.nn.size()
+        elif args.workload != "cfg2":
             line["motion_checks_per_s"] = run.m * world / (mv_ms * 1e-3)
             line["motion_valid_fraction"] = valid_frac
         if index:

@@ -37,6 +37,7 @@
  *   ompl_gpu_steer_device  the RRT extend step (nearest -> interpolate to range)
  *                          src/ompl/geometric/planners/rrt/src/RRT.cpp:137-146
  *   ompl_gpu_rrt_grow_device  the RRT loop itself                 RRT.cpp:128-192
+ *   ompl_gpu_prm_add_milestones  PRM* causal roadmap batches      prm/src/PRM.cpp:562-596
  *   ompl_gpu_nn_edges_device  the edges PRM / BIT* check after a neighbour query
  *                          prm/src/PRM.cpp:577-582, informedtrees/src/BITstar.cpp:815
  *
@@ -268,6 +269,23 @@ ompl_gpu_status ompl_gpu_mv_motion_states(ompl_gpu_mv *h, const double *s1, cons
                                           uint32_t count, int endpoints, double *out);
 ompl_gpu_status ompl_gpu_mv_motion_states_device(ompl_gpu_mv *h, const double *d_s1, const double *d_s2, size_t m,
                                                  uint32_t count, int endpoints, double *d_out);
+
+/* ---- PRM* roadmap construction, causal batches ------------------------------------
+ * PRM::addMilestone (geometric/planners/prm/src/PRM.cpp:562-596) with KStarStrategy
+ * (ConnectionStrategy.h:124-156) for m new milestones (host AoS, in insertion order) after the
+ * n0 states already stored: milestone j (id n0 + j) connects to its
+ * k_j = ceil(k_const * ln(n0 + j + 1)) nearest among ALL earlier vertices — the stored states and
+ * the milestones j' < j of the batch — sorted by (distance, id); every edge is checked with mv's
+ * checkMotion(state[neighbour], state[milestone]) (PRM.cpp:582, counters updated); then the m
+ * milestones are added to nn (PRM.cpp:593).  k_const = e + e / dim (PRM*).  Only milestones
+ * [j0, j1) get neighbours and edges (a rank's share of a batch every rank inserts whole; the full
+ * batch is [0, m)).  Outputs (device, caller-owned, (j1 - j0) x k_cap, k_cap >= the batch's largest
+ * k, <= 64): d_nbr neighbour ids (0xFFFFFFFF past d_cnt[r]), d_cnt, d_valid (1 = the edge is
+ * valid).  *edges (may be NULL) = edges checked.  Synchronous; equal to the sequential loop's
+ * result (tests/test_gpu_prm.py). */
+ompl_gpu_status ompl_gpu_prm_add_milestones(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const double *states, size_t m,
+                                            size_t j0, size_t j1, double k_const, uint32_t k_cap, uint32_t *d_nbr,
+                                            uint32_t *d_cnt, uint8_t *d_valid, uint64_t *edges);
 
 /* ---- RRT growth on device ----------------------------------------------------
  * The RRT loop (RRT.cpp:128-192) without its goal test, for ns samples in order: nearest

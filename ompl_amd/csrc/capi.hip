@@ -104,6 +104,7 @@ struct ompl_gpu_nn {
     uint32_t radius_slab = 64;      // per-query slab of the one-pass radius walk (adapts upward)
     uint64_t radius_one_pass = 0;   // radius calls answered by the one-pass walk
     DevBuf rrt_n, rrt_pd, rrt_pi;  // device RRT growth: live size, per-block partial minima
+    DevBuf prm_bf, prm_raw, prm_kj, prm_sd, prm_si, prm_len, prm_off, prm_eoff, prm_cnt64;  // PRM* batches
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
     double lo[kKeyDims] = {0}, hi[kKeyDims] = {0}, absmax = 0.0;
@@ -318,9 +319,16 @@ static ompl_gpu_status grow(ompl_gpu_nn *h, uint64_t need) {
     return OMPL_GPU_OK;
 }
 
+static ompl_gpu_status add_locked(ompl_gpu_nn *h, const double *states, size_t n, uint64_t *first_id);
+
 ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, uint64_t *first_id) {
     if (!h || (n && !states)) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
     std::lock_guard<std::mutex> lk(h->mu);
+    return add_locked(h, states, n, first_id);
+}
+
+// append n AoS states (caller holds the lock)
+static ompl_gpu_status add_locked(ompl_gpu_nn *h, const double *states, size_t n, uint64_t *first_id) {
     HIP_OR_FAIL(hipSetDevice(h->device));
     if (first_id) *first_id = h->n_total;
     if (n == 0) return OMPL_GPU_OK;
@@ -842,6 +850,30 @@ ompl_gpu_status ompl_gpu_nn_radius_device(ompl_gpu_nn *h, const double *d_querie
     return OMPL_GPU_OK;
 }
 
+// width of the AoS rows of the raw states (edge endpoints gathered by id)
+static int aos_width(const ompl_gpu_nn *h) { return (h->sp.dim + 1) & ~1; }
+
+// bring the AoS copy of the raw states up to date: rows of the ids added since the last call
+// (ids never move); caller holds the lock
+static ompl_gpu_status ensure_aos(ompl_gpu_nn *h) {
+    const int da = aos_width(h);
+    if (h->aos_n >= h->n_total) return OMPL_GPU_OK;
+    if (h->raw_aos.bytes < sizeof(double) * h->n_total * da) {
+        DevBuf nb;
+        HIP_OR_FAIL(nb.ensure(sizeof(double) * std::max<uint64_t>(h->cap, h->n_total) * da));
+        if (h->aos_n)
+            HIP_OR_FAIL(hipMemcpyAsync(nb.p, h->raw_aos.p, sizeof(double) * h->aos_n * da, hipMemcpyDeviceToDevice,
+                                       h->stream));
+        std::swap(h->raw_aos.p, nb.p);
+        std::swap(h->raw_aos.bytes, nb.bytes);
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // nb (the old buffer) is freed on return
+    }
+    HIP_OR_FAIL(launch_aos_rows(h->raw, h->cap, h->sp.dim, da, h->aos_n, h->n_total - h->aos_n, (double *)h->raw_aos.p,
+                                h->stream));
+    h->aos_n = h->n_total;
+    return OMPL_GPU_OK;
+}
+
 ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, const uint64_t *d_offsets,
                                          const uint32_t *d_ids, uint32_t stride, size_t m, int from_query,
                                          double *d_from, double *d_to) {
@@ -854,21 +886,10 @@ ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries
     HIP_OR_FAIL(hipSetDevice(h->device));
     // endpoints are gathered by random id: one contiguous row per state instead of one cache
     // line per coordinate of the SoA store
-    const int da = (h->sp.dim + 1) & ~1;
-    if (h->aos_n < h->n_total) {  // rows of the ids added since the last call (ids never move)
-        if (h->raw_aos.bytes < sizeof(double) * h->n_total * da) {
-            DevBuf nb;
-            HIP_OR_FAIL(nb.ensure(sizeof(double) * std::max<uint64_t>(h->cap, h->n_total) * da));
-            if (h->aos_n)
-                HIP_OR_FAIL(hipMemcpyAsync(nb.p, h->raw_aos.p, sizeof(double) * h->aos_n * da, hipMemcpyDeviceToDevice,
-                                           h->stream));
-            std::swap(h->raw_aos.p, nb.p);
-            std::swap(h->raw_aos.bytes, nb.bytes);
-            HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // nb (the old buffer) is freed on return
-        }
-        HIP_OR_FAIL(launch_aos_rows(h->raw, h->cap, h->sp.dim, da, h->aos_n, h->n_total - h->aos_n,
-                                    (double *)h->raw_aos.p, h->stream));
-        h->aos_n = h->n_total;
+    const int da = aos_width(h);
+    if (h->n_total) {
+        ompl_gpu_status s = ensure_aos(h);
+        if (s != OMPL_GPU_OK) return s;
     }
     HIP_OR_FAIL(launch_edges(h->sp, h->raw, h->cap, d_queries, (uint32_t)nq, d_offsets, d_ids, stride, m, from_query,
                              d_from, d_to, h->stream, h->n_total ? (const double *)h->raw_aos.p : nullptr, da));
@@ -1249,6 +1270,132 @@ ompl_gpu_status ompl_gpu_mv_motion_states(ompl_gpu_mv *h, const double *s1, cons
     HIP_OR_FAIL(hipMemcpyAsync(out, h->ms.p, ob, hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     return OMPL_GPU_OK;
+}
+
+// ------------------------------------------------------------------------------ PRM*
+
+ompl_gpu_status ompl_gpu_prm_add_milestones(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *states, size_t m,
+                                            size_t j0, size_t j1, double k_const, uint32_t k_cap, uint32_t *d_nbr,
+                                            uint32_t *d_cnt, uint8_t *d_valid, uint64_t *edges) {
+    if (!h || !mv || (m && !states) || (j1 > j0 && (!d_nbr || !d_cnt || !d_valid)))
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (j0 > j1 || j1 > m) return fail(OMPL_GPU_ERR_INVALID_ARG, "slice [j0, j1) outside the batch");
+    if (h->device != mv->device) return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles are on different devices");
+    if (h->sp.kind != mv->sp.kind || h->sp.dim != mv->sp.dim)
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles describe different state spaces");
+    if (m > 0x7FFFFFFFull || k_cap == 0 || k_cap > (uint32_t)kMaxK)
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "batch size or k_cap out of range (k_cap in [1, 64])");
+    std::scoped_lock lk(h->mu, mv->mu);
+    if (edges) *edges = 0;
+    if (m == 0) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    const uint64_t n0 = h->n_total;
+    if (n0 + m > 0xFFFFFFF0ull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "more than 2^32-16 states");
+    const int F = h->g.F, dim = h->sp.dim;
+    // k_i = ceil(k_const * log(n)) with n = the vertex count including milestone i
+    // (ConnectionStrategy.h:145-149, milestoneCount(), PRM.cpp:566) — host libm, as the reference
+    const size_t rows = j1 - j0;  // this rank's slice: neighbours and edges of milestones [j0, j1)
+    std::vector<uint32_t> kj(m);
+    uint32_t kmax = 0;
+    for (size_t j = 0; j < m; ++j) {
+        const double kk = std::ceil(k_const * std::log((double)(n0 + j + 1)));
+        kj[j] = kk > 0 ? (uint32_t)kk : 0u;
+        kmax = std::max(kmax, kj[j]);
+    }
+    if (kmax > k_cap) return fail(OMPL_GPU_ERR_INVALID_ARG, "k_cap below the largest k of the batch");
+    // batch features (host, as add() computes them) and raw rows
+    h->hfeat.resize(m * F);
+    for (size_t j = 0; j < m; ++j) host_features(h->sp, h->g, states + j * dim, h->hfeat.data() + j * F);
+    HIP_OR_FAIL(h->prm_bf.ensure(sizeof(double) * m * F));
+    HIP_OR_FAIL(h->prm_raw.ensure(sizeof(double) * m * dim));
+    HIP_OR_FAIL(h->prm_kj.ensure(sizeof(uint32_t) * m));
+    double *bf = (double *)h->prm_bf.p, *braw = (double *)h->prm_raw.p;
+    uint32_t *dkj = (uint32_t *)h->prm_kj.p;
+    HIP_OR_FAIL(hipMemcpyAsync(bf, h->hfeat.data(), sizeof(double) * m * F, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(braw, states, sizeof(double) * m * dim, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(dkj, kj.data(), sizeof(uint32_t) * m, hipMemcpyHostToDevice, h->stream));
+    if (rows == 0) return add_locked(h, states, m, nullptr);
+    // 1. the stored part: batched kNN of the slice's milestones (not yet inserted), k = min(kmax, live)
+    const uint32_t kq = (uint32_t)std::min<uint64_t>(kmax, h->n_live);
+    HIP_OR_FAIL(h->prm_sd.ensure(sizeof(double) * rows * std::max<uint32_t>(kq, 1)));
+    HIP_OR_FAIL(h->prm_si.ensure(sizeof(uint32_t) * rows * std::max<uint32_t>(kq, 1)));
+    double *sd = (double *)h->prm_sd.p;
+    uint32_t *si = (uint32_t *)h->prm_si.p;
+    if (kq > 0) {
+        ompl_gpu_status s = knn_features_locked(h, bf + j0 * F, rows, kq, si, sd);
+        if (s != OMPL_GPU_OK) return s;
+    }
+    // 2. in-batch causal candidates: count, offsets, fill, segmented sort by distance (stable:
+    //    stored entries first, candidates in id order, so ties resolve by id)
+    HIP_OR_FAIL(h->prm_len.ensure(sizeof(uint64_t) * (rows + 1)));
+    HIP_OR_FAIL(h->prm_off.ensure(sizeof(uint64_t) * (rows + 1)));
+    uint64_t *len = (uint64_t *)h->prm_len.p, *off = (uint64_t *)h->prm_off.p;
+    HIP_OR_FAIL(hipMemsetAsync(len + rows, 0, sizeof(uint64_t), h->stream));
+    HIP_OR_FAIL(launch_prm_causal(h->sp, h->g, false, bf, (uint32_t)j0, (uint32_t)rows, (uint32_t)n0, dkj, sd, si, kq,
+                                  len, nullptr, nullptr, nullptr, h->stream));
+    size_t sb = 0;
+    HIP_OR_FAIL(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, len, off, (int)rows + 1, h->stream));
+    HIP_OR_FAIL(h->tmp.ensure(sb));
+    sb = h->tmp.bytes;
+    HIP_OR_FAIL(hipcub::DeviceScan::ExclusiveSum(h->tmp.p, sb, len, off, (int)rows + 1, h->stream));
+    uint64_t tot = 0;
+    HIP_OR_FAIL(hipMemcpyAsync(&tot, off + rows, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (tot > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "in-batch candidate set above 2^31 entries");
+    HIP_OR_FAIL(h->dists.ensure(sizeof(double) * std::max<uint64_t>(tot, 1)));
+    HIP_OR_FAIL(h->ids.ensure(sizeof(uint32_t) * std::max<uint64_t>(tot, 1)));
+    HIP_OR_FAIL(h->sorted_d.ensure(sizeof(double) * std::max<uint64_t>(tot, 1)));
+    HIP_OR_FAIL(h->sorted_ids.ensure(sizeof(uint32_t) * std::max<uint64_t>(tot, 1)));
+    double *cd = (double *)h->dists.p, *sdd = (double *)h->sorted_d.p;
+    uint32_t *ci = (uint32_t *)h->ids.p, *sii = (uint32_t *)h->sorted_ids.p;
+    if (tot) {
+        HIP_OR_FAIL(launch_prm_causal(h->sp, h->g, true, bf, (uint32_t)j0, (uint32_t)rows, (uint32_t)n0, dkj, sd, si,
+                                      kq, nullptr, off, cd, ci, h->stream));
+        size_t tb = 0;
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, (const double *)cd, sdd,
+                                                                (const uint32_t *)ci, sii, (int)tot, (int)rows, off,
+                                                                off + 1, 0, 64, h->stream));
+        HIP_OR_FAIL(h->tmp.ensure(tb));
+        tb = h->tmp.bytes;
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb, (const double *)cd, sdd,
+                                                                (const uint32_t *)ci, sii, (int)tot, (int)rows, off,
+                                                                off + 1, 0, 64, h->stream));
+    }
+    HIP_OR_FAIL(launch_prm_take(sii, off, dkj + j0, (uint32_t)rows, k_cap, d_nbr, d_cnt, h->stream));
+    // 3. edges checkMotion(state[n], state[m]) (PRM.cpp:582): compact, check, scatter to [m][k_cap]
+    HIP_OR_FAIL(h->prm_eoff.ensure(sizeof(uint64_t) * (rows + 1)));
+    HIP_OR_FAIL(h->prm_cnt64.ensure(sizeof(uint64_t) * (rows + 1)));
+    uint64_t *eoff = (uint64_t *)h->prm_eoff.p, *c64 = (uint64_t *)h->prm_cnt64.p;
+    HIP_OR_FAIL(launch_widen_u32(d_cnt, (uint32_t)rows, c64, h->stream));
+    HIP_OR_FAIL(hipMemsetAsync(c64 + rows, 0, sizeof(uint64_t), h->stream));
+    size_t need = 0;
+    HIP_OR_FAIL(hipcub::DeviceScan::ExclusiveSum(nullptr, need, c64, eoff, (int)rows + 1, h->stream));
+    HIP_OR_FAIL(h->tmp.ensure(need));
+    sb = h->tmp.bytes;
+    HIP_OR_FAIL(hipcub::DeviceScan::ExclusiveSum(h->tmp.p, sb, c64, eoff, (int)rows + 1, h->stream));
+    uint64_t E = 0;
+    HIP_OR_FAIL(hipMemcpyAsync(&E, eoff + rows, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+    if (n0) {
+        ompl_gpu_status s = ensure_aos(h);
+        if (s != OMPL_GPU_OK) return s;
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (E > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many edges in one batch");
+    if (E) {
+        HIP_OR_FAIL(mv->s1.ensure(sizeof(double) * E * dim));
+        HIP_OR_FAIL(mv->s2.ensure(sizeof(double) * E * dim));
+        HIP_OR_FAIL(mv->valid.ensure(E));
+        HIP_OR_FAIL(launch_prm_edges(d_nbr, d_cnt, eoff, (uint32_t)rows, (uint32_t)j0, k_cap, (uint32_t)n0, dim,
+                                     n0 ? (const double *)h->raw_aos.p : nullptr, aos_width(h), braw,
+                                     (double *)mv->s1.p, (double *)mv->s2.p, h->stream));
+        HIP_OR_FAIL(launch_motion(mv->sp, mv->ck, (const double *)mv->s1.p, (const double *)mv->s2.p, (uint32_t)E,
+                                  (uint8_t *)mv->valid.p, nullptr, nullptr, mv->counters, h->stream));
+    }
+    HIP_OR_FAIL(launch_prm_scatter_valid((const uint8_t *)mv->valid.p, d_cnt, eoff, (uint32_t)rows, k_cap, d_valid,
+                                         h->stream));
+    if (edges) *edges = E;
+    // 4. the milestones join the structure (PRM.cpp:593)
+    return add_locked(h, states, m, nullptr);
 }
 
 // ------------------------------------------------------------------------------ RRT

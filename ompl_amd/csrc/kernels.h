@@ -203,6 +203,24 @@ hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, con
 // rows of ids [first, first + n) of the SoA store into aos[id][da]
 hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uint64_t first, uint64_t n, double *aos,
                            hipStream_t st);
+// ---- PRM* causal milestone batches (prm.hip) ------------------------------------------------
+// bf: [m][F] features of the batch; kj[m]: k of each milestone; sd / si: [m][kq] stored kNN lists.
+// fill = false: seg_len[j] = stored entries kept + in-batch candidates; fill = true: segments
+// written at seg_off (stored entries, then candidates j' < j with d <= the k_j-th stored distance)
+// rows j0 .. j0 + rows - 1 of the batch (this rank's slice; sd / si / seg_* indexed by row)
+hipError_t launch_prm_causal(const DevSpace &sp, const FeatGeom &g, bool fill, const double *bf, uint32_t j0,
+                             uint32_t rows, uint32_t n0, const uint32_t *kj, const double *sd, const uint32_t *si,
+                             uint32_t kq, uint64_t *seg_len, const uint64_t *seg_off, double *out_d, uint32_t *out_i,
+                             hipStream_t st);
+hipError_t launch_prm_take(const uint32_t *sorted_i, const uint64_t *seg_off, const uint32_t *kj, uint32_t m,
+                           uint32_t k_cap, uint32_t *nbr, uint32_t *cnt, hipStream_t st);
+hipError_t launch_prm_edges(const uint32_t *nbr, const uint32_t *cnt, const uint64_t *eoff, uint32_t m, uint32_t j0,
+                            uint32_t k_cap, uint32_t n0, int dim, const double *stored_aos, int da, const double *braw,
+                            double *s1, double *s2, hipStream_t st);
+hipError_t launch_widen_u32(const uint32_t *a, uint32_t n, uint64_t *b, hipStream_t st);
+hipError_t launch_prm_scatter_valid(const uint8_t *vc, const uint32_t *cnt, const uint64_t *eoff, uint32_t m,
+                                    uint32_t k_cap, uint8_t *valid, hipStream_t st);
+
 // ---- RRT growth on device (rrt.hip) -------------------------------------------------------
 size_t rrt_part_entries(uint64_t n_max);
 hipError_t launch_rrt_grow(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck, const FeatGeom &g,

@@ -1,0 +1,213 @@
+// prm.hip — PRM*'s causal milestone insertion on the device.
+//
+// PRM::addMilestone (geometric/planners/prm/src/PRM.cpp:562-596) with KStarStrategy
+// (ConnectionStrategy.h:124-156): milestone i is connected to its k_i = ceil((e + e/d) ln(i + 1))
+// nearest among the vertices added before it — the stored states AND the milestones of the same
+// batch that precede it — and every edge is checked with checkMotion(state[n], state[m]).  A batch
+// is answered exactly in three parts: the stored part by the batched kNN (certified fp32 screen),
+// the in-batch part by a causal scan (milestone j against milestones j' < j, fp64 in the
+// reference's operation order, keeping only those within the stored list's k_j-th distance), and
+// a segmented sort by (distance, id) of the union, whose first k_j entries are the answer.
+#include <hip/hip_runtime.h>
+
+#include "feat_dist.h"
+#include "kernels.h"
+#include "topk.h"
+
+namespace ompl_amd {
+
+namespace {
+
+// stored-list bound of milestone j: its k_j-th stored neighbour's distance (+inf when the stored
+// list has fewer than k_j entries)
+__device__ __forceinline__ double stored_bound(const double *sd, const uint32_t *si, uint32_t kq, uint32_t kj,
+                                               uint32_t j) {
+    if (kj == 0) return -1.0;  // k_0 = 0: no neighbour at all (PRM.cpp:566, log(1) = 0)
+    if (kj > kq) return __builtin_inf();
+    const size_t o = (size_t)j * kq + kj - 1;
+    return si[o] == kNoId ? __builtin_inf() : sd[o];
+}
+
+__device__ __forceinline__ uint32_t stored_take(const uint32_t *si, uint32_t kq, uint32_t kj, uint32_t j) {
+    uint32_t c = 0;
+    const uint32_t lim = kj < kq ? kj : kq;
+    for (uint32_t r = 0; r < lim; ++r) c += si[(size_t)j * kq + r] != kNoId ? 1u : 0u;
+    return c;
+}
+
+// one wave per milestone j: FILL = false counts the in-batch candidates j' < j with
+// d(j', j) <= bound; FILL = true writes the segment [stored entries | candidates in j' order]
+template <int SP, int F, int NMAX, bool FILL>
+__global__ __launch_bounds__(256) void prm_causal_kernel(const double *__restrict__ bf, uint32_t j0, uint32_t rows,
+                                                         uint32_t n0, DevSpace sp, const uint32_t *__restrict__ kj_arr,
+                                                         const double *__restrict__ sd, const uint32_t *__restrict__ si,
+                                                         uint32_t kq, uint64_t *__restrict__ seg_len,
+                                                         const uint64_t *__restrict__ seg_off,
+                                                         double *__restrict__ out_d, uint32_t *__restrict__ out_i) {
+    const uint32_t row = blockIdx.x * 4 + (threadIdx.x >> 6), j = j0 + row;  // row of this rank's slice
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const uint32_t kj = kj_arr[j];
+    const double bound = stored_bound(sd, si, kq, kj, row);
+    double qv[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qv[f] = bf[(size_t)j * F + f];
+    uint64_t pos = 0;
+    if (FILL) {
+        pos = seg_off[row];
+        const uint32_t st = stored_take(si, kq, kj, row);
+        for (uint32_t r = lane; r < st; r += 64) {  // stored entries first: (distance, id) sorted already
+            out_d[pos + r] = sd[(size_t)row * kq + r];
+            out_i[pos + r] = si[(size_t)row * kq + r];
+        }
+        pos += st;
+    }
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint64_t cnt = 0;
+    for (uint32_t b = 0; b < j; b += 64) {
+        const uint32_t jp = b + lane;
+        bool hit = false;
+        double d = 0.0;
+        if (jp < j && bound >= 0.0) {
+            double sv[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) sv[f] = bf[(size_t)jp * F + f];
+            d = feat_dist<SP, F, NMAX>(sv, qv, sp);  // fp64, the reference's operation order
+            hit = d <= bound;
+        }
+        const uint64_t bm = __ballot(hit);
+        if (FILL && hit) {
+            const uint64_t p = pos + cnt + (uint64_t)__popcll(bm & lt);
+            out_d[p] = d;
+            out_i[p] = n0 + jp;
+        }
+        cnt += (uint64_t)__popcll(bm);
+    }
+    if (!FILL && lane == 0) seg_len[row] = stored_take(si, kq, kj, row) + cnt;
+}
+
+// thread per (milestone, rank): the first min(k_j, segment) sorted entries
+__global__ void prm_take_kernel(const uint32_t *__restrict__ sorted_i, const uint64_t *__restrict__ seg_off,
+                                const uint32_t *__restrict__ kj_arr, uint32_t m, uint32_t k_cap,
+                                uint32_t *__restrict__ nbr, uint32_t *__restrict__ cnt) {  // kj_arr: this slice
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)m * k_cap) return;
+    const uint32_t j = (uint32_t)(t / k_cap), r = (uint32_t)(t % k_cap);
+    const uint64_t len = seg_off[j + 1] - seg_off[j];
+    const uint32_t c = (uint32_t)min((uint64_t)kj_arr[j], len);
+    nbr[t] = r < c ? sorted_i[seg_off[j] + r] : kNoId;
+    if (r == 0) cnt[j] = c;
+}
+
+// edge e = eoff[j] + r: checkMotion(state[nbr], state[milestone j]) (PRM.cpp:582)
+__global__ void prm_edges_kernel(const uint32_t *__restrict__ nbr, const uint32_t *__restrict__ cnt,
+                                 const uint64_t *__restrict__ eoff, uint32_t m, uint32_t j0, uint32_t k_cap, uint32_t n0,
+                                 int dim,
+                                 const double *__restrict__ stored_aos, int da, const double *__restrict__ braw,
+                                 double *__restrict__ s1, double *__restrict__ s2) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)m * k_cap) return;
+    const uint32_t j = (uint32_t)(t / k_cap), r = (uint32_t)(t % k_cap);
+    if (r >= cnt[j]) return;
+    const uint64_t e = eoff[j] + r;
+    const uint32_t id = nbr[t];
+    const double *a = id < n0 ? stored_aos + (size_t)id * da : braw + (size_t)(id - n0) * dim;
+    const double *b = braw + (size_t)(j0 + j) * dim;
+    for (int c = 0; c < dim; ++c) {
+        s1[e * dim + c] = a[c];
+        s2[e * dim + c] = b[c];
+    }
+}
+
+__global__ void prm_scatter_valid_kernel(const uint8_t *__restrict__ vc, const uint32_t *__restrict__ cnt,
+                                         const uint64_t *__restrict__ eoff, uint32_t m, uint32_t k_cap,
+                                         uint8_t *__restrict__ valid) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)m * k_cap) return;
+    const uint32_t j = (uint32_t)(t / k_cap), r = (uint32_t)(t % k_cap);
+    valid[t] = r < cnt[j] ? vc[eoff[j] + r] : 0;
+}
+
+template <int SP, int F, int NMAX>
+hipError_t run_prm_causal(const DevSpace &sp, bool fill, const double *bf, uint32_t j0, uint32_t rows, uint32_t n0,
+                          const uint32_t *kj, const double *sd, const uint32_t *si, uint32_t kq, uint64_t *seg_len,
+                          const uint64_t *seg_off, double *out_d, uint32_t *out_i, hipStream_t st) {
+    const dim3 grid((rows + 3) / 4), block(256);
+    if (fill)
+        hipLaunchKernelGGL((prm_causal_kernel<SP, F, NMAX, true>), grid, block, 0, st, bf, j0, rows, n0, sp, kj, sd, si,
+                           kq, seg_len, seg_off, out_d, out_i);
+    else
+        hipLaunchKernelGGL((prm_causal_kernel<SP, F, NMAX, false>), grid, block, 0, st, bf, j0, rows, n0, sp, kj, sd,
+                           si, kq, seg_len, seg_off, out_d, out_i);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+#define OMPL_AMD_SPACE_DISPATCH(FN, ...)                                                              \
+    switch (sp.kind) {                                                                               \
+    case OMPL_GPU_SPACE_REALVECTOR:                                                                  \
+        if (g.F == 4) return FN<OMPL_GPU_SPACE_REALVECTOR, 4, 0>(__VA_ARGS__);                       \
+        if (g.F == 8) return FN<OMPL_GPU_SPACE_REALVECTOR, 8, 0>(__VA_ARGS__);                       \
+        return FN<OMPL_GPU_SPACE_REALVECTOR, 16, 0>(__VA_ARGS__);                                    \
+    case OMPL_GPU_SPACE_SO3: return FN<OMPL_GPU_SPACE_SO3, 4, 0>(__VA_ARGS__);                       \
+    case OMPL_GPU_SPACE_SE3: return FN<OMPL_GPU_SPACE_SE3, 7, 0>(__VA_ARGS__);                       \
+    case OMPL_GPU_SPACE_KCHAIN:                                                                      \
+        if (g.nmax == 4) return FN<OMPL_GPU_SPACE_KCHAIN, 8, 4>(__VA_ARGS__);                        \
+        if (g.nmax == 8) return FN<OMPL_GPU_SPACE_KCHAIN, 16, 8>(__VA_ARGS__);                       \
+        if (g.nmax == 12) return FN<OMPL_GPU_SPACE_KCHAIN, 24, 12>(__VA_ARGS__);                     \
+        return FN<OMPL_GPU_SPACE_KCHAIN, 32, 16>(__VA_ARGS__);                                       \
+    }                                                                                                \
+    return hipErrorInvalidValue;
+
+hipError_t launch_prm_causal(const DevSpace &sp, const FeatGeom &g, bool fill, const double *bf, uint32_t j0,
+                             uint32_t rows, uint32_t n0, const uint32_t *kj, const double *sd, const uint32_t *si,
+                             uint32_t kq, uint64_t *seg_len, const uint64_t *seg_off, double *out_d, uint32_t *out_i,
+                             hipStream_t st) {
+    if (rows == 0) return hipSuccess;
+    OMPL_AMD_SPACE_DISPATCH(run_prm_causal, sp, fill, bf, j0, rows, n0, kj, sd, si, kq, seg_len, seg_off, out_d, out_i,
+                            st)
+}
+
+hipError_t launch_prm_take(const uint32_t *sorted_i, const uint64_t *seg_off, const uint32_t *kj, uint32_t m,
+                           uint32_t k_cap, uint32_t *nbr, uint32_t *cnt, hipStream_t st) {
+    const uint64_t n = (uint64_t)m * k_cap;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(prm_take_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sorted_i, seg_off, kj, m,
+                       k_cap, nbr, cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_prm_edges(const uint32_t *nbr, const uint32_t *cnt, const uint64_t *eoff, uint32_t m, uint32_t j0,
+                            uint32_t k_cap, uint32_t n0, int dim, const double *stored_aos, int da, const double *braw,
+                            double *s1, double *s2, hipStream_t st) {
+    const uint64_t n = (uint64_t)m * k_cap;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(prm_edges_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nbr, cnt, eoff, m, j0,
+                       k_cap, n0, dim, stored_aos, da, braw, s1, s2);
+    return hipGetLastError();
+}
+
+namespace {
+__global__ void widen_kernel(const uint32_t *__restrict__ a, uint32_t n, uint64_t *__restrict__ b) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) b[i] = a[i];
+}
+}  // namespace
+
+hipError_t launch_widen_u32(const uint32_t *a, uint32_t n, uint64_t *b, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(widen_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a, n, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_prm_scatter_valid(const uint8_t *vc, const uint32_t *cnt, const uint64_t *eoff, uint32_t m,
+                                    uint32_t k_cap, uint8_t *valid, hipStream_t st) {
+    const uint64_t n = (uint64_t)m * k_cap;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(prm_scatter_valid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, vc, cnt, eoff, m,
+                       k_cap, valid);
+    return hipGetLastError();
+}
+
+}  // namespace ompl_amd

@@ -216,6 +216,41 @@ class NearestNeighborsGPU:
         abi.check(abi.lib.ompl_gpu_rrt_grow_device(self._h, mv._h, C.c_void_p(d_samples), int(ns), float(max_distance),
                                                    C.c_void_p(d_nearest), C.c_void_p(d_added)))
 
+    def prm_add_milestones(self, mv, states, k_const: float, k_cap: int, j0: int = 0, j1: int | None = None):
+        """PRM* causal batch (PRM.cpp:562-596, KStarStrategy): the milestones, in order, connect to
+        their k_i nearest among every earlier vertex, edges checked with mv, then join the structure.
+        Returns host arrays (neighbours [m, k_cap] uint32 with 0xFFFFFFFF padding, counts [m],
+        edge validity [m, k_cap] bool) and the number of edges checked."""
+        import torch
+
+        x = abi.as_states(states, self.dim)
+        m = x.shape[0]
+        j1 = m if j1 is None else j1
+        r = j1 - j0
+        dev = torch.device("cuda", self.device)
+        nbr = torch.empty((max(r, 1), k_cap), dtype=torch.int32, device=dev)
+        cnt = torch.empty(max(r, 1), dtype=torch.int32, device=dev)
+        val = torch.empty((max(r, 1), k_cap), dtype=torch.uint8, device=dev)
+        e = C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_prm_add_milestones(self._h, mv._h, abi.dptr(x), m, int(j0), int(j1), float(k_const),
+                                                      int(k_cap), C.c_void_p(nbr.data_ptr()),
+                                                      C.c_void_p(cnt.data_ptr()), C.c_void_p(val.data_ptr()),
+                                                      C.byref(e)))
+        torch.cuda.synchronize(dev)
+        return (nbr[:r].cpu().numpy().view(np.uint32), cnt[:r].cpu().numpy().view(np.uint32),
+                val[:r].cpu().numpy().astype(bool), e.value)
+
+    def prm_add_milestones_device(self, mv, states, k_const: float, k_cap: int, d_nbr: int, d_cnt: int,
+                                  d_valid: int, j0: int = 0, j1: int | None = None) -> int:
+        """The same into caller-owned device buffers ((j1 - j0) rows); returns the number of edges checked."""
+        x = abi.as_states(states, self.dim)
+        j1 = x.shape[0] if j1 is None else j1
+        e = C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_prm_add_milestones(self._h, mv._h, abi.dptr(x), x.shape[0], int(j0), int(j1),
+                                                      float(k_const), int(k_cap), C.c_void_p(d_nbr),
+                                                      C.c_void_p(d_cnt), C.c_void_p(d_valid), C.byref(e)))
+        return e.value
+
     def steer_device(self, d_queries: int, nq: int, d_nearest: int, stride: int, max_distance: float,
                      d_from: int, d_to: int) -> None:
         abi.check(abi.lib.ompl_gpu_steer_device(self._h, C.c_void_p(d_queries), nq, C.c_void_p(d_nearest),

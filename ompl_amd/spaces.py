@@ -51,6 +51,10 @@ class StateSpace:
     def getMaximumExtent(self) -> float:
         raise NotImplementedError
 
+    def getDimension(self) -> int:
+        """Manifold dimension (StateSpace::getDimension); `dim` is the stored doubles per state."""
+        return self.dim
+
     def lvs(self):
         return (self.getMaximumExtent() * self.fraction, 0.0)
 
@@ -83,6 +87,9 @@ class SO3StateSpace(StateSpace):
     kind = abi.SPACE_SO3
     dim = 4
 
+    def getDimension(self):
+        return 3  # SO3StateSpace.cpp:246
+
     def getMaximumExtent(self):
         return 0.5 * math.pi
 
@@ -94,6 +101,9 @@ class SE3StateSpace(StateSpace):
 
     kind = abi.SPACE_SE3
     dim = 7
+
+    def getDimension(self):
+        return 6  # R^3 + SO(3), CompoundStateSpace::getDimension
 
     def __init__(self, low=0.0, high=1.0):
         super().__init__()

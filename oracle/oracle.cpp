@@ -393,3 +393,37 @@ void oracle_radius(const ompl_gpu_space *sp, const double *data, size_t n, const
 }
 
 }  // extern "C"
+
+/* PRM* roadmap construction, the reference's sequential loop: PRM::addMilestone
+ * (geometric/planners/prm/src/PRM.cpp:562-596) with KStarStrategy (ConnectionStrategy.h:145-149):
+ * vertex i asks the nearest-neighbour structure (which holds vertices 0..i-1) for its
+ * k_i = ceil(k_const * log(i + 1)) nearest, checks checkMotion(state[n], state[i]) for each, then
+ * is added.  Neighbours in (distance, index) order (NearestNeighborsLinear semantics). */
+extern "C" void oracle_prm_causal(const ompl_gpu_space *sp, const ompl_gpu_checker *ck, const double *states, size_t n,
+                                  double k_const, uint32_t k_cap, uint32_t *nbr, uint32_t *cnt, uint8_t *valid) {
+    const int dim = sp->dim;
+    std::vector<uint32_t> ids(k_cap);
+    std::vector<double> ds(k_cap), s1(k_cap * dim), s2(k_cap * dim);
+    std::vector<uint8_t> v(k_cap);
+    for (size_t i = 0; i < n; ++i) {
+        const double kk = std::ceil(k_const * std::log((double)(i + 1)));
+        uint32_t k = kk > 0 ? (uint32_t)kk : 0u;
+        if (k > k_cap) k = k_cap;
+        uint32_t c = 0;
+        if (k > 0 && i > 0) oracle_knn(sp, states, i, states + i * dim, 1, k, ids.data(), ds.data(), &c);
+        cnt[i] = c;
+        for (uint32_t r = 0; r < k_cap; ++r) {
+            nbr[i * k_cap + r] = r < c ? ids[r] : 0xFFFFFFFFu;
+            valid[i * k_cap + r] = 0;
+        }
+        for (uint32_t r = 0; r < c; ++r)
+            for (int d = 0; d < dim; ++d) {
+                s1[r * dim + d] = states[(size_t)ids[r] * dim + d];
+                s2[r * dim + d] = states[i * dim + d];
+            }
+        if (c) {
+            oracle_check_motions(sp, ck, s1.data(), s2.data(), c, v.data(), nullptr, nullptr);
+            for (uint32_t r = 0; r < c; ++r) valid[i * k_cap + r] = v[r];
+        }
+    }
+}

@@ -82,6 +82,11 @@ uint64_t oracle_gnat_radius_count(const oracle_gnat *g, const double *q, size_t 
 uint64_t oracle_check_motions_mt(const ompl_gpu_space *sp, const ompl_gpu_checker *ck, const double *s1,
                                  const double *s2, size_t m, uint8_t *valid, int nthreads);
 
+/* PRM* roadmap construction, sequential (PRM.cpp:562-596): out [n][k_cap] neighbours / validity,
+ * cnt[n] neighbours per vertex */
+void oracle_prm_causal(const ompl_gpu_space *sp, const ompl_gpu_checker *ck, const double *states, size_t n,
+                       double k_const, uint32_t k_cap, uint32_t *nbr, uint32_t *cnt, uint8_t *valid);
+
 /* ---- the reference's input streams (oracle/rng.cpp) ------------------- */
 uint32_t oracle_mt19937_10000th(void);
 uint32_t oracle_ranlux24_base_10000th(void);

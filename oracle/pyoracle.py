@@ -41,6 +41,7 @@ _ORACLE_SIGS = {
     "oracle_gnat_size": (C.c_size_t, [C.c_void_p]),
     "oracle_gnat_knn": (None, [C.c_void_p, _D, C.c_size_t, C.c_uint32, _U32, _D, _U32, C.c_int]),
     "oracle_gnat_radius_count": (C.c_uint64, [C.c_void_p, _D, C.c_size_t, C.c_double, _U64, C.c_int]),
+    "oracle_prm_causal": (None, [_SP, _CK, _D, C.c_size_t, C.c_double, C.c_uint32, _U32, _U32, _U8]),
     "oracle_mt19937_10000th": (C.c_uint32, []),
     "oracle_ranlux24_base_10000th": (C.c_uint32, []),
     "oracle_seed_stream": (None, [C.c_uint32, C.c_size_t, _U32]),
@@ -155,6 +156,19 @@ def radius(sp, data, queries, r):
     lib.oracle_radius(C.byref(s), abi.dptr(d), d.shape[0], abi.dptr(q), nq, float(r), off.ctypes.data_as(_U64),
                       ids.ctypes.data_as(_U32), abi.dptr(dist), cnt.ctypes.data_as(_U64))
     return off, ids[:tot], dist[:tot]
+
+
+def prm_causal(sp, ck, states, k_const, k_cap):
+    """Sequential PRM* construction: (neighbours [n, k_cap], counts [n], validity [n, k_cap])."""
+    s, c = sp.to_abi(), ck.to_abi()
+    x = _arr(states).reshape(-1, sp.dim)
+    n = x.shape[0]
+    nbr = np.zeros((n, k_cap), np.uint32)
+    cnt = np.zeros(n, np.uint32)
+    val = np.zeros((n, k_cap), np.uint8)
+    lib.oracle_prm_causal(C.byref(s), C.byref(c), abi.dptr(x), n, float(k_const), int(k_cap),
+                          nbr.ctypes.data_as(_U32), cnt.ctypes.data_as(_U32), val.ctypes.data_as(_U8))
+    return nbr, cnt, val
 
 
 def seed_stream(seed, n):
