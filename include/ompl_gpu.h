@@ -287,6 +287,15 @@ ompl_gpu_status ompl_gpu_prm_add_milestones(ompl_gpu_nn *nn, ompl_gpu_mv *mv, co
                                             size_t j0, size_t j1, double k_const, uint32_t k_cap, uint32_t *d_nbr,
                                             uint32_t *d_cnt, uint8_t *d_valid, uint64_t *edges);
 
+/* LazyPRM::addMilestone (geometric/planners/prm/src/LazyPRM.cpp:285-309) with its star strategy
+ * (LazyPRM.cpp:238-239): the same neighbours as ompl_gpu_prm_add_milestones, but no edge is
+ * checked (validity stays unknown until a path search needs it); d_dist (may be NULL) receives each
+ * edge's weight, motionCost = distance(milestone, neighbour) under the path-length objective
+ * (LazyPRM.cpp:299), +inf past d_cnt[r].  Synchronous. */
+ompl_gpu_status ompl_gpu_lazyprm_add_milestones(ompl_gpu_nn *nn, const double *states, size_t m, size_t j0, size_t j1,
+                                                double k_const, uint32_t k_cap, uint32_t *d_nbr, uint32_t *d_cnt,
+                                                double *d_dist);
+
 /* ---- RRT growth on device ----------------------------------------------------
  * The RRT loop (RRT.cpp:128-192) without its goal test, for ns samples in order: nearest
  * stored state (:137), steer to max_distance (:141-146), mv's checkMotion(nearest,

@@ -96,6 +96,8 @@ SIGNATURES = {
     "ompl_gpu_rrt_grow_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, _P, _P]),
     "ompl_gpu_prm_add_milestones": (C.c_int, [_P, _P, _D, C.c_size_t, C.c_size_t, C.c_size_t, C.c_double, C.c_uint32,
                                               _P, _P, _P, _U64]),
+    "ompl_gpu_lazyprm_add_milestones": (C.c_int, [_P, _D, C.c_size_t, C.c_size_t, C.c_size_t, C.c_double, C.c_uint32,
+                                                  _P, _P, _P]),
     "ompl_gpu_mv_create": (C.c_int, [C.POINTER(_P), C.POINTER(SpaceStruct), C.POINTER(CheckerStruct), C.c_int]),
     "ompl_gpu_mv_destroy": (C.c_int, [_P]),
     "ompl_gpu_mv_set_stream": (C.c_int, [_P, _P]),

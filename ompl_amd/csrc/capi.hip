@@ -1274,18 +1274,12 @@ ompl_gpu_status ompl_gpu_mv_motion_states(ompl_gpu_mv *h, const double *s1, cons
 
 // ------------------------------------------------------------------------------ PRM*
 
-ompl_gpu_status ompl_gpu_prm_add_milestones(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *states, size_t m,
-                                            size_t j0, size_t j1, double k_const, uint32_t k_cap, uint32_t *d_nbr,
-                                            uint32_t *d_cnt, uint8_t *d_valid, uint64_t *edges) {
-    if (!h || !mv || (m && !states) || (j1 > j0 && (!d_nbr || !d_cnt || !d_valid)))
-        return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
-    if (j0 > j1 || j1 > m) return fail(OMPL_GPU_ERR_INVALID_ARG, "slice [j0, j1) outside the batch");
-    if (h->device != mv->device) return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles are on different devices");
-    if (h->sp.kind != mv->sp.kind || h->sp.dim != mv->sp.dim)
-        return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles describe different state spaces");
-    if (m > 0x7FFFFFFFull || k_cap == 0 || k_cap > (uint32_t)kMaxK)
-        return fail(OMPL_GPU_ERR_INVALID_ARG, "batch size or k_cap out of range (k_cap in [1, 64])");
-    std::scoped_lock lk(h->mu, mv->mu);
+namespace {
+// One causal batch (PRM::addMilestone / LazyPRM::addMilestone for m milestones); mv == NULL is
+// the lazy form (no edge is checked).  Caller holds the locks and validated the arguments.
+ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *states, size_t m, size_t j0,
+                                 size_t j1, double k_const, uint32_t k_cap, uint32_t *d_nbr, uint32_t *d_cnt,
+                                 uint8_t *d_valid, double *d_dist, uint64_t *edges) {
     if (edges) *edges = 0;
     if (m == 0) return OMPL_GPU_OK;
     HIP_OR_FAIL(hipSetDevice(h->device));
@@ -1361,7 +1355,8 @@ ompl_gpu_status ompl_gpu_prm_add_milestones(ompl_gpu_nn *h, ompl_gpu_mv *mv, con
                                                                 (const uint32_t *)ci, sii, (int)tot, (int)rows, off,
                                                                 off + 1, 0, 64, h->stream));
     }
-    HIP_OR_FAIL(launch_prm_take(sii, off, dkj + j0, (uint32_t)rows, k_cap, d_nbr, d_cnt, h->stream));
+    HIP_OR_FAIL(launch_prm_take(sii, sdd, off, dkj + j0, (uint32_t)rows, k_cap, d_nbr, d_cnt, d_dist, h->stream));
+    if (!mv) return add_locked(h, states, m, nullptr);  // lazy: edge validity stays unknown (LazyPRM.cpp:302)
     // 3. edges checkMotion(state[n], state[m]) (PRM.cpp:582): compact, check, scatter to [m][k_cap]
     HIP_OR_FAIL(h->prm_eoff.ensure(sizeof(uint64_t) * (rows + 1)));
     HIP_OR_FAIL(h->prm_cnt64.ensure(sizeof(uint64_t) * (rows + 1)));
@@ -1396,6 +1391,40 @@ ompl_gpu_status ompl_gpu_prm_add_milestones(ompl_gpu_nn *h, ompl_gpu_mv *mv, con
     if (edges) *edges = E;
     // 4. the milestones join the structure (PRM.cpp:593)
     return add_locked(h, states, m, nullptr);
+}
+
+ompl_gpu_status prm_check_args(ompl_gpu_nn *h, const double *states, size_t m, size_t j0, size_t j1, uint32_t k_cap) {
+    if (j0 > j1 || j1 > m) return fail(OMPL_GPU_ERR_INVALID_ARG, "slice [j0, j1) outside the batch");
+    if (m > 0x7FFFFFFFull || k_cap == 0 || k_cap > (uint32_t)kMaxK)
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "batch size or k_cap out of range (k_cap in [1, 64])");
+    (void)h;
+    (void)states;
+    return OMPL_GPU_OK;
+}
+}  // namespace
+
+ompl_gpu_status ompl_gpu_prm_add_milestones(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *states, size_t m,
+                                            size_t j0, size_t j1, double k_const, uint32_t k_cap, uint32_t *d_nbr,
+                                            uint32_t *d_cnt, uint8_t *d_valid, uint64_t *edges) {
+    if (!h || !mv || (m && !states) || (j1 > j0 && (!d_nbr || !d_cnt || !d_valid)))
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    ompl_gpu_status s = prm_check_args(h, states, m, j0, j1, k_cap);
+    if (s != OMPL_GPU_OK) return s;
+    if (h->device != mv->device) return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles are on different devices");
+    if (h->sp.kind != mv->sp.kind || h->sp.dim != mv->sp.dim)
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles describe different state spaces");
+    std::scoped_lock lk(h->mu, mv->mu);
+    return prm_batch_locked(h, mv, states, m, j0, j1, k_const, k_cap, d_nbr, d_cnt, d_valid, nullptr, edges);
+}
+
+ompl_gpu_status ompl_gpu_lazyprm_add_milestones(ompl_gpu_nn *h, const double *states, size_t m, size_t j0, size_t j1,
+                                                double k_const, uint32_t k_cap, uint32_t *d_nbr, uint32_t *d_cnt,
+                                                double *d_dist) {
+    if (!h || (m && !states) || (j1 > j0 && (!d_nbr || !d_cnt))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    ompl_gpu_status s = prm_check_args(h, states, m, j0, j1, k_cap);
+    if (s != OMPL_GPU_OK) return s;
+    std::lock_guard<std::mutex> lk(h->mu);
+    return prm_batch_locked(h, nullptr, states, m, j0, j1, k_const, k_cap, d_nbr, d_cnt, nullptr, d_dist, nullptr);
 }
 
 // ------------------------------------------------------------------------------ RRT

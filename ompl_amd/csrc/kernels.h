@@ -212,8 +212,9 @@ hipError_t launch_prm_causal(const DevSpace &sp, const FeatGeom &g, bool fill, c
                              uint32_t rows, uint32_t n0, const uint32_t *kj, const double *sd, const uint32_t *si,
                              uint32_t kq, uint64_t *seg_len, const uint64_t *seg_off, double *out_d, uint32_t *out_i,
                              hipStream_t st);
-hipError_t launch_prm_take(const uint32_t *sorted_i, const uint64_t *seg_off, const uint32_t *kj, uint32_t m,
-                           uint32_t k_cap, uint32_t *nbr, uint32_t *cnt, hipStream_t st);
+hipError_t launch_prm_take(const uint32_t *sorted_i, const double *sorted_d, const uint64_t *seg_off,
+                           const uint32_t *kj, uint32_t m, uint32_t k_cap, uint32_t *nbr, uint32_t *cnt, double *dist,
+                           hipStream_t st);
 hipError_t launch_prm_edges(const uint32_t *nbr, const uint32_t *cnt, const uint64_t *eoff, uint32_t m, uint32_t j0,
                             uint32_t k_cap, uint32_t n0, int dim, const double *stored_aos, int da, const double *braw,
                             double *s1, double *s2, hipStream_t st);

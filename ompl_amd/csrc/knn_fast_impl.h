@@ -14,9 +14,9 @@
 //          every (super-)tile whose box is farther than each lane's current K2-th
 //          distance (a lower bound: the SO3 part of an SE3 distance is >= 0);
 //        chunked (SO3): the whole store, split in chunks along grid.y.
-//      Inside a tile, for SE3 the translation part is computed first and the rotation
-//      (acos) only where sqrt(t) can still beat the K2-th distance: with spatially
-//      ordered queries that branch is coherent across the wave.
+//      Inside a tile, for SE3 the chord bound fma(w1, c, w0 |t|) (c <= theta) is tested
+//      first and the angle polynomial evaluated only when some lane of the wave can still
+//      beat the K2-th distance.
 //   3. certify (fp64): merge the lists, recompute the K2 candidates exactly in the
 //      reference's operation order, keep the k best by (distance, id), and prove that no
 //      element outside the list can enter: |d32 - d64| <= e for every element, so if the
@@ -33,7 +33,8 @@
 //                       |p|^2 = 1 + eta_p, |q|^2 = 1 + eta_q the two differ by at most
 //                       2.25 sqrt(|eta_p + eta_q| / 2) (acos is 1/2-Hoelder with constant pi/sqrt 2);
 //                       + 4.5e-5 (the reference returns 0 for |dot| > 1 - 1e-9,
-//                       SO3StateSpace.cpp:258-260) + 2e-6 (fp32 evaluation, acos01's 2e-8)
+//                       SO3StateSpace.cpp:258-260) + 2e-6 (fp32 evaluation; chord_theta's
+//                       polynomial <= 1.1e-7, with its fp32 evaluation <= 1.8e-7)
 //   SO3 rotation      : 1.1 sqrt(2 * 6u) + 1e-6 + 4.5e-5 (the chunked screen keeps acos(|dot|))
 #pragma once
 // Included by one translation unit per space (knn_fast_{se3,so3,rv}.hip) so that the
@@ -302,7 +303,9 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-__device__ __forceinline__ float chord_angle(const float *p, const float *q) {
+// squared chord c^2 = min(|p - q|^2, |p + q|^2) of two quaternions, both sums on packed fp32
+// (one v_pk_add / v_pk_fma per component gives both)
+__device__ __forceinline__ float chord2(const float *p, const float *q) {
     f2 a = f2{p[0], p[0]} + f2{-q[0], q[0]};
     f2 c2 = a * a;
     a = f2{p[1], p[1]} + f2{-q[1], q[1]};
@@ -311,8 +314,27 @@ __device__ __forceinline__ float chord_angle(const float *p, const float *q) {
     c2 = pk_fma(a, a, c2);
     a = f2{p[3], p[3]} + f2{-q[3], q[3]};
     c2 = pk_fma(a, a, c2);
-    const float h = 0.5f * __builtin_amdgcn_sqrtf(fminf(c2.x, c2.y));  // c / 2 in [0, 0.7072]
-    return fmaf(-2.f, acos01(h), 3.14159265358979f);                    // 2 asin(c / 2)
+    return fminf(c2.x, c2.y);
+}
+
+// theta = 2 asin(c / 2) from the chord c and c^2: theta = c (1 + x R(x)), x = c^2 / 4 in
+// [0, 0.5], R a degree-5 fit of (asin(h) / h - 1) / h^2 (|error on theta| <= 1.1e-7, fp32
+// evaluation <= 1.8e-7 over the whole range; tools/fit_asin.py).  x R(x) >= 0, so the fp32
+// result is never below c: c is a lower bound of the screened angle, bit for bit.
+__device__ __forceinline__ float chord_theta(float c, float c2) {
+    const float x = 0.25f * c2;
+    float r = 0.11142297f;
+    r = fmaf(r, x, -0.07120271f);
+    r = fmaf(r, x, 0.070305005f);
+    r = fmaf(r, x, 0.036311187f);
+    r = fmaf(r, x, 0.07580938f);
+    r = fmaf(r, x, 0.16663891f);
+    return fmaf(c, x * r, c);
+}
+
+__device__ __forceinline__ float chord_angle(const float *p, const float *q) {
+    const float c2 = chord2(p, q);
+    return chord_theta(__builtin_amdgcn_sqrtf(c2), c2);
 }
 
 // Rotation pre-reject threshold: an element with |dot| <= cos(tau/w1 + 1e-5) has
@@ -350,7 +372,7 @@ __device__ __forceinline__ void screen_tile(const float *tile, const float *qf, 
                 if (v[u] * w0sq < top.tau2) {  // the translation term alone loses: skip the rotation
                     const float4 r = t4[(j0 + u) * 2 + 1];
                     const float p[4] = {r.x, r.y, r.z, r.w};
-                    const float d = w0 * __builtin_amdgcn_sqrtf(v[u]) + w1 * chord_angle(p, qf + 4);
+                    const float d = fmaf(w1, chord_angle(p, qf + 4), w0 * __builtin_amdgcn_sqrtf(v[u]));
                     const uint32_t id = id_of(j0 + u);
                     if (top.admits(d, id)) top.push(d, id);
                 }
@@ -522,7 +544,7 @@ __device__ __forceinline__ float state_dist32(const float *x, const float *q, fl
         float t = dx * dx;
         t = fmaf(dy, dy, t);
         t = fmaf(dz, dz, t);
-        return w0 * __builtin_amdgcn_sqrtf(t) + w1 * chord_angle(x + 3, q + 4);
+        return fmaf(w1, chord_angle(x + 3, q + 4), w0 * __builtin_amdgcn_sqrtf(t));
     } else {
         float acc = 0.f;
 #pragma unroll
@@ -734,7 +756,22 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         for (int g = 0; g < G; ++g) {
             if (!(readlane_f(lb[g % GH], tin + (g < GH ? 0 : 32)) < td[g])) continue;
             ++qscans;
-            offer(g, state_dist32<SP, F>(x, qscan(g), w0, w1), id);
+            if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+                // screened d = fma(w1, theta, w0 |t|) with theta >= c: when no lane's chord
+                // bound fma(w1, c, w0 |t|) is below the threshold, no lane's d is either, and
+                // the angle polynomial is skipped for the whole wave
+                const float *qq = qscan(g);
+                const float dx = x[0] - qq[0], dy = x[1] - qq[1], dz = x[2] - qq[2];
+                float t = dx * dx;
+                t = fmaf(dy, dy, t);
+                t = fmaf(dz, dz, t);
+                const float c2 = chord2(x + 3, qq + 4);
+                const float c = __builtin_amdgcn_sqrtf(c2), wt = w0 * __builtin_amdgcn_sqrtf(t);
+                if (!__ballot(fmaf(w1, c, wt) < td[g])) continue;
+                offer(g, fmaf(w1, chord_theta(c, c2), wt), id);
+            } else {
+                offer(g, state_dist32<SP, F>(x, qscan(g), w0, w1), id);
+            }
         }
     };
     // start at the super-tile holding the group's middle query on the Morton curve
@@ -1263,7 +1300,19 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
                 for (int g = 0; g < G; ++g) {
                     if (!(readlane_f(lb[g % GH], t + (g < GH ? 0 : 32)) <= thr[g])) continue;
                     ++qscans;
-                    bool hit = state_dist32<SP, F>(x, &qrow[g * FS], w0, w1) <= thr[g];  // NaN never hits
+                    bool hit;  // NaN never hits
+                    if constexpr (SP == OMPL_GPU_SPACE_SE3) {  // chord bound first, as in the kNN walk
+                        const float *qq = &qrow[g * FS];
+                        const float dx = x[0] - qq[0], dy = x[1] - qq[1], dz = x[2] - qq[2];
+                        float tt = dx * dx;
+                        tt = fmaf(dy, dy, tt);
+                        tt = fmaf(dz, dz, tt);
+                        const float c2 = chord2(x + 3, qq + 4);
+                        const float c = __builtin_amdgcn_sqrtf(c2), wt = w0 * __builtin_amdgcn_sqrtf(tt);
+                        hit = __ballot(fmaf(w1, c, wt) <= thr[g]) && fmaf(w1, chord_theta(c, c2), wt) <= thr[g];
+                    } else {
+                        hit = state_dist32<SP, F>(x, &qrow[g * FS], w0, w1) <= thr[g];
+                    }
                     double dd = 0.0;
                     if (hit) {  // exact decision from the sorted fp64 row (coalesced over the tile)
                         constexpr int FA = (F + 3) & ~3;

@@ -87,15 +87,17 @@ __global__ __launch_bounds__(256) void prm_causal_kernel(const double *__restric
 }
 
 // thread per (milestone, rank): the first min(k_j, segment) sorted entries
-__global__ void prm_take_kernel(const uint32_t *__restrict__ sorted_i, const uint64_t *__restrict__ seg_off,
-                                const uint32_t *__restrict__ kj_arr, uint32_t m, uint32_t k_cap,
-                                uint32_t *__restrict__ nbr, uint32_t *__restrict__ cnt) {  // kj_arr: this slice
+__global__ void prm_take_kernel(const uint32_t *__restrict__ sorted_i, const double *__restrict__ sorted_d,
+                                const uint64_t *__restrict__ seg_off, const uint32_t *__restrict__ kj_arr, uint32_t m,
+                                uint32_t k_cap, uint32_t *__restrict__ nbr, uint32_t *__restrict__ cnt,
+                                double *__restrict__ dist) {  // kj_arr: this slice; dist may be NULL
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (uint64_t)m * k_cap) return;
     const uint32_t j = (uint32_t)(t / k_cap), r = (uint32_t)(t % k_cap);
     const uint64_t len = seg_off[j + 1] - seg_off[j];
     const uint32_t c = (uint32_t)min((uint64_t)kj_arr[j], len);
     nbr[t] = r < c ? sorted_i[seg_off[j] + r] : kNoId;
+    if (dist) dist[t] = r < c ? sorted_d[seg_off[j] + r] : __builtin_inf();
     if (r == 0) cnt[j] = c;
 }
 
@@ -169,12 +171,13 @@ hipError_t launch_prm_causal(const DevSpace &sp, const FeatGeom &g, bool fill, c
                             st)
 }
 
-hipError_t launch_prm_take(const uint32_t *sorted_i, const uint64_t *seg_off, const uint32_t *kj, uint32_t m,
-                           uint32_t k_cap, uint32_t *nbr, uint32_t *cnt, hipStream_t st) {
+hipError_t launch_prm_take(const uint32_t *sorted_i, const double *sorted_d, const uint64_t *seg_off,
+                           const uint32_t *kj, uint32_t m, uint32_t k_cap, uint32_t *nbr, uint32_t *cnt, double *dist,
+                           hipStream_t st) {
     const uint64_t n = (uint64_t)m * k_cap;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(prm_take_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sorted_i, seg_off, kj, m,
-                       k_cap, nbr, cnt);
+    hipLaunchKernelGGL(prm_take_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sorted_i, sorted_d, seg_off,
+                       kj, m, k_cap, nbr, cnt, dist);
     return hipGetLastError();
 }
 

@@ -240,6 +240,26 @@ class NearestNeighborsGPU:
         return (nbr[:r].cpu().numpy().view(np.uint32), cnt[:r].cpu().numpy().view(np.uint32),
                 val[:r].cpu().numpy().astype(bool), e.value)
 
+    def lazyprm_add_milestones(self, states, k_const: float, k_cap: int, j0: int = 0, j1: int | None = None):
+        """LazyPRM::addMilestone for a batch (LazyPRM.cpp:285-309): the PRM* neighbours, no edge
+        checked; returns (neighbours [r, k_cap], counts [r], edge weights = distances [r, k_cap])."""
+        import torch
+
+        x = abi.as_states(states, self.dim)
+        m = x.shape[0]
+        j1 = m if j1 is None else j1
+        r = j1 - j0
+        dev = torch.device("cuda", self.device)
+        nbr = torch.empty((max(r, 1), k_cap), dtype=torch.int32, device=dev)
+        cnt = torch.empty(max(r, 1), dtype=torch.int32, device=dev)
+        dist = torch.empty((max(r, 1), k_cap), dtype=torch.float64, device=dev)
+        abi.check(abi.lib.ompl_gpu_lazyprm_add_milestones(self._h, abi.dptr(x), m, int(j0), int(j1), float(k_const),
+                                                          int(k_cap), C.c_void_p(nbr.data_ptr()),
+                                                          C.c_void_p(cnt.data_ptr()), C.c_void_p(dist.data_ptr())))
+        torch.cuda.synchronize(dev)
+        return (nbr[:r].cpu().numpy().view(np.uint32), cnt[:r].cpu().numpy().view(np.uint32),
+                dist[:r].cpu().numpy())
+
     def prm_add_milestones_device(self, mv, states, k_const: float, k_cap: int, d_nbr: int, d_cnt: int,
                                   d_valid: int, j0: int = 0, j1: int | None = None) -> int:
         """The same into caller-owned device buffers ((j1 - j0) rows); returns the number of edges checked."""

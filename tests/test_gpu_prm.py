@@ -97,3 +97,26 @@ def test_prm_star_rank_slices(gpu):
     np.testing.assert_array_equal(np.concatenate(got_n), on)
     np.testing.assert_array_equal(np.concatenate(got_v), ov.astype(bool))
     assert reps[0][0].size() == reps[1][0].size() == len(states)
+
+
+def test_lazy_prm_star_neighbours_and_weights(gpu):
+    """LazyPRM::addMilestone (LazyPRM.cpp:285-309): the same causal neighbours, no motion check,
+    edge weights = distance(milestone, neighbour) equal to the oracle metric."""
+    sp = KinematicChainSpace(12, 1.0 / 12)
+    ck = KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))
+    states, _ = W.reference_valid_states(sp, 900, lambda x: O.is_valid(sp, ck, x), seed=11, chunk=5000)
+    kc = math.e + math.e / sp.getDimension()
+    k_cap = max(1, int(math.ceil(kc * math.log(len(states)))))
+    nn = NearestNeighborsGPU(sp, gpu)
+    got = [nn.lazyprm_add_milestones(states[a:b], kc, k_cap) for a, b in ((0, 300), (300, 900))]
+    gn = np.concatenate([g[0] for g in got])
+    gc = np.concatenate([g[1] for g in got])
+    gd = np.concatenate([g[2] for g in got])
+    on, oc, _ = O.prm_causal(sp, ck, states, kc, k_cap)
+    np.testing.assert_array_equal(gc, oc)
+    np.testing.assert_array_equal(gn, on)
+    for i in range(len(states)):
+        for r in range(gc[i]):
+            assert gd[i, r] == O.distance(sp, states[i], states[gn[i, r]])
+        assert np.all(np.isinf(gd[i, gc[i]:]))
+    assert nn.size() == len(states)
