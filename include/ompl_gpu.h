@@ -308,6 +308,17 @@ ompl_gpu_status ompl_gpu_lazyprm_add_milestones(ompl_gpu_nn *nn, const double *s
  * synchronous on return. */
 ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
                                          double max_distance, uint32_t *d_nearest, uint32_t *d_added);
+/* The same loop with RRT's goal test (RRT.cpp:175-187): after each added state,
+ * GoalRegion::isSatisfied — distance(state, goal) < goal_threshold (GoalRegion.cpp:52-58; the
+ * threshold of ProblemDefinition::setStartAndGoalStates defaults to DBL_EPSILON) — ends the run:
+ * *solved_at = that iteration (~0 if none), the samples after it are not processed (their
+ * d_nearest / d_added are 0xFFFFFFFF).  Otherwise the added state strictly closest to the goal
+ * is the approximate solution: *approx_id / *approx_dist (0xFFFFFFFF / +inf if nothing was
+ * added).  goal: host, dim reals.  Output pointers may be NULL. */
+ompl_gpu_status ompl_gpu_rrt_solve_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
+                                          double max_distance, const double *goal, double goal_threshold,
+                                          uint32_t *d_nearest, uint32_t *d_added, uint64_t *solved_at,
+                                          uint32_t *approx_id, double *approx_dist);
 
 /* ---- the reference's input streams (host) ------------------------------------
  * ompl::RNG restated on the same standard-library engines (std::ranlux24_base seed generator,
@@ -318,6 +329,10 @@ ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const
 void ompl_gpu_rng_set_seed(uint32_t seed);
 uint32_t ompl_gpu_rng_get_seed(void);
 uint64_t ompl_gpu_rng_seeds_drawn(void); /* seeds handed out so far (observability) */
+/* the seed an RNG() constructed now would take (RandomNumbers.cpp:218-223): draws it from the
+ * generator — for mirroring the construction of an RNG that lives outside this library (a
+ * planner's rng_, a GNAT's pivot selector) in the reference's order */
+uint32_t ompl_gpu_rng_next_seed(void);
 /* n x RNG(local_seed).uniformReal(low, high): an explicitly seeded RNG (RandomNumbers.cpp:225-228),
  * which draws nothing from the seed generator */
 ompl_gpu_status ompl_gpu_rng_uniform_real(uint32_t local_seed, size_t n, double low, double high, double *out);

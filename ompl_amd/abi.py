@@ -94,6 +94,8 @@ SIGNATURES = {
     "ompl_gpu_nn_radius_cull_stats": (C.c_int, [_P, _U64, _U64]),
     "ompl_gpu_nn_edges_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P, C.c_uint32, C.c_size_t, C.c_int, _P, _P]),
     "ompl_gpu_rrt_grow_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, _P, _P]),
+    "ompl_gpu_rrt_solve_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, _D, C.c_double, _P, _P, _U64,
+                                            _U32, _D]),
     "ompl_gpu_prm_add_milestones": (C.c_int, [_P, _P, _D, C.c_size_t, C.c_size_t, C.c_size_t, C.c_double, C.c_uint32,
                                               _P, _P, _P, _U64]),
     "ompl_gpu_lazyprm_add_milestones": (C.c_int, [_P, _D, C.c_size_t, C.c_size_t, C.c_size_t, C.c_double, C.c_uint32,
@@ -114,6 +116,7 @@ SIGNATURES = {
     "ompl_gpu_rng_set_seed": (None, [C.c_uint32]),
     "ompl_gpu_rng_get_seed": (C.c_uint32, []),
     "ompl_gpu_rng_seeds_drawn": (C.c_uint64, []),
+    "ompl_gpu_rng_next_seed": (C.c_uint32, []),
     "ompl_gpu_rng_uniform_real": (C.c_int, [C.c_uint32, C.c_size_t, C.c_double, C.c_double, _D]),
     "ompl_gpu_sampler_create": (C.c_int, [C.POINTER(_P), C.POINTER(SpaceStruct), _D, _D]),
     "ompl_gpu_sampler_destroy": (C.c_int, [_P]),

@@ -103,7 +103,10 @@ struct ompl_gpu_nn {
         fb_i, fb_c, fb_cd, fb_ci, slab_i, slab_d;
     uint32_t radius_slab = 64;      // per-query slab of the one-pass radius walk (adapts upward)
     uint64_t radius_one_pass = 0;   // radius calls answered by the one-pass walk
-    DevBuf rrt_n, rrt_pd, rrt_pi;  // device RRT growth: live size, per-block partial minima
+    DevBuf rrt_n, rrt_pd, rrt_pi;  // device RRT growth: live size + barrier words, per-block partial minima
+    int rrt_coop = -1;             // persistent RRT grid size (0: two-launch form), found on first use
+    void *rrt_sync = nullptr;      // its uncached synchronisation record
+    DevBuf rrt_goal;               // goal record + goal reals of ompl_gpu_rrt_solve_device
     DevBuf prm_bf, prm_raw, prm_kj, prm_sd, prm_si, prm_len, prm_off, prm_eoff, prm_cnt64;  // PRM* batches
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
@@ -252,6 +255,7 @@ ompl_gpu_status ompl_gpu_nn_destroy(ompl_gpu_nn *h) {
     if (h->feat) (void)hipFree(h->feat);
     if (h->feat32) (void)hipFree(h->feat32);
     if (h->live) (void)hipFree(h->live);
+    if (h->rrt_sync) (void)hipFree(h->rrt_sync);
     free_sorted_store(&h->sorted);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
@@ -1429,8 +1433,10 @@ ompl_gpu_status ompl_gpu_lazyprm_add_milestones(ompl_gpu_nn *h, const double *st
 
 // ------------------------------------------------------------------------------ RRT
 
-ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
-                                         double max_distance, uint32_t *d_nearest, uint32_t *d_added) {
+namespace {
+ompl_gpu_status rrt_run(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples, size_t ns, double max_distance,
+                        const double *goal, double goal_threshold, uint32_t *d_nearest, uint32_t *d_added,
+                        uint64_t *solved_at, uint32_t *approx_id, double *approx_dist) {
     if (!h || !mv || (ns && (!d_samples || !d_nearest || !d_added))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
     if (h->device != mv->device) return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles are on different devices");
     if (h->sp.kind != mv->sp.kind || h->sp.dim != mv->sp.dim)
@@ -1439,6 +1445,9 @@ ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const 
         return fail(OMPL_GPU_ERR_UNSUPPORTED, "device RRT growth needs a space whose stored features are its reals");
     if (!(max_distance > 0.0)) return fail(OMPL_GPU_ERR_INVALID_ARG, "max_distance must be positive");
     std::scoped_lock lk(h->mu, mv->mu);
+    if (solved_at) *solved_at = ~0ull;
+    if (approx_id) *approx_id = kNoId;
+    if (approx_dist) *approx_dist = std::numeric_limits<double>::infinity();
     if (ns == 0) return OMPL_GPU_OK;
     if (ns > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many samples in one call");
     if (h->n_live == 0) return fail(OMPL_GPU_ERR_EMPTY, "No elements found in nearest neighbors data structure");
@@ -1457,6 +1466,25 @@ ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const 
     HIP_OR_FAIL(h->rrt_pi.ensure(sizeof(uint32_t) * parts));
     const uint64_t n0 = h->n_total;
     HIP_OR_FAIL(hipMemcpyAsync(h->rrt_n.p, &n0, sizeof(uint64_t), hipMemcpyHostToDevice, h->stream));
+    if (h->rrt_coop < 0) {
+        h->rrt_coop = (int)rrt_coop_blocks(h->device, h->sp, h->g);
+        if (h->rrt_coop > 0 && hipExtMallocWithFlags(&h->rrt_sync, rrt_sync_bytes(), hipDeviceMallocUncached) != hipSuccess) {
+            (void)hipGetLastError();
+            h->rrt_sync = nullptr;
+            h->rrt_coop = 0;  // no uncached memory: the two-launch form
+        }
+    }
+    if (h->rrt_sync) HIP_OR_FAIL(hipMemsetAsync(h->rrt_sync, 0, rrt_sync_bytes(), h->stream));
+    // goal record {solved iteration, approximate distance, its id} and the goal's reals
+    const uint64_t grec0[3] = {~0ull, 0x7FF0000000000000ull, (uint64_t)kNoId};
+    HIP_OR_FAIL(h->rrt_goal.ensure(sizeof(uint64_t) * 3 + sizeof(double) * dim));
+    uint64_t *grec = (uint64_t *)h->rrt_goal.p;
+    double *dgoal = (double *)(grec + 3);
+    HIP_OR_FAIL(hipMemcpyAsync(grec, grec0, sizeof(grec0), hipMemcpyHostToDevice, h->stream));
+    if (h->rrt_sync)  // the persistent form keeps the record in the uncached words [24, 27)
+        HIP_OR_FAIL(hipMemcpyAsync((uint64_t *)h->rrt_sync + 24, grec0, sizeof(grec0), hipMemcpyHostToDevice,
+                                   h->stream));
+    if (goal) HIP_OR_FAIL(hipMemcpyAsync(dgoal, goal, sizeof(double) * dim, hipMemcpyHostToDevice, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     const int nb = tracked_dims(h->sp);
     const int na = h->sp.kind == OMPL_GPU_SPACE_SE3 ? 3 : (h->sp.kind == OMPL_GPU_SPACE_SO3 ? 0 : dim);
@@ -1472,15 +1500,48 @@ ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const 
     if (h->sp.kind == OMPL_GPU_SPACE_SE3) h->qeta = std::max(h->qeta, 1e-12);
     HIP_OR_FAIL(launch_rrt_grow(h->sp, mv->sp, mv->ck, h->g, h->feat, h->feat32, h->rows32, h->cap, n0,
                                 (uint64_t *)h->rrt_n.p, d_samples, (uint32_t)ns, max_distance, (double *)h->rrt_pd.p,
-                                (uint32_t *)h->rrt_pi.p, d_nearest, d_added, mv->counters, h->stream));
+                                (uint32_t *)h->rrt_pi.p, d_nearest, d_added, mv->counters, (uint64_t *)h->rrt_sync,
+                                (uint32_t)h->rrt_coop, goal ? dgoal : nullptr, goal_threshold, grec, h->stream));
+    uint64_t grec_h[3] = {~0ull, 0, kNoId};
+    HIP_OR_FAIL(hipMemcpyAsync(grec_h, grec, sizeof(grec_h), hipMemcpyDeviceToHost, h->stream));
     uint64_t n1 = n0;
+    uint64_t bar_h[3] = {0, 0, 0};
+    if (h->rrt_sync) HIP_OR_FAIL(hipMemcpyAsync(bar_h, h->rrt_sync, sizeof(bar_h), hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(&n1, h->rrt_n.p, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (bar_h[2]) return fail(OMPL_GPU_ERR_DEVICE, "persistent RRT grid barrier timed out (grid not co-resident)");
+    if (goal && grec_h[0] != ~0ull && grec_h[0] + 1 < ns) {  // iterations after the solution did not run
+        HIP_OR_FAIL(hipMemsetAsync(d_nearest + grec_h[0] + 1, 0xFF, sizeof(uint32_t) * (ns - grec_h[0] - 1), h->stream));
+        HIP_OR_FAIL(hipMemsetAsync(d_added + grec_h[0] + 1, 0xFF, sizeof(uint32_t) * (ns - grec_h[0] - 1), h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    }
+    if (solved_at) *solved_at = grec_h[0];
+    if (approx_id) *approx_id = (uint32_t)grec_h[2];
+    if (approx_dist) {
+        double d;
+        std::memcpy(&d, &grec_h[1], sizeof(d));
+        *approx_dist = d;
+    }
     if (n1 > n0) HIP_OR_FAIL(hipMemsetAsync(h->live + n0, 1, n1 - n0, h->stream));
     h->n_live += n1 - n0;
     h->n_total = n1;
     h->removed.resize(h->n_total, 0);
     return OMPL_GPU_OK;
+}
+}  // namespace
+
+ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
+                                         double max_distance, uint32_t *d_nearest, uint32_t *d_added) {
+    return rrt_run(h, mv, d_samples, ns, max_distance, nullptr, 0.0, d_nearest, d_added, nullptr, nullptr, nullptr);
+}
+
+ompl_gpu_status ompl_gpu_rrt_solve_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
+                                          double max_distance, const double *goal, double goal_threshold,
+                                          uint32_t *d_nearest, uint32_t *d_added, uint64_t *solved_at,
+                                          uint32_t *approx_id, double *approx_dist) {
+    if (!goal) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL goal");
+    return rrt_run(h, mv, d_samples, ns, max_distance, goal, goal_threshold, d_nearest, d_added, solved_at, approx_id,
+                   approx_dist);
 }
 
 }  // extern "C"

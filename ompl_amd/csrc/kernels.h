@@ -224,10 +224,19 @@ hipError_t launch_prm_scatter_valid(const uint8_t *vc, const uint32_t *cnt, cons
 
 // ---- RRT growth on device (rrt.hip) -------------------------------------------------------
 size_t rrt_part_entries(uint64_t n_max);
+// blocks of the persistent (cooperative) RRT grid on this device, 0 when cooperative launches
+// are unavailable (the two-launch form is used then); its synchronisation record (uncached
+// device memory, zeroed before each launch) holds rrt_sync_bytes()
+size_t rrt_sync_bytes();
+uint32_t rrt_coop_blocks(int device, const DevSpace &sp, const FeatGeom &g);
 hipError_t launch_rrt_grow(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck, const FeatGeom &g,
                            double *feat, float *feat32, int rows32, uint64_t cap, uint64_t n0, uint64_t *n_dev,
                            const double *samples, uint32_t ns, double maxd, double *part_d, uint32_t *part_i,
-                           uint32_t *nearest, uint32_t *added, unsigned long long *counters, hipStream_t st);
+                           uint32_t *nearest, uint32_t *added, unsigned long long *counters, uint64_t *sync,
+                           uint32_t coop_blocks, const double *goal, double goal_threshold, uint64_t *grec,
+                           hipStream_t st);
+// goal record of a run (64-bit words, zero-initialised by the host as {~0, +inf bits, ~0})
+size_t rrt_goal_words();
 
 // radius search, pass 1 (count per (query, chunk)) and pass 2 (fill CSR in id order).
 struct RadiusPlan {

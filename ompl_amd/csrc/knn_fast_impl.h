@@ -499,7 +499,11 @@ __global__ __launch_bounds__(256) void knn32_screen_kernel(const float *__restri
 // insertion is one shift by a lane.  Tiles and super-tiles whose box is farther than every
 // query's current K2-th distance are skipped; the box bound covers the whole metric.
 
-// lower bound of the fp32 distance from query row q (FS layout) to any state inside box bx
+// lower bound of the fp32 distance from query row q (FS layout) to any state inside box bx.
+// (A packed-fp32 form of the gaps — v_pk_add pairs — measured no faster for the kNN walk and
+// 20% slower for the radius walk, whose register allocation it upsets.)
+__device__ __forceinline__ float gap(float a, float b) { return fmaxf(fmaxf(a, b), 0.f); }
+
 template <int SP, int F>
 __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w0, float w1) {
     constexpr int NB = Geo<SP, F>::NB;
@@ -507,7 +511,7 @@ __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w
         float tg = 0.f;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const float g = fmaxf(fmaxf(bx[c] - q[c], q[c] - bx[NB + c]), 0.f);
+            const float g = gap(bx[c] - q[c], q[c] - bx[NB + c]);
             tg = fmaf(g, g, tg);
         }
         // rotation: the screened 2 asin(c / 2) >= c = min(|p - q|, |p + q|) >= the distance
@@ -516,8 +520,8 @@ __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const float lo = bx[3 + c], hi = bx[NB + 3 + c], v = q[4 + c];
-            const float gp = fmaxf(fmaxf(lo - v, v - hi), 0.f);
-            const float gm = fmaxf(fmaxf(lo + v, -v - hi), 0.f);
+            const float gp = gap(lo - v, v - hi);
+            const float gm = gap(lo + v, -v - hi);
             rp = fmaf(gp, gp, rp);
             rm = fmaf(gm, gm, rm);
         }
@@ -526,7 +530,7 @@ __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w
         float acc = 0.f;
 #pragma unroll
         for (int c = 0; c < F; ++c) {
-            const float g = fmaxf(fmaxf(bx[c] - q[c], q[c] - bx[F + c]), 0.f);
+            const float g = gap(bx[c] - q[c], q[c] - bx[F + c]);
             acc = fmaf(g, g, acc);
         }
         return __builtin_amdgcn_sqrtf(acc);

@@ -16,6 +16,8 @@
 // features are then its reals, exactly as ompl_gpu_nn_add would store them.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "feat_dist.h"
 #include "kernels.h"
 #include "topk.h"
@@ -26,16 +28,19 @@ namespace {
 
 constexpr int kRrtItems = 4;                      // states per lane of the scan
 constexpr int kRrtBlockStates = 256 * kRrtItems;  // states per scan block
+constexpr uint32_t kRrtMaxCoopBlocks = 512;       // persistent grid: at most 2 blocks per CU
 
 template <int SP, int F>
 __global__ __launch_bounds__(256) void rrt_scan_kernel(const double *__restrict__ feat, uint64_t cap,
                                                        const uint64_t *__restrict__ n_dev,
                                                        const double *__restrict__ sample, DevSpace sp,
-                                                       double *__restrict__ part_d, uint32_t *__restrict__ part_i) {
+                                                       double *__restrict__ part_d, uint32_t *__restrict__ part_i,
+                                                       const uint64_t *__restrict__ done) {
     __shared__ double lds_d[4];
     __shared__ uint32_t lds_i[4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t n = *n_dev;
+    if (done && *done != ~0ull) return;  // solved earlier in the run: nothing left to do
     double qf[F];
 #pragma unroll
     for (int f = 0; f < F; ++f) qf[f] = f < sp.dim ? sample[f] : 0.0;
@@ -63,36 +68,24 @@ __global__ __launch_bounds__(256) void rrt_scan_kernel(const double *__restrict_
     }
 }
 
-template <int F>
-__global__ __launch_bounds__(256) void rrt_step_kernel(double *__restrict__ feat, float *__restrict__ feat32,
-                                                       int rows32, uint64_t cap, uint64_t *__restrict__ n_dev,
-                                                       const double *__restrict__ sample,
-                                                       const double *__restrict__ part_d,
-                                                       const uint32_t *__restrict__ part_i, uint32_t nparts,
-                                                       DevSpace sp, DevSpace msp, DevChecker ck, double maxd,
-                                                       uint32_t *__restrict__ nearest_out,
-                                                       uint32_t *__restrict__ added_out,
-                                                       unsigned long long *__restrict__ counters) {
-    __shared__ double lds_d[4];
-    __shared__ uint32_t lds_i[4];
-    __shared__ double s1[kChainMaxLinks], s2[kChainMaxLinks];
-    __shared__ int sh_nd, sh_bad, sh_ok;
-    TopK<1> top;
-    top.init();
-    for (uint32_t j = threadIdx.x; j < nparts; j += blockDim.x) top.offer(part_d[j], part_i[j]);
-    double rd;
-    uint32_t ri;
-    block_select<1>(top, lds_d, lds_i, rd, ri);
+// sample's nearest stored state ri (kNoId: none): steer to max_distance (RRT.cpp:141-146) and
+// check the motion with the whole block — the bit of DiscreteMotionValidator::checkMotion
+// (DiscreteMotionValidator.cpp:93-145) is the AND over s2 and the samples j / nd, whatever order
+// they are tested in.  Leaves s1 / s2 (the motion), *sh_ok (a neighbour exists) and *sh_bad (some
+// sample invalid) in LDS for every thread.
+template <class RowOf>
+__device__ void rrt_decide(RowOf row_of, const double *__restrict__ sample, uint32_t ri, const DevSpace &sp,
+                           const DevSpace &msp, const DevChecker &ck, double maxd, double *s1, double *s2, int *sh_nd,
+                           int *sh_bad, int *sh_ok) {
     const int dim = sp.dim;
     if (threadIdx.x == 0) {
-        sh_ok = ri != kNoId;
-        sh_bad = 0;
-        sh_nd = 0;
-        *nearest_out = ri;
-        if (sh_ok) {
+        *sh_ok = ri != kNoId;
+        *sh_bad = 0;
+        *sh_nd = 0;
+        if (ri != kNoId) {
             double a[kChainMaxLinks], b[kChainMaxLinks], o[kChainMaxLinks];
             for (int c = 0; c < dim; ++c) {
-                a[c] = feat[(uint64_t)c * cap + ri];
+                a[c] = row_of(c);
                 b[c] = sample[c];
             }
             const double d = raw_distance(sp, a, b);  // si_->distance(nmotion->state, rstate)  RRT.cpp:141
@@ -105,13 +98,13 @@ __global__ __launch_bounds__(256) void rrt_step_kernel(double *__restrict__ feat
                 s1[c] = a[c];
                 s2[c] = o[c];
             }
-            sh_nd = (int)valid_segment_count(msp, a, o);
+            *sh_nd = (int)valid_segment_count(msp, a, o);
         }
     }
     __syncthreads();
-    if (sh_ok) {
+    if (*sh_ok) {
         // sample 0 stands for s2 (DiscreteMotionValidator.cpp:96), samples j in [1, nd-1] for j/nd
-        const int nd = sh_nd;
+        const int nd = *sh_nd;
         const int ns = nd > 1 ? nd : 1;
         for (int j = threadIdx.x; j < ns; j += blockDim.x) {
             double t[kChainMaxLinks];
@@ -120,21 +113,246 @@ __global__ __launch_bounds__(256) void rrt_step_kernel(double *__restrict__ feat
             } else {
                 interpolate(msp, s1, s2, (double)j / (double)nd, t);
             }
-            if (!is_valid(msp, ck, t)) sh_bad = 1;
+            if (!is_valid(msp, ck, t)) *sh_bad = 1;
         }
     }
     __syncthreads();
+}
+
+// Goal test of RRT.cpp:175-187 after each added state: GoalRegion::isSatisfied (distance to the
+// goal < threshold, GoalRegion.cpp:52-58) ends the run at that iteration; otherwise the state
+// becomes the approximate solution when strictly closer than every earlier one.
+struct RrtGoal {
+    const double *goal;  // device, dim reals; nullptr: no goal test (the growth form)
+    double threshold;
+};
+// device record of the run (rrt_goal_words 64-bit words): [0] iteration that solved
+// (~0: none), [1] approximate-solution distance bits (+inf initially), [2] its id
+constexpr int kGoalWords = 3;
+
+__device__ __forceinline__ bool rrt_goal_test(const RrtGoal &gl, const DevSpace &sp, const double *x, uint32_t id,
+                                              uint32_t iter, uint64_t *rec) {
+    if (!gl.goal) return false;
+    double g[kChainMaxLinks];
+    for (int c = 0; c < sp.dim; ++c) g[c] = gl.goal[c];
+    const double d = raw_distance(sp, x, g);  // goal->isSatisfied(nmotion->state, &dist)  RRT.cpp:175
+    if (d < gl.threshold) {
+        rec[0] = iter;
+        return true;
+    }
+    if (d < __longlong_as_double((long long)rec[1])) {  // RRT.cpp:183-187
+        rec[1] = (uint64_t)__double_as_longlong(d);
+        rec[2] = id;
+    }
+    return false;
+}
+
+// append s2 at position n (its features are its reals: R^n, SO3, SE3) — one thread
+template <int F>
+__device__ __forceinline__ void rrt_append(double *__restrict__ feat, float *__restrict__ feat32, int rows32,
+                                           uint64_t cap, uint64_t n, const double *s2, int dim) {
+    for (int f = 0; f < F; ++f) feat[(uint64_t)f * cap + n] = f < dim ? s2[f] : 0.0;
+    for (int r = 0; r < rows32; ++r) feat32[(uint64_t)r * cap + n] = (float)(r < dim ? s2[r] : 0.0);
+}
+
+template <int F>
+__global__ __launch_bounds__(256) void rrt_step_kernel(double *__restrict__ feat, float *__restrict__ feat32,
+                                                       int rows32, uint64_t cap, uint64_t *__restrict__ n_dev,
+                                                       const double *__restrict__ sample,
+                                                       const double *__restrict__ part_d,
+                                                       const uint32_t *__restrict__ part_i, uint32_t nparts,
+                                                       DevSpace sp, DevSpace msp, DevChecker ck, double maxd,
+                                                       uint32_t *__restrict__ nearest_out,
+                                                       uint32_t *__restrict__ added_out,
+                                                       unsigned long long *__restrict__ counters, RrtGoal gl,
+                                                       uint64_t *__restrict__ grec, uint32_t iter) {
+    if (gl.goal && grec[0] != ~0ull) return;  // solved earlier: the host marks the rest
+    __shared__ double lds_d[4];
+    __shared__ uint32_t lds_i[4];
+    __shared__ double s1[kChainMaxLinks], s2[kChainMaxLinks];
+    __shared__ int sh_nd, sh_bad, sh_ok;
+    __shared__ uint32_t sh_ri;
+    TopK<1> top;
+    top.init();
+    for (uint32_t j = threadIdx.x; j < nparts; j += blockDim.x) top.offer(part_d[j], part_i[j]);
+    double rd;
+    uint32_t ri;
+    block_select<1>(top, lds_d, lds_i, rd, ri);
+    if (threadIdx.x == 0) sh_ri = ri;
+    __syncthreads();
+    ri = sh_ri;
+    rrt_decide([&](int c) { return feat[(uint64_t)c * cap + ri]; }, sample, ri, sp, msp, ck, maxd, s1, s2, &sh_nd,
+               &sh_bad, &sh_ok);
     if (threadIdx.x == 0) {
+        *nearest_out = ri;
         uint32_t added = kNoId;
         const uint64_t n = *n_dev;
         if (sh_ok && !sh_bad && n < cap) {
-            for (int f = 0; f < F; ++f) feat[(uint64_t)f * cap + n] = f < dim ? s2[f] : 0.0;
-            for (int r = 0; r < rows32; ++r) feat32[(uint64_t)r * cap + n] = (float)(r < dim ? s2[r] : 0.0);
+            rrt_append<F>(feat, feat32, rows32, cap, n, s2, sp.dim);
             *n_dev = n + 1;
             added = (uint32_t)n;
+            rrt_goal_test(gl, sp, s2, added, iter, grec);
         }
         *added_out = added;
         if (counters && sh_ok) atomicAdd(&counters[sh_bad ? 1 : 0], 1ull);  // valid_ / invalid_
+    }
+}
+
+
+// ---- persistent form: one cooperative launch for all iterations --------------------------
+// Every block owns a fixed slice of store positions.  Iteration i: each block scans its slice
+// for sample i's nearest state, publishes (distance, id) and arrives at a grid barrier.  The
+// LAST block to arrive merges the published minima, steers, checks the motion and publishes
+// the decision (size, neighbour, added, new state) and the next generation; the block whose
+// slice holds the new position appends the row — it is the only block that reads that
+// position later, so the store itself needs no cross-XCD coherence.
+//
+// All cross-block words (the partial minima, the barrier, the decision) live in an UNCACHED
+// device buffer (hipDeviceMallocUncached): every access goes to memory, so blocks on different
+// XCDs (each with its own L2) see each other's writes without L2 write-back / invalidate —
+// which agent-scope release / acquire would do once per block per iteration, flushing the L2
+// the other blocks are scanning from.  Ordering: a writer waits for its stores to complete
+// (s_waitcnt vmcnt(0)) before the word that announces them; a reader issues its loads after
+// the announcing load returned.  A waiting block gives up after kSpinLimit polls and raises the
+// abort word, which every block polls too, so a grid that cannot make progress drains instead
+// of hanging (the host reports it).
+constexpr uint32_t kSpinLimit = 1u << 22;  // ~0.1 s of s_sleep(1) polls per barrier
+
+// the uncached synchronisation record (rrt_sync_bytes): 64-bit words
+//   [0] arrivals  [1] generation  [2] abort  [3] size  [4] neighbour  [5] added  [6] solved
+//   [8 .. 8+16)  the new state      [24 .. 27) the goal record (RrtGoal), read and written by
+//   whichever block decides         [32 ..) partial distances (nb), partial ids (nb), and the
+//   rows of the partial minima (nb x 16): the deciding block may sit on another XCD than the
+//   block that scanned the winner, whose row it must not read through its own L2
+constexpr int kSyncState = 8, kSyncGoal = 24, kSyncParts = 32, kSyncRow = 16;
+
+__device__ __forceinline__ void stores_done() { __builtin_amdgcn_s_waitcnt(0); }  // vmcnt = expcnt = lgkmcnt = 0
+__device__ __forceinline__ uint64_t ld_sync(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sync(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int SP, int F>
+__global__ __launch_bounds__(256) void rrt_persistent_kernel(
+    double *__restrict__ feat, float *__restrict__ feat32, int rows32, uint64_t cap, uint64_t n0,
+    uint64_t *__restrict__ n_dev, const double *__restrict__ samples, uint32_t ns, uint64_t slice, DevSpace sp,
+    DevSpace msp, DevChecker ck, double maxd, uint64_t *__restrict__ sync, uint32_t *__restrict__ nearest_out,
+    uint32_t *__restrict__ added_out, unsigned long long *__restrict__ counters, RrtGoal gl,
+    uint64_t *__restrict__ grec) {
+    __shared__ double lds_d[4];
+    __shared__ uint32_t lds_i[4];
+    __shared__ double s1[kChainMaxLinks], s2[kChainMaxLinks];
+    __shared__ int sh_nd, sh_bad, sh_ok, sh_last, sh_run;
+    __shared__ uint32_t sh_ri;
+    __shared__ uint64_t sh_n, sh_added;
+    __shared__ double sh_row[F];
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    const int dim = sp.dim;
+    const uint64_t lo = (uint64_t)b * slice, hi = lo + slice;
+    uint64_t *pd = sync + kSyncParts, *pi = sync + kSyncParts + nb, *prow = sync + kSyncParts + 2 * nb;
+    uint64_t n = n0;
+    for (uint32_t i = 0; i < ns; ++i) {
+        const double *s = samples + (size_t)i * dim;
+        double qf[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) qf[f] = f < dim ? s[f] : 0.0;
+        // 1. this block's slice (RRT.cpp:137)
+        TopK<1> top;
+        top.init();
+        const uint64_t end = hi < n ? hi : n;
+        for (uint64_t id = lo + threadIdx.x; id < end; id += blockDim.x) {
+            double sf[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) sf[f] = feat[(uint64_t)f * cap + id];
+            top.offer(feat_dist<SP, F, 0>(sf, qf, sp), (uint32_t)id);
+        }
+        double rd;
+        uint32_t ri;
+        block_select<1>(top, lds_d, lds_i, rd, ri);
+        if (threadIdx.x == 0) {
+            st_sync(&pd[b], (uint64_t)__double_as_longlong(rd));
+            st_sync(&pi[b], ri);
+            if (ri != kNoId)
+                for (int f = 0; f < F; ++f)
+                    st_sync(&prow[(size_t)b * kSyncRow + f], (uint64_t)__double_as_longlong(feat[(uint64_t)f * cap + ri]));
+            stores_done();
+            const uint64_t prev = __hip_atomic_fetch_add(&sync[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh_last = prev == nb - 1;
+        }
+        __syncthreads();
+        if (sh_last) {
+            // 2. the last block: the global nearest, the steered state, the motion's bit
+            top.init();
+            for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x)
+                top.offer(__longlong_as_double((long long)ld_sync(&pd[j])), (uint32_t)ld_sync(&pi[j]));
+            block_select<1>(top, lds_d, lds_i, rd, ri);
+            if (threadIdx.x == 0) sh_ri = ri;
+            __syncthreads();
+            ri = sh_ri;
+            const uint64_t *wrow = prow + (size_t)(ri != kNoId ? ri / slice : 0) * kSyncRow;  // the winner's block
+            rrt_decide([&](int c) { return __longlong_as_double((long long)ld_sync(&wrow[c])); }, s, ri, sp, msp, ck,
+                       maxd, s1, s2, &sh_nd, &sh_bad, &sh_ok);
+            if (threadIdx.x == 0) {
+                uint32_t added = kNoId;
+                bool solved = false;
+                if (sh_ok && !sh_bad && n < cap) {
+                    added = (uint32_t)n;
+                    for (int f = 0; f < F; ++f) st_sync(&sync[kSyncState + f], (uint64_t)__double_as_longlong(s2[f]));
+                    solved = rrt_goal_test(gl, sp, s2, added, i, sync + kSyncGoal);
+                }
+                st_sync(&sync[6], solved);
+                nearest_out[i] = ri;
+                added_out[i] = added;
+                if (counters && sh_ok) atomicAdd(&counters[sh_bad ? 1 : 0], 1ull);  // valid_ / invalid_
+                st_sync(&sync[3], added != kNoId ? n + 1 : n);
+                st_sync(&sync[4], ri);
+                st_sync(&sync[5], added);
+                st_sync(&sync[0], 0);
+                stores_done();
+                st_sync(&sync[1], (uint64_t)i + 1);  // release the others
+                sh_run = 1;
+            }
+        } else if (threadIdx.x == 0) {
+            bool ok = true;
+            uint32_t spins = 0;
+            while (ld_sync(&sync[1]) == (uint64_t)i) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kSpinLimit || ld_sync(&sync[2])) {
+                    ok = false;
+                    break;
+                }
+            }
+            if (!ok) st_sync(&sync[2], 1);
+            sh_run = ok;
+        }
+        __syncthreads();
+        if (!sh_run) return;  // aborted: the host sees the abort word and fails the call
+        // 3. the decision, and the append by the block that owns the new position
+        if (threadIdx.x == 0) {
+            sh_n = ld_sync(&sync[3]);
+            sh_added = ld_sync(&sync[5]);
+            sh_last = (int)ld_sync(&sync[6]);  // solved: every block stops after this iteration
+        }
+        __syncthreads();
+        const uint64_t added = sh_added;
+        if (added != kNoId && added >= lo && added < hi) {
+            if (threadIdx.x < F) sh_row[threadIdx.x] = __longlong_as_double((long long)ld_sync(&sync[kSyncState + threadIdx.x]));
+            __syncthreads();
+            if (threadIdx.x == 0) rrt_append<F>(feat, feat32, rows32, cap, added, sh_row, dim);
+            // this CU's L1 may hold the line of the new row as loaded before the append: drop it
+            // before the next scan reads the row (one block per iteration pays the invalidate)
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        }
+        n = sh_n;
+        const bool stop = sh_last != 0;
+        __syncthreads();  // shared words are rewritten in the next iteration
+        if (stop) break;
+    }
+    if (b == 0 && threadIdx.x == 0) {
+        *n_dev = n;
+        for (int w = 0; w < kGoalWords; ++w) grec[w] = ld_sync(&sync[kSyncGoal + w]);
     }
 }
 
@@ -142,47 +360,87 @@ template <int SP, int F>
 hipError_t run_rrt(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck, double *feat, float *feat32,
                    int rows32, uint64_t cap, uint64_t n0, uint64_t *n_dev, const double *samples, uint32_t ns,
                    double maxd, double *part_d, uint32_t *part_i, uint32_t *nearest, uint32_t *added,
-                   unsigned long long *counters, hipStream_t st) {
+                   unsigned long long *counters, uint64_t *sync, uint32_t coop_blocks, RrtGoal gl, uint64_t *grec,
+                   hipStream_t st) {
     const int dim = sp.dim;
+    if (coop_blocks > 0 && sync) {
+        // slices of whole waves' worth of positions, covering the largest size of the run
+        const uint64_t nmax = n0 + ns;
+        uint64_t slice = (nmax + coop_blocks - 1) / coop_blocks;
+        slice = (slice + 255) & ~(uint64_t)255;
+        const uint32_t nb = (uint32_t)((nmax + slice - 1) / slice);
+        void *args[] = {&feat, &feat32, &rows32, &cap, &n0, &n_dev, &samples, &ns, &slice, (void *)&sp,
+                        (void *)&msp, (void *)&ck, &maxd, &sync, &nearest, &added, &counters, &gl, &grec};
+        return hipLaunchCooperativeKernel((const void *)rrt_persistent_kernel<SP, F>, dim3(nb), dim3(256), args, 0,
+                                          st);
+    }
     for (uint32_t i = 0; i < ns; ++i) {
         // before sample i the store holds at most n0 + i states
         const uint64_t nmax = n0 + i;
         const uint32_t blocks = (uint32_t)((nmax + kRrtBlockStates - 1) / kRrtBlockStates);
         const double *s = samples + (size_t)i * dim;
         hipLaunchKernelGGL((rrt_scan_kernel<SP, F>), dim3(blocks), dim3(256), 0, st, feat, cap, n_dev, s, sp, part_d,
-                           part_i);
+                           part_i, gl.goal ? grec : nullptr);
         hipLaunchKernelGGL((rrt_step_kernel<F>), dim3(1), dim3(256), 0, st, feat, feat32, rows32, cap, n_dev, s,
-                           part_d, part_i, blocks, sp, msp, ck, maxd, nearest + i, added + i, counters);
+                           part_d, part_i, blocks, sp, msp, ck, maxd, nearest + i, added + i, counters, gl, grec, i);
     }
     return hipGetLastError();
 }
 
 }  // namespace
 
+uint32_t rrt_coop_blocks(int device, const DevSpace &sp, const FeatGeom &g) {
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 3
+    return 0;  // A/B build: the two-launch form
+#endif
+    int coop = 0, cus = 0;
+    if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess || !coop) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 0;
+    const void *fn = nullptr;
+    switch (sp.kind) {
+    case OMPL_GPU_SPACE_SE3: fn = (const void *)rrt_persistent_kernel<OMPL_GPU_SPACE_SE3, 7>; break;
+    case OMPL_GPU_SPACE_SO3: fn = (const void *)rrt_persistent_kernel<OMPL_GPU_SPACE_SO3, 4>; break;
+    case OMPL_GPU_SPACE_REALVECTOR:
+        fn = g.F == 4 ? (const void *)rrt_persistent_kernel<OMPL_GPU_SPACE_REALVECTOR, 4>
+             : g.F == 8 ? (const void *)rrt_persistent_kernel<OMPL_GPU_SPACE_REALVECTOR, 8>
+                        : (const void *)rrt_persistent_kernel<OMPL_GPU_SPACE_REALVECTOR, 16>;
+        break;
+    default: return 0;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess || per_cu <= 0) return 0;
+    return (uint32_t)std::min<int64_t>((int64_t)cus * std::min(per_cu, 2), kRrtMaxCoopBlocks);
+}
+
 size_t rrt_part_entries(uint64_t n_max) { return (size_t)((n_max + kRrtBlockStates - 1) / kRrtBlockStates); }
+
+size_t rrt_goal_words() { return kGoalWords; }
+
+size_t rrt_sync_bytes() { return sizeof(uint64_t) * (kSyncParts + (2 + kSyncRow) * kRrtMaxCoopBlocks); }
 
 hipError_t launch_rrt_grow(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck, const FeatGeom &g,
                            double *feat, float *feat32, int rows32, uint64_t cap, uint64_t n0, uint64_t *n_dev,
                            const double *samples, uint32_t ns, double maxd, double *part_d, uint32_t *part_i,
-                           uint32_t *nearest, uint32_t *added, unsigned long long *counters, hipStream_t st) {
+                           uint32_t *nearest, uint32_t *added, unsigned long long *counters, uint64_t *sync,
+                           uint32_t coop_blocks, const double *goal, double goal_threshold, uint64_t *grec,
+                           hipStream_t st) {
+    const RrtGoal gl{goal, goal_threshold};
     if (ns == 0) return hipSuccess;
+    coop_blocks = std::min<uint32_t>(coop_blocks, kRrtMaxCoopBlocks);
+#define OMPL_AMD_RRT(SPK, FK)                                                                                      \
+    return run_rrt<SPK, FK>(sp, msp, ck, feat, feat32, rows32, cap, n0, n_dev, samples, ns, maxd, part_d, part_i, \
+                            nearest, added, counters, sync, coop_blocks, gl, grec, st)
     switch (sp.kind) {
     case OMPL_GPU_SPACE_SE3:
-        return run_rrt<OMPL_GPU_SPACE_SE3, 7>(sp, msp, ck, feat, feat32, rows32, cap, n0, n_dev, samples, ns, maxd,
-                                              part_d, part_i, nearest, added, counters, st);
+        OMPL_AMD_RRT(OMPL_GPU_SPACE_SE3, 7);
     case OMPL_GPU_SPACE_SO3:
-        return run_rrt<OMPL_GPU_SPACE_SO3, 4>(sp, msp, ck, feat, feat32, rows32, cap, n0, n_dev, samples, ns, maxd,
-                                              part_d, part_i, nearest, added, counters, st);
+        OMPL_AMD_RRT(OMPL_GPU_SPACE_SO3, 4);
     case OMPL_GPU_SPACE_REALVECTOR:
-        if (g.F == 4)
-            return run_rrt<OMPL_GPU_SPACE_REALVECTOR, 4>(sp, msp, ck, feat, feat32, rows32, cap, n0, n_dev, samples,
-                                                         ns, maxd, part_d, part_i, nearest, added, counters, st);
-        if (g.F == 8)
-            return run_rrt<OMPL_GPU_SPACE_REALVECTOR, 8>(sp, msp, ck, feat, feat32, rows32, cap, n0, n_dev, samples,
-                                                         ns, maxd, part_d, part_i, nearest, added, counters, st);
-        return run_rrt<OMPL_GPU_SPACE_REALVECTOR, 16>(sp, msp, ck, feat, feat32, rows32, cap, n0, n_dev, samples, ns,
-                                                      maxd, part_d, part_i, nearest, added, counters, st);
+        if (g.F == 4) OMPL_AMD_RRT(OMPL_GPU_SPACE_REALVECTOR, 4);
+        if (g.F == 8) OMPL_AMD_RRT(OMPL_GPU_SPACE_REALVECTOR, 8);
+        OMPL_AMD_RRT(OMPL_GPU_SPACE_REALVECTOR, 16);
     }
+#undef OMPL_AMD_RRT
     return hipErrorInvalidValue;
 }
 

@@ -38,6 +38,8 @@ uint32_t ompl_gpu_rng_get_seed(void) { return (uint32_t)ompl::RNG::getSeed(); }
 
 uint64_t ompl_gpu_rng_seeds_drawn(void) { return ompl::rng_detail::seedGenerator().drawn(); }
 
+uint32_t ompl_gpu_rng_next_seed(void) { return (uint32_t)ompl::rng_detail::seedGenerator().nextSeed(); }
+
 ompl_gpu_status ompl_gpu_rng_uniform_real(uint32_t local_seed, size_t n, double low, double high, double *out) {
     if (n && !out) {
         ompl_amd::set_last_error("NULL argument");

@@ -216,6 +216,22 @@ class NearestNeighborsGPU:
         abi.check(abi.lib.ompl_gpu_rrt_grow_device(self._h, mv._h, C.c_void_p(d_samples), int(ns), float(max_distance),
                                                    C.c_void_p(d_nearest), C.c_void_p(d_added)))
 
+    def rrt_solve_device(self, mv, d_samples: int, ns: int, max_distance: float, goal, goal_threshold: float,
+                         d_nearest: int, d_added: int):
+        """RRT iterations with the goal test (RRT.cpp:128-192): stops at the first added state
+        within goal_threshold of `goal`.  Returns (solved iteration or None, approximate-solution id
+        or None, its distance)."""
+        g = abi.as_states(goal, self.dim).reshape(-1)
+        sol = C.c_uint64(0)
+        aid = C.c_uint32(0)
+        ad = C.c_double(0.0)
+        abi.check(abi.lib.ompl_gpu_rrt_solve_device(self._h, mv._h, C.c_void_p(d_samples), int(ns),
+                                                    float(max_distance), abi.dptr(g), float(goal_threshold),
+                                                    C.c_void_p(d_nearest), C.c_void_p(d_added), C.byref(sol),
+                                                    C.byref(aid), C.byref(ad)))
+        return (None if sol.value == 2 ** 64 - 1 else sol.value, None if aid.value == abi.NO_ID32 else aid.value,
+                ad.value)
+
     def prm_add_milestones(self, mv, states, k_const: float, k_cap: int, j0: int = 0, j1: int | None = None):
         """PRM* causal batch (PRM.cpp:562-596, KStarStrategy): the milestones, in order, connect to
         their k_i nearest among every earlier vertex, edges checked with mv, then join the structure.

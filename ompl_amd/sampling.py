@@ -27,6 +27,12 @@ def get_seed() -> int:
     return int(abi.lib.ompl_gpu_rng_get_seed())
 
 
+def next_seed() -> int:
+    """The seed an RNG() constructed now would take (drawn from the generator), for mirroring an
+    RNG that lives outside this library (a planner's rng_, GNAT's pivot selector)."""
+    return int(abi.lib.ompl_gpu_rng_next_seed())
+
+
 def seeds_drawn() -> int:
     """Seeds the process-wide generator has handed out (RNG() constructions)."""
     return int(abi.lib.ompl_gpu_rng_seeds_drawn())
