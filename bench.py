@@ -192,40 +192,98 @@ def cpu_baseline(workload, sp, ck, tree, queries, k, budget_s, radius=None):
                            f"threads; index build {r['build_s']:.2f} s excluded"),
                 "single_thread": {"value": comb(qps1, mps1), "nn_queries_per_s": qps1, "motion_checks_per_s": mps1},
                 "nn_queries_per_s": qpsT, "motion_checks_per_s": mpsT, "gnat_build_s": r["build_s"]}
-    # brute force over 10^6 chain / 10^7 SE(3) states: time a few queries
-    dim = sp.dim
-    q = queries[:64]
-    t0 = time.perf_counter()
     if workload == "cfg4":
-        O.knn(sp, tree, q[:1], k)
-    else:
-        O.radius(sp, tree, q[:1], radius)
-    per = time.perf_counter() - t0
-    nq = int(min(64, max(1, 0.6 * budget_s / max(per, 1e-9))))
+        return _cpu_prm_causal(sp, ck, tree, queries, k, budget_s, T)
+    return _cpu_bitstar_radius(sp, ck, tree, queries, radius, budget_s, T)
+
+
+def _cpu_prm_causal(sp, ck, tree, milestones, k_cap, budget_s, T):
+    """PRM*'s causal insertion on the GNAT restatement (PRM.cpp:562-596, KStarStrategy
+    ConnectionStrategy.h:124-156): milestone i queries its k_i = ceil((e + e/d) ln(i + 1)) nearest
+    among every vertex before it, is inserted, and its edges checkMotion(state[n], state[m]) are
+    checked.  Causal, so one thread (the reference's roadmap construction is sequential); the
+    edges are also timed on T threads."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+
+    g = O.Gnat(sp)
     t0 = time.perf_counter()
-    if workload == "cfg4":
-        ids, _, _ = O.knn(sp, tree, q[:nq], k)
-        nb = tree[ids.reshape(-1).astype(np.int64)]
-        s1, s2 = nb, np.repeat(q[:nq], k, axis=0)                    # checkMotion(state[n], state[m])
-    else:
-        off, ids, _ = O.radius(sp, tree, q[:nq], radius)
-        s1 = np.repeat(q[:nq], np.diff(off).astype(np.int64), axis=0)  # checkMotion(vertex, sample)
-        s2 = tree[ids.astype(np.int64)]
-    t_nn = time.perf_counter() - t0
-    mps, reps = _motion_rate(sp, ck, s1.reshape(-1, dim), s2.reshape(-1, dim), 0.3 * budget_s, 1)
+    g.add(tree, bulk=True)
+    build_s = time.perf_counter() - t0
+    kc = math.e + math.e / sp.dim
+    n0 = len(tree)
+    s1, s2, nq = [], [], 0
+    t_nn = 0.0
+    for i, q in enumerate(milestones):
+        kq = min(int(math.ceil(kc * math.log(n0 + i + 1))), k_cap)
+        t0 = time.perf_counter()
+        ids, _, cnt = g.knn(q, kq)
+        g.add(q)
+        t_nn += time.perf_counter() - t0
+        nq += 1
+        for j in ids[0, :cnt[0]].astype(np.int64):
+            s1.append(tree[j] if j < n0 else milestones[j - n0])
+            s2.append(q)
+        if t_nn > 0.6 * budget_s:
+            break
+    s1, s2 = np.asarray(s1), np.asarray(s2)
+    mps1, reps = _motion_rate(sp, ck, s1, s2, 0.2 * budget_s, 1)
+    mpsT, _ = _motion_rate(sp, ck, s1, s2, 0.2 * budget_s, T)
     m = len(s1)
-    t_mv = m / mps
-    what = (f"nearestK(k={k})" if workload == "cfg4" else f"nearestR(r={radius:.4f})")
-    return {"value": (nq + m) / (t_nn + t_mv), "unit": UNIT, "cores": 1, "kind": "port",
-            "sample": (f"oracle Linear brute force (NearestNeighborsLinear semantics; the reference's GNAT is faster, "
-                       f"its index over {len(tree)} states is not built here) : {nq} {what} queries over the same "
-                       f"{len(tree)}-state set, then their {m} checkMotion edges x{reps} with the oracle "
-                       f"DiscreteMotionValidator"),
-            "nn_queries_per_s": nq / t_nn, "motion_checks_per_s": mps}
+    return {"value": (nq + m) / (t_nn + m / mps1), "unit": UNIT, "cores": 1, "kind": "port",
+            "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same {n0}-vertex "
+                       f"roadmap: the first {nq} milestones of the run inserted causally (k_i nearest, then add), "
+                       f"then their {m} checkMotion edges x{reps} with the oracle DiscreteMotionValidator, on 1 "
+                       f"thread; index build {build_s:.1f} s excluded"),
+            "nn_queries_per_s": nq / t_nn, "motion_checks_per_s": mps1, "gnat_build_s": build_s,
+            "threads": {"cores": T, "motion_checks_per_s": mpsT,
+                        "note": "causal inserts are sequential; only the edge checks use the threads"}}
 
 
-def single_query_scan(torch, nn, dev, reps, n_tree):
-    """RRT semantics (RRT.cpp:137): one nearest() per iteration -> the stream kernel, HBM/MALL bound."""
+def _cpu_bitstar_radius(sp, ck, tree, queries, radius, budget_s, T):
+    """BIT*'s batch on the GNAT restatement: nearestR(r) of each vertex over the sample set
+    (ImplicitGraph.cpp:313-320, GNAT nearestR NearestNeighborsGNAT.h:236-245) on 1 and T
+    threads (const queries), plus checkMotion(vertex, sample) of the edges.  The edges' motion
+    rate is measured on the pairs of a few queries answered by the oracle's brute force."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+
+    g = O.Gnat(sp)
+    t0 = time.perf_counter()
+    g.add(tree, bulk=True)
+    build_s = time.perf_counter() - t0
+    rate = {}
+    for nt in (1, T):
+        t0 = time.perf_counter()
+        g.radius_count(queries[:4 * nt], radius, nt)
+        per = (time.perf_counter() - t0) / (4 * nt)
+        nq = int(min(len(queries), max(4 * nt, 0.25 * budget_s / max(per, 1e-9))))
+        t0 = time.perf_counter()
+        cnt, tot = g.radius_count(queries[:nq], radius, nt)
+        rate[nt] = (nq, time.perf_counter() - t0, tot)
+    off, ids, _ = O.radius(sp, tree, queries[:8], radius)
+    s1 = np.repeat(queries[:8], np.diff(off).astype(np.int64), axis=0)
+    s2 = tree[ids.astype(np.int64)]
+    mps = {nt: _motion_rate(sp, ck, s1, s2, 0.15 * budget_s, nt) for nt in (1, T)}
+
+    def comb(nt):
+        nq, t, tot = rate[nt]
+        return (nq + tot) / (t + tot / mps[nt][0])
+
+    nqT, tT, totT = rate[T]
+    return {"value": comb(T), "unit": UNIT, "cores": T, "kind": "port",
+            "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same {len(tree)}-sample "
+                       f"set: {nqT} nearestR(r={radius:.4f}) of the run's vertices ({totT} neighbours) on {T} threads "
+                       f"(const queries), their checkMotion(vertex, sample) edges at the rate measured on "
+                       f"{len(s1)} edges of 8 vertices; index build {build_s:.1f} s excluded"),
+            "single_thread": {"value": comb(1), "nn_queries_per_s": rate[1][0] / rate[1][1],
+                              "motion_checks_per_s": mps[1][0]},
+            "nn_queries_per_s": nqT / tT, "motion_checks_per_s": mps[T][0], "gnat_build_s": build_s}
+
+
+def single_query_scan(torch, nn, dev, reps, n_tree, note=None):
+    """RRT semantics (RRT.cpp:137): one nearest() per iteration -> the fp32 stream kernel
+    (knn_stream32.hip: 28 B per SE(3) state, exact by in-chunk fp64 refinement), HBM bound."""
     from ompl_amd import workloads as W
 
     q = torch.from_numpy(W.uniform_se3(np.random.default_rng(99), reps)).to(dev)
@@ -234,6 +292,7 @@ def single_query_scan(torch, nn, dev, reps, n_tree):
     for i in range(5):
         nn.knn_device(q[i].data_ptr(), 1, 1, ids[i].data_ptr(), dd[i].data_ptr())
     torch.cuda.synchronize(dev)
+    nn.profile(True)
     ms0, n0, _ = nn.kernel_time()
     t0 = time.perf_counter()
     for i in range(reps):
@@ -242,12 +301,28 @@ def single_query_scan(torch, nn, dev, reps, n_tree):
     wall = time.perf_counter() - t0
     ms1, n1, name = nn.kernel_time()
     kern_ms = (ms1 - ms0) / max(n1 - n0, 1)
-    achieved = n_tree * B_SE3["f64"] / (kern_ms * 1e-3) / 1e9
-    return {"queries_per_s": reps / wall, "kernel": name, "kernel_us": kern_ms * 1e3,
+    b = B_SE3["f32"] if "stream32" in name else B_SE3["f64"]
+    achieved = n_tree * b / (kern_ms * 1e-3) / 1e9
+    return {"queries_per_s": reps / wall, "kernel": name, "kernel_us": kern_ms * 1e3, "tree_states": n_tree,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "algorithmic": f"{n_tree} states x {B_SE3['f64']} B per query (fp64 SoA)",
-                         "note": "the 56 MB store is Infinity-Cache resident across back-to-back scans"}}
+                         "algorithmic": f"{n_tree} states x {b} B per query ({'fp32' if b == 28 else 'fp64'} SoA rows)",
+                         "note": note or ""}}
+
+
+def single_query_large(torch, dev, reps, n=10_000_000):
+    """The same one-query scan over a 10^7-state SE(3) store (280 MB of fp32 rows, larger than
+    the 256 MB Infinity Cache): the HBM-bound case of SURVEY M2(i)."""
+    from ompl_amd import NearestNeighborsGPU, workloads as W
+    from ompl_amd.spaces import SE3StateSpace
+
+    nn = NearestNeighborsGPU(SE3StateSpace(), dev.index or 0)
+    nn.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    nn.add(W.uniform_se3(np.random.default_rng(1234), n))
+    r = single_query_scan(torch, nn, dev, reps, n, "10^7 states: 280 MB of fp32 rows, above the 256 MB Infinity "
+                                                   "Cache, so every scan streams from HBM")
+    del nn
+    return r
 
 
 def _timed(torch, stream, fn, reps):
@@ -661,7 +736,7 @@ def main():
     else:
         valid_frac = None
 
-    single = rrt = spheres = rrt_star = index = None
+    single = single_large = rrt = spheres = rrt_star = index = None
     if rank == 0 and args.workload in ("cfg3", "cfg2") and not args.no_extras:
         index = index_maintenance(torch, run, local)
     if rank == 0 and args.workload == "cfg3" and not args.no_extras:
@@ -669,7 +744,10 @@ def main():
         if args.rrt_star_queries > 0:
             rrt_star = rrt_star_knn(torch, run, args.tree, args.rrt_star_queries)
     if rank == 0 and args.workload == "cfg3" and args.single_query_reps > 0:
-        single = single_query_scan(torch, run.nn, dev, args.single_query_reps, args.tree)
+        single = single_query_scan(torch, run.nn, dev, args.single_query_reps, args.tree,
+                                   "the 28 MB of fp32 rows stay Infinity-Cache resident across back-to-back scans")
+        if not args.no_extras:
+            single_large = single_query_large(torch, dev, args.single_query_reps)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.workload, run.sp, run.ck, run.tree, run.q_host, run.k, args.cpu_seconds, run.radius)
@@ -717,6 +795,8 @@ def main():
             line["rrt_star_knn"] = rrt_star
         if single:
             line["single_query"] = single
+        if single_large:
+            line["single_query_1e7"] = single_large
         if rrt:
             line["rrt_device"] = rrt
         print(json.dumps(line), flush=True)

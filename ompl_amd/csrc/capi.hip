@@ -562,6 +562,15 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
                                      h->stream));
         return OMPL_GPU_OK;
     }
+    if (h->fast && screen_safe(h) && h->rows32 && stream32_supported(h->sp, h->g, (uint32_t)nq, k)) {
+        // one / few queries (RRT's nearest per iteration): stream the fp32 rows, exact by
+        // in-chunk fp64 refinement (knn_stream32.hip) — half the bytes of the fp64 stream
+        HIP_OR_FAIL(h->ws.ensure(stream32_workspace_bytes((uint32_t)nq, n_end)));
+        HIP_OR_FAIL(launch_knn_stream32(h->sp, h->g, h->feat32, h->feat, h->cap, n_end, d_qf, (uint32_t)nq, k,
+                                        (float)h->absmax * (1.0f + 1e-6f), (float)h->qeta * 1.01f, d_dist, d_ids,
+                                        h->ws.p, h->ws.bytes, h->stream));
+        return OMPL_GPU_OK;
+    }
     const size_t wsb = knn_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus);
     HIP_OR_FAIL(h->ws.ensure(wsb));
     HIP_OR_FAIL(launch_knn(h->sp, h->g, h->feat, h->cap, n_end, d_qf, (uint32_t)nq, k, d_dist, d_ids, h->ws.p,
@@ -1498,10 +1507,20 @@ ompl_gpu_status rrt_run(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples
     }
     // appended states are slerp interpolations of unit quaternions (fp64): a conservative excess
     if (h->sp.kind == OMPL_GPU_SPACE_SE3) h->qeta = std::max(h->qeta, 1e-12);
+    // the persistent form screens in fp32 (rrt.hip): it needs the fp32 rows and screenable
+    // coordinates, and starts from the store's bounds (words 7 = B, 28 = eta of its record)
+    const bool coop = h->rrt_sync && h->rows32 && screen_safe(h);
+    if (coop) {
+        const double B = h->absmax * (1.0 + 1e-6), eta = h->qeta * 1.01;
+        HIP_OR_FAIL(hipMemcpyAsync((uint64_t *)h->rrt_sync + 7, &B, sizeof(double), hipMemcpyHostToDevice, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync((uint64_t *)h->rrt_sync + 28, &eta, sizeof(double), hipMemcpyHostToDevice, h->stream));
+    }
     HIP_OR_FAIL(launch_rrt_grow(h->sp, mv->sp, mv->ck, h->g, h->feat, h->feat32, h->rows32, h->cap, n0,
                                 (uint64_t *)h->rrt_n.p, d_samples, (uint32_t)ns, max_distance, (double *)h->rrt_pd.p,
                                 (uint32_t *)h->rrt_pi.p, d_nearest, d_added, mv->counters, (uint64_t *)h->rrt_sync,
-                                (uint32_t)h->rrt_coop, goal ? dgoal : nullptr, goal_threshold, grec, h->stream));
+                                coop ? (uint32_t)h->rrt_coop : 0u, goal ? dgoal : nullptr, goal_threshold, grec,
+                                h->stream));
+    if (coop) HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // B / eta above are host locals
     uint64_t grec_h[3] = {~0ull, 0, kNoId};
     HIP_OR_FAIL(hipMemcpyAsync(grec_h, grec, sizeof(grec_h), hipMemcpyDeviceToHost, h->stream));
     uint64_t n1 = n0;

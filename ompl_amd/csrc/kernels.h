@@ -146,6 +146,14 @@ hipError_t launch_knn_fast(const DevSpace &sp, const FeatGeom &g, const double *
                            uint64_t cap, uint64_t n_end, const SortedStore *sorted, const double *qfeat64, uint32_t nq,
                            uint32_t k, const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes,
                            int num_cus, hipStream_t st, uint32_t **fail_count, uint32_t **fail_list);
+// ---- small batches (nq < kStreamMaxQ) over the fp32 rows, exact by in-chunk fp64 refinement
+// (knn_stream32.hip): SE3 and R^n, k <= kStream32MaxK
+constexpr uint32_t kStream32MaxK = 16;
+bool stream32_supported(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k);
+size_t stream32_workspace_bytes(uint32_t nq, uint64_t n_end);
+hipError_t launch_knn_stream32(const DevSpace &sp, const FeatGeom &g, const float *feat32, const double *feat64,
+                               uint64_t cap, uint64_t n_end, const double *qfeat, uint32_t nq, uint32_t k, float absmax,
+                               float qeta, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes, hipStream_t st);
 // ---- large k (k > 32; RRT* k ~ 6e3): histogram threshold + candidate sort (knn_large.hip)
 // dmax: bound of the distances between stored states (the histogram's range; larger
 // distances fall into an overflow bin and are still handled exactly).

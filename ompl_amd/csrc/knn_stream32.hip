@@ -1,0 +1,219 @@
+// knn_stream32.hip — exact small-batch kNN (nq < kStreamMaxQ: RRT's one nearest() per
+// iteration, RRT.cpp:137 / NearestNeighborsGNAT.h:209-219) streaming the fp32 SoA rows.
+//
+// The fp64 stream (knn.hip knn_stream_kernel) reads 56 B per SE(3) state; this one reads the
+// fp32 screening rows, 28 B per state, which is what bounds a scan of 10^7 states (280 MB,
+// larger than the 256 MB Infinity Cache): HBM.  Exactness without a certificate round trip:
+// a block owns a contiguous chunk of 256 * ITEMS states; it
+//   1. screens the chunk in fp32 (state_dist32, error bound screen_error: |d32 - d64| <= E/2),
+//      keeping the distances in registers, and finds t = the chunk's K-th smallest d32;
+//   2. evaluates the exact fp64 distance (reference operation order, feat_dist) of every state
+//      of the chunk with d32 <= thr = (t + E)(1 + 32u), reading its fp64 row (a handful per
+//      chunk), and keeps the chunk's exact top-K by (distance, id).
+// A state with d32 > thr has d64 > t + E/2 >= the d64 of each of the K states with d32 <= t,
+// so it is not among the chunk's K best: the chunk's list is exact, and the merge of all
+// chunks' lists (knn_stream32_merge_kernel) is the exact top-K of the store.
+#include "knn_fast_impl.h"
+
+namespace ompl_amd {
+
+namespace {
+
+constexpr int kS32Threads = 256;
+
+// one block = one chunk of 256 * ITEMS consecutive store positions of query blockIdx.y.  Lane
+// loads are float4 (4 consecutive states of a row): load j of thread t covers positions
+// base + j * 1024 + 4 t .. + 3, so a wave reads 1 KB per row per load instruction.
+template <int SP, int F, int K, int ITEMS>
+__global__ __launch_bounds__(kS32Threads) void knn_stream32_kernel(const float *__restrict__ feat32,
+                                                                   const double *__restrict__ feat64, uint64_t cap,
+                                                                   uint64_t n_end, const double *__restrict__ qfeat,
+                                                                   DevSpace sp, float absmax, float qeta,
+                                                                   double *__restrict__ part_d,
+                                                                   uint32_t *__restrict__ part_i) {
+    static_assert(ITEMS % 4 == 0, "float4 loads");
+    constexpr int FS = Geo<SP, F>::FS;
+    constexpr int NV = ITEMS / 4;
+    __shared__ double lds_d[4 * K];
+    __shared__ uint32_t lds_i[4 * K];
+    __shared__ double sh_thr;
+    const uint32_t q = blockIdx.y;
+    double qv[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qv[f] = qfeat[(size_t)q * F + f];
+    float q32[FS];
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) q32[c] = (float)qv[c];
+        q32[3] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) q32[4 + c] = (float)qv[3 + c];
+    } else {
+#pragma unroll
+        for (int f = 0; f < F; ++f) q32[f] = (float)qv[f];
+    }
+    const float w0 = (float)sp.w0, w1 = (float)sp.w1;
+    const uint64_t base = (uint64_t)blockIdx.x * (kS32Threads * ITEMS) + 4 * threadIdx.x;
+    // 1. fp32 screen: every row load of the chunk issued before the first distance
+    const float nan4 = __builtin_nanf("");
+    float4 x[NV][F];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const uint64_t p = base + (uint64_t)j * (4 * kS32Threads);
+#pragma unroll
+        for (int f = 0; f < F; ++f)
+            x[j][f] = p < n_end ? *reinterpret_cast<const float4 *>(feat32 + (uint64_t)f * cap + p)
+                                : make_float4(nan4, nan4, nan4, nan4);
+    }
+    float d32[ITEMS];
+    TopK<K> top;
+    top.init();
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float s[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) s[f] = u == 0 ? x[j][f].x : u == 1 ? x[j][f].y : u == 2 ? x[j][f].z : x[j][f].w;
+            const float d = state_dist32<SP, F>(s, q32, w0, w1);  // NaN row 0: unused / removed slot
+            d32[j * 4 + u] = d;
+            const uint32_t id = (uint32_t)(base + (uint64_t)j * (4 * kS32Threads) + u);
+            if (top.admits((double)d, id)) top.push((double)d, id);
+        }
+    }
+    double rd;
+    uint32_t ri;
+    block_select<K>(top, lds_d, lds_i, rd, ri);
+    if (threadIdx.x == K - 1) {
+        // t = the chunk's K-th fp32 distance (+inf: fewer than K live states, all refined)
+        const double t = rd;
+        double B = absmax;
+        const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : F;
+        for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qv[c]));
+        const double E = screen_error<SP>(sp, B, t, (double)qeta + query_eta<SP>(qv));
+        sh_thr = (t + E) * (1.0 + 32.0 * kU);
+    }
+    __syncthreads();
+    const double thr = sh_thr;
+    // 2. exact fp64 distance of the chunk's candidates (reference order)
+    top.init();
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if ((double)d32[j * 4 + u] <= thr) {  // NaN never passes
+                const uint64_t id = base + (uint64_t)j * (4 * kS32Threads) + u;
+                double sv[F];
+#pragma unroll
+                for (int f = 0; f < F; ++f) sv[f] = feat64[(uint64_t)f * cap + id];
+                top.offer(feat_dist<SP, F, 0>(sv, qv, sp), (uint32_t)id);
+            }
+        }
+    }
+    __syncthreads();  // lds_d / lds_i are reused
+    block_select<K>(top, lds_d, lds_i, rd, ri);
+    if (threadIdx.x < K) {
+        const size_t o = ((size_t)q * gridDim.x + blockIdx.x) * K + threadIdx.x;
+        part_d[o] = rd;
+        part_i[o] = ri;
+    }
+}
+
+// block per query: the exact top-out_k of its P chunk lists
+template <int K>
+__global__ __launch_bounds__(256) void knn_stream32_merge_kernel(const double *__restrict__ pd,
+                                                                 const uint32_t *__restrict__ pi, uint32_t P,
+                                                                 double *__restrict__ out_d,
+                                                                 uint32_t *__restrict__ out_i, uint32_t out_k) {
+    __shared__ double lds_d[4 * K];
+    __shared__ uint32_t lds_i[4 * K];
+    const uint32_t q = blockIdx.x;
+    TopK<K> top;
+    top.init();
+    const size_t base = (size_t)q * P * K;
+    for (size_t j = threadIdx.x; j < (size_t)P * K; j += blockDim.x) top.offer(pd[base + j], pi[base + j]);
+    double rd;
+    uint32_t ri;
+    block_select<K>(top, lds_d, lds_i, rd, ri);
+    if (threadIdx.x < out_k) {
+        out_d[(size_t)q * out_k + threadIdx.x] = rd;
+        out_i[(size_t)q * out_k + threadIdx.x] = ri;
+    }
+}
+
+template <int SP, int F, int K, int ITEMS>
+hipError_t run_stream32(const DevSpace &sp, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_end,
+                        const double *qfeat, uint32_t nq, uint32_t k, float absmax, float qeta, double *out_d,
+                        uint32_t *out_i, void *ws, size_t ws_bytes, hipStream_t st) {
+    const uint32_t P = (uint32_t)((n_end + kS32Threads * ITEMS - 1) / (kS32Threads * ITEMS));
+    const size_t need = (size_t)nq * P * K * (sizeof(double) + sizeof(uint32_t));
+    if (ws_bytes < need) return hipErrorInvalidValue;
+    double *pd = (double *)ws;
+    uint32_t *pi = (uint32_t *)(pd + (size_t)nq * P * K);
+    timer_begin(st, "knn_stream32_kernel");
+    hipLaunchKernelGGL((knn_stream32_kernel<SP, F, K, ITEMS>), dim3(P, nq), dim3(kS32Threads), 0, st, feat32, feat64,
+                       cap, n_end, qfeat, sp, absmax, qeta, pd, pi);
+    timer_end(st);
+    hipLaunchKernelGGL((knn_stream32_merge_kernel<K>), dim3(nq), dim3(256), 0, st, pd, pi, P, out_d, out_i, k);
+    return hipGetLastError();
+}
+
+// states per block: 2048 from 4 M states up (HBM-resident stores: more bytes in flight per
+// wave), 1024 below (a 10^6 store still spreads over ~1,000 blocks)
+template <int SP, int F, int K>
+hipError_t stream32_items(const DevSpace &sp, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_end,
+                          const double *qfeat, uint32_t nq, uint32_t k, float absmax, float qeta, double *out_d,
+                          uint32_t *out_i, void *ws, size_t ws_bytes, hipStream_t st) {
+    if (n_end >= (4ull << 20))
+        return run_stream32<SP, F, K, 8>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
+                                         ws_bytes, st);
+    return run_stream32<SP, F, K, 4>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
+                                     ws_bytes, st);
+}
+
+template <int SP, int F>
+hipError_t stream32_k(const DevSpace &sp, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_end,
+                      const double *qfeat, uint32_t nq, uint32_t k, float absmax, float qeta, double *out_d,
+                      uint32_t *out_i, void *ws, size_t ws_bytes, hipStream_t st) {
+    if (k <= 1)
+        return stream32_items<SP, F, 1>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
+                                        ws_bytes, st);
+    if (k <= 4)
+        return stream32_items<SP, F, 4>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
+                                        ws_bytes, st);
+    return stream32_items<SP, F, 16>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
+                                     ws_bytes, st);
+}
+
+}  // namespace
+
+bool stream32_supported(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k) {
+    if (nq == 0 || nq >= kStreamMaxQ || k == 0 || k > kStream32MaxK) return false;
+    if (sp.kind == OMPL_GPU_SPACE_SE3) return g.F == 7;
+    if (sp.kind == OMPL_GPU_SPACE_REALVECTOR) return g.F == 4 || g.F == 8 || g.F == 16;
+    return false;
+}
+
+size_t stream32_workspace_bytes(uint32_t nq, uint64_t n_end) {
+    const uint64_t P = (n_end + kS32Threads * 4 - 1) / (kS32Threads * 4);
+    return (size_t)nq * P * 16 * (sizeof(double) + sizeof(uint32_t));
+}
+
+hipError_t launch_knn_stream32(const DevSpace &sp, const FeatGeom &g, const float *feat32, const double *feat64,
+                               uint64_t cap, uint64_t n_end, const double *qfeat, uint32_t nq, uint32_t k, float absmax,
+                               float qeta, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes, hipStream_t st) {
+    if (!stream32_supported(sp, g, nq, k) || (cap & 3) || n_end > cap) return hipErrorInvalidValue;
+    if (sp.kind == OMPL_GPU_SPACE_SE3)
+        return stream32_k<OMPL_GPU_SPACE_SE3, 7>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d,
+                                                 out_i, ws, ws_bytes, st);
+    if (g.F == 4)
+        return stream32_k<OMPL_GPU_SPACE_REALVECTOR, 4>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta,
+                                                        out_d, out_i, ws, ws_bytes, st);
+    if (g.F == 8)
+        return stream32_k<OMPL_GPU_SPACE_REALVECTOR, 8>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta,
+                                                        out_d, out_i, ws, ws_bytes, st);
+    return stream32_k<OMPL_GPU_SPACE_REALVECTOR, 16>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d,
+                                                     out_i, ws, ws_bytes, st);
+}
+
+}  // namespace ompl_amd
