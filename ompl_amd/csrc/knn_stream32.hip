@@ -21,6 +21,21 @@ namespace {
 
 constexpr int kS32Threads = 256;
 
+#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 1 || OMPL_AMD_VARIANT == 3)
+__device__ __forceinline__ float4 load_row4(const float *p) {  // A/B build: non-temporal stream
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+#else
+__device__ __forceinline__ float4 load_row4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+#endif
+#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 2 || OMPL_AMD_VARIANT == 3)
+constexpr int kS32LargeItems = 8;  // A/B build: 2,048 states per block from 4 M states up
+#else
+constexpr int kS32LargeItems = 4;  // measured: 1,024 states per block (8 waves / SIMD) streams ~10 % faster at 10^7
+#endif
+
 // one block = one chunk of 256 * ITEMS consecutive store positions of query blockIdx.y.  Lane
 // loads are float4 (4 consecutive states of a row): load j of thread t covers positions
 // base + j * 1024 + 4 t .. + 3, so a wave reads 1 KB per row per load instruction.
@@ -62,8 +77,7 @@ __global__ __launch_bounds__(kS32Threads) void knn_stream32_kernel(const float *
         const uint64_t p = base + (uint64_t)j * (4 * kS32Threads);
 #pragma unroll
         for (int f = 0; f < F; ++f)
-            x[j][f] = p < n_end ? *reinterpret_cast<const float4 *>(feat32 + (uint64_t)f * cap + p)
-                                : make_float4(nan4, nan4, nan4, nan4);
+            x[j][f] = p < n_end ? load_row4(feat32 + (uint64_t)f * cap + p) : make_float4(nan4, nan4, nan4, nan4);
     }
     float d32[ITEMS];
     TopK<K> top;
@@ -158,14 +172,13 @@ hipError_t run_stream32(const DevSpace &sp, const float *feat32, const double *f
     return hipGetLastError();
 }
 
-// states per block: 2048 from 4 M states up (HBM-resident stores: more bytes in flight per
-// wave), 1024 below (a 10^6 store still spreads over ~1,000 blocks)
+// states per block: 1,024 (kS32LargeItems from 4 M states up; the A/B build tries 2,048 there)
 template <int SP, int F, int K>
 hipError_t stream32_items(const DevSpace &sp, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_end,
                           const double *qfeat, uint32_t nq, uint32_t k, float absmax, float qeta, double *out_d,
                           uint32_t *out_i, void *ws, size_t ws_bytes, hipStream_t st) {
     if (n_end >= (4ull << 20))
-        return run_stream32<SP, F, K, 8>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
+        return run_stream32<SP, F, K, kS32LargeItems>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
                                          ws_bytes, st);
     return run_stream32<SP, F, K, 4>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
                                      ws_bytes, st);

@@ -197,39 +197,65 @@ __global__ __launch_bounds__(256) void rrt_step_kernel(double *__restrict__ feat
 
 
 // ---- persistent form: one cooperative launch for all iterations --------------------------
-// One block per CU; block b owns the store positions [b * slice, (b + 1) * slice) for the whole
-// run, so its slice of the fp32 rows (28 B per SE3 state; 10^6 states = 3.5 MB per XCD) stays in
-// its XCD's L2 from one iteration to the next.  Iteration i:
-//   1. every block screens its slice in fp32 for sample i (per thread the two smallest d32),
-//      refines the candidates within the screen's error bound of the block's fp32 minimum in
-//      fp64 (the reference's operation order) and so finds the slice's exact nearest (d, id):
-//      a state with d32 > thr = (m + E)(1 + 32u) has d64 > m + E/2 >= d64 of the block's fp32
-//      argmin (the knn_stream32.hip argument with K = 1); a thread whose second smallest d32 is
-//      within thr rescans its own positions;
-//   2. it publishes (d, id, fp64 row) in its own record and raises its own arrival flag (no
-//      shared counter: a same-address atomic per block per iteration serialises in memory);
-//   3. block 0 — the decider — polls the nb flags with nb threads, merges the records, steers,
-//      checks the motion with the whole block (rrt_decide), runs the goal test, and publishes the
-//      decision and the next generation; the other blocks poll the generation word;
-//   4. the block owning the new position appends the row (fp64 + fp32): it is the only block that
-//      reads that position later, so the store needs no cross-XCD coherence.
-// All cross-block words live in an UNCACHED device buffer (hipDeviceMallocUncached): every access
-// goes to memory, so blocks on different XCDs (each with its own L2) see each other's writes
-// without L2 write-back / invalidate.  A writer waits for its stores to complete (s_waitcnt) before
-// the word that announces them; a reader issues its loads after the announcing load returned.  A
-// waiting block gives up after kSpinLimit polls and raises the abort word, which every waiter polls
-// too, so a grid that cannot make progress drains instead of hanging (the host reports it).
-// The screen's error bound needs B >= every |coordinate| and (SE3) eta >= every |q|^2 - 1 of the
-// store and the query: the host passes them for the initial store, the decider extends them with
-// each appended state, every block with each sample.
-constexpr uint32_t kSpinLimit = 1u << 22;  // ~0.1 s of s_sleep(1) polls per wait
-constexpr uint32_t kRrtMaxCoopBlocks = 256;  // <= blockDim: the decider polls one flag per thread
+// Scanning blocks (one per CU) each own the store positions [b * slice, (b + 1) * slice) for the
+// whole run, so their slice of the fp32 rows (28 B per SE3 state; 10^6 states = 3.5 MB per XCD)
+// stays in their XCD's L2.  One more block, the decider, owns no slice.
+//
+// Scanning runs AHEAD of the decisions by L samples: a block answers sample s over the positions
+// below n_{s-L} (the store size before decision s - L; n0 for s < L), which needs only the decisions
+// up to s - L - 1, and publishes the slice's exact nearest (d, id, fp64 row) in its record ring; the
+// decider answers sample j from the records of all slices plus the states that decisions
+// j - L .. j - 1 appended (positions [n_{j-L}, n_j), at most L, kept in its LDS), steers, checks the
+// motion, runs the goal test and publishes decision j.  The scan is off the critical path: an
+// iteration costs the decider's own round trips (flags, records, decision) and its arithmetic.
+//
+// A slice's exact nearest: the fp32 screen keeps each thread's two smallest d32; candidates within
+// the screen's error bound of the block's fp32 minimum m are refined in fp64 (reference operation
+// order): a state with d32 > thr = (m + E)(1 + 32u) has d64 > m + E/2 >= d64 of the block's fp32
+// argmin (knn_stream32.hip's argument with K = 1); a thread whose second smallest d32 is within thr
+// rescans its own positions.  E needs B >= every |coordinate| and (SE3) eta >= every |q|^2 - 1 of
+// the store and the query: the host passes them for the initial store, each decision extends them.
+//
+// The block owning an appended position writes its row (fp64 + fp32) when it processes that
+// decision, before it next scans: it is the only block that reads that position, so the store needs
+// no cross-XCD coherence.  All cross-block words live in an UNCACHED buffer (hipDeviceMallocUncached):
+// every access goes to memory, so blocks on different XCDs see each other's writes without L2
+// write-back / invalidate.  A writer waits for its stores (s_waitcnt) before the word announcing them;
+// a reader loads after the announcing load returned.  Rings of depth R = L + 2 (records, decisions):
+// slot s mod R is rewritten only after every reader is done with it (a block publishes record s + R
+// after decision s + R - L - 1 > s, which the decider made after reading record s; the decider makes
+// decision j + R after record j + R of every block, which each block wrote after reading decision j).
+// The decision's generation word is written in 8 copies 512 B apart, block b polling copy b % 8, so
+// the pollers spread over memory channels.  A waiting block gives up after kSpinLimit polls and
+// raises the abort word, which every waiter polls too: a grid that cannot progress drains (the host
+// reports it).
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 4  // phase timer build (s_memrealtime, 100 MHz)
+#define RRT_T0() uint64_t t_prev = __builtin_amdgcn_s_memrealtime()
+#define RRT_T(k)                                                 \
+    do {                                                         \
+        const uint64_t t_now = __builtin_amdgcn_s_memrealtime(); \
+        tph[k] += t_now - t_prev;                                \
+        t_prev = t_now;                                          \
+    } while (0)
+#else
+#define RRT_T0() (void)0
+#define RRT_T(k) (void)0
+#endif
+constexpr uint32_t kSpinLimit = 1u << 22;    // ~0.1 s of s_sleep(1) polls per wait
+constexpr uint32_t kRrtMaxCoopBlocks = 256;  // scanning blocks + the decider; the decider polls one flag per thread
+constexpr int kLook = 2;                     // samples the scans run ahead of the decisions
+constexpr int kRing = kLook + 2;             // record / decision ring depth
 
-// the uncached synchronisation record (rrt_sync_bytes): 64-bit words
-//   [1] generation  [2] abort  [3] size  [4] neighbour  [5] added  [6] solved  [7] B  [28] eta
-//   [8 .. 8+16)  the new state      [24 .. 27) the goal record (RrtGoal), read and written by the
-//   decider        [32 ..) per block: arrival flag (nb), distance (nb), id (nb), row (nb x 16)
-constexpr int kSyncState = 8, kSyncGoal = 24, kSyncB = 7, kSyncEta = 28, kSyncParts = 32, kSyncRow = 16;
+// the uncached synchronisation record (rrt_sync_bytes), 64-bit words:
+//   [2] abort  [7] B of the initial store  [24 .. 27) goal record  [28] eta of the initial store
+//   [64 + 64 c] (c < 8) generation copies: index + 1 of the latest decision
+//   [kSyncDec + kDecWords r]  decision slot r: [1] added  [2] solved  [3] B  [4] eta  [8 .. 8+F) row
+//   [kSyncFlags + b]  block b's published records: index + 1 of the latest sample
+//   [kSyncRec + kRecWords (r nb + b)]  block b's record slot r: [0] distance  [1] id  [2 .. 2+F) row
+constexpr int kSyncB = 7, kSyncGoal = 24, kSyncEta = 28, kSyncGen = 64, kGenCopies = 8, kGenStride = 64;
+constexpr int kSyncDec = kSyncGen + kGenCopies * kGenStride, kDecWords = 32;
+constexpr int kSyncFlags = kSyncDec + kRing * kDecWords, kSyncRec = kSyncFlags + (int)kRrtMaxCoopBlocks;
+constexpr int kRecWords = 18;  // distance, id, F <= 16 reals
 
 __device__ __forceinline__ void stores_done() { __builtin_amdgcn_s_waitcnt(0); }  // vmcnt = expcnt = lgkmcnt = 0
 __device__ __forceinline__ uint64_t ld_sync(const uint64_t *p) {
@@ -240,6 +266,16 @@ __device__ __forceinline__ void st_sync(uint64_t *p, uint64_t v) {
 }
 __device__ __forceinline__ uint64_t dbits(double v) { return (uint64_t)__double_as_longlong(v); }
 __device__ __forceinline__ double bitsd(uint64_t v) { return __longlong_as_double((long long)v); }
+
+// poll *p until it reaches `want` (false: the spin limit passed or some block aborted)
+__device__ __forceinline__ bool wait_for(const uint64_t *p, uint64_t want, uint64_t *abort_word) {
+    uint32_t spins = 0;
+    while (ld_sync(p) < want) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kSpinLimit || ld_sync(abort_word)) return false;
+    }
+    return true;
+}
 
 // block-wide argmin of (d, i) by (distance, id); every thread returns the result
 __device__ __forceinline__ void block_argmin(double &d, uint32_t &i, double *lds_d, uint32_t *lds_i) {
@@ -270,7 +306,7 @@ __device__ __forceinline__ float block_minf(float v, float *lds) {
     return v;
 }
 
-// max |coordinate| (the screen's B: SE3 translation, R^n every coordinate) and SE3 |q|^2 - 1
+// max |coordinate| (the screen's B: SE3 translation, R^n every coordinate)
 template <int SP, int F>
 __device__ __forceinline__ double coord_absmax(const double *x) {
     const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : F;
@@ -280,217 +316,283 @@ __device__ __forceinline__ double coord_absmax(const double *x) {
 }
 
 template <int SP, int F>
+__device__ __forceinline__ void load_sample(const double *s, int dim, double *qv) {
+#pragma unroll
+    for (int f = 0; f < F; ++f) qv[f] = f < dim ? s[f] : 0.0;
+}
+
+// exact nearest of sample qv among positions [lo, end) of the store (see the header); every
+// thread returns (d, id), and row = its fp64 row in LDS (valid when id != kNoId)
+template <int SP, int F>
+__device__ void slice_nearest(const double *__restrict__ feat, const float *__restrict__ feat32, uint64_t cap,
+                              uint64_t lo, uint64_t end, const double *qv, const DevSpace &sp, double Bst, double eta_st,
+                              double &wd, uint32_t &wi, double *row, double *lds_d, uint32_t *lds_i, float *lds_f) {
+    constexpr int FS = Geo<SP, F>::FS;
+    float q32[FS];
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) q32[c] = (float)qv[c];
+        q32[3] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) q32[4 + c] = (float)qv[3 + c];
+    } else {
+#pragma unroll
+        for (int f = 0; f < F; ++f) q32[f] = (float)qv[f];
+    }
+    const float w0 = (float)sp.w0, w1 = (float)sp.w1;
+    float c0 = __builtin_inff(), c1 = __builtin_inff();
+    uint32_t i0 = kNoId;
+#pragma unroll 2
+    for (uint64_t p = lo + 4 * threadIdx.x; p < end; p += 1024) {
+        float4 x[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) x[f] = *reinterpret_cast<const float4 *>(feat32 + (uint64_t)f * cap + p);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float v[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) v[f] = u == 0 ? x[f].x : u == 1 ? x[f].y : u == 2 ? x[f].z : x[f].w;
+            float d = state_dist32<SP, F>(v, q32, w0, w1);
+            if (p + u >= end) d = __builtin_nanf("");
+            if (d < c1) {  // NaN never passes; positions ascend, so ties keep the smaller id first
+                if (d < c0) {
+                    c1 = c0;
+                    c0 = d;
+                    i0 = (uint32_t)(p + u);
+                } else {
+                    c1 = d;
+                }
+            }
+        }
+    }
+    const float m = block_minf(c0, lds_f);
+    double bd = __builtin_inf();
+    uint32_t bi = kNoId;
+    double brow[F];
+    if (m == m && m < __builtin_inff()) {
+        const double B = fmax(Bst, coord_absmax<SP, F>(qv));
+        const double E = screen_error<SP>(sp, B, (double)m, eta_st + query_eta<SP>(qv));
+        const double thr = ((double)m + E) * (1.0 + 32.0 * kU);
+        auto refine = [&](uint32_t id) {
+            double sv[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) sv[f] = feat[(uint64_t)f * cap + id];
+            const double d = feat_dist<SP, F, 0>(sv, qv, sp);
+            if (lex_less(d, id, bd, bi)) {
+                bd = d;
+                bi = id;
+#pragma unroll
+                for (int f = 0; f < F; ++f) brow[f] = sv[f];
+            }
+        };
+        if ((double)c1 <= thr) {  // maybe more than two of this thread's states qualify: rescan them
+            for (uint64_t p = lo + 4 * threadIdx.x; p < end; p += 1024)
+                for (int u = 0; u < 4 && p + u < end; ++u) {
+                    float v[F];
+#pragma unroll
+                    for (int f = 0; f < F; ++f) v[f] = feat32[(uint64_t)f * cap + p + u];
+                    if ((double)state_dist32<SP, F>(v, q32, w0, w1) <= thr) refine((uint32_t)(p + u));
+                }
+        } else if ((double)c0 <= thr) {
+            refine(i0);
+        }
+    }
+    wd = bd;
+    wi = bi;
+    block_argmin(wd, wi, lds_d, lds_i);
+    if (wi != kNoId && bi == wi) {  // the winning thread (ids are unique)
+#pragma unroll
+        for (int f = 0; f < F; ++f) row[f] = brow[f];
+    }
+    __syncthreads();
+}
+
+template <int SP, int F>
 __global__ __launch_bounds__(256) void rrt_persistent_kernel(
     double *__restrict__ feat, float *__restrict__ feat32, int rows32, uint64_t cap, uint64_t n0,
     uint64_t *__restrict__ n_dev, const double *__restrict__ samples, uint32_t ns, uint64_t slice, DevSpace sp,
     DevSpace msp, DevChecker ck, double maxd, uint64_t *__restrict__ sync, uint32_t *__restrict__ nearest_out,
     uint32_t *__restrict__ added_out, unsigned long long *__restrict__ counters, RrtGoal gl,
     uint64_t *__restrict__ grec) {
-    constexpr int FS = Geo<SP, F>::FS;
     __shared__ double lds_d[4];
     __shared__ uint32_t lds_i[4];
     __shared__ float lds_f[4];
-    __shared__ double s1[kChainMaxLinks], s2[kChainMaxLinks];
-    __shared__ int sh_nd, sh_bad, sh_ok, sh_run, sh_stop;
-    __shared__ uint64_t sh_n, sh_added;
-    __shared__ double sh_row[F], sh_B, sh_eta;
-    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    __shared__ double s1[kChainMaxLinks], s2[kChainMaxLinks], sh_q[F];
+    __shared__ int sh_nd, sh_bad, sh_ok, sh_go, sh_stop;
+    __shared__ uint64_t sh_added;
+    __shared__ double sh_row[F];
+    const uint32_t nsb = gridDim.x - 1, b = blockIdx.x;  // block nsb decides
     const int dim = sp.dim;
-    const uint64_t lo = (uint64_t)b * slice, hi = lo + slice;
-    uint64_t *flag = sync + kSyncParts, *pd = flag + nb, *pi = pd + nb, *prow = pi + nb;
-    uint64_t n = n0;
+    uint64_t *abort_word = sync + 2, *flag = sync + kSyncFlags, *rec = sync + kSyncRec;
     double Bst = bitsd(ld_sync(&sync[kSyncB])), eta_st = bitsd(ld_sync(&sync[kSyncEta]));
-    const float w0 = (float)sp.w0, w1 = (float)sp.w1;
-    for (uint32_t i = 0; i < ns; ++i) {
-        const double *s = samples + (size_t)i * dim;
-        double qv[F];
-#pragma unroll
-        for (int f = 0; f < F; ++f) qv[f] = f < dim ? s[f] : 0.0;
-        float q32[FS];
-        if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) q32[c] = (float)qv[c];
-            q32[3] = 0.f;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) q32[4 + c] = (float)qv[3 + c];
-        } else {
-#pragma unroll
-            for (int f = 0; f < F; ++f) q32[f] = (float)qv[f];
-        }
-        // 1. this block's slice (RRT.cpp:137): fp32 screen, two smallest per thread
-        const uint64_t end = hi < n ? hi : n;
-        float c0 = __builtin_inff(), c1 = __builtin_inff();
-        uint32_t i0 = kNoId;
-        const float nanf_ = __builtin_nanf("");
-#pragma unroll 2
-        for (uint64_t p = lo + 4 * threadIdx.x; p < end; p += 1024) {
-            float4 x[F];
-#pragma unroll
-            for (int f = 0; f < F; ++f) x[f] = *reinterpret_cast<const float4 *>(feat32 + (uint64_t)f * cap + p);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                float v[F];
-#pragma unroll
-                for (int f = 0; f < F; ++f) v[f] = u == 0 ? x[f].x : u == 1 ? x[f].y : u == 2 ? x[f].z : x[f].w;
-                float d = state_dist32<SP, F>(v, q32, w0, w1);
-                if (p + u >= end) d = nanf_;
-                if (d < c1) {  // NaN never passes; positions ascend, so ties keep the smaller id first
-                    if (d < c0) {
-                        c1 = c0;
-                        c0 = d;
-                        i0 = (uint32_t)(p + u);
-                    } else {
-                        c1 = d;
-                    }
-                }
-            }
-        }
-        const float m = block_minf(c0, lds_f);
-        double bd = __builtin_inf();
-        uint32_t bi = kNoId;
-        double brow[F];
-        if (m == m && m < __builtin_inff()) {
-            const double B = fmax(Bst, coord_absmax<SP, F>(qv));
-            const double E = screen_error<SP>(sp, B, (double)m, eta_st + query_eta<SP>(qv));
-            const double thr = ((double)m + E) * (1.0 + 32.0 * kU);
-            auto refine = [&](uint32_t id) {
-                double sv[F];
-#pragma unroll
-                for (int f = 0; f < F; ++f) sv[f] = feat[(uint64_t)f * cap + id];
-                const double d = feat_dist<SP, F, 0>(sv, qv, sp);
-                if (lex_less(d, id, bd, bi)) {
-                    bd = d;
-                    bi = id;
-#pragma unroll
-                    for (int f = 0; f < F; ++f) brow[f] = sv[f];
-                }
-            };
-            if ((double)c1 <= thr) {  // maybe more than two of this thread's states qualify: rescan them
-                for (uint64_t p = lo + 4 * threadIdx.x; p < end; p += 1024)
-                    for (int u = 0; u < 4 && p + u < end; ++u) {
-                        float v[F];
-#pragma unroll
-                        for (int f = 0; f < F; ++f) v[f] = feat32[(uint64_t)f * cap + p + u];
-                        if ((double)state_dist32<SP, F>(v, q32, w0, w1) <= thr) refine((uint32_t)(p + u));
-                    }
-            } else if ((double)c0 <= thr) {
-                refine(i0);
-            }
-        }
-        double wd = bd;
-        uint32_t wi = bi;
-        block_argmin(wd, wi, lds_d, lds_i);
-        if (wi != kNoId && bi == wi) {  // the winning thread (ids are unique)
-#pragma unroll
-            for (int f = 0; f < F; ++f) sh_row[f] = brow[f];
-        }
-        __syncthreads();
-        // 2. publish: record, then the arrival flag
-        if (threadIdx.x == 0) {
-            st_sync(&pd[b], dbits(wd));
-            st_sync(&pi[b], wi);
-            if (wi != kNoId)
-                for (int f = 0; f < F; ++f) st_sync(&prow[(size_t)b * kSyncRow + f], dbits(sh_row[f]));
-            stores_done();
-            st_sync(&flag[b], (uint64_t)i + 1);
-        }
-        if (b == 0) {
-            // 3. the decider: wait for every block's flag, merge, decide
-            int ok = 1;
-            if (threadIdx.x < nb) {
-                uint32_t spins = 0;
-                while (ld_sync(&flag[threadIdx.x]) <= (uint64_t)i) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > kSpinLimit || ld_sync(&sync[2])) {
-                        ok = 0;
-                        break;
-                    }
-                }
-            }
-            if (!__syncthreads_and(ok)) {
-                if (threadIdx.x == 0) st_sync(&sync[2], 1);
-                return;  // aborted: the host sees the abort word and fails the call
-            }
-            double gd = __builtin_inf();
-            uint32_t gi = kNoId;
-            if (threadIdx.x < nb) {
-                gd = bitsd(ld_sync(&pd[threadIdx.x]));
-                gi = (uint32_t)ld_sync(&pi[threadIdx.x]);
-            }
-            block_argmin(gd, gi, lds_d, lds_i);
-            const uint32_t ri = gi;
-            const uint64_t *wrow = prow + (size_t)(ri != kNoId ? ri / slice : 0) * kSyncRow;  // the winner's block
-            rrt_decide([&](int c) { return bitsd(ld_sync(&wrow[c])); }, s, ri, sp, msp, ck, maxd, s1, s2, &sh_nd,
-                       &sh_bad, &sh_ok);
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 4
+    uint64_t tph[4] = {0, 0, 0, 0};
+#endif
+    if (b < nsb) {
+        // ---- a scanning block
+        const uint64_t lo = (uint64_t)b * slice, hi = lo + slice;
+        const uint64_t *gen = sync + kSyncGen + (b % kGenCopies) * kGenStride;
+        uint64_t n = n0;       // n_{s-L}: the store size the scan of sample s sees
+        uint32_t next_dec = 0;  // decisions processed so far
+        // decision j: the new size, the appended row (this block's slice), the bounds; false = stop
+        auto process = [&](uint32_t j) -> bool {
+            const uint64_t *dec = sync + kSyncDec + (j % kRing) * kDecWords;
             if (threadIdx.x == 0) {
-                uint32_t added = kNoId;
-                bool solved = false;
-                if (sh_ok && !sh_bad && n < cap) {
-                    added = (uint32_t)n;
-                    double x[F];
-                    for (int f = 0; f < F; ++f) x[f] = f < dim ? s2[f] : 0.0;
-                    for (int f = 0; f < F; ++f) st_sync(&sync[kSyncState + f], dbits(x[f]));
-                    Bst = fmax(Bst, coord_absmax<SP, F>(x));
-                    eta_st = fmax(eta_st, query_eta<SP>(x));
-                    st_sync(&sync[kSyncB], dbits(Bst));
-                    st_sync(&sync[kSyncEta], dbits(eta_st));
-                    solved = rrt_goal_test(gl, sp, x, added, i, sync + kSyncGoal);
+                sh_go = wait_for(gen, (uint64_t)j + 1, abort_word);
+                if (!sh_go) st_sync(abort_word, 1);
+                sh_added = ld_sync(&dec[1]);
+                sh_stop = (int)ld_sync(&dec[2]);
+                lds_d[0] = bitsd(ld_sync(&dec[3]));
+                lds_d[1] = bitsd(ld_sync(&dec[4]));
+            }
+            __syncthreads();
+            if (!sh_go) return false;
+            const uint64_t added = sh_added;
+            Bst = lds_d[0];
+            eta_st = lds_d[1];
+            const bool stop = sh_stop != 0;
+            if (added != kNoId) {
+                n = added + 1;
+                if (added >= lo && added < hi) {
+                    if (threadIdx.x < F) sh_row[threadIdx.x] = bitsd(ld_sync(&dec[8 + threadIdx.x]));
+                    __syncthreads();
+                    if (threadIdx.x == 0) rrt_append<F>(feat, feat32, rows32, cap, added, sh_row, dim);
+                    // this CU's L1 may hold the line of the new row as loaded before the append: drop
+                    // it before the next scan reads the row
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
                 }
-                st_sync(&sync[6], solved);
-                nearest_out[i] = ri;
-                added_out[i] = added;
-                if (counters && sh_ok) atomicAdd(&counters[sh_bad ? 1 : 0], 1ull);  // valid_ / invalid_
-                st_sync(&sync[3], added != kNoId ? n + 1 : n);
-                st_sync(&sync[5], added);
+            }
+            next_dec = j + 1;
+            __syncthreads();  // shared words are rewritten by the next call
+            return !stop;
+        };
+        for (uint32_t s = 0; s < ns; ++s) {
+            RRT_T0();
+            if (s >= (uint32_t)kLook + 1 && !process(s - kLook - 1)) return;
+            RRT_T(1);
+            double qv[F];
+            load_sample<SP, F>(samples + (size_t)s * dim, dim, qv);
+            double wd;
+            uint32_t wi;
+            slice_nearest<SP, F>(feat, feat32, cap, lo, hi < n ? hi : n, qv, sp, Bst, eta_st, wd, wi, sh_row, lds_d,
+                                 lds_i, lds_f);
+            RRT_T(0);
+            if (threadIdx.x == 0) {  // record slot s mod R, then the flag
+                uint64_t *r = rec + ((size_t)(s % kRing) * nsb + b) * kRecWords;
+                st_sync(&r[0], dbits(wd));
+                st_sync(&r[1], wi);
+                if (wi != kNoId)
+                    for (int f = 0; f < F; ++f) st_sync(&r[2 + f], dbits(sh_row[f]));
                 stores_done();
-                st_sync(&sync[1], (uint64_t)i + 1);  // release the others
+                st_sync(&flag[b], (uint64_t)s + 1);
             }
-            __syncthreads();
-        } else if (threadIdx.x == 0) {
-            bool ok = true;
-            uint32_t spins = 0;
-            while (ld_sync(&sync[1]) <= (uint64_t)i) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > kSpinLimit || ld_sync(&sync[2])) {
-                    ok = false;
-                    break;
+            RRT_T(2);
+        }
+        // the decisions not processed yet: their rows still go into the store
+        for (uint32_t j = next_dec; j < ns;)
+            if (!process(j++)) break;
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 4
+        if (threadIdx.x == 0 && (b == 0 || b == nsb - 1))
+            printf("rrt-phases block%u: scan %.2f us, wait-decision %.2f us, publish %.2f us (nsb %u, slice %lu)\n", b,
+                   tph[0] * 0.01 / ns, tph[1] * 0.01 / ns, tph[2] * 0.01 / ns, nsb, (unsigned long)slice);
+#endif
+        return;
+    }
+    // ---- the decider
+    __shared__ double xrow[kLook][F];     // rows appended by the last L decisions, slot = decision % L
+    __shared__ uint32_t xid[kLook], xdec[kLook];
+    if (threadIdx.x < kLook) {
+        xid[threadIdx.x] = kNoId;
+        xdec[threadIdx.x] = 0;
+    }
+    uint64_t n = n0;
+    uint32_t j = 0;
+    for (; j < ns; ++j) {
+        RRT_T0();
+        const double *s = samples + (size_t)j * dim;
+        if (threadIdx.x < F) sh_q[threadIdx.x] = threadIdx.x < (uint32_t)dim ? s[threadIdx.x] : 0.0;
+        // 1. every slice's record of sample j
+        int ok = 1;
+        if (threadIdx.x < nsb) ok = wait_for(&flag[threadIdx.x], (uint64_t)j + 1, abort_word);
+        if (!__syncthreads_and(ok)) {
+            if (threadIdx.x == 0) st_sync(abort_word, 1);
+            return;  // aborted: the host sees the abort word and fails the call
+        }
+        RRT_T(0);
+        double gd = __builtin_inf();
+        uint32_t gi = kNoId;
+        double row[F];
+        if (threadIdx.x < nsb) {
+            const uint64_t *r = rec + ((size_t)(j % kRing) * nsb + threadIdx.x) * kRecWords;
+            gd = bitsd(ld_sync(&r[0]));
+            gi = (uint32_t)ld_sync(&r[1]);
+#pragma unroll
+            for (int f = 0; f < F; ++f) row[f] = bitsd(ld_sync(&r[2 + f]));
+        } else if (threadIdx.x >= 256 - kLook) {
+            // 2. the states appended by decisions j - L .. j - 1, which no scan of sample j saw
+            const int e = 255 - threadIdx.x;
+            if (xid[e] != kNoId && xdec[e] + kLook >= j) {
+                double qv[F];
+#pragma unroll
+                for (int f = 0; f < F; ++f) {
+                    row[f] = xrow[e][f];
+                    qv[f] = sh_q[f];
                 }
+                gd = feat_dist<SP, F, 0>(row, qv, sp);
+                gi = xid[e];
             }
-            if (!ok) st_sync(&sync[2], 1);
-            sh_run = ok;
         }
-        if (b != 0) {
-            __syncthreads();
-            if (!sh_run) return;  // aborted: the host sees the abort word and fails the call
-        }
-        // 4. the decision, and the append by the block that owns the new position
-        if (threadIdx.x == 0) {
-            sh_n = ld_sync(&sync[3]);
-            sh_added = ld_sync(&sync[5]);
-            sh_stop = (int)ld_sync(&sync[6]);  // solved: every block stops after this iteration
-            sh_B = bitsd(ld_sync(&sync[kSyncB]));
-            sh_eta = bitsd(ld_sync(&sync[kSyncEta]));
+        const uint32_t mine = gi;
+        block_argmin(gd, gi, lds_d, lds_i);
+        if (gi != kNoId && mine == gi) {
+#pragma unroll
+            for (int f = 0; f < F; ++f) sh_row[f] = row[f];
         }
         __syncthreads();
-        const uint64_t added = sh_added;
-        Bst = sh_B;
-        eta_st = sh_eta;
-        if (added != kNoId && added >= lo && added < hi) {
-            if (threadIdx.x < F) sh_row[threadIdx.x] = bitsd(ld_sync(&sync[kSyncState + threadIdx.x]));
-            __syncthreads();
-            if (threadIdx.x == 0) rrt_append<F>(feat, feat32, rows32, cap, added, sh_row, dim);
-            // this CU's L1 may hold the line of the new row as loaded before the append: drop it
-            // before the next scan reads the row (one block per iteration pays the invalidate)
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        RRT_T(1);
+        // 3. steer, check the motion, goal test (RRT.cpp:137-187)
+        const uint32_t ri = gi;
+        rrt_decide([&](int c) { return sh_row[c]; }, sh_q, ri, sp, msp, ck, maxd, s1, s2, &sh_nd, &sh_bad, &sh_ok);
+        if (threadIdx.x == 0) {
+            uint64_t *dec = sync + kSyncDec + (j % kRing) * kDecWords;
+            uint32_t added = kNoId;
+            bool solved = false;
+            if (sh_ok && !sh_bad && n < cap) {
+                added = (uint32_t)n;
+                double x[F];
+                for (int f = 0; f < F; ++f) x[f] = f < dim ? s2[f] : 0.0;
+                for (int f = 0; f < F; ++f) st_sync(&dec[8 + f], dbits(x[f]));
+                Bst = fmax(Bst, coord_absmax<SP, F>(x));
+                eta_st = fmax(eta_st, query_eta<SP>(x));
+                solved = rrt_goal_test(gl, sp, x, added, j, sync + kSyncGoal);
+                const int e = j % kLook;
+                for (int f = 0; f < F; ++f) xrow[e][f] = x[f];
+                xid[e] = added;
+                xdec[e] = j;
+                n += 1;
+            }
+            st_sync(&dec[1], added == kNoId ? (uint64_t)kNoId : (uint64_t)added);
+            st_sync(&dec[2], solved);
+            st_sync(&dec[3], dbits(Bst));
+            st_sync(&dec[4], dbits(eta_st));
+            nearest_out[j] = ri;
+            added_out[j] = added;
+            if (counters && sh_ok) atomicAdd(&counters[sh_bad ? 1 : 0], 1ull);  // valid_ / invalid_
+            stores_done();
+            for (int c = 0; c < kGenCopies; ++c) st_sync(&sync[kSyncGen + c * kGenStride], (uint64_t)j + 1);
+            sh_go = !solved;
         }
-        n = sh_n;
-        const bool stop = sh_stop != 0;
-        __syncthreads();  // shared words are rewritten in the next iteration
-        if (stop) break;
+        __syncthreads();
+        RRT_T(2);
+        if (!sh_go) break;
     }
-    if (b == 0 && threadIdx.x == 0) {
+    if (threadIdx.x == 0) {
         *n_dev = n;
         for (int w = 0; w < kGoalWords; ++w) grec[w] = ld_sync(&sync[kSyncGoal + w]);
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 4
+        printf("rrt-phases decider: wait-flags %.2f us, merge %.2f us, decide %.2f us\n", tph[0] * 0.01 / ns,
+               tph[1] * 0.01 / ns, tph[2] * 0.01 / ns);
+#endif
     }
 }
 
@@ -505,9 +607,10 @@ hipError_t run_rrt(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck
         if (coop_blocks > 0 && sync) {
             // slices of whole block-steps (1,024 positions), covering the largest size of the run
             const uint64_t nmax = n0 + ns;
-            uint64_t slice = (nmax + coop_blocks - 1) / coop_blocks;
+            const uint32_t nscan = coop_blocks - 1;  // one block decides
+            uint64_t slice = (nmax + nscan - 1) / nscan;
             slice = (slice + 1023) & ~(uint64_t)1023;
-            const uint32_t nb = (uint32_t)((nmax + slice - 1) / slice);
+            const uint32_t nb = (uint32_t)((nmax + slice - 1) / slice) + 1;
             void *args[] = {&feat, &feat32, &rows32, &cap, &n0, &n_dev, &samples, &ns, &slice, (void *)&sp,
                             (void *)&msp, (void *)&ck, &maxd, &sync, &nearest, &added, &counters, &gl, &grec};
             return hipLaunchCooperativeKernel((const void *)rrt_persistent_kernel<SP, F>, dim3(nb), dim3(256), args,
@@ -548,14 +651,17 @@ uint32_t rrt_coop_blocks(int device, const DevSpace &sp, const FeatGeom &g) {
     }
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess || per_cu <= 0) return 0;
-    return (uint32_t)std::min<int64_t>(cus, kRrtMaxCoopBlocks);  // one block per CU
+    if (cus < 2) return 0;
+    // one block per CU, one of them decides; the decider's last kLook threads fold in the states
+    // of the last decisions, the others read one slice's record each
+    return (uint32_t)std::min<int64_t>(cus, kRrtMaxCoopBlocks - kLook);
 }
 
 size_t rrt_part_entries(uint64_t n_max) { return (size_t)((n_max + kRrtBlockStates - 1) / kRrtBlockStates); }
 
 size_t rrt_goal_words() { return kGoalWords; }
 
-size_t rrt_sync_bytes() { return sizeof(uint64_t) * (kSyncParts + (3 + kSyncRow) * kRrtMaxCoopBlocks); }
+size_t rrt_sync_bytes() { return sizeof(uint64_t) * (kSyncRec + (size_t)kRing * kRrtMaxCoopBlocks * kRecWords); }
 
 hipError_t launch_rrt_grow(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck, const FeatGeom &g,
                            double *feat, float *feat32, int rows32, uint64_t cap, uint64_t n0, uint64_t *n_dev,
