@@ -320,6 +320,24 @@ ompl_gpu_status ompl_gpu_rrt_solve_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, cons
                                           uint32_t *d_nearest, uint32_t *d_added, uint64_t *solved_at,
                                           uint32_t *approx_id, double *approx_dist);
 
+/* ---- BIT* batch sampling -----------------------------------------------------
+ * BITstar::ImplicitGraph::updateSamples before a solution exists (ImplicitGraph.cpp:924-1000: the
+ * informed sampler draws from its base sampler while the cost bound is infinite,
+ * PathLengthDirectInfSampler.cpp:350-368): tries = 0; while tries < max_tries and
+ * numSamples < num_required: draw one state from smp (sampleUniform), check it with mv's
+ * StateValidityChecker, keep it if valid; then addToSamples appends the kept states to nn
+ * (ImplicitGraph.cpp:682-692).  The caller passes num_samples = numSamples_ and
+ * num_required = numSamples_ + numNewSamplesInCurrentBatch_, max_tries =
+ * averageNumOfAllowedFailedAttemptsWhenSampling_ (2) * num_required.  The validity checks run
+ * on the device in batches; smp's streams are left exactly after the last try the sequential
+ * loop makes.  *tries = states drawn (= isValid calls, numStateCollisionChecks_), *first_id =
+ * the first new id, *added = states appended.  nn, mv and smp describe the same space.
+ * Synchronous.  Output pointers may be NULL. */
+typedef struct ompl_gpu_sampler ompl_gpu_sampler;
+ompl_gpu_status ompl_gpu_bitstar_update_samples(ompl_gpu_nn *nn, ompl_gpu_mv *mv, ompl_gpu_sampler *smp,
+                                                uint64_t num_samples, uint64_t num_required, uint64_t max_tries,
+                                                uint64_t *tries, uint64_t *first_id, uint64_t *added);
+
 /* ---- the reference's input streams (host) ------------------------------------
  * ompl::RNG restated on the same standard-library engines (std::ranlux24_base seed generator,
  * std::mt19937 + std::uniform_real_distribution per RNG, RandomNumbers.cpp:53-279).
@@ -336,7 +354,6 @@ uint32_t ompl_gpu_rng_next_seed(void);
 /* n x RNG(local_seed).uniformReal(low, high): an explicitly seeded RNG (RandomNumbers.cpp:225-228),
  * which draws nothing from the seed generator */
 ompl_gpu_status ompl_gpu_rng_uniform_real(uint32_t local_seed, size_t n, double low, double high, double *out);
-typedef struct ompl_gpu_sampler ompl_gpu_sampler;
 /* allocStateSampler of the space: SE3 = CompoundStateSampler + R^3 + SO3 samplers (3 seeds),
  * R^n / KCHAIN one RealVectorStateSampler, SO3 one SO3StateSampler.  low / high: bounds of the
  * R^n part (dim reals; SE3: 3), NULL = [0, 1] (KCHAIN: [-pi, pi], KinematicChain.h:87-100). */

@@ -100,6 +100,7 @@ SIGNATURES = {
                                               _P, _P, _P, _U64]),
     "ompl_gpu_lazyprm_add_milestones": (C.c_int, [_P, _D, C.c_size_t, C.c_size_t, C.c_size_t, C.c_double, C.c_uint32,
                                                   _P, _P, _P]),
+    "ompl_gpu_bitstar_update_samples": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint64, C.c_uint64, _U64, _U64, _U64]),
     "ompl_gpu_mv_create": (C.c_int, [C.POINTER(_P), C.POINTER(SpaceStruct), C.POINTER(CheckerStruct), C.c_int]),
     "ompl_gpu_mv_destroy": (C.c_int, [_P]),
     "ompl_gpu_mv_set_stream": (C.c_int, [_P, _P]),

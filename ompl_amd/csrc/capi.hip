@@ -21,6 +21,7 @@
 
 #include "../../include/ompl_gpu.h"
 #include "kernels.h"
+#include "sampler_impl.h"
 #include "topk.h"
 
 using namespace ompl_amd;
@@ -1561,6 +1562,64 @@ ompl_gpu_status ompl_gpu_rrt_solve_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const
     if (!goal) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL goal");
     return rrt_run(h, mv, d_samples, ns, max_distance, goal, goal_threshold, d_nearest, d_added, solved_at, approx_id,
                    approx_dist);
+}
+
+// ------------------------------------------------------------------------------ BIT*
+
+ompl_gpu_status ompl_gpu_bitstar_update_samples(ompl_gpu_nn *h, ompl_gpu_mv *mv, ompl_gpu_sampler *smp,
+                                                uint64_t num_samples, uint64_t num_required, uint64_t max_tries,
+                                                uint64_t *tries, uint64_t *first_id, uint64_t *added) {
+    if (!h || !mv || !smp) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (h->device != mv->device) return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles are on different devices");
+    if (h->sp.kind != mv->sp.kind || h->sp.dim != mv->sp.dim || smp->kind != h->sp.kind || smp->dim != h->sp.dim)
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "nn, mv and sampler describe different state spaces");
+    std::scoped_lock lk(h->mu, mv->mu);
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    if (first_id) *first_id = h->n_total;
+    const int dim = h->sp.dim;
+    uint64_t t = 0, have = num_samples, got_all = 0;
+    double frac = 1.0;  // valid fraction seen so far: sizes the next batch of tries
+    std::vector<double> rows, keep;
+    std::vector<uint8_t> bits;
+    // ImplicitGraph.cpp:966-990: tries < max_tries && numSamples_ < numRequiredSamples
+    while (t < max_tries && have < num_required) {
+        const uint64_t need = num_required - have;
+        uint64_t chunk = (uint64_t)std::ceil((double)need / std::max(frac, 1e-3) * 1.05) + 32;
+        chunk = std::min<uint64_t>({chunk, max_tries - t, (uint64_t)1 << 20});
+        const ompl_amd::SamplerMark mark(*smp);
+        rows.resize((size_t)chunk * dim);
+        bits.resize(chunk);
+        smp->sample(chunk, rows.data());
+        HIP_OR_FAIL(mv->s1.ensure(sizeof(double) * rows.size()));
+        HIP_OR_FAIL(mv->valid.ensure(chunk));
+        HIP_OR_FAIL(hipMemcpyAsync(mv->s1.p, rows.data(), sizeof(double) * rows.size(), hipMemcpyHostToDevice,
+                                   mv->stream));
+        HIP_OR_FAIL(launch_state_valid(mv->sp, mv->ck, (const double *)mv->s1.p, (uint32_t)chunk,
+                                       (uint8_t *)mv->valid.p, mv->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(bits.data(), mv->valid.p, chunk, hipMemcpyDeviceToHost, mv->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(mv->stream));
+        // the reference loop stops at the try that brings the count to numRequiredSamples
+        uint64_t used = 0, got = 0;
+        keep.clear();
+        for (; used < chunk && got < need; ++used)
+            if (bits[used]) {
+                keep.insert(keep.end(), rows.begin() + used * dim, rows.begin() + (used + 1) * dim);
+                ++got;
+            }
+        if (used < chunk) {  // leave the streams exactly after try `used`
+            mark.rewind(*smp);
+            smp->sample(used, rows.data());
+        }
+        ompl_gpu_status s = add_locked(h, keep.data(), (size_t)got, nullptr);  // addToSamples (:688-692)
+        if (s != OMPL_GPU_OK) return s;
+        t += used;
+        have += got;
+        got_all += got;
+        frac = (double)got_all / (double)t;
+    }
+    if (tries) *tries = t;
+    if (added) *added = got_all;
+    return OMPL_GPU_OK;
 }
 
 }  // extern "C"

@@ -12,19 +12,18 @@
 //   SO3StateSampler::sampleUniform            base/spaces/src/SO3StateSpace.cpp:99-102 -> RNG::quaternion
 //   KinematicChainSpace (RealVectorStateSpace(n) with bounds [-pi, pi])  demos/KinematicChain.h:87-100
 #include <cstring>
-#include <memory>
 #include <new>
-#include <vector>
 
-#include "../../include/ompl_amd/ompl_surface_rng.h"
 #include "../../include/ompl_gpu.h"
+#include "sampler_impl.h"
 
-struct ompl_gpu_sampler {
-    int kind = 0, dim = 0, nrn = 0;  // nrn: reals of the R^n part (SE3: 3; SO3: 0)
-    std::vector<double> low, high;
-    // construction order of the reference: [compound], R^n / SO3 component samplers
-    std::unique_ptr<ompl::RNG> compound, rn, so3;
-};
+void ompl_gpu_sampler::sample(size_t n, double *out) {
+    for (size_t i = 0; i < n; ++i) {
+        double *o = out + i * dim;
+        for (int c = 0; c < nrn; ++c) o[c] = rn->uniformReal(low[c], high[c]);
+        if (so3) so3->quaternion(o + nrn);
+    }
+}
 
 namespace ompl_amd {
 void set_last_error(const char *msg);  // capi.hip
@@ -109,11 +108,7 @@ ompl_gpu_status ompl_gpu_sampler_sample_uniform(ompl_gpu_sampler *s, size_t n, d
         ompl_amd::set_last_error("NULL argument");
         return OMPL_GPU_ERR_INVALID_ARG;
     }
-    for (size_t i = 0; i < n; ++i) {
-        double *o = out + i * s->dim;
-        for (int c = 0; c < s->nrn; ++c) o[c] = s->rn->uniformReal(s->low[c], s->high[c]);
-        if (s->so3) s->so3->quaternion(o + s->nrn);
-    }
+    s->sample(n, out);
     return OMPL_GPU_OK;
 }
 

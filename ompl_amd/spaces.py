@@ -28,6 +28,14 @@ def _rv_extent(low, high) -> float:
     return math.sqrt(e)
 
 
+def _rv_measure(low, high) -> float:
+    # RealVectorStateSpace::getMeasure — RealVectorStateSpace.cpp:178-186
+    m = 1.0
+    for lo, hi in zip(low, high):
+        m *= hi - lo
+    return m
+
+
 class StateSpace:
     kind = -1
     dim = 0
@@ -47,6 +55,9 @@ class StateSpace:
             raise ValueError("The multiplicative factor for the valid segment count between two states must be "
                              "strictly positive")
         self.factor = int(factor)
+
+    def getMeasure(self) -> float:
+        raise NotImplementedError(type(self).__name__)
 
     def getMaximumExtent(self) -> float:
         raise NotImplementedError
@@ -82,6 +93,9 @@ class RealVectorStateSpace(StateSpace):
     def getMaximumExtent(self):
         return _rv_extent(self.low, self.high)
 
+    def getMeasure(self):
+        return _rv_measure(self.low, self.high)
+
 
 class SO3StateSpace(StateSpace):
     kind = abi.SPACE_SO3
@@ -92,6 +106,9 @@ class SO3StateSpace(StateSpace):
 
     def getMaximumExtent(self):
         return 0.5 * math.pi
+
+    def getMeasure(self):
+        return math.pi * math.pi  # SO3StateSpace.cpp:171-175
 
 
 class SE3StateSpace(StateSpace):
@@ -114,6 +131,10 @@ class SE3StateSpace(StateSpace):
     def getMaximumExtent(self):
         # CompoundStateSpace::getMaximumExtent — StateSpace.cpp:996-1003
         return self.weights[0] * _rv_extent(self.low, self.high) + self.weights[1] * (0.5 * math.pi)
+
+    def getMeasure(self):
+        # CompoundStateSpace::getMeasure (StateSpace.cpp:1005-1012): product of weighted components
+        return (self.weights[0] * _rv_measure(self.low, self.high)) * (self.weights[1] * (math.pi * math.pi))
 
     def lvs(self):
         return (_rv_extent(self.low, self.high) * self.fraction, (0.5 * math.pi) * self.fraction)
