@@ -12,31 +12,94 @@
 // by first_invalid: the first failing j in linear order, nd when only s2 fails.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace ompl_amd {
 
+// Kernels are specialised on the space kind SP and a compile-time state width DIM (DIM = 0:
+// the runtime width, up to kChainMaxLinks).  With DIM fixed every state array is indexed by
+// constants after unrolling and lives in registers; the generic form keeps them in scratch.
+// The arithmetic is the same code either way (device_space.h), so results are identical.
+template <int DIM>
+struct Width {
+    static constexpr int N = DIM > 0 ? DIM : kChainMaxLinks;
+};
+
+template <int DIM>
 __device__ __forceinline__ void load_state(const double *__restrict__ p, int dim, double *o) {
-    for (int c = 0; c < dim; ++c) o[c] = p[c];
+    if constexpr (DIM > 0) {
+#pragma unroll
+        for (int c = 0; c < DIM; ++c) o[c] = p[c];
+    } else {
+        for (int c = 0; c < dim; ++c) o[c] = p[c];
+    }
 }
 
-__global__ __launch_bounds__(256) void motion_kernel(DevSpace sp, DevChecker ck, const double *__restrict__ s1,
-                                                     const double *__restrict__ s2, uint32_t m,
-                                                     uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out,
-                                                     int32_t *__restrict__ fi_out,
-                                                     unsigned long long *__restrict__ counters, int rot) {
+// the space descriptor with the specialisation's constants folded in
+template <int SP, int DIM>
+__device__ __forceinline__ DevSpace fixed_space(DevSpace sp) {
+    if constexpr (DIM > 0) {
+        sp.kind = SP;
+        sp.dim = DIM;
+    }
+    return sp;
+}
+
+// HypercubeBenchmark's predicate (device_space.h hypercube_valid, HypercubeBenchmark.cpp:57-72)
+// unrolled over the fixed width: the reference's loop i = ndim - 1 .. 0 with the same early
+// exit (a violation decides the result; later indices no longer matter)
+template <int DIM>
+__device__ __forceinline__ bool hypercube_valid_fixed(const double *s, int ndim, double edge) {
+    bool found = false, ok = true;
+#pragma unroll
+    for (int i = DIM - 1; i >= 0; i--) {
+        if (i < ndim && ok) {
+            if (!found) {
+                if (s[i] > edge) found = true;
+            } else if (s[i] < (1. - edge)) {
+                ok = false;
+            }
+        }
+    }
+    return ok;
+}
+
+// is_valid (device_space.h) for the fixed forms, which never see the KinematicChain checker
+// (dispatch_width sends it to the runtime-width form)
+template <int DIM>
+__device__ __forceinline__ bool valid_t(const DevSpace &sp, const DevChecker &ck, const double *s) {
+    if constexpr (DIM > 0) {
+        switch (ck.kind) {
+        case OMPL_GPU_CHECK_ALL_VALID: return true;
+        case OMPL_GPU_CHECK_HYPERCUBE: return hypercube_valid_fixed<DIM>(s, ck.ndim, ck.edge);
+        case OMPL_GPU_CHECK_SPHERES: return spheres_valid(s, ck.data, ck.count);
+        default: return circles_valid(s, ck.data, ck.count);
+        }
+    } else {
+        return is_valid(sp, ck, s);
+    }
+}
+
+template <int SP, int DIM>
+__global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
+    DevSpace sp_in, DevChecker ck, const double *__restrict__ s1, const double *__restrict__ s2, uint32_t m,
+    uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out, int32_t *__restrict__ fi_out,
+    unsigned long long *__restrict__ counters, int rot) {
+    const DevSpace sp = fixed_space<SP, DIM>(sp_in);
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     bool result = true;
     uint32_t checks = 0;
     if (e < m) {
         const int dim = sp.dim;
-        double a[kChainMaxLinks], b[kChainMaxLinks], t[kChainMaxLinks];
-        load_state(s1 + (size_t)e * dim, dim, a);
-        load_state(s2 + (size_t)e * dim, dim, b);
+        double a[Width<DIM>::N], b[Width<DIM>::N], t[Width<DIM>::N];
+        load_state<DIM>(s1 + (size_t)e * dim, dim, a);
+        load_state<DIM>(s2 + (size_t)e * dim, dim, b);
         const int nd = (int)valid_segment_count(sp, a, b);
         if (nd_out) nd_out[e] = nd;
         ++checks;
-        result = is_valid(sp, ck, b);  // :96
+        result = valid_t<DIM>(sp, ck, b);  // :96
         if (result && nd >= 2) {
             // level-order walk of the FIFO bisection :104-134
             bool any = true;
@@ -62,7 +125,7 @@ __global__ __launch_bounds__(256) void motion_kernel(DevSpace sp, DevChecker ck,
                     const int mid = (lo + hi) / 2;
                     interpolate(sp, a, b, (double)mid / (double)nd, t, rot != 0);
                     ++checks;
-                    if (!is_valid(sp, ck, t)) result = false;
+                    if (!valid_t<DIM>(sp, ck, t)) result = false;
                 }
             }
         }
@@ -73,7 +136,7 @@ __global__ __launch_bounds__(256) void motion_kernel(DevSpace sp, DevChecker ck,
                 // linear sweep :57-69, then s2 :73-79
                 for (int j = 1; j < nd; ++j) {
                     interpolate(sp, a, b, (double)j / (double)nd, t, rot != 0);
-                    if (!is_valid(sp, ck, t)) {
+                    if (!valid_t<DIM>(sp, ck, t)) {
                         fi = j;
                         break;
                     }
@@ -101,13 +164,39 @@ __global__ __launch_bounds__(256) void motion_kernel(DevSpace sp, DevChecker ck,
     }
 }
 
-__global__ __launch_bounds__(256) void state_valid_kernel(DevSpace sp, DevChecker ck, const double *__restrict__ s,
-                                                          uint32_t m, uint8_t *__restrict__ valid) {
+template <int SP, int DIM>
+__global__ __launch_bounds__(256) __attribute__((flatten)) void state_valid_kernel(
+    DevSpace sp_in, DevChecker ck, const double *__restrict__ s, uint32_t m, uint8_t *__restrict__ valid) {
+    const DevSpace sp = fixed_space<SP, DIM>(sp_in);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
-    double a[kChainMaxLinks];
-    load_state(s + (size_t)i * sp.dim, sp.dim, a);
-    valid[i] = is_valid(sp, ck, a) ? 1 : 0;
+    double a[Width<DIM>::N];
+    load_state<DIM>(s + (size_t)i * sp.dim, sp.dim, a);
+    valid[i] = valid_t<DIM>(sp, ck, a) ? 1 : 0;
+}
+
+// the specialisations: SE3 (7 reals), SO3 (4), R^2 / R^3 / R^6 (the closed checker set's
+// spaces); everything else (other R^n, KinematicChain) takes the runtime-width form.  A
+// hypercube over more coordinates than the fixed width, and the KinematicChain checker, never
+// take a fixed form.
+template <class F>
+static hipError_t dispatch_width(const DevSpace &sp, const DevChecker &ck, F &&launch) {
+    const bool fixed_ok = (ck.kind == OMPL_GPU_CHECK_ALL_VALID || ck.kind == OMPL_GPU_CHECK_SPHERES ||
+                           ck.kind == OMPL_GPU_CHECK_CIRCLES2D ||
+                           (ck.kind == OMPL_GPU_CHECK_HYPERCUBE && ck.ndim <= sp.dim));
+    if (fixed_ok) {
+        if (sp.kind == OMPL_GPU_SPACE_SE3 && sp.dim == 7) return launch(std::integral_constant<int, OMPL_GPU_SPACE_SE3>{}, std::integral_constant<int, 7>{});
+        if (sp.kind == OMPL_GPU_SPACE_SO3 && sp.dim == 4) return launch(std::integral_constant<int, OMPL_GPU_SPACE_SO3>{}, std::integral_constant<int, 4>{});
+        if (sp.kind == OMPL_GPU_SPACE_REALVECTOR) {
+            switch (sp.dim) {
+            case 2: return launch(std::integral_constant<int, OMPL_GPU_SPACE_REALVECTOR>{}, std::integral_constant<int, 2>{});
+            case 3: return launch(std::integral_constant<int, OMPL_GPU_SPACE_REALVECTOR>{}, std::integral_constant<int, 3>{});
+            case 6: return launch(std::integral_constant<int, OMPL_GPU_SPACE_REALVECTOR>{}, std::integral_constant<int, 6>{});
+            default: break;
+            }
+        }
+    }
+    return launch(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
 }
 
 static bool needs_rotation(const DevSpace &sp, const DevChecker &ck) {
@@ -125,9 +214,12 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
                          uint8_t *valid, int32_t *nd, int32_t *first_invalid, unsigned long long *counters,
                          hipStream_t st) {
     if (m == 0) return hipSuccess;
-    hipLaunchKernelGGL(motion_kernel, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd,
-                       first_invalid, counters, needs_rotation(sp, ck) ? 1 : 0);
-    return hipGetLastError();
+    const int rot = needs_rotation(sp, ck) ? 1 : 0;
+    return dispatch_width(sp, ck, [&](auto kind, auto width) {
+        hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value>), dim3((m + 255) / 256),
+                           dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd, first_invalid, counters, rot);
+        return hipGetLastError();
+    });
 }
 
 // SpaceInformation::getMotionStates (SpaceInformation.cpp:201-275, alloc = true): thread per
@@ -152,8 +244,8 @@ __global__ __launch_bounds__(256) void motion_states_kernel(DevSpace sp, const d
     }
     const uint32_t j = endpoints ? k : k + 1;
     double x[kChainMaxLinks], y[kChainMaxLinks], r[kChainMaxLinks];
-    load_state(a, dim, x);
-    load_state(b, dim, y);
+    load_state<0>(a, dim, x);
+    load_state<0>(b, dim, y);
     interpolate(sp, x, y, (double)j / (double)(count + 1), r);
     for (int c = 0; c < dim; ++c) o[c] = r[c];
 }
@@ -171,8 +263,11 @@ hipError_t launch_motion_states(const DevSpace &sp, const double *s1, const doub
 hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const double *s, uint32_t m, uint8_t *valid,
                               hipStream_t st) {
     if (m == 0) return hipSuccess;
-    hipLaunchKernelGGL(state_valid_kernel, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s, m, valid);
-    return hipGetLastError();
+    return dispatch_width(sp, ck, [&](auto kind, auto width) {
+        hipLaunchKernelGGL((state_valid_kernel<decltype(kind)::value, decltype(width)::value>), dim3((m + 255) / 256),
+                           dim3(256), 0, st, sp, ck, s, m, valid);
+        return hipGetLastError();
+    });
 }
 
 }  // namespace ompl_amd
