@@ -617,7 +617,7 @@ __device__ __forceinline__ void wave_merge_sorted(float &Ld, uint32_t &Li, float
 constexpr int kBulkThreshold = 8;
 
 // K2: lanes per query in the output (16 / 32 / 64); k2 <= K2: the list length the walk keeps
-// (the certificate's margin: k + 2 for the culled spaces, whose screen error is small)
+// (the certificate's margin: k + 3 for the culled spaces, whose screen error is small)
 template <int SP, int F, int K2, int G, int MINW, bool QS>
 __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
@@ -1392,7 +1392,7 @@ __global__ void scatter_results_kernel(const double *__restrict__ d, const uint3
 // ---- host orchestration -----------------------------------------------------------------
 struct FastPlan {
     int K2, K;   // K2: lanes / slots per query list (16 / 32 / 64); K: the certificate's k bucket
-    int k2;      // entries the walk keeps (<= K2): k + 2 for the culled walks, K2 otherwise
+    int k2;      // entries the walk keeps (<= K2): k + 3 for the culled walks, K2 otherwise
     bool cull;
     uint32_t chunks, chunk_len;
 };
@@ -1403,9 +1403,11 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
     p.K = k_bucket(k);
     p.k2 = p.K2;
     p.cull = cull;
-    if (cull) {  // group walk: one list per query, k + 2 entries in the smallest slot bucket
-        p.k2 = (int)k + 2;
-        int lanes = k_bucket(k + 2);
+    if (cull) {  // group walk: one list per query, k + 3 entries in the smallest slot bucket
+        // k + 3: measured on cfg3 (SE3 10^6, k = 10, 10^5 queries), k + 2 left 250 of 10^5
+        // queries uncertified (a 90 us bounded re-run), k + 3 none, for +0.01 ms of walk
+        p.k2 = (int)k + 3;
+        int lanes = k_bucket(k + 3);
         if (lanes < 16) lanes = 16;
         if (p.K2 > 0 && lanes <= p.K2) p.K2 = lanes;
         p.chunks = 1;
