@@ -468,13 +468,16 @@ __global__ void store_soa_kernel(const double *__restrict__ aos, uint32_t n, int
     soa[c * cap + first + i] = aos[t];
 }
 
-__global__ void steer_kernel(DevSpace sp, const double *__restrict__ raw, uint64_t cap, const double *__restrict__ q,
+// SP / W: fixed-width form (device_space.h; W = 0: runtime width, states in scratch)
+template <int SP, int W>
+__global__ void steer_kernel(DevSpace sp_in, const double *__restrict__ raw, uint64_t cap, const double *__restrict__ q,
                              uint32_t nq, const uint32_t *__restrict__ nearest, uint32_t stride, double maxd,
                              double *__restrict__ from, double *__restrict__ to) {
+    const DevSpace sp = fixed_space<SP, W>(sp_in);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nq) return;
     const int dim = sp.dim;
-    double a[kChainMaxLinks], b[kChainMaxLinks], o[kChainMaxLinks];
+    double a[Width<W>::N], b[Width<W>::N], o[Width<W>::N];
     const uint32_t nid = nearest[(size_t)i * stride];
     for (int c = 0; c < dim; ++c) {
         a[c] = raw[(uint64_t)c * cap + nid];
@@ -829,8 +832,12 @@ hipError_t launch_steer(const DevSpace &sp, const double *raw, uint64_t cap, con
                         const uint32_t *nearest, uint32_t stride, double maxd, double *from, double *to,
                         hipStream_t st) {
     if (nq == 0) return hipSuccess;
-    hipLaunchKernelGGL(steer_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, sp, raw, cap, q, nq, nearest, stride,
-                       maxd, from, to);
+    if (sp.kind == OMPL_GPU_SPACE_SE3 && sp.dim == 7)
+        hipLaunchKernelGGL((steer_kernel<OMPL_GPU_SPACE_SE3, 7>), dim3((nq + 255) / 256), dim3(256), 0, st, sp, raw, cap,
+                           q, nq, nearest, stride, maxd, from, to);
+    else
+        hipLaunchKernelGGL((steer_kernel<0, 0>), dim3((nq + 255) / 256), dim3(256), 0, st, sp, raw, cap, q, nq, nearest,
+                           stride, maxd, from, to);
     return hipGetLastError();
 }
 

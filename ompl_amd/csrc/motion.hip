@@ -19,68 +19,7 @@
 namespace ompl_amd {
 
 // Kernels are specialised on the space kind SP and a compile-time state width DIM (DIM = 0:
-// the runtime width, up to kChainMaxLinks).  With DIM fixed every state array is indexed by
-// constants after unrolling and lives in registers; the generic form keeps them in scratch.
-// The arithmetic is the same code either way (device_space.h), so results are identical.
-template <int DIM>
-struct Width {
-    static constexpr int N = DIM > 0 ? DIM : kChainMaxLinks;
-};
-
-template <int DIM>
-__device__ __forceinline__ void load_state(const double *__restrict__ p, int dim, double *o) {
-    if constexpr (DIM > 0) {
-#pragma unroll
-        for (int c = 0; c < DIM; ++c) o[c] = p[c];
-    } else {
-        for (int c = 0; c < dim; ++c) o[c] = p[c];
-    }
-}
-
-// the space descriptor with the specialisation's constants folded in
-template <int SP, int DIM>
-__device__ __forceinline__ DevSpace fixed_space(DevSpace sp) {
-    if constexpr (DIM > 0) {
-        sp.kind = SP;
-        sp.dim = DIM;
-    }
-    return sp;
-}
-
-// HypercubeBenchmark's predicate (device_space.h hypercube_valid, HypercubeBenchmark.cpp:57-72)
-// unrolled over the fixed width: the reference's loop i = ndim - 1 .. 0 with the same early
-// exit (a violation decides the result; later indices no longer matter)
-template <int DIM>
-__device__ __forceinline__ bool hypercube_valid_fixed(const double *s, int ndim, double edge) {
-    bool found = false, ok = true;
-#pragma unroll
-    for (int i = DIM - 1; i >= 0; i--) {
-        if (i < ndim && ok) {
-            if (!found) {
-                if (s[i] > edge) found = true;
-            } else if (s[i] < (1. - edge)) {
-                ok = false;
-            }
-        }
-    }
-    return ok;
-}
-
-// is_valid (device_space.h) for the fixed forms, which never see the KinematicChain checker
-// (dispatch_width sends it to the runtime-width form)
-template <int DIM>
-__device__ __forceinline__ bool valid_t(const DevSpace &sp, const DevChecker &ck, const double *s) {
-    if constexpr (DIM > 0) {
-        switch (ck.kind) {
-        case OMPL_GPU_CHECK_ALL_VALID: return true;
-        case OMPL_GPU_CHECK_HYPERCUBE: return hypercube_valid_fixed<DIM>(s, ck.ndim, ck.edge);
-        case OMPL_GPU_CHECK_SPHERES: return spheres_valid(s, ck.data, ck.count);
-        default: return circles_valid(s, ck.data, ck.count);
-        }
-    } else {
-        return is_valid(sp, ck, s);
-    }
-}
+// the runtime width, up to kChainMaxLinks): device_space.h Width / fixed_space / valid_t.
 
 template <int SP, int DIM>
 __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(

@@ -70,17 +70,24 @@ __global__ __launch_bounds__(256) void rrt_scan_kernel(const double *__restrict_
 // (DiscreteMotionValidator.cpp:93-145) is the AND over s2 and the samples j / nd, whatever order
 // they are tested in.  Leaves s1 / s2 (the motion), *sh_ok (a neighbour exists) and *sh_bad (some
 // sample invalid) in LDS for every thread.
-template <class RowOf>
-__device__ void rrt_decide(RowOf row_of, const double *__restrict__ sample, uint32_t ri, const DevSpace &sp,
-                           const DevSpace &msp, const DevChecker &ck, double maxd, double *s1, double *s2, int *sh_nd,
+// fixed width of the persistent kernel's decider: SE3 states are 7 reals (the checkers allowed
+// with SE3 — mv_create — all have fixed forms); other spaces keep the runtime width
+template <int SP>
+constexpr int kRrtWidth = SP == OMPL_GPU_SPACE_SE3 ? 7 : 0;
+
+// SP / W: fixed-width form (device_space.h fixed_space; W = 0: runtime width)
+template <int SP, int W, class RowOf>
+__device__ void rrt_decide(RowOf row_of, const double *__restrict__ sample, uint32_t ri, const DevSpace &sp_in,
+                           const DevSpace &msp_in, const DevChecker &ck, double maxd, double *s1, double *s2, int *sh_nd,
                            int *sh_bad, int *sh_ok) {
+    const DevSpace sp = fixed_space<SP, W>(sp_in), msp = fixed_space<SP, W>(msp_in);
     const int dim = sp.dim;
     if (threadIdx.x == 0) {
         *sh_ok = ri != kNoId;
         *sh_bad = 0;
         *sh_nd = 0;
         if (ri != kNoId) {
-            double a[kChainMaxLinks], b[kChainMaxLinks], o[kChainMaxLinks];
+            double a[Width<W>::N], b[Width<W>::N], o[Width<W>::N];
             for (int c = 0; c < dim; ++c) {
                 a[c] = row_of(c);
                 b[c] = sample[c];
@@ -104,13 +111,20 @@ __device__ void rrt_decide(RowOf row_of, const double *__restrict__ sample, uint
         const int nd = *sh_nd;
         const int ns = nd > 1 ? nd : 1;
         for (int j = threadIdx.x; j < ns; j += blockDim.x) {
-            double t[kChainMaxLinks];
+            double t[Width<W>::N];
             if (j == 0) {
                 for (int c = 0; c < dim; ++c) t[c] = s2[c];
+            } else if constexpr (W > 0) {
+                double u[W], v[W];  // the motion's ends from LDS into registers
+                for (int c = 0; c < W; ++c) {
+                    u[c] = s1[c];
+                    v[c] = s2[c];
+                }
+                interpolate(msp, u, v, (double)j / (double)nd, t);
             } else {
                 interpolate(msp, s1, s2, (double)j / (double)nd, t);
             }
-            if (!is_valid(msp, ck, t)) *sh_bad = 1;
+            if (!valid_t<W>(msp, ck, t)) *sh_bad = 1;
         }
     }
     __syncthreads();
@@ -127,10 +141,12 @@ struct RrtGoal {
 // (~0: none), [1] approximate-solution distance bits (+inf initially), [2] its id
 constexpr int kGoalWords = 3;
 
-__device__ __forceinline__ bool rrt_goal_test(const RrtGoal &gl, const DevSpace &sp, const double *x, uint32_t id,
+template <int SP, int W>
+__device__ __forceinline__ bool rrt_goal_test(const RrtGoal &gl, const DevSpace &sp_in, const double *x, uint32_t id,
                                               uint32_t iter, uint64_t *rec) {
     if (!gl.goal) return false;
-    double g[kChainMaxLinks];
+    const DevSpace sp = fixed_space<SP, W>(sp_in);
+    double g[Width<W>::N];
     for (int c = 0; c < sp.dim; ++c) g[c] = gl.goal[c];
     const double d = raw_distance(sp, x, g);  // goal->isSatisfied(nmotion->state, &dist)  RRT.cpp:175
     if (d < gl.threshold) {
@@ -178,7 +194,7 @@ __global__ __launch_bounds__(256) void rrt_step_kernel(double *__restrict__ feat
     if (threadIdx.x == 0) sh_ri = ri;
     __syncthreads();
     ri = sh_ri;
-    rrt_decide([&](int c) { return feat[(uint64_t)c * cap + ri]; }, sample, ri, sp, msp, ck, maxd, s1, s2, &sh_nd,
+    rrt_decide<0, 0>([&](int c) { return feat[(uint64_t)c * cap + ri]; }, sample, ri, sp, msp, ck, maxd, s1, s2, &sh_nd,
                &sh_bad, &sh_ok);
     if (threadIdx.x == 0) {
         *nearest_out = ri;
@@ -188,7 +204,7 @@ __global__ __launch_bounds__(256) void rrt_step_kernel(double *__restrict__ feat
             rrt_append<F>(feat, feat32, rows32, cap, n, s2, sp.dim);
             *n_dev = n + 1;
             added = (uint32_t)n;
-            rrt_goal_test(gl, sp, s2, added, iter, grec);
+            rrt_goal_test<0, 0>(gl, sp, s2, added, iter, grec);
         }
         *added_out = added;
         if (counters && sh_ok) atomicAdd(&counters[sh_bad ? 1 : 0], 1ull);  // valid_ / invalid_
@@ -552,7 +568,8 @@ __global__ __launch_bounds__(256) void rrt_persistent_kernel(
         RRT_T(1);
         // 3. steer, check the motion, goal test (RRT.cpp:137-187)
         const uint32_t ri = gi;
-        rrt_decide([&](int c) { return sh_row[c]; }, sh_q, ri, sp, msp, ck, maxd, s1, s2, &sh_nd, &sh_bad, &sh_ok);
+        rrt_decide<SP, kRrtWidth<SP>>([&](int c) { return sh_row[c]; }, sh_q, ri, sp, msp, ck, maxd, s1, s2, &sh_nd,
+                                      &sh_bad, &sh_ok);
         if (threadIdx.x == 0) {
             uint64_t *dec = sync + kSyncDec + (j % kRing) * kDecWords;
             uint32_t added = kNoId;
@@ -564,7 +581,7 @@ __global__ __launch_bounds__(256) void rrt_persistent_kernel(
                 for (int f = 0; f < F; ++f) st_sync(&dec[8 + f], dbits(x[f]));
                 Bst = fmax(Bst, coord_absmax<SP, F>(x));
                 eta_st = fmax(eta_st, query_eta<SP>(x));
-                solved = rrt_goal_test(gl, sp, x, added, j, sync + kSyncGoal);
+                solved = rrt_goal_test<SP, kRrtWidth<SP>>(gl, sp, x, added, j, sync + kSyncGoal);
                 const int e = j % kLook;
                 for (int f = 0; f < F; ++f) xrow[e][f] = x[f];
                 xid[e] = added;
