@@ -614,6 +614,9 @@ class Runner:
             flop = {"cfg3": F_SE3, "cfg2": F_L2_6, "cfg4": F_CHAIN, "cfg5": F_SE3}[wl]
             dt = "f32" if kern_name.startswith("knn32") else "f64"
             what = f"{nq} x {n} (query, state) pairs per launch x {flop} flop (SURVEY §8d), brute force"
+            if kern_name == "knn32_wave_scan_kernel":
+                what += ("; every pair counted at the full 84 flop although a wave skips the remaining links once "
+                         "no lane's partial sum is below its list threshold (an upper bound of the work done)")
         achieved = pairs * flop / (kern_ms * 1e-3) / 1e12
         return {"bound": "valu", "achieved": achieved, "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
                 "frac": achieved / PEAK_TFLOPS[dt], "traffic": traffic["bytes"] if traffic else None,

@@ -859,6 +859,23 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             load_state((uint32_t)s * kSuperTiles + t, x, id);
         }
         if (sn >= 0) load_tbox((uint32_t)sn, bx);  // prefetch: bx is dead once lb / m exist
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 8
+        (void)tn;  // A/B build: no next-tile prefetch (fewer VGPRs)
+        (void)idn;
+        (void)xn;
+        while (have) {
+            scan_state(x, id, t, lb);
+            ++visited;
+            bool still = false;
+#pragma unroll
+            for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
+            m &= fold_tiles(__ballot(still));
+            if (!m) break;
+            t = __builtin_ctz(m);
+            m &= m - 1;
+            load_state((uint32_t)s * kSuperTiles + t, x, id);
+        }
+#else
         while (have) {
             const bool more = m != 0;
             if (more) {  // prefetch the next tile while this one is scanned
@@ -879,6 +896,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             id = idn;
             t = tn;
         }
+#endif
         s = sn;
     }
     if (counters && lane == 0) {
@@ -910,17 +928,6 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 // positions, chain_positions), and query g's K2-list lives across the wave (lane j = entry j).
 // The store is split in chunks along grid.y; the certificate merges the chunk lists.
 constexpr int kWaveGroup = 8;
-
-__device__ __forceinline__ float chain_dist32(const float *x, const float *q, int NM, float link, int nlinks) {
-    float acc = 0.f;
-    for (int i = 0; i < NM; ++i) {
-        if (i < nlinks) {
-            const float dx = x[i] - q[i], dy = x[NM + i] - q[NM + i];
-            acc += __builtin_amdgcn_sqrtf(fmaf(dy, dy, dx * dx));
-        }
-    }
-    return acc * link;
-}
 
 template <int F, int K2, int G>
 __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__restrict__ f32, uint64_t cap,
@@ -986,7 +993,33 @@ __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__rest
         const uint32_t id = (uint32_t)(base + lane);
         asm volatile("" : "+s"(qoff));
 #pragma unroll
-        for (int g = 0; g < G; ++g) offer(g, chain_dist32(x, &qrow[qoff + g * F], NM, link, nlinks), id);
+        for (int g = 0; g < G; ++g) {
+            // link * sum_i |P_i(a) - P_i(b)| (joint positions) with a wave-wide early exit: the partial sums only grow (fp32 addition
+            // of non-negative terms is monotone, so is the final * link), so once no lane's
+            // partial distance is below the threshold no lane's full distance is either, and
+            // the query's list could not change
+            // Two links per step on packed fp32 (v_pk_add / v_pk_mul / v_pk_fma: per element the
+            // same operations as fmaf(dy, dy, dx * dx), so the same bits); the sum stays in link order.
+            const float *qq = &qrow[qoff + g * F];
+            float acc = 0.f;
+            bool alive = true;
+            static_assert(NM % 2 == 0, "joint positions come in link pairs");
+#pragma unroll
+            for (int i = 0; i < NM; i += 2) {
+                if (i < nlinks) {
+                    const f2 dx = f2{x[i], x[i + 1]} - f2{qq[i], qq[i + 1]};
+                    const f2 dy = f2{x[NM + i], x[NM + i + 1]} - f2{qq[NM + i], qq[NM + i + 1]};
+                    const f2 s2 = pk_fma(dy, dy, dx * dx);
+                    acc += __builtin_amdgcn_sqrtf(s2.x);
+                    if (i + 1 < nlinks) acc += __builtin_amdgcn_sqrtf(s2.y);
+                }
+                if ((i & 3) == 2 && i + 2 < NM && i + 2 < nlinks && !__ballot(acc * link < td[g])) {
+                    alive = false;
+                    break;
+                }
+            }
+            if (alive) offer(g, acc * link, id);
+        }
         if (more) {
 #pragma unroll
             for (int f = 0; f < F; ++f) x[f] = xn[f];
@@ -1492,7 +1525,12 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             constexpr int G = group_queries<SP>();
-            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
+#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 8 || OMPL_AMD_VARIANT == 9)
+            constexpr int kMinW = 8;  // A/B build: 8 waves per SIMD (<= 64 VGPRs)
+#else
+            constexpr int kMinW = 1;
+#endif
+            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, kMinW, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
                                ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0,
                                q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, kBulkThreshold,
                                p.k2);

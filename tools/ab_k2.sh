@@ -6,9 +6,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/ab_k2; mkdir -p "$out"
 args="--steps 10 --warmup 3 --no-cpu-baseline --no-extras --single-query-reps 0 --rrt-iters 0"
+vars=${VARS:-5 6}
 for r in 1 2; do
   timeout -k 10 200 python -u bench.py $args > "$out/p_$r.json" 2>/dev/null || exit 1
-  for v in 5 6; do
+  for v in $vars; do
     OMPL_GPU_LIB=tools/bin/libompl_gpu_var$v.so timeout -k 10 200 python -u bench.py $args > "$out/v${v}_$r.json" 2>/dev/null || exit 1
   done
 done
