@@ -859,23 +859,6 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             load_state((uint32_t)s * kSuperTiles + t, x, id);
         }
         if (sn >= 0) load_tbox((uint32_t)sn, bx);  // prefetch: bx is dead once lb / m exist
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 8
-        (void)tn;  // A/B build: no next-tile prefetch (fewer VGPRs)
-        (void)idn;
-        (void)xn;
-        while (have) {
-            scan_state(x, id, t, lb);
-            ++visited;
-            bool still = false;
-#pragma unroll
-            for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
-            m &= fold_tiles(__ballot(still));
-            if (!m) break;
-            t = __builtin_ctz(m);
-            m &= m - 1;
-            load_state((uint32_t)s * kSuperTiles + t, x, id);
-        }
-#else
         while (have) {
             const bool more = m != 0;
             if (more) {  // prefetch the next tile while this one is scanned
@@ -896,7 +879,6 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             id = idn;
             t = tn;
         }
-#endif
         s = sn;
     }
     if (counters && lane == 0) {
@@ -1525,12 +1507,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             constexpr int G = group_queries<SP>();
-#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 8 || OMPL_AMD_VARIANT == 9)
-            constexpr int kMinW = 8;  // A/B build: 8 waves per SIMD (<= 64 VGPRs)
-#else
-            constexpr int kMinW = 1;
-#endif
-            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, kMinW, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
+            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
                                ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0,
                                q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, kBulkThreshold,
                                p.k2);
