@@ -57,3 +57,18 @@ def test_large_k_more_than_stored(gpu):
     oi, od, _ = O.knn(sp, data[keep], q, 299)
     assert_knn_parity(ids[:, :299], d[:, :299], keep[oi], od, 299)
     assert np.isinf(d[:, 299:]).all()
+
+
+def test_large_k_se3_rrtstar_1e6(gpu):
+    """M2(iii): RRT*'s k at the headline tree size, k = ceil(446.5 ln(n + 1)) = 6,169 at n = 10^6
+    (RRTstar.cpp:603-618), on the reference RNG streams, a few queries."""
+    sp = SE3StateSpace()
+    data, q = W.reference_states(sp, [1_000_000, 4], seed=42)
+    k_rrt = W.rrt_star_k(1_000_000, 6)
+    assert k_rrt == 6169
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    ids, d, cnt = nn.nearestKBatch(q, k_rrt)
+    assert (cnt == k_rrt).all()
+    oi, od, _ = O.knn(sp, data, q, k_rrt + 8)
+    assert_knn_parity(ids, d, oi, od, k_rrt)
