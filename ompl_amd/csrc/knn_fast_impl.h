@@ -1497,7 +1497,12 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys, idx,
                        (p.cull && ss) ? ss->nodes : nullptr, (p.cull && ss) ? ss->kd_tiles : 0u);
     size_t cb = L.cub_bytes;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + L.cub, cb, keys, keys2, idx, perm, (int)nq, 0, 32, st);
+    // home-tile keys are below kd_tiles: sort only their bits (half the radix passes at 10^6
+    // states); Morton keys use all 32
+    const bool home_keys = p.cull && ss && ss->nodes && ss->kd_tiles > 1;
+    const int key_bits = home_keys ? 32 - __builtin_clz(ss->kd_tiles - 1) : 32;
+    hipError_t e =
+        hipcub::DeviceRadixSort::SortPairs(ws + L.cub, cb, keys, keys2, idx, perm, (int)nq, 0, key_bits, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
     e = hipMemsetAsync(fail, 0, 4, st);
@@ -1640,8 +1645,9 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
         hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys,
                            idx, ss->nodes, ss->kd_tiles);
         size_t cb = L.cub_bytes;
-        if ((e = hipcub::DeviceRadixSort::SortPairs(ws + L.cub, cb, keys, keys2, idx, perm, (int)nq, 0, 32, st)) !=
-            hipSuccess)
+        const int key_bits = ss->nodes && ss->kd_tiles > 1 ? 32 - __builtin_clz(ss->kd_tiles - 1) : 32;  // home tiles
+        if ((e = hipcub::DeviceRadixSort::SortPairs(ws + L.cub, cb, keys, keys2, idx, perm, (int)nq, 0, key_bits,
+                                                    st)) != hipSuccess)
             return e;
         hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
         if ((e = hipMemsetAsync(counts + nq, 0, 8, st)) != hipSuccess) return e;
