@@ -495,7 +495,10 @@ static ompl_gpu_status ensure_sorted(ompl_gpu_nn *h) {
 // knn on device-resident features (queries already converted); caller holds the lock
 static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, size_t nq, uint32_t k, uint32_t *d_ids,
                                            double *d_dist) {
-    const bool large = k > 32 && large_k_supported(h->sp) && (h->fast || k > (uint32_t)kMaxK) && screen_safe(h);
+    // large-k path: every k above the register buckets; from 33 on where it beats them (not the
+    // chain, whose wave scan serves PRM*'s k <= 64 itself)
+    const bool mid_k = k > 32 && h->fast && h->sp.kind != OMPL_GPU_SPACE_KCHAIN;
+    const bool large = (k > (uint32_t)kMaxK || mid_k) && large_k_supported(h->sp) && screen_safe(h);
     if (k > (uint32_t)kMaxK && !large)
         return fail(OMPL_GPU_ERR_UNSUPPORTED, screen_safe(h) ? "k above 64 is not supported for this state space"
                                                              : "k above 64 needs stored coordinates below 1e18");
@@ -518,6 +521,10 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
             double e = 0.0;
             for (int c = 0; c < 3; ++c) e += (h->hi[c] - h->lo[c]) * (h->hi[c] - h->lo[c]);
             dmax = h->sp.w0 * std::sqrt(e) + h->sp.w1 * 0.5 * M_PI;
+        } else if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN) {
+            // link * sum_i |P_i(a) - P_i(b)| with |P_i| <= i: at most link * n (n + 1)
+            const double n = (double)h->sp.dim;
+            dmax = h->sp.link * n * (n + 1.0);
         } else {
             dmax = 2.0 * h->absmax * std::sqrt((double)h->sp.dim);
         }

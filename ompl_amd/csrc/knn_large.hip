@@ -41,10 +41,22 @@ __device__ __forceinline__ float abs1(float x) {
     return a > 1.f ? 1.f : a;
 }
 
-// fp32 screening distance (element row s, query row q)
+// fp32 screening distance (element row s, query row q); KinematicChain: rows are the joint
+// positions (knn_fast.hip chain rows), w0 = the link length, nl = the number of links
 template <int SP, int FS>
-__device__ __forceinline__ float d32(const float *s, const float *q, float w0, float w1) {
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+__device__ __forceinline__ float d32(const float *s, const float *q, float w0, float w1, int nl) {
+    if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+        constexpr int NM = FS / 2;
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+            if (i < nl) {
+                const float dx = s[i] - q[i], dy = s[NM + i] - q[NM + i];
+                acc += __builtin_amdgcn_sqrtf(fmaf(dy, dy, dx * dx));
+            }
+        }
+        return acc * w0;
+    } else if constexpr (SP == OMPL_GPU_SPACE_SE3) {
         const float dx = s[0] - q[0], dy = s[1] - q[1], dz = s[2] - q[2];
         float t = dx * dx;
         t = fmaf(dy, dy, t);
@@ -95,6 +107,17 @@ __global__ void rows32_kernel(const double *__restrict__ qf, uint32_t nq, float 
     if constexpr (SP == OMPL_GPU_SPACE_SE3) {
         o[0] = (float)s[0]; o[1] = (float)s[1]; o[2] = (float)s[2]; o[3] = 0.f;
         o[4] = (float)s[3]; o[5] = (float)s[4]; o[6] = (float)s[5]; o[7] = (float)s[6];
+    } else if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+        // joint positions: prefix sums of the cumulative cos / sin features in fp64, then
+        // rounded (the stored rows' recipe)
+        constexpr int NM = F / 2;
+        double cx = 0.0, cy = 0.0;
+        for (int i = 0; i < NM; ++i) {
+            cx += s[i];
+            cy += s[NM + i];
+            o[i] = (float)cx;
+            o[NM + i] = (float)cy;
+        }
     } else {
         for (int f = 0; f < FS; ++f) o[f] = (float)s[f];
     }
@@ -103,7 +126,7 @@ __global__ void rows32_kernel(const double *__restrict__ qf, uint32_t nq, float 
 template <int SP, int F>
 __global__ __launch_bounds__(256) void hist_kernel(const float *__restrict__ f32, uint64_t cap, uint64_t n_end,
                                                    const float *__restrict__ q32, uint32_t nq, uint32_t chunk_len,
-                                                   float w0, float w1, float inv_bin,
+                                                   float w0, float w1, int nl, float inv_bin,
                                                    unsigned int *__restrict__ hist) {
     constexpr int FS = Row<SP, F>::FS;
     __shared__ __attribute__((aligned(16))) float tile[kTile * FS];
@@ -118,7 +141,7 @@ __global__ __launch_bounds__(256) void hist_kernel(const float *__restrict__ f32
         stage_tile<SP, FS>(tile, f32, cap, base + threadIdx.x);
         __syncthreads();
         for (int s = 0; s < kTile; ++s) {
-            const float d = d32<SP, FS>(&tile[s * FS], qf, w0, w1);
+            const float d = d32<SP, FS>(&tile[s * FS], qf, w0, w1, nl);
             if (d == d) {  // NaN (removed / padding / idle thread) is not counted
                 const float x = d * inv_bin;
                 const int b = x < (float)(kBins - 1) ? (int)x : kBins - 1;
@@ -141,7 +164,11 @@ __device__ __forceinline__ double screen_err(const DevSpace &sp, double B, doubl
         e = sp.w0 * (6.0 * 1.7320508075688772 * kU * B) + 6.0 * kU * L + sp.w1 * (1.1 * sqrt(12.0 * kU) + 1e-6 + 4.5e-5);
     else if constexpr (SP == OMPL_GPU_SPACE_SO3)
         e = 1.1 * sqrt(12.0 * kU) + 1e-6 + 4.5e-5;
-    else
+    else if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {  // knn_fast_impl.h screen_error<KCHAIN>
+        const double n = (double)sp.dim;
+        e = sp.link * 8.0 * kU * n * (n + 1.0) + (n + 2.0) * kU * L + sp.link * n * sqrt(2.0 * 1.1754943508222875e-38);
+        return 2.0 * e;
+    } else
         e = 6.0 * sqrt((double)sp.dim) * kU * B + 6.0 * kU * L;
     e += sqrt(16.0 * 1.1754943508222875e-38);  // underflow of the squares (knn_fast_impl.h screen_error)
     return 2.0 * e;
@@ -164,7 +191,7 @@ __global__ void threshold_kernel(const unsigned int *__restrict__ hist, const do
     }
     const double r_hi = (double)(b + 1) * bin_w * (1.0 + 1e-5);  // slack for the float bin index
     double B = absmax;
-    const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_SO3 ? 0 : F);
+    const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_REALVECTOR ? F : 0);
     for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qf64[(size_t)q * F + c]));
     const double e = screen_err<SP>(sp, B, r_hi + 1.0);
     radius[q] = (float)((r_hi + 2.0 * e) * (1.0 + 16.0 * kU));
@@ -199,14 +226,15 @@ __global__ __launch_bounds__(256) void select_kernel(const float *__restrict__ f
         stage_tile<SP, FS>(tile, f32, cap, base + threadIdx.x);
         __syncthreads();
         for (int s = 0; s < kTile; ++s) {
-            const float d = d32<SP, FS>(&tile[s * FS], qf, (float)sp.w0, (float)sp.w1);
+            const float d = SP == OMPL_GPU_SPACE_KCHAIN ? d32<SP, FS>(&tile[s * FS], qf, (float)sp.link, 0.f, sp.dim)
+                                                        : d32<SP, FS>(&tile[s * FS], qf, (float)sp.w0, (float)sp.w1, 0);
             if (d <= r) {
                 if (FILL) {
                     const uint32_t id = (uint32_t)(base + s);
                     double sv[F];
 #pragma unroll
                     for (int f = 0; f < F; ++f) sv[f] = f64[(uint64_t)f * cap + id];
-                    od[out] = feat_dist<SP, F, 0>(sv, qv, sp);
+                    od[out] = feat_dist<SP, F, SP == OMPL_GPU_SPACE_KCHAIN ? F / 2 : 0>(sv, qv, sp);
                     oi[out] = id;
                     ++out;
                 } else {
@@ -282,8 +310,9 @@ hipError_t run_large(const DevSpace &sp, const double *f64, const float *f32, ui
     hipLaunchKernelGGL((rows32_kernel<SP, F>), dim3((nq + 255) / 256), dim3(256), 0, st, qf64, nq, q32);
     const dim3 grid((nq + kTile - 1) / kTile, p.chunks);
     timer_begin(st, "hist_kernel");
-    hipLaunchKernelGGL((hist_kernel<SP, F>), grid, dim3(kTile), 0, st, f32, cap, n_end, q32, nq, p.chunk_len,
-                       (float)sp.w0, (float)sp.w1, 1.0f / bin_w, hist);
+    const float w0 = SP == OMPL_GPU_SPACE_KCHAIN ? (float)sp.link : (float)sp.w0;
+    hipLaunchKernelGGL((hist_kernel<SP, F>), grid, dim3(kTile), 0, st, f32, cap, n_end, q32, nq, p.chunk_len, w0,
+                       (float)sp.w1, sp.dim, 1.0f / bin_w, hist);
     timer_end(st);
     hipLaunchKernelGGL((threshold_kernel<SP, F>), dim3((nq + 255) / 256), dim3(256), 0, st, hist, qf64, nq, k, bin_w,
                        absmax, sp, radius);
@@ -368,7 +397,10 @@ hipError_t run_large(const DevSpace &sp, const double *f64, const float *f32, ui
 
 }  // namespace
 
-bool large_k_supported(const DevSpace &sp) { return sp.kind != OMPL_GPU_SPACE_KCHAIN; }
+bool large_k_supported(const DevSpace &sp) {
+    return sp.kind == OMPL_GPU_SPACE_SE3 || sp.kind == OMPL_GPU_SPACE_SO3 || sp.kind == OMPL_GPU_SPACE_REALVECTOR ||
+           sp.kind == OMPL_GPU_SPACE_KCHAIN;
+}
 
 hipError_t launch_knn_large(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32,
                             uint64_t cap, uint64_t n_end, const double *qfeat64, uint32_t nq, uint32_t k, float absmax,
@@ -391,6 +423,17 @@ hipError_t launch_knn_large(const DevSpace &sp, const FeatGeom &g, const double 
                                                             dmax, out_d, out_i, mem_budget, num_cus, st);
         return run_large<OMPL_GPU_SPACE_REALVECTOR, 16>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, dmax,
                                                          out_d, out_i, mem_budget, num_cus, st);
+    case OMPL_GPU_SPACE_KCHAIN:  // features: cos / sin of the cumulative angles, nmax links each
+#define OMPL_AMD_LARGE_CHAIN(NMX)                                                                                  \
+    if (g.nmax == NMX)                                                                                             \
+        return run_large<OMPL_GPU_SPACE_KCHAIN, 2 * NMX>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, dmax, \
+                                                         out_d, out_i, mem_budget, num_cus, st);
+        OMPL_AMD_LARGE_CHAIN(4)
+        OMPL_AMD_LARGE_CHAIN(8)
+        OMPL_AMD_LARGE_CHAIN(12)
+        OMPL_AMD_LARGE_CHAIN(16)
+#undef OMPL_AMD_LARGE_CHAIN
+        return hipErrorInvalidValue;
     }
     return hipErrorInvalidValue;
 }

@@ -6,7 +6,7 @@ import pytest
 import pyoracle as O
 from ompl_amd import NearestNeighborsGPU
 from ompl_amd import workloads as W
-from ompl_amd.spaces import RealVectorStateSpace, SE3StateSpace, SO3StateSpace
+from ompl_amd.spaces import KinematicChainSpace, RealVectorStateSpace, SE3StateSpace, SO3StateSpace
 from parity import assert_knn_parity
 
 pytestmark = pytest.mark.gpu
@@ -29,13 +29,15 @@ def test_large_k_se3_rrtstar(gpu, nq):
         assert_knn_parity(ids, d, oi, od, k)
 
 
-@pytest.mark.parametrize("name", ["r6", "so3"])
+@pytest.mark.parametrize("name", ["r6", "so3", "chain12"])
 def test_large_k_other_spaces(gpu, name):
     rng = np.random.default_rng(7)
     if name == "r6":
         sp, data, q = RealVectorStateSpace(6), W.uniform_rv(rng, 50000, 6), W.uniform_rv(rng, 100, 6)
-    else:
+    elif name == "so3":
         sp, data, q = SO3StateSpace(), W.uniform_quat(rng, 50000), W.uniform_quat(rng, 100)
+    else:  # KinematicChain R^12 (RRT* on the chain: k in the thousands)
+        sp, data, q = KinematicChainSpace(12, 1.0 / 12), W.uniform_chain(rng, 50000, 12), W.uniform_chain(rng, 100, 12)
     nn = NearestNeighborsGPU(sp, gpu)
     nn.add(data)
     oi, od, _ = O.knn(sp, data, q, 508)

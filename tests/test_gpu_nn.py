@@ -129,10 +129,14 @@ def test_k_edge_cases(gpu):
     assert nn.nearestR(data[3], float("inf"))[0] == 3
     ids, d, cnt = nn.nearestKBatch(data[3:5], 65)         # large-k path: k > n -> n results
     assert (cnt == 50).all() and list(ids[0, :50]) == [int(x) for x in oi[0]]
-    ch = NearestNeighborsGPU(KinematicChainSpace(12, 1 / 12), gpu)
-    ch.add(W.uniform_chain(rng, 100, 12))
-    with pytest.raises(abi.GpuError):
-        ch.nearestKBatch(W.uniform_chain(rng, 2, 12), 65)  # chain: register buckets only (k <= 64)
+    csp = KinematicChainSpace(12, 1 / 12)
+    ch = NearestNeighborsGPU(csp, gpu)
+    cdata, cq = W.uniform_chain(rng, 100, 12), W.uniform_chain(rng, 2, 12)
+    ch.add(cdata)
+    ids, d, cnt = ch.nearestKBatch(cq, 65)                 # chain, large-k path
+    oi, od, _ = O.knn(csp, cdata, cq, 65)
+    assert (cnt == 65).all()
+    assert_knn_parity(ids, d, oi, od, 65)
 
 
 def test_remove_and_clear(gpu, path):
