@@ -35,10 +35,12 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
         double a[Width<DIM>::N], b[Width<DIM>::N], t[Width<DIM>::N];
         load_state<DIM>(s1 + (size_t)e * dim, dim, a);
         load_state<DIM>(s2 + (size_t)e * dim, dim, b);
-        const int nd = (int)valid_segment_count(sp, a, b);
-        if (nd_out) nd_out[e] = nd;
         ++checks;
-        result = valid_t<DIM>(sp, ck, b);  // :96
+        result = valid_t<DIM>(sp, ck, b);  // :96 — s2 first, as the reference
+        // the segment count (an arc cosine for SE3) only when something reads it: the sweep of a
+        // motion whose s2 is valid, the lastValid sweep, or the caller
+        const int nd = (result || nd_out || fi_out) ? (int)valid_segment_count(sp, a, b) : 0;
+        if (nd_out) nd_out[e] = nd;
         if (result && nd >= 2) {
             // level-order walk of the FIFO bisection :104-134
             bool any = true;

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/ab_k2; mkdir -p "$out"
-args="--steps 10 --warmup 3 --no-cpu-baseline --no-extras --single-query-reps 0 --rrt-iters 0"
+args="--workload ${WL:-cfg3} --steps 10 --warmup 3 --no-cpu-baseline --no-extras --single-query-reps 0 --rrt-iters 0"
 vars=${VARS:-5 6}
 for r in 1 2; do
   timeout -k 10 200 python -u bench.py $args > "$out/p_$r.json" 2>/dev/null || exit 1
@@ -17,6 +17,6 @@ for f in "$out"/*.json; do
   python - "$f" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print(sys.argv[1].split('/')[-1], round(d["value"] / 1e6, 2), "M/s step", round(d["ms_per_step"], 4), "walk", round(d["roofline"]["kernel_ms"], 4), "nn", round(d["phase_ms"]["nn"], 4), "reruns", d["fast_path"]["exact_reruns"])
+print(sys.argv[1].split("/")[-1], round(d["value"] / 1e6, 2), "M/s step", round(d["ms_per_step"], 4), "walk", round(d["roofline"]["kernel_ms"], 4), "phases", d["phase_ms"])
 PY
 done
