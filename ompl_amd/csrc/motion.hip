@@ -97,10 +97,20 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
             ni += __shfl_xor(ni, off, 64);
             nc += __shfl_xor(nc, off, 64);
         }
+        // then block-aggregated: one atomic per counter per block — same-address atomics from
+        // every wave of the grid serialise at the L2 and cost more than the checks themselves
+        __shared__ unsigned long long part[3][4];
+        const int w = threadIdx.x >> 6;
         if ((threadIdx.x & 63) == 0) {
-            if (nv) atomicAdd(&counters[0], nv);
-            if (ni) atomicAdd(&counters[1], ni);
-            if (nc) atomicAdd(&counters[2], nc);
+            part[0][w] = nv;
+            part[1][w] = ni;
+            part[2][w] = nc;
+        }
+        __syncthreads();
+        if (threadIdx.x < 3) {
+            unsigned long long v = 0;
+            for (int i = 0; i < (int)(blockDim.x >> 6); ++i) v += part[threadIdx.x][i];
+            if (v) atomicAdd(&counters[threadIdx.x], v);
         }
     }
 }
