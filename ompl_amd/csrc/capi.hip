@@ -485,8 +485,9 @@ static ompl_gpu_status ensure_sorted(ompl_gpu_nn *h) {
         h->sorted_builds++;
     }
     if (!h->cull_counter.p) {
-        HIP_OR_FAIL(h->cull_counter.ensure(kCullCounters * sizeof(unsigned long long)));
-        HIP_OR_FAIL(hipMemsetAsync(h->cull_counter.p, 0, kCullCounters * sizeof(unsigned long long), h->stream));
+        const size_t bytes = sizeof(unsigned long long) * kCounterSlots * kCounterStride;
+        HIP_OR_FAIL(h->cull_counter.ensure(bytes));
+        HIP_OR_FAIL(hipMemsetAsync(h->cull_counter.p, 0, bytes, h->stream));
     }
     s.counters = (unsigned long long *)h->cull_counter.p;
     return OMPL_GPU_OK;
@@ -917,15 +918,28 @@ ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries
     return OMPL_GPU_OK;
 }
 
+
+// the walk counters summed over their slot copies (kernels.h kCounterSlots); caller holds the lock
+static ompl_gpu_status read_cull_counters(ompl_gpu_nn *h, unsigned long long (&c)[kCullCounters]) {
+    for (auto &v : c) v = 0;
+    if (!h->cull_counter.p) return OMPL_GPU_OK;
+    std::vector<unsigned long long> all((size_t)kCounterSlots * kCounterStride);
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(hipMemcpyAsync(all.data(), h->cull_counter.p, sizeof(unsigned long long) * all.size(),
+                               hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    for (int sl = 0; sl < kCounterSlots; ++sl)
+        for (int i = 0; i < kCullCounters; ++i) c[i] += all[(size_t)sl * kCounterStride + i];
+    return OMPL_GPU_OK;
+}
+
 #ifdef OMPL_AMD_PROBE
 // probe build only: the raw walk counters
 extern "C" ompl_gpu_status ompl_gpu_probe_counters(ompl_gpu_nn *h, uint64_t *out, int n) {
     std::lock_guard<std::mutex> lk(h->mu);
-    unsigned long long c[kCullCounters] = {};
-    if (h->cull_counter.p) {
-        HIP_OR_FAIL(hipMemcpyAsync(c, h->cull_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
-        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
-    }
+    unsigned long long c[kCullCounters];
+    ompl_gpu_status st = read_cull_counters(h, c);
+    if (st != OMPL_GPU_OK) return st;
     for (int i = 0; i < n && i < kCullCounters; ++i) out[i] = c[i];
     return OMPL_GPU_OK;
 }
@@ -934,12 +948,9 @@ extern "C" ompl_gpu_status ompl_gpu_probe_counters(ompl_gpu_nn *h, uint64_t *out
 ompl_gpu_status ompl_gpu_nn_radius_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *query_tiles) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
-    unsigned long long c[kCullCounters] = {0, 0, 0, 0, 0};
-    if (h->cull_counter.p) {
-        HIP_OR_FAIL(hipSetDevice(h->device));
-        HIP_OR_FAIL(hipMemcpyAsync(c, h->cull_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
-        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
-    }
+    unsigned long long c[kCullCounters];
+    ompl_gpu_status st = read_cull_counters(h, c);
+    if (st != OMPL_GPU_OK) return st;
     if (tiles_scanned) *tiles_scanned = c[3];
     if (query_tiles) *query_tiles = c[4];
     return OMPL_GPU_OK;
@@ -1000,12 +1011,9 @@ ompl_gpu_status ompl_gpu_nn_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, 
                                        uint64_t *query_tiles) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
     std::lock_guard<std::mutex> lk(h->mu);
-    unsigned long long c[kCullCounters] = {0, 0, 0, 0, 0};
-    if (h->cull_counter.p) {
-        HIP_OR_FAIL(hipSetDevice(h->device));
-        HIP_OR_FAIL(hipMemcpyAsync(c, h->cull_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
-        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
-    }
+    unsigned long long c[kCullCounters];
+    ompl_gpu_status st = read_cull_counters(h, c);
+    if (st != OMPL_GPU_OK) return st;
     if (tiles_scanned) *tiles_scanned = c[0];
     if (tiles_total) *tiles_total = c[1];
     if (query_tiles) *query_tiles = c[2];

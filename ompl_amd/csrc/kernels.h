@@ -11,6 +11,10 @@ namespace ompl_amd {
 
 constexpr int kTile = 256;          // states per LDS tile / threads per block
 constexpr int kMaxK = 64;           // largest register top-K bucket
+// walk statistics counters (SortedStore::counters): kCounterSlots copies of kCounterStride words,
+// a wave adds into copy blockIdx.x % kCounterSlots (same-address atomics from every wave of a
+// 25,000-wave launch would serialise at the L2); readers sum the copies
+constexpr int kCounterSlots = 64, kCounterStride = 16;
 constexpr uint32_t kStreamMaxQ = 64; // below this many queries the stream mapping is used
 
 // Optional HIP-event bracket around the dominant kernel of a launch (the scan), armed by

@@ -882,15 +882,16 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         s = sn;
     }
     if (counters && lane == 0) {
-        atomicAdd(&counters[0], (unsigned long long)visited);  // tiles scanned
-        atomicAdd(&counters[1], (unsigned long long)ntiles);   // tiles of a brute-force walk
-        atomicAdd(&counters[2], (unsigned long long)qscans);   // (tile, query) pairs scanned
+        unsigned long long *cs = counters + (blockIdx.x % kCounterSlots) * kCounterStride;
+        atomicAdd(&cs[0], (unsigned long long)visited);  // tiles scanned
+        atomicAdd(&cs[1], (unsigned long long)ntiles);   // tiles of a brute-force walk
+        atomicAdd(&cs[2], (unsigned long long)qscans);   // (tile, query) pairs scanned
 #ifdef OMPL_AMD_PROBE
-        atomicAdd(&counters[5], (unsigned long long)pr_offers);
-        atomicAdd(&counters[6], (unsigned long long)pr_bulk);
-        atomicAdd(&counters[7], (unsigned long long)pr_ins);
-        atomicAdd(&counters[8], (unsigned long long)pr_supers);
-        atomicAdd(&counters[9], (unsigned long long)pr_rounds);
+        atomicAdd(&cs[5], (unsigned long long)pr_offers);
+        atomicAdd(&cs[6], (unsigned long long)pr_bulk);
+        atomicAdd(&cs[7], (unsigned long long)pr_ins);
+        atomicAdd(&cs[8], (unsigned long long)pr_supers);
+        atomicAdd(&cs[9], (unsigned long long)pr_rounds);
 #endif
     }
 #pragma unroll
@@ -1372,8 +1373,9 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
                 if (g0 + g < nq) counts[qo[g]] = cnt[g];
         }
         if (MODE != 0 && counters) {
-            atomicAdd(&counters[3], (unsigned long long)visited);  // tiles fetched by the radius walk
-            atomicAdd(&counters[4], (unsigned long long)qscans);   // (tile, query) pairs scanned
+            unsigned long long *cs = counters + (blockIdx.x % kCounterSlots) * kCounterStride;
+            atomicAdd(&cs[3], (unsigned long long)visited);  // tiles fetched by the radius walk
+            atomicAdd(&cs[4], (unsigned long long)qscans);   // (tile, query) pairs scanned
         }
     }
 }
