@@ -117,6 +117,7 @@ struct ompl_gpu_nn {
     // its Morton-ordered tail, removals are tombstoned in place (kernels.h SortedStore)
     SortedStore sorted;
     DevBuf raw_aos;         // [n_total][da] fp64 raw states by id (edge endpoints), appended lazily
+    DevBuf edge_q;          // per-edge CSR segment (query) of ompl_gpu_nn_edges_device
     uint64_t aos_n = 0;     // ids [0, aos_n) converted
     uint64_t sorted_builds = 0, sorted_appends = 0;  // device k-d builds / tail appends
     bool cull = true;         // ompl_gpu_nn_set_exact(h, 2) disables the culled screen
@@ -913,8 +914,13 @@ ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries
         ompl_gpu_status s = ensure_aos(h);
         if (s != OMPL_GPU_OK) return s;
     }
+    uint32_t *qidx = nullptr;  // the CSR segment of every edge (edge_query_kernel)
+    if (d_offsets) {
+        HIP_OR_FAIL(h->edge_q.ensure(sizeof(uint32_t) * m));
+        qidx = (uint32_t *)h->edge_q.p;
+    }
     HIP_OR_FAIL(launch_edges(h->sp, h->raw, h->cap, d_queries, (uint32_t)nq, d_offsets, d_ids, stride, m, from_query,
-                             d_from, d_to, h->stream, h->n_total ? (const double *)h->raw_aos.p : nullptr, da));
+                             d_from, d_to, h->stream, h->n_total ? (const double *)h->raw_aos.p : nullptr, da, qidx));
     return OMPL_GPU_OK;
 }
 

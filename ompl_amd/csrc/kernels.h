@@ -211,7 +211,7 @@ hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_
 // aos (optional): [n][da] copy of the raw states (launch_aos_rows), read instead of the SoA store
 hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
                         const uint64_t *offsets, const uint32_t *ids, uint32_t stride, uint64_t m, int from_query,
-                        double *from, double *to, hipStream_t st, const double *aos = nullptr, int da = 0);
+                        double *from, double *to, hipStream_t st, const double *aos, int da, uint32_t *qidx);
 // rows of ids [first, first + n) of the SoA store into aos[id][da]
 hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uint64_t first, uint64_t n, double *aos,
                            hipStream_t st);

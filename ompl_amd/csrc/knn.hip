@@ -802,12 +802,44 @@ hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_
     return hipGetLastError();
 }
 
+// CSR segment of every edge: qidx[e] = q for off[q] <= e < off[q + 1] (thread per query)
+__global__ void edge_query_kernel(const uint64_t *__restrict__ off, uint32_t nq, uint32_t *__restrict__ qidx) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    for (uint64_t e = off[q], e1 = off[q + 1]; e < e1; ++e) qidx[e] = q;
+}
+
+// thread per (edge, coordinate): consecutive threads write consecutive reals of the AoS
+// endpoint rows (edges_kernel's per-edge threads wrote 56-B strided rows and binary-searched
+// the CSR per edge)
+__global__ void edges_copy_kernel(const double *__restrict__ raw, uint64_t cap, int dim, const double *__restrict__ q,
+                                  const uint32_t *__restrict__ qidx, const uint32_t *__restrict__ ids,
+                                  uint32_t stride, uint64_t m, int from_query, double *__restrict__ from,
+                                  double *__restrict__ to, const double *__restrict__ aos, int da) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m * (uint64_t)dim) return;
+    const uint64_t e = t / (uint64_t)dim;
+    const int c = (int)(t - e * (uint64_t)dim);
+    const uint32_t qi = qidx ? qidx[e] : (uint32_t)(e / stride);
+    const uint32_t id = ids[e];
+    const double qv = q[(size_t)qi * dim + c];
+    (from_query ? from : to)[t] = qv;
+    (from_query ? to : from)[t] = id == kNoId ? qv : (aos ? aos[(uint64_t)id * da + c] : raw[(uint64_t)c * cap + id]);
+}
+
 hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
                         const uint64_t *offsets, const uint32_t *ids, uint32_t stride, uint64_t m, int from_query,
-                        double *from, double *to, hipStream_t st, const double *aos, int da) {
+                        double *from, double *to, hipStream_t st, const double *aos, int da, uint32_t *qidx) {
     if (m == 0) return hipSuccess;
-    hipLaunchKernelGGL(edges_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, sp, raw, cap, q, nq, offsets,
-                       ids, stride, m, from_query, from, to, aos, da);
+    if (offsets && !qidx) {  // no scratch: the per-edge search form
+        hipLaunchKernelGGL(edges_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, sp, raw, cap, q, nq,
+                           offsets, ids, stride, m, from_query, from, to, aos, da);
+        return hipGetLastError();
+    }
+    if (offsets) hipLaunchKernelGGL(edge_query_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, offsets, nq, qidx);
+    const uint64_t n = m * (uint64_t)sp.dim;
+    hipLaunchKernelGGL(edges_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, raw, cap, sp.dim, q,
+                       offsets ? qidx : nullptr, ids, stride, m, from_query, from, to, aos, da);
     return hipGetLastError();
 }
 
