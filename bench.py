@@ -803,6 +803,15 @@ def main():
         if rrt:
             line["rrt_device"] = rrt
         print(json.dumps(line), flush=True)
+    # release every library handle while the HIP runtime (and a profiler attached to it) is up
+    torch.cuda.synchronize(dev)
+    from ompl_amd import abi
+    abi.close_all()
+    torch.cuda.synchronize(dev)
+    maps = os.environ.get("OMPL_AMD_MAPS")  # library load addresses, to symbolise an exit-time fault
+    if maps:
+        with open("/proc/self/maps") as fi, open(maps, "w") as fo:
+            fo.write(fi.read())
     if dist:
         dist.destroy_process_group()
 

@@ -222,7 +222,8 @@ ompl_gpu_status ompl_gpu_nn_radius_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_sc
  * (d_queries, AoS) with stored state d_ids[e]: e in [d_offsets[q], d_offsets[q+1]) for a CSR
  * result (nn_radius_device), or, with d_offsets NULL, e = q * stride + j for a dense
  * nq x stride id matrix (nn_knn_device; m == nq * stride).  A missing id (0xFFFFFFFF)
- * pairs q with itself.  Writes m AoS rows to d_from / d_to; asynchronous. */
+ * pairs q with itself.  Writes m AoS rows to d_from / d_to; asynchronous.  With a CSR,
+ * m may differ from d_offsets[nq]: only edges e < min(m, d_offsets[nq]) are written. */
 ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries, size_t nq, const uint64_t *d_offsets,
                                          const uint32_t *d_ids, uint32_t stride, size_t m, int from_query,
                                          double *d_from, double *d_to);

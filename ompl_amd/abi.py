@@ -6,8 +6,11 @@ every handle constructor raises :class:`GpuError` (``OMPL_GPU_ERR_DEVICE``).
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
+import itertools
 import os
+import weakref
 
 import numpy as np
 
@@ -184,3 +187,65 @@ def as_states(x, dim: int) -> np.ndarray:
     if a.shape[-1] != dim:
         raise ValueError(f"expected states with {dim} reals, got shape {a.shape}")
     return a
+
+
+# ---- handle lifetime -------------------------------------------------------------
+# Every C handle is released by close() (idempotent), by __del__, or — for the ones still
+# alive when the interpreter exits — by the atexit hook below, newest first, while the HIP
+# runtime (and a profiler attached to it) is still up.  After that hook no destroy call
+# runs: a handle left to the C library's static teardown would call into a HIP runtime
+# that may already be gone (round-2 exit-time SIGSEGV under rocprofv3).
+_live: dict = {}
+_serial = itertools.count()
+_closed_all = False
+
+
+class Handle:
+    """Owner of one C handle (`_h`) released with the C function named `_destroy_fn`."""
+
+    _destroy_fn = ""
+    _h = None
+
+    def _own(self, h) -> None:
+        self._h = h
+        self._serial = next(_serial)
+        _live[self._serial] = weakref.ref(self)
+
+    def close(self) -> None:
+        h = self._h
+        self._h = None
+        if h is not None and h.value and not _closed_all:
+            self._destroy(h)
+        _live.pop(getattr(self, "_serial", None), None)
+
+    def _destroy(self, h) -> None:
+        getattr(lib, self._destroy_fn)(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter teardown: modules may already be cleared
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+
+def close_all() -> None:
+    """Destroy every live handle, newest first (samplers / validators before the NN
+    structures they were created after).  Registered with atexit."""
+    global _closed_all
+    for key in sorted(_live, reverse=True):
+        ref = _live.get(key)
+        obj = ref() if ref is not None else None
+        if obj is not None:
+            obj.close()
+    _live.clear()
+    _closed_all = True
+
+
+atexit.register(close_all)

@@ -802,11 +802,18 @@ hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_
     return hipGetLastError();
 }
 
-// CSR segment of every edge: qidx[e] = q for off[q] <= e < off[q + 1] (thread per query)
-__global__ void edge_query_kernel(const uint64_t *__restrict__ off, uint32_t nq, uint32_t *__restrict__ qidx) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= nq) return;
-    for (uint64_t e = off[q], e1 = off[q + 1]; e < e1; ++e) qidx[e] = q;
+// CSR segment of every edge: qidx[e] = q for off[q] <= e < min(off[q + 1], m); edges past
+// off[nq] get kNoId (left unwritten by edges_copy_kernel).  A wave per segment (grid-stride),
+// so a query with 10^5 neighbours is written 64 entries per step, not by one lane.
+__global__ void edge_query_kernel(const uint64_t *__restrict__ off, uint32_t nq, uint64_t m,
+                                  uint32_t *__restrict__ qidx) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t q = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; q <= nq; q += nw) {
+        const uint64_t e0 = off[q], e1 = q < nq ? min(off[q + 1], m) : m;
+        const uint32_t v = q < nq ? q : kNoId;
+        for (uint64_t e = e0 + lane; e < e1; e += 64) qidx[e] = v;
+    }
 }
 
 // thread per (edge, coordinate): consecutive threads write consecutive reals of the AoS
@@ -821,6 +828,7 @@ __global__ void edges_copy_kernel(const double *__restrict__ raw, uint64_t cap, 
     const uint64_t e = t / (uint64_t)dim;
     const int c = (int)(t - e * (uint64_t)dim);
     const uint32_t qi = qidx ? qidx[e] : (uint32_t)(e / stride);
+    if (qi == kNoId) return;  // past the CSR's last segment
     const uint32_t id = ids[e];
     const double qv = q[(size_t)qi * dim + c];
     (from_query ? from : to)[t] = qv;
@@ -836,7 +844,9 @@ hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, con
                            offsets, ids, stride, m, from_query, from, to, aos, da);
         return hipGetLastError();
     }
-    if (offsets) hipLaunchKernelGGL(edge_query_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, offsets, nq, qidx);
+    if (offsets)
+        hipLaunchKernelGGL(edge_query_kernel, dim3(std::min<uint32_t>(nq / 4 + 1, 8192)), dim3(256), 0, st, offsets, nq,
+                           (uint64_t)m, qidx);
     const uint64_t n = m * (uint64_t)sp.dim;
     hipLaunchKernelGGL(edges_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, raw, cap, sp.dim, q,
                        offsets ? qidx : nullptr, ids, stride, m, from_query, from, to, aos, da);

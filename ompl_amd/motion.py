@@ -13,7 +13,9 @@ from .checkers import Checker
 from .spaces import StateSpace
 
 
-class DiscreteMotionValidatorGPU:
+class DiscreteMotionValidatorGPU(abi.Handle):
+    _destroy_fn = "ompl_gpu_mv_destroy"
+
     def __init__(self, space: StateSpace, checker: Checker, device: int = 0):
         self.space = space
         self.checker = checker
@@ -23,13 +25,7 @@ class DiscreteMotionValidatorGPU:
         h = C.c_void_p()
         abi.check(abi.lib.ompl_gpu_mv_create(C.byref(h), C.byref(self._space_struct),
                                              C.byref(self._checker_struct), int(device)))
-        self._h = h
-
-    def __del__(self):
-        h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            abi.lib.ompl_gpu_mv_destroy(h)
-            self._h = None
+        self._own(h)
 
     def checkMotions(self, s1, s2, want_nd: bool = False, want_first_invalid: bool = False):
         a = abi.as_states(s1, self.dim)

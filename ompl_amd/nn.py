@@ -18,22 +18,19 @@ from . import abi
 from .spaces import StateSpace
 
 
-class NearestNeighborsGPU:
+class NearestNeighborsGPU(abi.Handle):
+    _destroy_fn = "ompl_gpu_nn_destroy"
+
     def __init__(self, space: StateSpace, device: int = 0):
         self.space = space
         self.dim = space.dim
         self._space_struct = space.to_abi()
         h = C.c_void_p()
         abi.check(abi.lib.ompl_gpu_nn_create(C.byref(h), C.byref(self._space_struct), int(device)))
-        self._h = h
+        self._own(h)
         self._removed: set[int] = set()
         self.device = device
 
-    def __del__(self):
-        h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            abi.lib.ompl_gpu_nn_destroy(h)
-            self._h = None
 
     # ---- container ---------------------------------------------------------
     def reportsSortedResults(self) -> bool:

@@ -38,8 +38,10 @@ def seeds_drawn() -> int:
     return int(abi.lib.ompl_gpu_rng_seeds_drawn())
 
 
-class StateSampler:
+class StateSampler(abi.Handle):
     """allocStateSampler() of `space`; bounds of the R^n part from the space descriptor."""
+
+    _destroy_fn = "ompl_gpu_sampler_destroy"
 
     def __init__(self, space: StateSpace):
         self.space = space
@@ -51,13 +53,7 @@ class StateSampler:
         h = C.c_void_p()
         abi.check(abi.lib.ompl_gpu_sampler_create(C.byref(h), C.byref(s), abi.dptr(lo) if lo is not None else None,
                                                   abi.dptr(hi) if hi is not None else None))
-        self._h = h
-
-    def __del__(self):
-        h = getattr(self, "_h", None)
-        if h is not None and h.value and abi is not None and abi.lib is not None:
-            abi.lib.ompl_gpu_sampler_destroy(h)
-            self._h = None
+        self._own(h)
 
     def sample_uniform(self, n: int) -> np.ndarray:
         out = np.empty((int(n), self.space.dim), dtype=np.float64)

@@ -86,6 +86,8 @@ def merge_csr(offsets: list, ids: list, dists: list):
     seg_d, seg_i, seg_q = [], [], []
     for off, ii, dd in zip(offsets, ids, dists):
         cnt = off[1:] - off[:-1]
+        tot = int(off[-1])  # capacity-sized buffers (radius_device) hold more than the CSR
+        ii, dd = ii[:tot], dd[:tot]
         seg_q.append(torch.repeat_interleave(torch.arange(nq, dtype=torch.int64, device=off.device), cnt))
         seg_i.append(ii.to(torch.int64))
         seg_d.append(dd)
@@ -103,6 +105,8 @@ def allgather_radius(offsets: torch.Tensor, ids_global: torch.Tensor, dists: tor
     """Tree-sharded nearestR (SURVEY §8e "Radius search"): every rank answers the same queries
     on its slice of the states; the variable-size CSR results are exchanged as a count
     all_gather followed by padded payload all_gathers, and merged on every rank."""
+    tot = int(offsets[-1])
+    ids_global, dists = ids_global[:tot], dists[:tot]
     offs, _ = _allgather_varlen(offsets.to(torch.int64).contiguous(), group)
     ii, _ = _allgather_varlen(ids_global.to(torch.int64).contiguous(), group)
     dd, _ = _allgather_varlen(dists.contiguous(), group)
