@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--rrt-iters", type=int, default=2000, help="device RRT iterations after the bench (0 = skip)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra measurements (index maintenance, sphere checker, RRT* k) after the timed steps")
+    ap.add_argument("--bitstar-knn", action="store_true",
+                    help="cfg5: BIT*'s default kNN neighbourhood (useKNearest_, bitstar/ImplicitGraph.h:463), "
+                         "k = ceil(1.1 (e + e/6) ln n) = 57 at 10^7, instead of the radius mode")
     ap.add_argument("--rrt-star-queries", type=int, default=1000,
                     help="cfg3: batch of RRT* neighbourhood queries at k = 6,169 (0 = skip)")
     a = ap.parse_args()
@@ -194,7 +197,7 @@ def cpu_baseline(workload, sp, ck, tree, queries, k, budget_s, radius=None):
                 "nn_queries_per_s": qpsT, "motion_checks_per_s": mpsT, "gnat_build_s": r["build_s"]}
     if workload == "cfg4":
         return _cpu_prm_causal(sp, ck, tree, queries, k, budget_s, T)
-    return _cpu_bitstar_radius(sp, ck, tree, queries, radius, budget_s, T)
+    return _cpu_bitstar_radius(sp, ck, tree, queries, radius, budget_s, T, k)
 
 
 def _cpu_prm_causal(sp, ck, tree, milestones, k_cap, budget_s, T):
@@ -240,11 +243,11 @@ def _cpu_prm_causal(sp, ck, tree, milestones, k_cap, budget_s, T):
                         "note": "causal inserts are sequential; only the edge checks use the threads"}}
 
 
-def _cpu_bitstar_radius(sp, ck, tree, queries, radius, budget_s, T):
-    """BIT*'s batch on the GNAT restatement: nearestR(r) of each vertex over the sample set
-    (ImplicitGraph.cpp:313-320, GNAT nearestR NearestNeighborsGNAT.h:236-245) on 1 and T
-    threads (const queries), plus checkMotion(vertex, sample) of the edges.  The edges' motion
-    rate is measured on the pairs of a few queries answered by the oracle's brute force."""
+def _cpu_bitstar_radius(sp, ck, tree, queries, radius, budget_s, T, k=0):
+    """BIT*'s batch on the GNAT restatement: nearestR(r) — or, with k, nearestK(k) (BIT*'s kNN
+    mode) — of each vertex over the sample set (ImplicitGraph.cpp:313-320, GNAT nearestR / nearestK
+    NearestNeighborsGNAT.h:222-245) on 1 and T threads (const queries), plus checkMotion(vertex,
+    sample) of the edges.  The edges' motion rate is measured on the pairs of a few queries."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
 
@@ -253,17 +256,29 @@ def _cpu_bitstar_radius(sp, ck, tree, queries, radius, budget_s, T):
     g.add(tree, bulk=True)
     build_s = time.perf_counter() - t0
     rate = {}
+
+    def query(qs, nt):
+        if k:
+            g.knn(qs, k, nt)
+            return len(qs) * k
+        return g.radius_count(qs, radius, nt)[1]
+
     for nt in (1, T):
         t0 = time.perf_counter()
-        g.radius_count(queries[:4 * nt], radius, nt)
+        query(queries[:4 * nt], nt)
         per = (time.perf_counter() - t0) / (4 * nt)
         nq = int(min(len(queries), max(4 * nt, 0.25 * budget_s / max(per, 1e-9))))
         t0 = time.perf_counter()
-        cnt, tot = g.radius_count(queries[:nq], radius, nt)
+        tot = query(queries[:nq], nt)
         rate[nt] = (nq, time.perf_counter() - t0, tot)
-    off, ids, _ = O.radius(sp, tree, queries[:8], radius)
-    s1 = np.repeat(queries[:8], np.diff(off).astype(np.int64), axis=0)
-    s2 = tree[ids.astype(np.int64)]
+    if k:
+        ids, _, _ = O.knn(sp, tree, queries[:8], k)
+        s1 = np.repeat(queries[:8], k, axis=0)
+        s2 = tree[ids.reshape(-1).astype(np.int64)]
+    else:
+        off, ids, _ = O.radius(sp, tree, queries[:8], radius)
+        s1 = np.repeat(queries[:8], np.diff(off).astype(np.int64), axis=0)
+        s2 = tree[ids.astype(np.int64)]
     mps = {nt: _motion_rate(sp, ck, s1, s2, 0.15 * budget_s, nt) for nt in (1, T)}
 
     def comb(nt):
@@ -271,9 +286,10 @@ def _cpu_bitstar_radius(sp, ck, tree, queries, radius, budget_s, T):
         return (nq + tot) / (t + tot / mps[nt][0])
 
     nqT, tT, totT = rate[T]
+    what = f"nearestK(k={k})" if k else f"nearestR(r={radius:.4f})"
     return {"value": comb(T), "unit": UNIT, "cores": T, "kind": "port",
             "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same {len(tree)}-sample "
-                       f"set: {nqT} nearestR(r={radius:.4f}) of the run's vertices ({totT} neighbours) on {T} threads "
+                       f"set: {nqT} {what} of the run's vertices ({totT} neighbours) on {T} threads "
                        f"(const queries), their checkMotion(vertex, sample) edges at the rate measured on "
                        f"{len(s1)} edges of 8 vertices; index build {build_s:.1f} s excluded"),
             "single_thread": {"value": comb(1), "nn_queries_per_s": rate[1][0] / rate[1][1],
@@ -472,7 +488,8 @@ class Runner:
         if wl in ("cfg3", "cfg2"):
             self.k = k
         elif wl == "cfg5":
-            self.k = 0
+            # BIT* kNN mode: k = ceil(1.1 (e + e/d) ln n) (bitstar/src/ImplicitGraph.cpp:313-316, 1383-1387)
+            self.k = int(math.ceil(1.1 * (math.e + math.e / 6.0) * math.log(args.tree))) if args.bitstar_knn else 0
         self.mv = DiscreteMotionValidatorGPU(self.sp, self.ck, local)
         if wl == "cfg5":  # sample sets hold valid states (ImplicitGraph.cpp:981)
             self.tree, q = reference_inputs(self.sp, args.tree, nq, rank, valid=self.mv.isValid)
@@ -495,14 +512,14 @@ class Runner:
         self.nn.set_stream(stream.cuda_stream)
         self.mv.set_stream(stream.cuda_stream)
         dim = self.sp.dim
-        if wl in ("cfg3", "cfg2", "cfg4"):
+        if wl in ("cfg3", "cfg2", "cfg4") or self.k:
             self.ids = torch.empty((nq, self.k), dtype=torch.int32, device=dev)
             self.dd = torch.empty((nq, self.k), dtype=torch.float64, device=dev)
         if wl == "cfg4":
             self.cnt = torch.empty(nq, dtype=torch.int32, device=dev)
             self.evalid = torch.empty((nq, self.k), dtype=torch.uint8, device=dev)
-        m = nq * self.k if wl == "cfg4" else nq
-        if wl == "cfg5":
+        m = nq * self.k if (wl == "cfg4" or (wl == "cfg5" and self.k)) else nq
+        if wl == "cfg5" and not self.k:
             self.off = torch.empty(nq + 1, dtype=torch.int64, device=dev)
             m = self.nn.radius_device(self.queries.data_ptr(), nq, self.radius, self.off.data_ptr(), 0, 0, 0)
             self.cap = m
@@ -529,7 +546,7 @@ class Runner:
             return
         if e:
             e[0].record(self.stream)
-        if a.workload == "cfg5":
+        if a.workload == "cfg5" and not self.k:
             self.m = nn.radius_device(q, self.nq, self.radius, self.off.data_ptr(), self.ids.data_ptr(),
                                       self.dd.data_ptr(), self.cap)
         else:
@@ -541,6 +558,9 @@ class Runner:
                             self.s_to.data_ptr())
         elif a.workload == "cfg4":           # PRM: checkMotion(state[n], state[m])  PRM.cpp:582
             nn.edges_device(q, self.nq, None, self.ids.data_ptr(), self.k, self.m, False, self.s_from.data_ptr(),
+                            self.s_to.data_ptr())
+        elif self.k:                         # BIT* kNN mode: checkMotion(vertex, sample)  BITstar.cpp:815
+            nn.edges_device(q, self.nq, None, self.ids.data_ptr(), self.k, self.m, True, self.s_from.data_ptr(),
                             self.s_to.data_ptr())
         else:                                # BIT*: checkMotion(vertex, sample)  BITstar.cpp:815
             nn.edges_device(q, self.nq, self.off.data_ptr(), self.ids.data_ptr(), 0, self.m, True,
@@ -565,7 +585,8 @@ class Runner:
         if wl == "cfg4":
             return "NN queries/sec + motion checks/sec, PRM* KinematicChain R^12, 10^6-vertex roadmap", UNIT
         if wl == "cfg5":
-            return "NN queries/sec + motion checks/sec, BIT* SE(3) radius batch, 10^7 samples", UNIT
+            mode = f"kNN (k={self.k})" if self.k else "radius"
+            return f"NN queries/sec + motion checks/sec, BIT* SE(3) {mode} batch, 10^7 samples", UNIT
         return METRIC, UNIT
 
     def config(self, world):
@@ -587,6 +608,12 @@ class Runner:
                         edges_last_step=self.m,
                         note=("roadmap vertices and milestones are valid states (rejection); the batch's "
                               "milestones are uploaded from the host inside each step (~1 MB, <0.1% of the step)"))
+        elif self.k:
+            base.update(workload="configs[4]: BIT* batch on SE(3), kNN mode (useKNearest_ default, "
+                                 "bitstar/ImplicitGraph.h:463) — nearestK(k = ceil(1.1 (e + e/6) ln n)) + "
+                                 "checkMotion(vertex, sample) per edge, 32 spheres r=0.1",
+                        k=self.k, state_space="SE3 [0,1]^3", edges_per_step=self.m,
+                        note="samples and vertices are valid states (rejection)")
         else:
             base.update(workload="configs[4]: BIT* batch on SE(3) — nearestR(r = 1.1 r_RGG (ln n / n)^(1/6)) + "
                                  "checkMotion(vertex, sample) per edge, 32 spheres r=0.1",
@@ -605,7 +632,7 @@ class Runner:
                     f"the culled radius walk scanned {frac_of} of the {nq} x {n} pairs")
         elif kern_name == "knn32_group_kernel":
             pairs = (after["kq"] - before["kq"]) * 64 / launches
-            flop = F_SE3 if wl == "cfg3" else F_L2_6
+            flop = F_L2_6 if wl == "cfg2" else F_SE3
             dt = "f32"
             what = (f"{pairs:.4g} (query, state) fp32 distance evaluations per launch x {flop} flop (SURVEY §8d); "
                     f"the culled walk scanned {pairs / (float(nq) * n):.4%} of the {nq} x {n} pairs")

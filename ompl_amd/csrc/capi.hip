@@ -499,7 +499,10 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
                                            double *d_dist) {
     // large-k path: every k above the register buckets; from 33 on where it beats them (not the
     // chain, whose wave scan serves PRM*'s k <= 64 itself)
-    const bool mid_k = k > 32 && h->fast && h->sp.kind != OMPL_GPU_SPACE_KCHAIN;
+    // (the culled group walk serves k <= 61 on SE3 / R^n: fast_k2)
+    const bool walk_k = h->fast && h->cull && cull_supported(h->sp) && screen_safe(h) &&
+                        fast_k2(h->sp, k, (uint32_t)nq, true) > 0;
+    const bool mid_k = k > 32 && h->fast && h->sp.kind != OMPL_GPU_SPACE_KCHAIN && !walk_k;
     const bool large = (k > (uint32_t)kMaxK || mid_k) && large_k_supported(h->sp) && screen_safe(h);
     if (k > (uint32_t)kMaxK && !large)
         return fail(OMPL_GPU_ERR_UNSUPPORTED, screen_safe(h) ? "k above 64 is not supported for this state space"
@@ -536,7 +539,7 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
                                      size_t(4) << 30, h->num_cus, h->stream));
         return OMPL_GPU_OK;
     }
-    if (h->fast && screen_safe(h) && fast_k2(h->sp, k, (uint32_t)nq) > 0) {
+    if (h->fast && screen_safe(h) && fast_k2(h->sp, k, (uint32_t)nq, h->cull) > 0) {
         // fp32 screen + fp64 certificate (knn_fast.hip); uncertified queries re-run exactly
         const bool cull = h->cull && cull_supported(h->sp);
         if (cull) {

@@ -135,7 +135,7 @@ hipError_t append_sorted_store(const DevSpace &sp, const FeatGeom &g, const floa
 hipError_t tombstone_sorted_store(SortedStore *s, uint64_t id, hipStream_t st);
 void free_sorted_store(SortedStore *s);
 
-int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq);  // screening list size, 0 = not eligible
+int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq, bool cull);  // screening list size, 0 = not eligible
 int fp32_rows(const DevSpace &sp, const FeatGeom &g);     // rows of the fp32 SoA copy
 // fp32 screening rows of stored states [first, first + n): the features, or for KCHAIN the
 // joint positions (prefix sums of the cos / sin features)

@@ -5,10 +5,18 @@
 
 namespace ompl_amd {
 // K2: the smallest list bucket >= max(k + 6, 16); the certify kernel's K bucket fits inside it.
-int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq) {
+// The culled group walk (SE3, R^n) keeps k + 3 entries spread over the wave (one per lane), so
+// it serves every k <= 61 — BIT*'s default nearestK at 10^7 samples is k = 57
+// (bitstar/src/ImplicitGraph.cpp:313-316, 1383-1387).  The chunked thread-per-query screens
+// hold their lists in registers and stop at k <= 32 (the chain's wave scan at k <= 58).
+int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq, bool cull) {
     if (nq < kStreamMaxQ || k == 0) return 0;
     const int K = k_bucket(k);
-    // the exact path serves k > 32 (k > 58 for the chain, whose k = 41 of PRM* takes the screen)
+    if (cull && cull_supported(sp)) {
+        if (K == 0 || k + 3 > 64) return 0;
+        const int K2 = k_bucket(k + 3);
+        return K2 < 16 ? 16 : K2;
+    }
     if (K == 0 || (K > 32 && sp.kind != OMPL_GPU_SPACE_KCHAIN)) return 0;
     int K2 = k_bucket(k + 6);
     if (K2 < 16) K2 = 16;

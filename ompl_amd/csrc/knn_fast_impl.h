@@ -1416,7 +1416,7 @@ struct FastPlan {
 
 FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, int num_cus, bool cull) {
     FastPlan p{};
-    p.K2 = fast_k2(sp, k, nq);
+    p.K2 = fast_k2(sp, k, nq, cull);
     p.K = k_bucket(k);
     p.k2 = p.K2;
     p.cull = cull;
@@ -1547,8 +1547,12 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
                            b.qeta, b.n_live, (uint32_t)p.k2, od, oi, k, fail, fail + 1);
     } else {
         if (p.cull) return hipErrorInvalidValue;  // position lists need the wave certificate
-        hipLaunchKernelGGL((knn_certify_kernel<SP, F, K2, K>), dim3((nq + 255) / 256), b256, 0, st, pd, pi, p.chunks,
-                           nq, perm, f64, cap, qf64, sp, b.absmax, b.qeta, b.n_live, od, oi, k, fail, fail + 1);
+        if constexpr (K == 64 && SP != OMPL_GPU_SPACE_KCHAIN) {
+            return hipErrorInvalidValue;  // culled walk only
+        } else {
+            hipLaunchKernelGGL((knn_certify_kernel<SP, F, K2, K>), dim3((nq + 255) / 256), b256, 0, st, pd, pi, p.chunks,
+                               nq, perm, f64, cap, qf64, sp, b.absmax, b.qeta, b.n_live, od, oi, k, fail, fail + 1);
+        }
     }
     return hipGetLastError();
 }
@@ -1566,8 +1570,10 @@ hipError_t run_fast_k(const DevSpace &sp, const FastPlan &p, const FastLayout &L
             return run_fast<SP, F, K2, 32>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
         break;
     case 64:
-        if constexpr (K2 >= 64 && SP == OMPL_GPU_SPACE_KCHAIN)  // PRM* k = 41 (ConnectionStrategy.h:147)
-            return run_fast<SP, F, K2, 64>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
+        // PRM* k = 41 on the chain (ConnectionStrategy.h:147); BIT* k = 57 on the culled walk
+        if constexpr (K2 >= 64)
+            if (SP == OMPL_GPU_SPACE_KCHAIN || p.cull)
+                return run_fast<SP, F, K2, 64>(sp, p, L, ws, f32, f64, cap, n_end, ss, qf64, nq, k, b, od, oi, st);
         break;
     }
     return hipErrorInvalidValue;

@@ -52,3 +52,14 @@ def assert_knn_parity(gi, gd, oi_ext, od_ext, k):
             j = e + 1
     assert mism == 0, f"{mism} tie classes with different ids"
     return exact
+
+
+def oracle_knn_mt(O, sp, data, queries, k, threads=8):
+    """The oracle's brute force over query slices on `threads` threads (ctypes drops the GIL),
+    for parity checks at the configs' full store sizes."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    parts = np.array_split(np.arange(len(queries)), min(threads, len(queries)))
+    with ThreadPoolExecutor(len(parts)) as ex:
+        res = list(ex.map(lambda ix: O.knn(sp, data, queries[ix], k), parts))
+    return (np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res]))
