@@ -41,6 +41,7 @@
 // template instantiations compile in parallel; knn_fast.hip holds the dispatch.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/rocprim.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -1691,9 +1692,9 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
 // level L by the L bits of its path; its tile range follows from the path, its pre-order index
 // too (left child = index + 1, right child = index + floor(T/2)).  Per level, every node picks
 // the widest coordinate of its box and its states are sorted by (node, coordinate) — one radix
-// sort of (tile-range start << 32 | ordered coordinate) keys for all nodes of the level — which
-// puts the floor(T/2) * 64 smallest on the left: the host median split (std::nth_element) of
-// round 1, as one sort per level on the device.
+// sort of (path << 16 | coordinate quantised over the node's extent) keys, L + 16 bits, for all
+// nodes of the level — which puts the floor(T/2) * 64 smallest on the left: the host median
+// split (std::nth_element) of round 1, as one sort per level on the device.
 struct KdNodeRef {
     uint32_t t0, T, pidx;
     bool valid;
@@ -1719,148 +1720,9 @@ __device__ __forceinline__ KdNodeRef kd_node_at(uint32_t ntiles, int level, uint
     return r;
 }
 
-// box coordinate d of state id (SE3: translation, then the sign-canonical quaternion w >= 0)
-template <int SP, int F>
-__device__ __forceinline__ float kd_coord(const float *__restrict__ f32, uint64_t cap, uint32_t id, int d) {
-    float v = f32[(uint64_t)d * cap + id];
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        if (d >= 3 && f32[6ull * cap + id] < 0.f) v = -v;
-    }
-    return v;
-}
-
-__device__ __forceinline__ uint32_t ordered_bits(float v) {  // monotone float -> uint32 (NaN last)
-    if (!(v == v)) return 0xFFFFFFFFu;
-    const uint32_t u = __float_as_uint(v);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-
 __global__ void kd_live_flags_kernel(const uint8_t *__restrict__ live, uint64_t n, uint8_t *__restrict__ flags) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) flags[i] = live[i];
-}
-
-// level boxes of the tiles of the current order: box of positions [t * 64, t * 64 + 64) ∩ [0, n)
-template <int SP, int F>
-__global__ void kd_tile_boxes_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ perm,
-                                     uint32_t n, uint32_t ntiles, float *__restrict__ tb) {
-    constexpr int NB = Geo<SP, F>::NB;
-    const uint32_t t = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (t >= ntiles) return;
-    const uint32_t p = t * kCullTile + lane;
-    const bool in = p < n;
-    const uint32_t id = in ? perm[p] : 0u;
-#pragma unroll
-    for (int d = 0; d < NB; ++d) {
-        float lo = in ? kd_coord<SP, F>(f32, cap, id, d) : __builtin_inff();
-        float hi = in ? lo : -__builtin_inff();
-        if (!(lo == lo)) {
-            lo = __builtin_inff();
-            hi = -__builtin_inff();
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            lo = fminf(lo, __shfl_xor(lo, o));
-            hi = fmaxf(hi, __shfl_xor(hi, o));
-        }
-        if (lane == 0) {
-            tb[(size_t)t * 2 * NB + d] = lo;
-            tb[(size_t)t * 2 * NB + NB + d] = hi;
-        }
-    }
-}
-
-// one block per node of the level: widest box coordinate -> ndim[path]
-template <int SP, int F>
-__global__ __launch_bounds__(256) void kd_node_dim_kernel(const float *__restrict__ tb, uint32_t ntiles, int level,
-                                                          uint32_t *__restrict__ ndim) {
-    constexpr int NB = Geo<SP, F>::NB;
-    __shared__ float slo[NB][256], shi[NB][256];
-    const KdNodeRef nd = kd_node_at(ntiles, level, blockIdx.x);
-    if (!nd.valid || nd.T <= 1) return;
-    float lo[NB], hi[NB];
-#pragma unroll
-    for (int d = 0; d < NB; ++d) {
-        lo[d] = __builtin_inff();
-        hi[d] = -__builtin_inff();
-    }
-    for (uint32_t t = nd.t0 + threadIdx.x; t < nd.t0 + nd.T; t += blockDim.x)
-#pragma unroll
-        for (int d = 0; d < NB; ++d) {
-            lo[d] = fminf(lo[d], tb[(size_t)t * 2 * NB + d]);
-            hi[d] = fmaxf(hi[d], tb[(size_t)t * 2 * NB + NB + d]);
-        }
-#pragma unroll
-    for (int d = 0; d < NB; ++d) {
-        slo[d][threadIdx.x] = lo[d];
-        shi[d][threadIdx.x] = hi[d];
-    }
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w)
-#pragma unroll
-            for (int d = 0; d < NB; ++d) {
-                slo[d][threadIdx.x] = fminf(slo[d][threadIdx.x], slo[d][threadIdx.x + w]);
-                shi[d][threadIdx.x] = fmaxf(shi[d][threadIdx.x], shi[d][threadIdx.x + w]);
-            }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        int bd = 0;
-        float be = -1.f;
-        for (int d = 0; d < NB; ++d) {
-            const float e = shi[d][0] - slo[d][0];
-            if (e > be) {  // first widest, as the host build
-                be = e;
-                bd = d;
-            }
-        }
-        ndim[blockIdx.x] = (uint32_t)bd;
-    }
-}
-
-// sort key of position p at this level: (start tile of its node << 32) | ordered coordinate
-// (0 once its node is a leaf, which keeps leaves in place under the stable sort)
-template <int SP, int F>
-__global__ void kd_keys_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ perm,
-                               uint32_t n, uint32_t ntiles, int level, const uint32_t *__restrict__ ndim,
-                               uint64_t *__restrict__ keys) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const uint32_t t = p / kCullTile;
-    uint32_t t0 = 0, T = ntiles, path = 0;
-    int l = 0;
-    for (; l < level && T > 1; ++l) {
-        const uint32_t tl = T >> 1;
-        const uint32_t right = t >= t0 + tl ? 1u : 0u;
-        path = (path << 1) | right;
-        if (right) {
-            t0 += tl;
-            T -= tl;
-        } else {
-            T = tl;
-        }
-    }
-    uint32_t low = 0;
-    if (l == level && T > 1) low = ordered_bits(kd_coord<SP, F>(f32, cap, perm[p], (int)ndim[path]));
-    keys[p] = ((uint64_t)t0 << 32) | low;
-}
-
-// node records of the level (pre-order): split = first coordinate of the right part
-template <int SP, int F>
-__global__ void kd_split_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ perm,
-                                uint32_t n, uint32_t ntiles, int level, const uint32_t *__restrict__ ndim,
-                                KdNode *__restrict__ nodes) {
-    const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;
-    if (level < 31 && path >= (1u << level)) return;
-    const KdNodeRef nd = kd_node_at(ntiles, level, path);
-    if (!nd.valid || nd.T <= 1) return;
-    const uint32_t tl = nd.T >> 1;
-    const uint32_t pos = (nd.t0 + tl) * kCullTile;
-    const int d = (int)ndim[path];
-    const float split = pos < n ? kd_coord<SP, F>(f32, cap, perm[pos], d) : __builtin_inff();
-    nodes[nd.pidx] = KdNode{(uint32_t)d, split, tl, nd.pidx + tl};
 }
 
 // rows / ids of positions [p0, p1): ids from src (index p - p0) for p - p0 < cnt, else padding
@@ -1994,6 +1856,267 @@ __global__ void super_box_range_kernel(const float *__restrict__ tbox, uint32_t 
     }
 }
 
+// ---- build over physically permuted rows ---------------------------------------------------
+// The level loop keeps the states' box coordinates in a working array of AoS rows in the current
+// order (KdRow: the NB box coordinates — SE3 quaternion sign-canonical — and the id's bits,
+// padded to a multiple of 4 floats: 32 B per SE3 state), so every per-level pass (tile boxes,
+// sort keys) reads contiguous rows, and one gather of whole rows per level follows the sort.
+// (Round 2 gathered each of the 8 coordinates by id in two passes per level: 8 cache lines per
+// state, 1.5 ms per level at 10^7 states.)
+template <int SP, int F>
+struct KdRow {
+    static constexpr int NB = Geo<SP, F>::NB;
+    static constexpr int W = (NB + 1 + 3) & ~3;  // floats per row (last used slot: the id)
+};
+
+template <int SP, int F>
+__global__ void kd_rows_init_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ sel,
+                                    uint32_t n, float *__restrict__ W) {
+    constexpr int NB = KdRow<SP, F>::NB, RW = KdRow<SP, F>::W;
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t id = sel[p];
+    float r[RW];
+#pragma unroll
+    for (int d = 0; d < RW; ++d) r[d] = 0.f;
+#pragma unroll
+    for (int d = 0; d < NB; ++d) r[d] = f32[(uint64_t)d * cap + id];
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        if (r[6] < 0.f)
+#pragma unroll
+            for (int d = 3; d < 7; ++d) r[d] = -r[d];
+    }
+    r[NB] = __uint_as_float(id);
+    float4 *o = reinterpret_cast<float4 *>(W + (size_t)p * RW);
+#pragma unroll
+    for (int c = 0; c < RW / 4; ++c) o[c] = make_float4(r[4 * c], r[4 * c + 1], r[4 * c + 2], r[4 * c + 3]);
+}
+
+// boxes of the 64-row tiles of the current order (a wave per tile, contiguous rows)
+template <int SP, int F>
+__global__ void kd_row_tile_boxes_kernel(const float *__restrict__ W, uint32_t n, uint32_t ntiles,
+                                         float *__restrict__ tb) {
+    constexpr int NB = KdRow<SP, F>::NB, RW = KdRow<SP, F>::W;
+    const uint32_t t = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= ntiles) return;
+    const uint32_t p = t * kCullTile + lane;
+    float r[RW];
+    if (p < n) {
+        const float4 *w4 = reinterpret_cast<const float4 *>(W + (size_t)p * RW);
+#pragma unroll
+        for (int c = 0; c < RW / 4; ++c) {
+            const float4 v = w4[c];
+            r[4 * c] = v.x; r[4 * c + 1] = v.y; r[4 * c + 2] = v.z; r[4 * c + 3] = v.w;
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < NB; ++d) {
+        float lo = p < n ? r[d] : __builtin_inff();
+        float hi = p < n ? r[d] : -__builtin_inff();
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            lo = fminf(lo, __shfl_xor(lo, o));
+            hi = fmaxf(hi, __shfl_xor(hi, o));
+        }
+        if (lane == 0) {
+            tb[(size_t)t * 2 * NB + d] = lo;
+            tb[(size_t)t * 2 * NB + NB + d] = hi;
+        }
+    }
+}
+
+// one block per node of the level: widest box coordinate -> nsplit[path] = {dim, lo, 65535 / extent}
+template <int SP, int F>
+__global__ __launch_bounds__(256) void kd_node_split_dim_kernel(const float *__restrict__ tb, uint32_t ntiles,
+                                                                int level, float4 *__restrict__ nsplit) {
+    constexpr int NB = Geo<SP, F>::NB;
+    __shared__ float slo[NB][256], shi[NB][256];
+    const KdNodeRef nd = kd_node_at(ntiles, level, blockIdx.x);
+    if (!nd.valid || nd.T <= 1) return;
+    float lo[NB], hi[NB];
+#pragma unroll
+    for (int d = 0; d < NB; ++d) {
+        lo[d] = __builtin_inff();
+        hi[d] = -__builtin_inff();
+    }
+    for (uint32_t t = nd.t0 + threadIdx.x; t < nd.t0 + nd.T; t += blockDim.x)
+#pragma unroll
+        for (int d = 0; d < NB; ++d) {
+            lo[d] = fminf(lo[d], tb[(size_t)t * 2 * NB + d]);
+            hi[d] = fmaxf(hi[d], tb[(size_t)t * 2 * NB + NB + d]);
+        }
+    if (nd.T <= 64) {  // small node: one wave reduces (the other waves hold empty boxes)
+        if (threadIdx.x >= 64) return;
+#pragma unroll
+        for (int d = 0; d < NB; ++d)
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                lo[d] = fminf(lo[d], __shfl_xor(lo[d], o));
+                hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], o));
+            }
+    } else {
+#pragma unroll
+        for (int d = 0; d < NB; ++d) {
+            slo[d][threadIdx.x] = lo[d];
+            shi[d][threadIdx.x] = hi[d];
+        }
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w)
+#pragma unroll
+                for (int d = 0; d < NB; ++d) {
+                    slo[d][threadIdx.x] = fminf(slo[d][threadIdx.x], slo[d][threadIdx.x + w]);
+                    shi[d][threadIdx.x] = fmaxf(shi[d][threadIdx.x], shi[d][threadIdx.x + w]);
+                }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int d = 0; d < NB; ++d) {
+            lo[d] = slo[d][0];
+            hi[d] = shi[d][0];
+        }
+    }
+    if (threadIdx.x == 0) {
+        int bd = 0;
+        float be = -1.f;
+#pragma unroll
+        for (int d = 0; d < NB; ++d) {
+            const float e = hi[d] - lo[d];
+            if (e > be) {  // first widest, as the host build
+                be = e;
+                bd = d;
+            }
+        }
+        const float inv = be > 0.f ? 65535.f / be : 0.f;
+        nsplit[blockIdx.x] = make_float4(__uint_as_float((uint32_t)bd), lo[bd], inv, 0.f);
+    }
+}
+
+// sort key of position p at this level: (node path, extended by zeros for a node that is
+// already a leaf) << 16 | its split coordinate quantised to 16 bits over the node's extent
+// (0 in a leaf, which keeps it in place under the stable sort).  Quantisation only decides
+// how states with nearly equal coordinates straddle the split: the left part still gets
+// exactly floor(T/2) tiles, and every tile / super-tile box is computed from the states it
+// holds, so the walks' bounds do not depend on it.
+template <int SP, int F, typename Key>
+__global__ void kd_row_keys_kernel(const float *__restrict__ W, uint32_t n, uint32_t ntiles, int level,
+                                   const float4 *__restrict__ nsplit, Key *__restrict__ keys,
+                                   uint32_t *__restrict__ vals) {
+    constexpr int RW = KdRow<SP, F>::W;
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t t = p / kCullTile;
+    uint32_t t0 = 0, T = ntiles, path = 0;
+    int l = 0;
+    for (; l < level && T > 1; ++l) {
+        const uint32_t tl = T >> 1;
+        const uint32_t right = t >= t0 + tl ? 1u : 0u;
+        path = (path << 1) | right;
+        if (right) {
+            t0 += tl;
+            T -= tl;
+        } else {
+            T = tl;
+        }
+    }
+    uint32_t q = 0;
+    if (l == level && T > 1) {
+        const float4 ns = nsplit[path];
+        const float v = W[(size_t)p * RW + (int)__float_as_uint(ns.x)];
+        const float x = (v - ns.y) * ns.z;
+        q = x > 0.f ? (x < 65535.f ? (uint32_t)x : 65535u) : 0u;
+    } else {
+        path <<= (level - l);
+    }
+    keys[p] = ((Key)path << 16) | (Key)q;
+    vals[p] = p;
+}
+
+template <int SP, int F>
+__global__ void kd_row_gather_kernel(const float *__restrict__ W, const uint32_t *__restrict__ src, uint32_t n,
+                                     float *__restrict__ W2) {
+    constexpr int RW = KdRow<SP, F>::W;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // (position, float4 column)
+    if (t >= n * (RW / 4)) return;
+    const uint32_t p = t / (RW / 4), c = t % (RW / 4);
+    reinterpret_cast<float4 *>(W2)[t] = reinterpret_cast<const float4 *>(W)[(size_t)src[p] * (RW / 4) + c];
+}
+
+// node records of the level (pre-order): split = first coordinate of the right part
+template <int SP, int F>
+__global__ void kd_row_split_kernel(const float *__restrict__ W, uint32_t n, uint32_t ntiles, int level,
+                                    const float4 *__restrict__ nsplit, KdNode *__restrict__ nodes) {
+    constexpr int RW = KdRow<SP, F>::W;
+    const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;
+    if (level < 31 && path >= (1u << level)) return;
+    const KdNodeRef nd = kd_node_at(ntiles, level, path);
+    if (!nd.valid || nd.T <= 1) return;
+    const uint32_t tl = nd.T >> 1;
+    const uint32_t pos = (nd.t0 + tl) * kCullTile;
+    const int d = (int)__float_as_uint(nsplit[path].x);
+    const float split = pos < n ? W[(size_t)pos * RW + d] : __builtin_inff();
+    nodes[nd.pidx] = KdNode{(uint32_t)d, split, tl, nd.pidx + tl};
+}
+
+// the sorted fp32 rows / ids / inverse map from the final working rows (positions [0, p_end);
+// rows past n are padding)
+template <int SP, int F>
+__global__ void kd_rows_store_kernel(const float *__restrict__ W, uint32_t n, uint32_t p_end, uint32_t n_pad,
+                                     float *__restrict__ rows, uint32_t *__restrict__ ids,
+                                     uint32_t *__restrict__ inv) {
+    constexpr int R = Geo<SP, F>::R, RW = KdRow<SP, F>::W, NB = KdRow<SP, F>::NB;
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= p_end) return;
+    if (p < n) {
+        float r[RW];
+        const float4 *w4 = reinterpret_cast<const float4 *>(W + (size_t)p * RW);
+#pragma unroll
+        for (int c = 0; c < RW / 4; ++c) {
+            const float4 v = w4[c];
+            r[4 * c] = v.x; r[4 * c + 1] = v.y; r[4 * c + 2] = v.z; r[4 * c + 3] = v.w;
+        }
+        const uint32_t id = __float_as_uint(r[NB]);
+#pragma unroll
+        for (int c = 0; c < R; ++c) rows[(size_t)c * n_pad + p] = r[c];
+        ids[p] = id;
+        inv[id] = p;
+    } else {
+#pragma unroll
+        for (int c = 0; c < R; ++c) rows[(size_t)c * n_pad + p] = __builtin_nanf("");
+        ids[p] = kNoId;
+    }
+}
+
+// fp64 features by id, AoS (fa per row, zero padded): the transpose of the SoA store, both
+// sides coalesced, so that the sorted fp64 rows are then gathered one contiguous row per state
+__global__ void feat_aos_kernel(const double *__restrict__ f64, uint64_t cap, int F, int fa, uint64_t n,
+                                double *__restrict__ aos) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (column, id): coalesced reads
+    if (t >= n * fa) return;
+    const int c = (int)(t / n);
+    const uint64_t id = t - (uint64_t)c * n;
+    aos[id * fa + c] = c < F ? f64[(uint64_t)c * cap + id] : 0.0;
+}
+
+__global__ void rows64_gather_kernel(const double *__restrict__ aos, int F, int fa, const uint32_t *__restrict__ ids,
+                                     uint32_t p_end, double *__restrict__ rows64) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (slot, double2 column)
+    const int h = fa / 2;
+    if (t >= (uint64_t)p_end * h) return;
+    const uint64_t p = t / h;
+    const int c = (int)(t % h);
+    const uint32_t id = ids[p];
+    double2 v;
+    if (id == kNoId) {  // padding: NaN features, zero pad columns
+        v.x = 2 * c < F ? __builtin_nan("") : 0.0;
+        v.y = 2 * c + 1 < F ? __builtin_nan("") : 0.0;
+    } else {
+        v = reinterpret_cast<const double2 *>(aos)[(uint64_t)id * h + c];
+    }
+    reinterpret_cast<double2 *>(rows64)[t] = v;
+}
+
 inline hipError_t scratch_ensure(SortedStore *s, size_t bytes) {
     if (bytes <= s->scratch_bytes) return hipSuccess;
     if (s->scratch) (void)hipFree(s->scratch);
@@ -2065,66 +2188,97 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
     if ((e = sorted_alloc<SP, F>(s, main_sup_tiles + tail_tiles, main_tiles, std::max<uint64_t>(cap, n_total), fa,
                                  st)) != hipSuccess)
         return e;
-    // scratch: flags | perm x2 | keys x2 | tile boxes | node dims | selected count | cub temp
+    // scratch: flags | sel / sorted positions | keys x2 | positions | rows x2 | tile boxes | node
+    // splits | selected count | rocPRIM temp.  The two row buffers are adjacent: after the level
+    // loop they hold the fp64 features by id (feat_aos_kernel) for the rows64 gather.
     const size_t n = std::max<uint64_t>(n_total, 1);
+    const uint32_t nl = std::max<uint32_t>(n_live, 1);
+    constexpr int RW = KdRow<SP, F>::W;
     int depth = 0;
     while ((1u << depth) < main_tiles) ++depth;
-    int tbits = 1;
-    while ((1u << tbits) <= main_tiles) ++tbits;
-    size_t cub_sel = 0, cub_sort = 0;
-    hipcub::CountingInputIterator<uint32_t> count_it(0);
-    (void)hipcub::DeviceSelect::Flagged(nullptr, cub_sel, count_it, (const uint8_t *)nullptr, (uint32_t *)nullptr,
-                                        (uint32_t *)nullptr, (int)n);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_sort, (uint64_t *)nullptr, (uint64_t *)nullptr,
-                                             (uint32_t *)nullptr, (uint32_t *)nullptr, (int)std::max<uint32_t>(n_live, 1),
-                                             0, 32 + tbits);
+    const bool wide = depth + 16 > 32;  // 64-bit keys once path bits + 16 exceed 32
+    size_t tmp_sel = 0, tmp_sort = 0;
+    rocprim::counting_iterator<uint32_t> count_it(0);
+    if ((e = rocprim::select(nullptr, tmp_sel, count_it, (const uint8_t *)nullptr, (uint32_t *)nullptr,
+                             (uint32_t *)nullptr, n, st)) != hipSuccess)
+        return e;
+    if (wide)
+        e = rocprim::radix_sort_pairs(nullptr, tmp_sort, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                      (uint32_t *)nullptr, (uint32_t *)nullptr, nl, 0, depth + 16, st);
+    else
+        e = rocprim::radix_sort_pairs(nullptr, tmp_sort, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                      (uint32_t *)nullptr, (uint32_t *)nullptr, nl, 0, depth + 16, st);
+    if (e != hipSuccess) return e;
+    const size_t row_bytes = std::max<size_t>(4ull * RW * nl, 4ull * fa * n);  // each half of the pair
     size_t off = 0;
     auto take = [&](size_t b) {
         const size_t o = off;
         off += align_up(b);
         return o;
     };
-    const size_t o_flags = take(n), o_p0 = take(4 * n), o_p1 = take(4 * n), o_k0 = take(8 * n), o_k1 = take(8 * n),
-                 o_tb = take(4ull * main_tiles * 2 * NB), o_nd = take(4ull * main_tiles + 4), o_cnt = take(8),
-                 o_cub = take(std::max(cub_sel, cub_sort));
+    const size_t o_flags = take(n), o_sel = take(4 * n), o_k0 = take(8ull * nl), o_k1 = take(8ull * nl),
+                 o_v0 = take(4ull * nl), o_w = take(2 * row_bytes), o_tb = take(4ull * main_tiles * 2 * NB),
+                 o_ns = take(16ull * main_tiles + 16), o_cnt = take(8), o_tmp = take(std::max(tmp_sel, tmp_sort));
     if ((e = scratch_ensure(s, off)) != hipSuccess) return e;
     char *w = (char *)s->scratch;
     uint8_t *flags = (uint8_t *)(w + o_flags);
-    uint32_t *perm = (uint32_t *)(w + o_p0), *perm2 = (uint32_t *)(w + o_p1);
-    uint64_t *keys = (uint64_t *)(w + o_k0), *keys2 = (uint64_t *)(w + o_k1);
+    uint32_t *sel = (uint32_t *)(w + o_sel), *vals = (uint32_t *)(w + o_v0), *nsel = (uint32_t *)(w + o_cnt);
+    float *W0 = (float *)(w + o_w), *W1 = (float *)(w + o_w + row_bytes);
     float *tb = (float *)(w + o_tb);
-    uint32_t *ndim = (uint32_t *)(w + o_nd), *nsel = (uint32_t *)(w + o_cnt);
+    float4 *nsplit = (float4 *)(w + o_ns);
     const dim3 b256(256);
-    hipLaunchKernelGGL(kd_live_flags_kernel, dim3((unsigned)((n_total + 255) / 256)), b256, 0, st, live, n_total, flags);
-    size_t cb = std::max(cub_sel, cub_sort);
-    if ((e = hipcub::DeviceSelect::Flagged(w + o_cub, cb, count_it, flags, perm, nsel, (int)n_total, st)) != hipSuccess)
+    if (n_total)
+        hipLaunchKernelGGL(kd_live_flags_kernel, dim3((unsigned)((n_total + 255) / 256)), b256, 0, st, live, n_total,
+                           flags);
+    size_t tb_bytes = std::max(tmp_sel, tmp_sort);
+    if ((e = rocprim::select(w + o_tmp, tb_bytes, count_it, flags, sel, nsel, (size_t)n_total, st)) != hipSuccess)
         return e;
+    hipLaunchKernelGGL((kd_rows_init_kernel<SP, F>), dim3((nl + 255) / 256), b256, 0, st, f32, cap, sel, n_live, W0);
+    const uint32_t gather_threads = n_live * (RW / 4);
     for (int level = 0; level < depth; ++level) {
-        hipLaunchKernelGGL((kd_tile_boxes_kernel<SP, F>), dim3((main_tiles + 3) / 4), b256, 0, st, f32, cap, perm,
-                           n_live, main_tiles, tb);
-        hipLaunchKernelGGL((kd_node_dim_kernel<SP, F>), dim3(1u << level), b256, 0, st, tb, main_tiles, level, ndim);
-        hipLaunchKernelGGL((kd_keys_kernel<SP, F>), dim3((n_live + 255) / 256), b256, 0, st, f32, cap, perm, n_live,
-                           main_tiles, level, ndim, keys);
-        cb = std::max(cub_sel, cub_sort);
-        if ((e = hipcub::DeviceRadixSort::SortPairs(w + o_cub, cb, keys, keys2, perm, perm2, (int)n_live, 0, 32 + tbits,
-                                                    st)) != hipSuccess)
-            return e;
-        std::swap(perm, perm2);
-        hipLaunchKernelGGL((kd_split_kernel<SP, F>), dim3(((1u << level) + 255) / 256), b256, 0, st, f32, cap, perm,
-                           n_live, main_tiles, level, ndim, s->nodes);
+        hipLaunchKernelGGL((kd_row_tile_boxes_kernel<SP, F>), dim3((main_tiles + 3) / 4), b256, 0, st, W0, n_live,
+                           main_tiles, tb);
+        hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F>), dim3(1u << level), b256, 0, st, tb, main_tiles, level,
+                           nsplit);
+        tb_bytes = std::max(tmp_sel, tmp_sort);
+        if (wide) {
+            uint64_t *k0 = (uint64_t *)(w + o_k0), *k1 = (uint64_t *)(w + o_k1);
+            hipLaunchKernelGGL((kd_row_keys_kernel<SP, F, uint64_t>), dim3((nl + 255) / 256), b256, 0, st, W0, n_live,
+                               main_tiles, level, nsplit, k0, vals);
+            e = rocprim::radix_sort_pairs(w + o_tmp, tb_bytes, k0, k1, vals, sel, n_live, 0, level + 16, st);
+        } else {
+            uint32_t *k0 = (uint32_t *)(w + o_k0), *k1 = (uint32_t *)(w + o_k1);
+            hipLaunchKernelGGL((kd_row_keys_kernel<SP, F, uint32_t>), dim3((nl + 255) / 256), b256, 0, st, W0, n_live,
+                               main_tiles, level, nsplit, k0, vals);
+            e = rocprim::radix_sort_pairs(w + o_tmp, tb_bytes, k0, k1, vals, sel, n_live, 0, level + 16, st);
+        }
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((kd_row_gather_kernel<SP, F>), dim3((gather_threads + 255) / 256), b256, 0, st, W0, sel,
+                           n_live, W1);
+        std::swap(W0, W1);
+        hipLaunchKernelGGL((kd_row_split_kernel<SP, F>), dim3(((1u << level) + 255) / 256), b256, 0, st, W0, n_live,
+                           main_tiles, level, nsplit, s->nodes);
     }
     if ((e = hipMemsetAsync(s->inv, 0xFF, 4ull * s->cap_inv, st)) != hipSuccess) return e;
     const uint32_t p_end = (main_sup_tiles + tail_tiles) * kCullTile;  // padding: gap and tail region NaN
-    hipLaunchKernelGGL((sorted_gather_kernel<SP, F>), dim3((p_end + 255) / 256), b256, 0, st, f32, cap, perm, n_live,
-                       0u, p_end, s->n_pad, s->rows, s->ids, s->inv);
+    hipLaunchKernelGGL((kd_rows_store_kernel<SP, F>), dim3((p_end + 255) / 256), b256, 0, st, W0, n_live, p_end,
+                       s->n_pad, s->rows, s->ids, s->inv);
     hipLaunchKernelGGL((tile_box_range_kernel<SP, F>), dim3((main_sup_tiles + 3) / 4), b256, 0, st, s->rows, s->n_pad,
                        0u, main_sup_tiles, s->tbox);
     const uint32_t nsup = main_sup_tiles / kSuperTiles;
     hipLaunchKernelGGL((super_box_range_kernel<SP, F>), dim3((nsup + 255) / 256), b256, 0, st, s->tbox, main_sup_tiles,
                        0u, nsup, s->sbox);
-    const uint64_t c64 = (uint64_t)main_sup_tiles * kCullTile * fa;
-    hipLaunchKernelGGL(rows64_range_kernel, dim3((unsigned)((c64 + 255) / 256)), b256, 0, st, f64, cap, F, fa, s->ids,
-                       0u, main_sup_tiles * kCullTile, s->rows64);
+    // fp64 rows in sorted order: transpose the SoA features by id into the (now free) row
+    // buffers, then one contiguous row per slot
+    double *aos = (double *)(w + o_w);
+    const uint64_t ta = (uint64_t)n_total * fa;
+    if (ta)
+        hipLaunchKernelGGL(feat_aos_kernel, dim3((unsigned)((ta + 255) / 256)), b256, 0, st, f64, cap, F, fa,
+                           (uint64_t)n_total, aos);
+    const uint32_t p64 = main_sup_tiles * kCullTile;
+    const uint64_t c64 = (uint64_t)p64 * (fa / 2);
+    hipLaunchKernelGGL(rows64_gather_kernel, dim3((unsigned)((c64 + 255) / 256)), b256, 0, st, aos, F, fa, s->ids, p64,
+                       s->rows64);
     s->kd_tiles = main_tiles;
     s->nnodes = main_tiles - 1;
     s->main_live = n_live;
