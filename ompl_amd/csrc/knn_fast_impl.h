@@ -194,97 +194,6 @@ __global__ void query_gather_kernel(const float *__restrict__ q32u, const uint32
     q32[t] = q32u[(size_t)perm[qs] * FS + f];
 }
 
-// ---- sorted store (culled screen) ----------------------------------------------------------
-template <int SP, int F>
-__global__ void tree_gather_kernel(const float *__restrict__ f32, uint64_t cap, const uint32_t *__restrict__ ids_sorted,
-                                   uint32_t n, uint32_t n_pad, float *__restrict__ rows, uint32_t *__restrict__ ids) {
-    constexpr int R = Geo<SP, F>::R;
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_pad) return;
-    if (p < n) {
-        const uint32_t id = ids_sorted[p];
-        float x[R];
-        for (int r = 0; r < R; ++r) x[r] = f32[(uint64_t)r * cap + id];
-        if constexpr (SP == OMPL_GPU_SPACE_SE3) {  // |dot| is sign-invariant: store w >= 0
-            if (x[6] < 0.f)
-                for (int r = 3; r < 7; ++r) x[r] = -x[r];
-        }
-        for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = x[r];
-        ids[p] = id;
-    } else {
-        for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = __builtin_nanf("");
-        ids[p] = kNoId;
-    }
-}
-
-template <int SP, int F>
-__global__ void tile_box_kernel(const float *__restrict__ rows, uint32_t n_pad, uint32_t ntiles,
-                                const uint32_t *__restrict__ keys_sorted, uint32_t n, float *__restrict__ tbox,
-                                uint32_t *__restrict__ tkey0) {
-    constexpr int NB = Geo<SP, F>::NB, BW = Geo<SP, F>::BW;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntiles) return;
-    float lo[NB], hi[NB];
-    for (int c = 0; c < NB; ++c) {
-        lo[c] = __builtin_inff();
-        hi[c] = -__builtin_inff();
-    }
-    float eta = 0.f;
-    for (int j = 0; j < kCullTile; ++j) {
-        const uint32_t p = t * kCullTile + j;
-        float x[NB];
-        for (int c = 0; c < NB; ++c) x[c] = rows[(size_t)c * n_pad + p];
-        if (!(x[0] == x[0])) continue;  // padding / removed
-        for (int c = 0; c < NB; ++c) {
-            lo[c] = fminf(lo[c], x[c]);
-            hi[c] = fmaxf(hi[c], x[c]);
-        }
-        if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-            float n2 = x[3] * x[3];
-            n2 = fmaf(x[4], x[4], n2);
-            n2 = fmaf(x[5], x[5], n2);
-            n2 = fmaf(x[6], x[6], n2);
-            eta = fmaxf(eta, n2 - 1.f);
-        }
-    }
-    float *o = tbox + (size_t)t * BW;
-    for (int c = 0; c < NB; ++c) {
-        o[c] = lo[c];
-        o[NB + c] = hi[c];
-    }
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        o[2 * NB] = eta * 1.00001f;
-        o[2 * NB + 1] = 0.f;
-    }
-    tkey0[t] = t;  // queries carry their home leaf as key (kd_home_tile)
-    (void)keys_sorted;
-    (void)n;
-}
-
-template <int SP, int F>
-__global__ void super_box_kernel(const float *__restrict__ tbox, uint32_t ntiles, uint32_t nsuper,
-                                 float *__restrict__ sbox) {
-    constexpr int NB = Geo<SP, F>::NB, BW = Geo<SP, F>::BW;
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nsuper) return;
-    const uint32_t t0 = s * kSuperTiles, t1 = min((s + 1) * kSuperTiles, ntiles);
-    for (int c = 0; c < NB; ++c) {
-        float lo = __builtin_inff(), hi = -__builtin_inff();
-        for (uint32_t t = t0; t < t1; ++t) {
-            lo = fminf(lo, tbox[(size_t)t * BW + c]);
-            hi = fmaxf(hi, tbox[(size_t)t * BW + NB + c]);
-        }
-        sbox[(size_t)s * BW + c] = lo;
-        sbox[(size_t)s * BW + NB + c] = hi;
-    }
-    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        float eta = 0.f;
-        for (uint32_t t = t0; t < t1; ++t) eta = fmaxf(eta, tbox[(size_t)t * BW + 2 * NB]);
-        sbox[(size_t)s * BW + 2 * NB] = eta;
-        sbox[(size_t)s * BW + 2 * NB + 1] = 0.f;
-    }
-}
-
 // ---- screening --------------------------------------------------------------------------
 // acos on [0, 1] (Abramowitz & Stegun 4.4.46, |error| <= 2e-8; fp32 evaluation adds
 // < 1e-6, inside the screen's error bound).  NaN propagates.
@@ -538,6 +447,44 @@ __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w
     }
 }
 
+// lower bound for one 64-state tile (the group walk's tile masks).  SE3: the translation gaps of
+// the box, and for the rotation either the box (variant 0: the distance from q and -q to the
+// quaternion box, 8 gaps) or the tile's rotation cap (1: chord(q, c) - rho, one packed chord;
+// 2: the larger of both).  chord(q, p) >= chord(q, c) - chord(c, p) >= chord(q, c) - rho, and
+// the screened angle is >= the chord; the margin covers the fp32 rounding of both chords.
+template <int SP, int F, int LBV>
+__device__ __forceinline__ float tile_lb(const float *bx, const float *q, float w0, float w1) {
+    if constexpr (SP == OMPL_GPU_SPACE_SE3 && LBV != 0) {
+        constexpr int NB = Geo<SP, F>::NB;
+        float tg = 0.f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float g = gap(bx[c] - q[c], q[c] - bx[NB + c]);
+            tg = fmaf(g, g, tg);
+        }
+        if constexpr (LBV == 3) return w0 * __builtin_amdgcn_sqrtf(tg);  // translation only
+        float cc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cc[c] = 0.5f * (bx[3 + c] + bx[NB + 3 + c]);
+        float rot = fmaxf(__builtin_amdgcn_sqrtf(chord2(q + 4, cc)) - bx[2 * NB + 1] - 1e-5f, 0.f);
+        if constexpr (LBV == 2) {
+            float rp = 0.f, rm = 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float lo = bx[3 + c], hi = bx[NB + 3 + c], v = q[4 + c];
+                const float gp = gap(lo - v, v - hi);
+                const float gm = gap(lo + v, -v - hi);
+                rp = fmaf(gp, gp, rp);
+                rm = fmaf(gm, gm, rm);
+            }
+            rot = fmaxf(rot, __builtin_amdgcn_sqrtf(fminf(rp, rm)));
+        }
+        return w0 * __builtin_amdgcn_sqrtf(tg) + w1 * rot;
+    } else {
+        return box_lb<SP, F>(bx, q, w0, w1);
+    }
+}
+
 // fp32 screened distance of a lane's state x (R stored coordinates) to query row q.  SE3:
 // translation as the reference, rotation by the chord (error bound in the header):
 // theta = 2 asin(c / 2) = pi - 2 acos(c / 2), c^2 = min(|p - q|^2, |p + q|^2), both sums on
@@ -619,7 +566,7 @@ constexpr int kBulkThreshold = 8;
 
 // K2: lanes per query in the output (16 / 32 / 64); k2 <= K2: the list length the walk keeps
 // (the certificate's margin: k + 3 for the culled spaces, whose screen error is small)
-template <int SP, int F, int K2, int G, int MINW, bool QS>
+template <int SP, int F, int K2, int G, int MINW, bool QS, int LBV = 0>
 __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
@@ -699,7 +646,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         bool need = false;
 #pragma unroll
         for (int j = 0; j < GH; ++j) {
-            lb[j] = box_lb<SP, F>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
+            lb[j] = tile_lb<SP, F, LBV>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
             need |= lb[j] < (half ? td[GH + j] : td[j]);
         }
         return fold_tiles(__ballot(need));
@@ -1515,10 +1462,20 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             constexpr int G = group_queries<SP>();
-            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
-                               ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0,
-                               q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, kBulkThreshold,
-                               p.k2);
+            // tile bound variant (tile_lb): OMPL_GPU_TILE_LB = 0 box, 1 cap, 2 both, 3 translation only
+            static const int lbv = [] {
+                const char *v = std::getenv("OMPL_GPU_TILE_LB");
+                return v ? std::atoi(v) : 0;
+            }();
+#define OMPL_AMD_GROUP(V)                                                                                          \
+    hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true, V>), dim3((nq + G - 1) / G), dim3(64), 0, st,   \
+                       ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0, q32, keys2, \
+                       nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, kBulkThreshold, p.k2)
+            if (SP == OMPL_GPU_SPACE_SE3 && lbv == 1) OMPL_AMD_GROUP(1);
+            else if (SP == OMPL_GPU_SPACE_SE3 && lbv == 2) OMPL_AMD_GROUP(2);
+            else if (SP == OMPL_GPU_SPACE_SE3 && lbv == 3) OMPL_AMD_GROUP(3);
+            else OMPL_AMD_GROUP(0);
+#undef OMPL_AMD_GROUP
             timer_end(st);
             walked = true;
         }
@@ -1825,9 +1782,25 @@ __global__ void tile_box_range_kernel(const float *__restrict__ rows, uint32_t n
         }
     }
     if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        // rotation cap: chord radius rho of the tile's quaternions around the centre c of their
+        // box (tile_lb); the chord min(|p - c|, |p + c|) is a metric on any 4-vectors
+        float cc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float lo = ok ? x[3 + c] : __builtin_inff(), hi = ok ? x[3 + c] : -__builtin_inff();
+#pragma unroll
+            for (int sh = 32; sh > 0; sh >>= 1) {
+                lo = fminf(lo, __shfl_xor(lo, sh));
+                hi = fmaxf(hi, __shfl_xor(hi, sh));
+            }
+            cc[c] = 0.5f * (lo + hi);
+        }
+        float r2 = ok ? chord2(x + 3, cc) : 0.f;
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) r2 = fmaxf(r2, __shfl_xor(r2, sh));
         if (lane == 0) {
             o[2 * NB] = eta * 1.00001f;
-            o[2 * NB + 1] = 0.f;
+            o[2 * NB + 1] = __builtin_amdgcn_sqrtf(r2) * 1.000001f + 1e-6f;
         }
     }
 }
