@@ -306,7 +306,9 @@ ompl_gpu_status ompl_gpu_lazyprm_add_milestones(ompl_gpu_nn *nn, const double *s
  * 0xFFFFFFFF.  d_samples are ns AoS rows (device).  Both handles must describe the same
  * space (R^n, SO3 or SE3) on the same device; mv's valid / invalid counters are updated.
  * All iterations are queued on the NN handle's stream with no host round trip;
- * synchronous on return. */
+ * synchronous on return.  The persistent one-launch form gives up when a grid-wide wait
+ * outlives its spin limit (the device shared with a long kernel); the batch is then re-run in
+ * the two-launch form from the same start (counters restored), with identical results. */
 ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
                                          double max_distance, uint32_t *d_nearest, uint32_t *d_added);
 /* The same loop with RRT's goal test (RRT.cpp:175-187): after each added state,
@@ -316,6 +318,8 @@ ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const
  * d_nearest / d_added are 0xFFFFFFFF).  Otherwise the added state strictly closest to the goal
  * is the approximate solution: *approx_id / *approx_dist (0xFFFFFFFF / +inf if nothing was
  * added).  goal: host, dim reals.  Output pointers may be NULL. */
+/* Persistent RRT runs that gave up and were re-run in the two-launch form (diagnostics). */
+ompl_gpu_status ompl_gpu_rrt_aborts(const ompl_gpu_nn *nn, uint64_t *aborts);
 ompl_gpu_status ompl_gpu_rrt_solve_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
                                           double max_distance, const double *goal, double goal_threshold,
                                           uint32_t *d_nearest, uint32_t *d_added, uint64_t *solved_at,

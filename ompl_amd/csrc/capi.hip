@@ -108,6 +108,8 @@ struct ompl_gpu_nn {
     int rrt_coop = -1;             // persistent RRT grid size (0: two-launch form), found on first use
     void *rrt_sync = nullptr;      // its uncached synchronisation record
     DevBuf rrt_goal;               // goal record + goal reals of ompl_gpu_rrt_solve_device
+    DevBuf rrt_save;               // motion-validator counters before a persistent run (restored on abort)
+    uint64_t rrt_aborts = 0;       // persistent runs that aborted and re-ran in the two-launch form
     DevBuf prm_bf, prm_raw, prm_kj, prm_sd, prm_si, prm_len, prm_off, prm_eoff, prm_cnt64;  // PRM* batches
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
@@ -1536,9 +1538,24 @@ ompl_gpu_status rrt_run(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples
     // coordinates, and starts from the store's bounds (words 7 = B, 28 = eta of its record)
     const bool coop = h->rrt_sync && h->rows32 && screen_safe(h);
     if (coop) {
+        // OMPL_GPU_RRT_SPIN_LIMIT (tests): a small spin limit forces the abort-and-re-run path
+        const char *lim = std::getenv("OMPL_GPU_RRT_SPIN_LIMIT");
+        if (lim && std::atoll(lim) > 0) {
+            const uint64_t v = (uint64_t)std::atoll(lim);
+            HIP_OR_FAIL(hipMemcpyAsync((uint64_t *)h->rrt_sync + 4, &v, sizeof(v), hipMemcpyHostToDevice, h->stream));
+            HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // v is a host local
+        }
         const double B = h->absmax * (1.0 + 1e-6), eta = h->qeta * 1.01;
         HIP_OR_FAIL(hipMemcpyAsync((uint64_t *)h->rrt_sync + 7, &B, sizeof(double), hipMemcpyHostToDevice, h->stream));
         HIP_OR_FAIL(hipMemcpyAsync((uint64_t *)h->rrt_sync + 28, &eta, sizeof(double), hipMemcpyHostToDevice, h->stream));
+    }
+    // the persistent grid's counters / goal record / live size are restored if it aborts (a wait
+    // past kSpinLimit: the device shared with a long kernel), and the batch re-runs in the
+    // two-launch form — the store rows it wrote past n0 are not committed (n_total unchanged)
+    if (coop) {
+        HIP_OR_FAIL(h->rrt_save.ensure(4 * sizeof(unsigned long long)));
+        HIP_OR_FAIL(hipMemcpyAsync(h->rrt_save.p, mv->counters, 4 * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToDevice, h->stream));
     }
     HIP_OR_FAIL(launch_rrt_grow(h->sp, mv->sp, mv->ck, h->g, h->feat, h->feat32, h->rows32, h->cap, n0,
                                 (uint64_t *)h->rrt_n.p, d_samples, (uint32_t)ns, max_distance, (double *)h->rrt_pd.p,
@@ -1547,13 +1564,24 @@ ompl_gpu_status rrt_run(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples
                                 h->stream));
     if (coop) HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // B / eta above are host locals
     uint64_t grec_h[3] = {~0ull, 0, kNoId};
-    HIP_OR_FAIL(hipMemcpyAsync(grec_h, grec, sizeof(grec_h), hipMemcpyDeviceToHost, h->stream));
     uint64_t n1 = n0;
     uint64_t bar_h[3] = {0, 0, 0};
-    if (h->rrt_sync) HIP_OR_FAIL(hipMemcpyAsync(bar_h, h->rrt_sync, sizeof(bar_h), hipMemcpyDeviceToHost, h->stream));
+    if (coop) HIP_OR_FAIL(hipMemcpyAsync(bar_h, h->rrt_sync, sizeof(bar_h), hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (bar_h[2]) {  // aborted: restore and re-run the whole batch in the two-launch form
+        h->rrt_aborts++;
+        HIP_OR_FAIL(hipMemcpyAsync(mv->counters, h->rrt_save.p, 4 * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToDevice, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(h->rrt_n.p, &n0, sizeof(uint64_t), hipMemcpyHostToDevice, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(grec, grec0, sizeof(grec0), hipMemcpyHostToDevice, h->stream));
+        HIP_OR_FAIL(launch_rrt_grow(h->sp, mv->sp, mv->ck, h->g, h->feat, h->feat32, h->rows32, h->cap, n0,
+                                    (uint64_t *)h->rrt_n.p, d_samples, (uint32_t)ns, max_distance,
+                                    (double *)h->rrt_pd.p, (uint32_t *)h->rrt_pi.p, d_nearest, d_added, mv->counters,
+                                    nullptr, 0u, goal ? dgoal : nullptr, goal_threshold, grec, h->stream));
+    }
+    HIP_OR_FAIL(hipMemcpyAsync(grec_h, grec, sizeof(grec_h), hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(&n1, h->rrt_n.p, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
-    if (bar_h[2]) return fail(OMPL_GPU_ERR_DEVICE, "persistent RRT grid barrier timed out (grid not co-resident)");
     if (goal && grec_h[0] != ~0ull && grec_h[0] + 1 < ns) {  // iterations after the solution did not run
         HIP_OR_FAIL(hipMemsetAsync(d_nearest + grec_h[0] + 1, 0xFF, sizeof(uint32_t) * (ns - grec_h[0] - 1), h->stream));
         HIP_OR_FAIL(hipMemsetAsync(d_added + grec_h[0] + 1, 0xFF, sizeof(uint32_t) * (ns - grec_h[0] - 1), h->stream));
@@ -1573,6 +1601,12 @@ ompl_gpu_status rrt_run(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples
     return OMPL_GPU_OK;
 }
 }  // namespace
+
+ompl_gpu_status ompl_gpu_rrt_aborts(const ompl_gpu_nn *h, uint64_t *aborts) {
+    if (!h || !aborts) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    *aborts = h->rrt_aborts;
+    return OMPL_GPU_OK;
+}
 
 ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
                                          double max_distance, uint32_t *d_nearest, uint32_t *d_added) {

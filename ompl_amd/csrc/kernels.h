@@ -236,9 +236,9 @@ hipError_t launch_prm_scatter_valid(const uint8_t *vc, const uint32_t *cnt, cons
 
 // ---- RRT growth on device (rrt.hip) -------------------------------------------------------
 size_t rrt_part_entries(uint64_t n_max);
-// blocks of the persistent (cooperative) RRT grid on this device, 0 when cooperative launches
-// are unavailable (the two-launch form is used then); its synchronisation record (uncached
-// device memory, zeroed before each launch) holds rrt_sync_bytes()
+// blocks of the persistent RRT grid on this device (one per CU, an ordinary launch), 0 when it
+// cannot run (the two-launch form is used then); its synchronisation record (uncached device
+// memory, zeroed before each launch) holds rrt_sync_bytes()
 size_t rrt_sync_bytes();
 uint32_t rrt_coop_blocks(int device, const DevSpace &sp, const FeatGeom &g);
 hipError_t launch_rrt_grow(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck, const FeatGeom &g,

@@ -263,7 +263,7 @@ constexpr int kLook = 2;                     // samples the scans run ahead of t
 constexpr int kRing = kLook + 2;             // record / decision ring depth
 
 // the uncached synchronisation record (rrt_sync_bytes), 64-bit words:
-//   [2] abort  [7] B of the initial store  [24 .. 27) goal record  [28] eta of the initial store
+//   [2] abort  [4] spin limit override (0: kSpinLimit)  [7] B of the initial store  [24 .. 27) goal record  [28] eta of the initial store
 //   [64 + 64 c] (c < 8) generation copies: index + 1 of the latest decision
 //   [kSyncDec + kDecWords r]  decision slot r: [1] added  [2] solved  [3] B  [4] eta  [8 .. 8+F) row
 //   [kSyncFlags + b]  block b's published records: index + 1 of the latest sample
@@ -284,11 +284,14 @@ __device__ __forceinline__ uint64_t dbits(double v) { return (uint64_t)__double_
 __device__ __forceinline__ double bitsd(uint64_t v) { return __longlong_as_double((long long)v); }
 
 // poll *p until it reaches `want` (false: the spin limit passed or some block aborted)
+// (word [4] of the record, when non-zero, replaces kSpinLimit: the tests force an abort with it)
 __device__ __forceinline__ bool wait_for(const uint64_t *p, uint64_t want, uint64_t *abort_word) {
     uint32_t spins = 0;
+    const uint64_t lim = ld_sync(abort_word + 2);
+    const uint32_t limit = lim ? (uint32_t)lim : kSpinLimit;
     while (ld_sync(p) < want) {
         __builtin_amdgcn_s_sleep(2);
-        if (++spins > kSpinLimit || ld_sync(abort_word)) return false;
+        if (++spins > limit || ld_sync(abort_word)) return false;
     }
     return true;
 }
@@ -628,10 +631,15 @@ hipError_t run_rrt(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck
             uint64_t slice = (nmax + nscan - 1) / nscan;
             slice = (slice + 1023) & ~(uint64_t)1023;
             const uint32_t nb = (uint32_t)((nmax + slice - 1) / slice) + 1;
-            void *args[] = {&feat, &feat32, &rows32, &cap, &n0, &n_dev, &samples, &ns, &slice, (void *)&sp,
-                            (void *)&msp, (void *)&ck, &maxd, &sync, &nearest, &added, &counters, &gl, &grec};
-            return hipLaunchCooperativeKernel((const void *)rrt_persistent_kernel<SP, F>, dim3(nb), dim3(256), args,
-                                              0, st);
+            // one 256-thread block per CU: the grid is co-resident on any device that runs it at all
+            // (a CU holds 8 such blocks), so an ordinary launch; a wait that outlives kSpinLimit
+            // (the device shared with a long kernel) aborts the grid and the caller re-runs the batch
+            // in the two-launch form.  (hipLaunchCooperativeKernel's queue made the HIP runtime's
+            // exit-time teardown fault under rocprofv3: profiles/r3_extras.)
+            hipLaunchKernelGGL((rrt_persistent_kernel<SP, F>), dim3(nb), dim3(256), 0, st, feat, feat32, rows32, cap,
+                               n0, n_dev, samples, ns, slice, sp, msp, ck, maxd, sync, nearest, added, counters, gl,
+                               grec);
+            return hipGetLastError();
         }
     }
     for (uint32_t i = 0; i < ns; ++i) {
@@ -653,8 +661,7 @@ uint32_t rrt_coop_blocks(int device, const DevSpace &sp, const FeatGeom &g) {
 #if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 3
     return 0;  // A/B build: the two-launch form
 #endif
-    int coop = 0, cus = 0;
-    if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess || !coop) return 0;
+    int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 0;
     const void *fn = nullptr;
     switch (sp.kind) {

@@ -213,6 +213,12 @@ class NearestNeighborsGPU(abi.Handle):
         abi.check(abi.lib.ompl_gpu_rrt_grow_device(self._h, mv._h, C.c_void_p(d_samples), int(ns), float(max_distance),
                                                    C.c_void_p(d_nearest), C.c_void_p(d_added)))
 
+    def rrt_aborts(self) -> int:
+        """Persistent RRT runs that gave up (spin limit) and were re-run in the two-launch form."""
+        a = C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_rrt_aborts(self._h, C.byref(a)))
+        return a.value
+
     def rrt_solve_device(self, mv, d_samples: int, ns: int, max_distance: float, goal, goal_threshold: float,
                          d_nearest: int, d_added: int):
         """RRT iterations with the goal test (RRT.cpp:128-192): stops at the first added state

@@ -139,8 +139,13 @@ def _rrt_oracle(sp, ck, tree0, samples, maxd):
     return np.array(near), np.array(added, dtype=np.int64), np.array(tree)
 
 
-@pytest.mark.parametrize("case", ["r6_allvalid", "se3_spheres"])
-def test_rrt_grow_matches_sequential_loop(gpu, case):
+@pytest.mark.parametrize("case", ["r6_allvalid", "se3_spheres", "se3_spheres_abort"])
+def test_rrt_grow_matches_sequential_loop(gpu, case, monkeypatch):
+    """The persistent grid, and (case *_abort: a spin limit of 1 poll makes the grid give up at
+    its first wait) the abort path: counters restored, the batch re-run in the two-launch form
+     — the same answer as the sequential loop either way."""
+    if case.endswith("abort"):
+        monkeypatch.setenv("OMPL_GPU_RRT_SPIN_LIMIT", "1")
     rng = np.random.default_rng(84)
     if case == "r6_allvalid":
         sp, ck = RealVectorStateSpace(6), AllValidChecker()
@@ -158,6 +163,8 @@ def test_rrt_grow_matches_sequential_loop(gpu, case):
     near = torch.empty(300, dtype=torch.int32, device=dev)
     added = torch.empty(300, dtype=torch.int32, device=dev)
     nn.rrt_grow_device(mv, ds.data_ptr(), 300, maxd, near.data_ptr(), added.data_ptr())
+    if case.endswith("abort"):
+        assert nn.rrt_aborts() == 1, "the persistent grid did not abort"
     en, ea, tree = _rrt_oracle(sp, ck, tree0, samples, maxd)
     np.testing.assert_array_equal(near.cpu().numpy().astype(np.int64), en)
     np.testing.assert_array_equal(added.cpu().numpy().astype(np.uint32).astype(np.int64), ea)

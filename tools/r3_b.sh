@@ -12,7 +12,7 @@ timeout -k 10 200 python -u tools/build_probe.py > "$out/build.json" 2> "$out/bu
 rc=$?; cat "$out/build.json"; tail -2 "$out/build.err"; if fatal $rc; then echo "build rc=$rc"; exit 1; fi
 args="--steps 6 --warmup 2 --no-cpu-baseline --no-extras --single-query-reps 0 --rrt-iters 0"
 for r in 1 2; do
-  for v in ${LBV:-0 1 2 3}; do
+  for v in ${LBV-0 1 2 3}; do
     OMPL_GPU_TILE_LB=$v timeout -k 10 200 python -u bench.py $args > "$out/lb${v}_$r.json" 2>/dev/null
     rc=$?; if fatal $rc; then echo "lb$v rc=$rc"; exit 1; fi
     python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[1].split('/')[-1], round(d['value']/1e6,2), 'walk_ms', round(r['kernel_ms'],4), 'pairs', r['algorithmic'][:10], 'reruns', d['fast_path'])" "$out/lb${v}_$r.json"
