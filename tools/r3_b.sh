@@ -25,4 +25,4 @@ sq) a="--rrt-iters 0 --single-query-reps 200 --no-extras";;
 esac
 OMPL_AMD_MAPS=$out/maps.txt timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/iso" -o trace --output-format csv \
     -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline $a > "$out/iso.log" 2>&1
-echo "iso($2) rc=$?"
+rc=$?; echo "iso($2) rc=$rc"; exit $rc
