@@ -72,3 +72,27 @@ def test_boundary_runs_on_gpu(tmp_path, gpu):
     exe = _build(str(tmp_path / "boundary_run"), [], BOUNDARY_SRC)
     r = subprocess.run([exe, "run"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "BOUNDARY OK" in r.stdout, r.stdout + r.stderr
+
+
+VERTEX_SRC = os.path.join(ROOT, "tests", "cpp", "vertex_plugin_test.cpp")
+
+
+def test_vertex_plugin_compiles_standalone(tmp_path):
+    """NearestNeighborsGPU<std::size_t> + ElementPacker (PRM Vertex / Blaze VertexID) compiles."""
+    exe = _build(str(tmp_path / "vertex_sa"), [], VERTEX_SRC)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0 and "VERTEX PLUGIN COMPILED" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_SRC, "ompl/datastructures/NearestNeighbors.h")),
+                    reason="reference sources absent")
+def test_vertex_plugin_compiles_against_reference_interface(tmp_path):
+    _build(str(tmp_path / "vertex_ref"), ["-DOMPL_AMD_WITH_OMPL", "-I", REF_SRC], VERTEX_SRC)
+
+
+@pytest.mark.gpu
+def test_vertex_plugin_runs_on_gpu(tmp_path, gpu):
+    """PRM*-style causal nearestK over vertex ids, Blaze-style nearestR, removal, batched kNN."""
+    exe = _build(str(tmp_path / "vertex_run"), [], VERTEX_SRC)
+    r = subprocess.run([exe, "run"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "VERTEX PLUGIN OK" in r.stdout, r.stdout + r.stderr
