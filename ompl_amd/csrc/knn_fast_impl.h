@@ -447,44 +447,6 @@ __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w
     }
 }
 
-// lower bound for one 64-state tile (the group walk's tile masks).  SE3: the translation gaps of
-// the box, and for the rotation either the box (variant 0: the distance from q and -q to the
-// quaternion box, 8 gaps) or the tile's rotation cap (1: chord(q, c) - rho, one packed chord;
-// 2: the larger of both).  chord(q, p) >= chord(q, c) - chord(c, p) >= chord(q, c) - rho, and
-// the screened angle is >= the chord; the margin covers the fp32 rounding of both chords.
-template <int SP, int F, int LBV>
-__device__ __forceinline__ float tile_lb(const float *bx, const float *q, float w0, float w1) {
-    if constexpr (SP == OMPL_GPU_SPACE_SE3 && LBV != 0) {
-        constexpr int NB = Geo<SP, F>::NB;
-        float tg = 0.f;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float g = gap(bx[c] - q[c], q[c] - bx[NB + c]);
-            tg = fmaf(g, g, tg);
-        }
-        if constexpr (LBV == 3) return w0 * __builtin_amdgcn_sqrtf(tg);  // translation only
-        float cc[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) cc[c] = 0.5f * (bx[3 + c] + bx[NB + 3 + c]);
-        float rot = fmaxf(__builtin_amdgcn_sqrtf(chord2(q + 4, cc)) - bx[2 * NB + 1] - 1e-5f, 0.f);
-        if constexpr (LBV == 2) {
-            float rp = 0.f, rm = 0.f;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float lo = bx[3 + c], hi = bx[NB + 3 + c], v = q[4 + c];
-                const float gp = gap(lo - v, v - hi);
-                const float gm = gap(lo + v, -v - hi);
-                rp = fmaf(gp, gp, rp);
-                rm = fmaf(gm, gm, rm);
-            }
-            rot = fmaxf(rot, __builtin_amdgcn_sqrtf(fminf(rp, rm)));
-        }
-        return w0 * __builtin_amdgcn_sqrtf(tg) + w1 * rot;
-    } else {
-        return box_lb<SP, F>(bx, q, w0, w1);
-    }
-}
-
 // fp32 screened distance of a lane's state x (R stored coordinates) to query row q.  SE3:
 // translation as the reference, rotation by the chord (error bound in the header):
 // theta = 2 asin(c / 2) = pi - 2 acos(c / 2), c^2 = min(|p - q|^2, |p + q|^2), both sums on
@@ -566,7 +528,7 @@ constexpr int kBulkThreshold = 8;
 
 // K2: lanes per query in the output (16 / 32 / 64); k2 <= K2: the list length the walk keeps
 // (the certificate's margin: k + 3 for the culled spaces, whose screen error is small)
-template <int SP, int F, int K2, int G, int MINW, bool QS, int LBV = 0>
+template <int SP, int F, int K2, int G, int MINW, bool QS>
 __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
@@ -646,7 +608,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         bool need = false;
 #pragma unroll
         for (int j = 0; j < GH; ++j) {
-            lb[j] = tile_lb<SP, F, LBV>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
+            lb[j] = box_lb<SP, F>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
             need |= lb[j] < (half ? td[GH + j] : td[j]);
         }
         return fold_tiles(__ballot(need));
@@ -1462,20 +1424,10 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             constexpr int G = group_queries<SP>();
-            // tile bound variant (tile_lb): OMPL_GPU_TILE_LB = 0 box, 1 cap, 2 both, 3 translation only
-            static const int lbv = [] {
-                const char *v = std::getenv("OMPL_GPU_TILE_LB");
-                return v ? std::atoi(v) : 0;
-            }();
-#define OMPL_AMD_GROUP(V)                                                                                          \
-    hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true, V>), dim3((nq + G - 1) / G), dim3(64), 0, st,   \
-                       ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0, q32, keys2, \
-                       nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, kBulkThreshold, p.k2)
-            if (SP == OMPL_GPU_SPACE_SE3 && lbv == 1) OMPL_AMD_GROUP(1);
-            else if (SP == OMPL_GPU_SPACE_SE3 && lbv == 2) OMPL_AMD_GROUP(2);
-            else if (SP == OMPL_GPU_SPACE_SE3 && lbv == 3) OMPL_AMD_GROUP(3);
-            else OMPL_AMD_GROUP(0);
-#undef OMPL_AMD_GROUP
+            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
+                               ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0,
+                               q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, kBulkThreshold,
+                               p.k2);
             timer_end(st);
             walked = true;
         }
@@ -1782,25 +1734,9 @@ __global__ void tile_box_range_kernel(const float *__restrict__ rows, uint32_t n
         }
     }
     if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-        // rotation cap: chord radius rho of the tile's quaternions around the centre c of their
-        // box (tile_lb); the chord min(|p - c|, |p + c|) is a metric on any 4-vectors
-        float cc[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            float lo = ok ? x[3 + c] : __builtin_inff(), hi = ok ? x[3 + c] : -__builtin_inff();
-#pragma unroll
-            for (int sh = 32; sh > 0; sh >>= 1) {
-                lo = fminf(lo, __shfl_xor(lo, sh));
-                hi = fmaxf(hi, __shfl_xor(hi, sh));
-            }
-            cc[c] = 0.5f * (lo + hi);
-        }
-        float r2 = ok ? chord2(x + 3, cc) : 0.f;
-#pragma unroll
-        for (int sh = 32; sh > 0; sh >>= 1) r2 = fmaxf(r2, __shfl_xor(r2, sh));
         if (lane == 0) {
             o[2 * NB] = eta * 1.00001f;
-            o[2 * NB + 1] = __builtin_amdgcn_sqrtf(r2) * 1.000001f + 1e-6f;
+            o[2 * NB + 1] = 0.f;
         }
     }
 }
@@ -1836,6 +1772,9 @@ __global__ void super_box_range_kernel(const float *__restrict__ tbox, uint32_t 
 // sort keys) reads contiguous rows, and one gather of whole rows per level follows the sort.
 // (Round 2 gathered each of the 8 coordinates by id in two passes per level: 8 cache lines per
 // state, 1.5 ms per level at 10^7 states.)
+constexpr int kKdQBits = 12;                       // split-coordinate quantisation of the build's sort keys
+constexpr uint32_t kKdQ = (1u << kKdQBits) - 1u;
+
 template <int SP, int F>
 struct KdRow {
     static constexpr int NB = Geo<SP, F>::NB;
@@ -1899,7 +1838,7 @@ __global__ void kd_row_tile_boxes_kernel(const float *__restrict__ W, uint32_t n
     }
 }
 
-// one block per node of the level: widest box coordinate -> nsplit[path] = {dim, lo, 65535 / extent}
+// one block per node of the level: widest box coordinate -> nsplit[path] = {dim, lo, kKdQ / extent}
 template <int SP, int F>
 __global__ __launch_bounds__(256) void kd_node_split_dim_kernel(const float *__restrict__ tb, uint32_t ntiles,
                                                                 int level, float4 *__restrict__ nsplit) {
@@ -1961,20 +1900,26 @@ __global__ __launch_bounds__(256) void kd_node_split_dim_kernel(const float *__r
                 bd = d;
             }
         }
-        const float inv = be > 0.f ? 65535.f / be : 0.f;
+        const float inv = be > 0.f ? (float)kKdQ / be : 0.f;
         nsplit[blockIdx.x] = make_float4(__uint_as_float((uint32_t)bd), lo[bd], inv, 0.f);
     }
 }
 
 // sort key of position p at this level: (node path, extended by zeros for a node that is
-// already a leaf) << 16 | its split coordinate quantised to 16 bits over the node's extent
-// (0 in a leaf, which keeps it in place under the stable sort).  Quantisation only decides
-// how states with nearly equal coordinates straddle the split: the left part still gets
-// exactly floor(T/2) tiles, and every tile / super-tile box is computed from the states it
-// holds, so the walks' bounds do not depend on it.
-template <int SP, int F, typename Key>
+// already a leaf) << kKdQBits | its split coordinate quantised to kKdQBits bits over the node's
+// extent (0 in a leaf, which keeps it in place under the stable sort).  Quantisation only decides
+// how states with nearly equal coordinates straddle the split: the left part still gets exactly
+// floor(T/2) tiles, and every tile / super-tile box is computed from the states it holds, so the
+// walks' bounds do not depend on it.  path bits + kKdQBits <= 32 for every level the global loop
+// runs (the LDS finish takes the deep ones), so the keys are 32-bit.
+__device__ __forceinline__ uint32_t kd_quant(float v, float4 ns) {
+    const float x = (v - ns.y) * ns.z;
+    return x > 0.f ? (x < (float)kKdQ ? (uint32_t)x : kKdQ) : 0u;
+}
+
+template <int SP, int F>
 __global__ void kd_row_keys_kernel(const float *__restrict__ W, uint32_t n, uint32_t ntiles, int level,
-                                   const float4 *__restrict__ nsplit, Key *__restrict__ keys,
+                                   const float4 *__restrict__ nsplit, uint32_t *__restrict__ keys,
                                    uint32_t *__restrict__ vals) {
     constexpr int RW = KdRow<SP, F>::W;
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1996,24 +1941,49 @@ __global__ void kd_row_keys_kernel(const float *__restrict__ W, uint32_t n, uint
     uint32_t q = 0;
     if (l == level && T > 1) {
         const float4 ns = nsplit[path];
-        const float v = W[(size_t)p * RW + (int)__float_as_uint(ns.x)];
-        const float x = (v - ns.y) * ns.z;
-        q = x > 0.f ? (x < 65535.f ? (uint32_t)x : 65535u) : 0u;
+        q = kd_quant(W[(size_t)p * RW + (int)__float_as_uint(ns.x)], ns);
     } else {
         path <<= (level - l);
     }
-    keys[p] = ((Key)path << 16) | (Key)q;
+    keys[p] = (path << kKdQBits) | q;
     vals[p] = p;
 }
 
+// rows of the new order (W2[p] = W[src[p]], a wave per 64-row tile, one contiguous row read per
+// lane) and, from the rows in hand, the boxes of the new order's tiles for the next level
 template <int SP, int F>
-__global__ void kd_row_gather_kernel(const float *__restrict__ W, const uint32_t *__restrict__ src, uint32_t n,
-                                     float *__restrict__ W2) {
-    constexpr int RW = KdRow<SP, F>::W;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // (position, float4 column)
-    if (t >= n * (RW / 4)) return;
-    const uint32_t p = t / (RW / 4), c = t % (RW / 4);
-    reinterpret_cast<float4 *>(W2)[t] = reinterpret_cast<const float4 *>(W)[(size_t)src[p] * (RW / 4) + c];
+__global__ void kd_row_gather_boxes_kernel(const float *__restrict__ W, const uint32_t *__restrict__ src, uint32_t n,
+                                           uint32_t ntiles, float *__restrict__ W2, float *__restrict__ tb) {
+    constexpr int NB = KdRow<SP, F>::NB, RW = KdRow<SP, F>::W;
+    const uint32_t t = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= ntiles) return;
+    const uint32_t p = t * kCullTile + lane;
+    float r[RW];
+    if (p < n) {
+        const float4 *w4 = reinterpret_cast<const float4 *>(W + (size_t)src[p] * RW);
+        float4 *o4 = reinterpret_cast<float4 *>(W2 + (size_t)p * RW);
+#pragma unroll
+        for (int c = 0; c < RW / 4; ++c) {
+            const float4 v = w4[c];
+            o4[c] = v;
+            r[4 * c] = v.x; r[4 * c + 1] = v.y; r[4 * c + 2] = v.z; r[4 * c + 3] = v.w;
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < NB; ++d) {
+        float lo = p < n ? r[d] : __builtin_inff();
+        float hi = p < n ? r[d] : -__builtin_inff();
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            lo = fminf(lo, __shfl_xor(lo, o));
+            hi = fmaxf(hi, __shfl_xor(hi, o));
+        }
+        if (lane == 0) {
+            tb[(size_t)t * 2 * NB + d] = lo;
+            tb[(size_t)t * 2 * NB + NB + d] = hi;
+        }
+    }
 }
 
 // node records of the level (pre-order): split = first coordinate of the right part
@@ -2030,6 +2000,153 @@ __global__ void kd_row_split_kernel(const float *__restrict__ W, uint32_t n, uin
     const int d = (int)__float_as_uint(nsplit[path].x);
     const float split = pos < n ? W[(size_t)pos * RW + d] : __builtin_inff();
     nodes[nd.pidx] = KdNode{(uint32_t)d, split, tl, nd.pidx + tl};
+}
+
+// The deep levels in LDS: one block per node of level L0 (at most kd_lds_tiles<SP, F>() tiles,
+// so its rows fit in LDS) splits its whole subtree there — per sub-level the same steps as the
+// global loop (tile boxes of the current order, the widest coordinate of every splitting
+// sub-node, (sub-path, quantised coordinate) keys) with a bitonic sort of (key, row index) in
+// LDS instead of a device-wide radix sort, then writes the node records and its rows in leaf
+// order.  Padding slots (past the last state) sort last with key 0xFFFFFFFF.
+template <int SP, int F>
+constexpr uint32_t kd_lds_tiles() {
+    constexpr int RW = KdRow<SP, F>::W;
+    return RW <= 8 ? 32u : (RW <= 12 ? 16u : 8u);  // <= 64 KiB of rows
+}
+
+template <int SP, int F>
+__global__ __launch_bounds__(256) void kd_lds_finish_kernel(const float *__restrict__ W, float *__restrict__ Wout,
+                                                            uint32_t n, uint32_t ntiles, int L0, int depth,
+                                                            KdNode *__restrict__ nodes) {
+    constexpr int NB = KdRow<SP, F>::NB, RW = KdRow<SP, F>::W;
+    constexpr uint32_t LT = kd_lds_tiles<SP, F>(), NMAX = LT * kCullTile;
+    __shared__ __attribute__((aligned(16))) float rows[NMAX * RW];
+    __shared__ uint32_t key[NMAX];
+    __shared__ uint16_t idx[NMAX];
+    __shared__ float tbs[LT][2 * NB];
+    __shared__ float4 nsp[LT];
+    const KdNodeRef nd = kd_node_at(ntiles, L0, blockIdx.x);
+    if (!nd.valid) return;
+    const uint32_t P0 = nd.t0 * kCullTile, T = nd.T;
+    const uint32_t cnt = min(T * kCullTile, n > P0 ? n - P0 : 0u);
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t e = tid; e < cnt * (RW / 4); e += blockDim.x)
+        reinterpret_cast<float4 *>(rows)[e] = reinterpret_cast<const float4 *>(W + (size_t)P0 * RW)[e];
+    uint32_t N2 = 1;
+    while (N2 < T * kCullTile) N2 <<= 1;
+    for (uint32_t e = tid; e < N2; e += blockDim.x) idx[e] = (uint16_t)e;
+    __syncthreads();
+    const int lanes = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int l = 0; L0 + l < depth && T > 1; ++l) {
+        // 1. tile boxes of the current order (a wave per tile)
+        for (uint32_t t = wave; t < T; t += blockDim.x / 64) {
+            const uint32_t e = t * kCullTile + lanes;
+            const bool in = e < cnt;
+            const float *r = rows + (size_t)idx[in ? e : 0] * RW;
+#pragma unroll
+            for (int d = 0; d < NB; ++d) {
+                float lo = in ? r[d] : __builtin_inff(), hi = in ? r[d] : -__builtin_inff();
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    lo = fminf(lo, __shfl_xor(lo, o));
+                    hi = fmaxf(hi, __shfl_xor(hi, o));
+                }
+                if (lanes == 0) {
+                    tbs[t][d] = lo;
+                    tbs[t][NB + d] = hi;
+                }
+            }
+        }
+        __syncthreads();
+        // 2. widest coordinate of every sub-node that splits at this sub-level
+        const uint32_t nsub = 1u << l;
+        for (uint32_t sp = tid; sp < nsub; sp += blockDim.x) {
+            const KdNodeRef sn = kd_node_at(T, l, sp);
+            if (!sn.valid || sn.T <= 1) continue;
+            int bd = 0;
+            float be = -1.f, blo = 0.f;
+            for (int d = 0; d < NB; ++d) {
+                float lo = __builtin_inff(), hi = -__builtin_inff();
+                for (uint32_t t = sn.t0; t < sn.t0 + sn.T; ++t) {
+                    lo = fminf(lo, tbs[t][d]);
+                    hi = fmaxf(hi, tbs[t][NB + d]);
+                }
+                if (hi - lo > be) {  // first widest, as the global levels
+                    be = hi - lo;
+                    bd = d;
+                    blo = lo;
+                }
+            }
+            nsp[sp] = make_float4(__uint_as_float((uint32_t)bd), blo, be > 0.f ? (float)kKdQ / be : 0.f, 0.f);
+        }
+        __syncthreads();
+        // 3. keys of the current order
+        for (uint32_t e = tid; e < N2; e += blockDim.x) {
+            uint32_t kk = 0xFFFFFFFFu;
+            if (e < cnt) {
+                const uint32_t t = e / kCullTile;
+                uint32_t t0 = 0, TT = T, path = 0;
+                int ll = 0;
+                for (; ll < l && TT > 1; ++ll) {
+                    const uint32_t tl = TT >> 1;
+                    const uint32_t right = t >= t0 + tl ? 1u : 0u;
+                    path = (path << 1) | right;
+                    if (right) {
+                        t0 += tl;
+                        TT -= tl;
+                    } else {
+                        TT = tl;
+                    }
+                }
+                uint32_t q = 0;
+                if (ll == l && TT > 1) {
+                    const float4 ns = nsp[path];
+                    q = kd_quant(rows[(size_t)idx[e] * RW + (int)__float_as_uint(ns.x)], ns);
+                } else {
+                    path <<= (l - ll);
+                }
+                kk = (path << kKdQBits) | q;
+            }
+            key[e] = kk;
+        }
+        __syncthreads();
+        // 4. bitonic sort of (key, idx) over N2 slots (ties: any order — boxes come from contents)
+        for (uint32_t k = 2; k <= N2; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t e = tid; e < N2; e += blockDim.x) {
+                    const uint32_t o = e ^ j;
+                    if (o > e) {
+                        const bool up = (e & k) == 0;
+                        const uint32_t ka = key[e], kb = key[o];
+                        if ((ka > kb) == up) {
+                            key[e] = kb;
+                            key[o] = ka;
+                            const uint16_t ia = idx[e];
+                            idx[e] = idx[o];
+                            idx[o] = ia;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        // 5. node records of the sub-level (pre-order index = the node's + the relative one)
+        for (uint32_t sp = tid; sp < nsub; sp += blockDim.x) {
+            const KdNodeRef sn = kd_node_at(T, l, sp);
+            if (!sn.valid || sn.T <= 1) continue;
+            const uint32_t tl = sn.T >> 1, e = (sn.t0 + tl) * kCullTile;
+            const int d = (int)__float_as_uint(nsp[sp].x);
+            const float split = e < cnt ? rows[(size_t)idx[e] * RW + d] : __builtin_inff();
+            const uint32_t pidx = nd.pidx + sn.pidx;
+            nodes[pidx] = KdNode{(uint32_t)d, split, tl, pidx + tl};
+        }
+        __syncthreads();
+    }
+    for (uint32_t e = tid; e < cnt; e += blockDim.x) {
+        const float4 *src = reinterpret_cast<const float4 *>(rows + (size_t)idx[e] * RW);
+        float4 *dst = reinterpret_cast<float4 *>(Wout + (size_t)(P0 + e) * RW);
+#pragma unroll
+        for (int c = 0; c < RW / 4; ++c) dst[c] = src[c];
+    }
 }
 
 // the sorted fp32 rows / ids / inverse map from the final working rows (positions [0, p_end);
@@ -2061,15 +2178,20 @@ __global__ void kd_rows_store_kernel(const float *__restrict__ W, uint32_t n, ui
     }
 }
 
-// fp64 features by id, AoS (fa per row, zero padded): the transpose of the SoA store, both
-// sides coalesced, so that the sorted fp64 rows are then gathered one contiguous row per state
+// fp64 features by id, AoS (fa per row, zero padded): the transpose of the SoA store, a thread per
+// id (coalesced column reads, one contiguous row written), so that the sorted fp64 rows are then
+// gathered one contiguous row per state
 __global__ void feat_aos_kernel(const double *__restrict__ f64, uint64_t cap, int F, int fa, uint64_t n,
                                 double *__restrict__ aos) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (column, id): coalesced reads
-    if (t >= n * fa) return;
-    const int c = (int)(t / n);
-    const uint64_t id = t - (uint64_t)c * n;
-    aos[id * fa + c] = c < F ? f64[(uint64_t)c * cap + id] : 0.0;
+    const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n) return;
+    double2 *o = reinterpret_cast<double2 *>(aos + id * fa);
+    for (int c = 0; c < fa; c += 2) {
+        double2 v;
+        v.x = c < F ? f64[(uint64_t)c * cap + id] : 0.0;
+        v.y = c + 1 < F ? f64[(uint64_t)(c + 1) * cap + id] : 0.0;
+        o[c / 2] = v;
+    }
 }
 
 __global__ void rows64_gather_kernel(const double *__restrict__ aos, int F, int fa, const uint32_t *__restrict__ ids,
@@ -2169,19 +2291,18 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
     constexpr int RW = KdRow<SP, F>::W;
     int depth = 0;
     while ((1u << depth) < main_tiles) ++depth;
-    const bool wide = depth + 16 > 32;  // 64-bit keys once path bits + 16 exceed 32
+    // global levels while some node holds more tiles than one block's LDS: level Lg is the first
+    // whose nodes (ceil(main_tiles / 2^L) tiles at most) fit; kd_lds_finish_kernel does the rest
+    int Lg = 0;
+    while (Lg < depth && ((main_tiles + (1u << Lg) - 1) >> Lg) > kd_lds_tiles<SP, F>()) ++Lg;
     size_t tmp_sel = 0, tmp_sort = 0;
     rocprim::counting_iterator<uint32_t> count_it(0);
     if ((e = rocprim::select(nullptr, tmp_sel, count_it, (const uint8_t *)nullptr, (uint32_t *)nullptr,
                              (uint32_t *)nullptr, n, st)) != hipSuccess)
         return e;
-    if (wide)
-        e = rocprim::radix_sort_pairs(nullptr, tmp_sort, (uint64_t *)nullptr, (uint64_t *)nullptr,
-                                      (uint32_t *)nullptr, (uint32_t *)nullptr, nl, 0, depth + 16, st);
-    else
-        e = rocprim::radix_sort_pairs(nullptr, tmp_sort, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                      (uint32_t *)nullptr, (uint32_t *)nullptr, nl, 0, depth + 16, st);
-    if (e != hipSuccess) return e;
+    if ((e = rocprim::radix_sort_pairs(nullptr, tmp_sort, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                       (uint32_t *)nullptr, (uint32_t *)nullptr, nl, 0, 32, st)) != hipSuccess)
+        return e;
     const size_t row_bytes = std::max<size_t>(4ull * RW * nl, 4ull * fa * n);  // each half of the pair
     size_t off = 0;
     auto take = [&](size_t b) {
@@ -2189,13 +2310,14 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
         off += align_up(b);
         return o;
     };
-    const size_t o_flags = take(n), o_sel = take(4 * n), o_k0 = take(8ull * nl), o_k1 = take(8ull * nl),
+    const size_t o_flags = take(n), o_sel = take(4 * n), o_k0 = take(4ull * nl), o_k1 = take(4ull * nl),
                  o_v0 = take(4ull * nl), o_w = take(2 * row_bytes), o_tb = take(4ull * main_tiles * 2 * NB),
                  o_ns = take(16ull * main_tiles + 16), o_cnt = take(8), o_tmp = take(std::max(tmp_sel, tmp_sort));
     if ((e = scratch_ensure(s, off)) != hipSuccess) return e;
     char *w = (char *)s->scratch;
     uint8_t *flags = (uint8_t *)(w + o_flags);
     uint32_t *sel = (uint32_t *)(w + o_sel), *vals = (uint32_t *)(w + o_v0), *nsel = (uint32_t *)(w + o_cnt);
+    uint32_t *k0 = (uint32_t *)(w + o_k0), *k1 = (uint32_t *)(w + o_k1);
     float *W0 = (float *)(w + o_w), *W1 = (float *)(w + o_w + row_bytes);
     float *tb = (float *)(w + o_tb);
     float4 *nsplit = (float4 *)(w + o_ns);
@@ -2207,30 +2329,28 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
     if ((e = rocprim::select(w + o_tmp, tb_bytes, count_it, flags, sel, nsel, (size_t)n_total, st)) != hipSuccess)
         return e;
     hipLaunchKernelGGL((kd_rows_init_kernel<SP, F>), dim3((nl + 255) / 256), b256, 0, st, f32, cap, sel, n_live, W0);
-    const uint32_t gather_threads = n_live * (RW / 4);
-    for (int level = 0; level < depth; ++level) {
+    if (Lg > 0)
         hipLaunchKernelGGL((kd_row_tile_boxes_kernel<SP, F>), dim3((main_tiles + 3) / 4), b256, 0, st, W0, n_live,
                            main_tiles, tb);
+    for (int level = 0; level < Lg; ++level) {
         hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F>), dim3(1u << level), b256, 0, st, tb, main_tiles, level,
                            nsplit);
+        hipLaunchKernelGGL((kd_row_keys_kernel<SP, F>), dim3((nl + 255) / 256), b256, 0, st, W0, n_live, main_tiles,
+                           level, nsplit, k0, vals);
         tb_bytes = std::max(tmp_sel, tmp_sort);
-        if (wide) {
-            uint64_t *k0 = (uint64_t *)(w + o_k0), *k1 = (uint64_t *)(w + o_k1);
-            hipLaunchKernelGGL((kd_row_keys_kernel<SP, F, uint64_t>), dim3((nl + 255) / 256), b256, 0, st, W0, n_live,
-                               main_tiles, level, nsplit, k0, vals);
-            e = rocprim::radix_sort_pairs(w + o_tmp, tb_bytes, k0, k1, vals, sel, n_live, 0, level + 16, st);
-        } else {
-            uint32_t *k0 = (uint32_t *)(w + o_k0), *k1 = (uint32_t *)(w + o_k1);
-            hipLaunchKernelGGL((kd_row_keys_kernel<SP, F, uint32_t>), dim3((nl + 255) / 256), b256, 0, st, W0, n_live,
-                               main_tiles, level, nsplit, k0, vals);
-            e = rocprim::radix_sort_pairs(w + o_tmp, tb_bytes, k0, k1, vals, sel, n_live, 0, level + 16, st);
-        }
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((kd_row_gather_kernel<SP, F>), dim3((gather_threads + 255) / 256), b256, 0, st, W0, sel,
-                           n_live, W1);
+        if ((e = rocprim::radix_sort_pairs(w + o_tmp, tb_bytes, k0, k1, vals, sel, n_live, 0, level + kKdQBits, st)) !=
+            hipSuccess)
+            return e;
+        hipLaunchKernelGGL((kd_row_gather_boxes_kernel<SP, F>), dim3((main_tiles + 3) / 4), b256, 0, st, W0, sel,
+                           n_live, main_tiles, W1, tb);
         std::swap(W0, W1);
         hipLaunchKernelGGL((kd_row_split_kernel<SP, F>), dim3(((1u << level) + 255) / 256), b256, 0, st, W0, n_live,
                            main_tiles, level, nsplit, s->nodes);
+    }
+    if (Lg < depth) {  // every node of level Lg finishes its subtree in LDS
+        hipLaunchKernelGGL((kd_lds_finish_kernel<SP, F>), dim3(1u << Lg), b256, 0, st, W0, W1, n_live, main_tiles, Lg,
+                           depth, s->nodes);
+        std::swap(W0, W1);
     }
     if ((e = hipMemsetAsync(s->inv, 0xFF, 4ull * s->cap_inv, st)) != hipSuccess) return e;
     const uint32_t p_end = (main_sup_tiles + tail_tiles) * kCullTile;  // padding: gap and tail region NaN
@@ -2244,9 +2364,8 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
     // fp64 rows in sorted order: transpose the SoA features by id into the (now free) row
     // buffers, then one contiguous row per slot
     double *aos = (double *)(w + o_w);
-    const uint64_t ta = (uint64_t)n_total * fa;
-    if (ta)
-        hipLaunchKernelGGL(feat_aos_kernel, dim3((unsigned)((ta + 255) / 256)), b256, 0, st, f64, cap, F, fa,
+    if (n_total)
+        hipLaunchKernelGGL(feat_aos_kernel, dim3((unsigned)((n_total + 255) / 256)), b256, 0, st, f64, cap, F, fa,
                            (uint64_t)n_total, aos);
     const uint32_t p64 = main_sup_tiles * kCullTile;
     const uint64_t c64 = (uint64_t)p64 * (fa / 2);
