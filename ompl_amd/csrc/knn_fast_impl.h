@@ -522,6 +522,42 @@ __device__ __forceinline__ void wave_merge_sorted(float &Ld, uint32_t &Li, float
 #pragma unroll
     for (int j = 32; j > 0; j >>= 1) bitonic_step(Ld, Li, j, (lane & j) == 0);
 }
+// (distance, id) as one 64-bit key: the walk's distances are >= 0 (or +inf / NaN), so their
+// IEEE bits (sign cleared) order as unsigned integers and the key orders (distance, id)
+// lexicographically — one 64-bit compare instead of the lex_less32 pair of compares and the
+// SALU mask logic around it
+__device__ __forceinline__ uint64_t kpack(float d, uint32_t id) {
+    return ((uint64_t)(__float_as_uint(d) & 0x7FFFFFFFu) << 32) | id;
+}
+__device__ __forceinline__ float kdist(uint64_t k) { return __uint_as_float((uint32_t)(k >> 32)); }
+constexpr uint64_t kMaxKey = (0x7F800000ull << 32) | 0xFFFFFFFFull;  // (+inf, kNoId)
+__device__ __forceinline__ uint64_t readlane_k(uint64_t v, int l) {
+    return ((uint64_t)readlane_u((uint32_t)(v >> 32), l) << 32) | readlane_u((uint32_t)v, l);
+}
+__device__ __forceinline__ uint64_t shr1_k(uint64_t v, uint64_t first) {
+    return ((uint64_t)shr1_u((uint32_t)(v >> 32), (uint32_t)(first >> 32)) << 32) | shr1_u((uint32_t)v, (uint32_t)first);
+}
+__device__ __forceinline__ uint64_t shfl_k(uint64_t v, int src) {
+    return ((uint64_t)(uint32_t)__shfl((int)(v >> 32), src) << 32) | (uint32_t)__shfl((int)v, src);
+}
+__device__ __forceinline__ uint64_t shfl_xor_k(uint64_t v, int j) {
+    return ((uint64_t)(uint32_t)__shfl_xor((int)(v >> 32), j) << 32) | (uint32_t)__shfl_xor((int)v, j);
+}
+__device__ __forceinline__ void bitonic_step_k(uint64_t &k, int j, bool keep_min) {
+    const uint64_t o = shfl_xor_k(k, j);
+    if ((o < k) == keep_min) k = o;
+}
+// wave_merge_sorted on packed keys: candidates c (non-candidates kMaxKey) into the sorted list L
+__device__ __forceinline__ void wave_merge_sorted_k(uint64_t &L, uint64_t c, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) bitonic_step_k(c, j, ((lane & j) == 0) == ((lane & k) == 0));
+    const uint64_t r = shfl_k(c, 63 - lane);
+    if (r < L) L = r;
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) bitonic_step_k(L, j, (lane & j) == 0);
+}
 // candidates in one ballot above which the bulk merge is used.  Measured (G = 4): SE3 1.58 /
 // 1.42 / 1.41 ms at 64 / 8 / 32; R^6 1.60 / 1.12 / 1.13 / 1.21 ms at 64 / 8 / 16 / 32
 constexpr int kBulkThreshold = 8;
@@ -562,16 +598,14 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     auto qscan = [&](int g) -> const float * { return &qrow[qoff + g * FS]; };
     // the lists (lane j = entry j) and their K2-th entries (wave-uniform); a padding query
     // gets threshold -inf so that it admits nothing and needs no tile
-    float Ld[G];
-    uint32_t Li[G];
-    float td[G];
-    uint32_t ti[G];
+    uint64_t Lk[G];  // packed (distance, id) list entries (kpack)
+    float td[G];     // the K2-th distance (box and ballot tests)
+    uint64_t tk[G];  // the K2-th entry: a candidate enters iff its key is below it
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        Ld[g] = __builtin_inff();
-        Li[g] = kNoId;
+        Lk[g] = kMaxKey;
         td[g] = g0 + g < nq ? __builtin_inff() : -__builtin_inff();
-        ti[g] = kNoId;
+        tk[g] = g0 + g < nq ? kMaxKey : 0ull;
     }
     uint32_t visited = 0, qscans = 0;  // tiles fetched; (tile, query) scans
 #ifdef OMPL_AMD_PROBE
@@ -636,31 +670,25 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 #ifdef OMPL_AMD_PROBE
                 ++pr_bulk;
 #endif
-                const bool c = d < td[g];
-                wave_merge_sorted(Ld[g], Li[g], c ? d : __builtin_inff(), c ? id : kNoId, lane);
-                td[g] = readlane_f(Ld[g], k2 - 1);
-                ti[g] = readlane_u(Li[g], k2 - 1);
+                wave_merge_sorted_k(Lk[g], d < td[g] ? kpack(d, id) : kMaxKey, lane);
+                tk[g] = readlane_k(Lk[g], k2 - 1);
+                td[g] = kdist(tk[g]);
                 return;
             }
+            const uint64_t mk = kpack(d, id);
             while (bm) {
                 const int l = __builtin_ctzll(bm);
                 bm &= bm - 1;
-                const float cd = readlane_f(d, l);
-                const uint32_t ci = readlane_u(id, l);
-                if (cd < td[g] || (cd == td[g] && ci < ti[g])) {
+                const uint64_t ck = readlane_k(mk, l);
+                if (ck < tk[g]) {
 #ifdef OMPL_AMD_PROBE
                     ++pr_ins;
 #endif
-                    const float pv = shr1_f(Ld[g], -__builtin_inff());
-                    const uint32_t pv_i = shr1_u(Li[g], 0u);
-                    const bool lt_cur = cd < Ld[g] || (cd == Ld[g] && ci < Li[g]);
-                    const bool lt_prev = lane > 0 && (cd < pv || (cd == pv && ci < pv_i));
-                    const float nd = lt_prev ? pv : (lt_cur ? cd : Ld[g]);
-                    const uint32_t ni = lt_prev ? pv_i : (lt_cur ? ci : Li[g]);
-                    Ld[g] = nd;
-                    Li[g] = ni;
-                    td[g] = readlane_f(Ld[g], k2 - 1);
-                    ti[g] = readlane_u(Li[g], k2 - 1);
+                    const uint64_t pv = shr1_k(Lk[g], 0ull);
+                    const bool lt_prev = lane > 0 && ck < pv;
+                    Lk[g] = lt_prev ? pv : (ck < Lk[g] ? ck : Lk[g]);
+                    tk[g] = readlane_k(Lk[g], k2 - 1);
+                    td[g] = kdist(tk[g]);
                 }
             }
     };
@@ -808,8 +836,8 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     for (int g = 0; g < G; ++g)
         if (g0 + g < nq && lane < K2) {
             const size_t o = (size_t)(g0 + g) * K2 + lane;
-            pd[o] = lane < k2 ? Ld[g] : __builtin_inff();
-            pi[o] = lane < k2 ? Li[g] : kNoId;
+            pd[o] = lane < k2 ? kdist(Lk[g]) : __builtin_inff();
+            pi[o] = lane < k2 ? (uint32_t)Lk[g] : kNoId;
         }
 }
 
@@ -1839,11 +1867,11 @@ __global__ void kd_row_tile_boxes_kernel(const float *__restrict__ W, uint32_t n
 }
 
 // one block per node of the level: widest box coordinate -> nsplit[path] = {dim, lo, kKdQ / extent}
-template <int SP, int F>
-__global__ __launch_bounds__(256) void kd_node_split_dim_kernel(const float *__restrict__ tb, uint32_t ntiles,
+template <int SP, int F, int BS>
+__global__ __launch_bounds__(BS) void kd_node_split_dim_kernel(const float *__restrict__ tb, uint32_t ntiles,
                                                                 int level, float4 *__restrict__ nsplit) {
     constexpr int NB = Geo<SP, F>::NB;
-    __shared__ float slo[NB][256], shi[NB][256];
+    __shared__ float slo[NB][BS], shi[NB][BS];
     const KdNodeRef nd = kd_node_at(ntiles, level, blockIdx.x);
     if (!nd.valid || nd.T <= 1) return;
     float lo[NB], hi[NB];
@@ -1874,7 +1902,7 @@ __global__ __launch_bounds__(256) void kd_node_split_dim_kernel(const float *__r
             shi[d][threadIdx.x] = hi[d];
         }
         __syncthreads();
-        for (int w = 128; w > 0; w >>= 1) {
+        for (int w = BS / 2; w > 0; w >>= 1) {
             if ((int)threadIdx.x < w)
 #pragma unroll
                 for (int d = 0; d < NB; ++d) {
@@ -2005,44 +2033,52 @@ __global__ void kd_row_split_kernel(const float *__restrict__ W, uint32_t n, uin
 // The deep levels in LDS: one block per node of level L0 (at most kd_lds_tiles<SP, F>() tiles,
 // so its rows fit in LDS) splits its whole subtree there — per sub-level the same steps as the
 // global loop (tile boxes of the current order, the widest coordinate of every splitting
-// sub-node, (sub-path, quantised coordinate) keys) with a bitonic sort of (key, row index) in
-// LDS instead of a device-wide radix sort, then writes the node records and its rows in leaf
-// order.  Padding slots (past the last state) sort last with key 0xFFFFFFFF.
+// sub-node, (sub-path, quantised coordinate) keys), the sort being rocPRIM's block radix sort of
+// packed (key << 11 | row index) words in LDS instead of a device-wide one; then it writes the
+// node records and its rows in leaf order.  Padding slots (past the last state) get the largest
+// key and stay last.
 template <int SP, int F>
 constexpr uint32_t kd_lds_tiles() {
     constexpr int RW = KdRow<SP, F>::W;
     return RW <= 8 ? 32u : (RW <= 12 ? 16u : 8u);  // <= 64 KiB of rows
 }
+template <int SP, int F>
+constexpr uint32_t kd_lds_block() {
+    constexpr uint32_t rows = kd_lds_tiles<SP, F>() * kCullTile;
+    return (rows < 1024u) ? rows : 1024u;
+}
+constexpr int kKdIdxBits = 11;  // row index inside the node (<= 2,048 rows)
 
 template <int SP, int F>
-__global__ __launch_bounds__(256) void kd_lds_finish_kernel(const float *__restrict__ W, float *__restrict__ Wout,
-                                                            uint32_t n, uint32_t ntiles, int L0, int depth,
-                                                            KdNode *__restrict__ nodes) {
+__global__ __launch_bounds__(1024) void kd_lds_finish_kernel(
+    const float *__restrict__ W, float *__restrict__ Wout, uint32_t n, uint32_t ntiles, int L0, int depth,
+    KdNode *__restrict__ nodes) {
     constexpr int NB = KdRow<SP, F>::NB, RW = KdRow<SP, F>::W;
-    constexpr uint32_t LT = kd_lds_tiles<SP, F>(), NMAX = LT * kCullTile;
+    constexpr uint32_t LT = kd_lds_tiles<SP, F>(), NMAX = LT * kCullTile, BS = kd_lds_block<SP, F>();
+    constexpr uint32_t IPT = NMAX / BS;
+    static_assert(NMAX <= (1u << kKdIdxBits), "row index bits");
+    using BlockSort = rocprim::block_radix_sort<uint32_t, BS, IPT>;
     __shared__ __attribute__((aligned(16))) float rows[NMAX * RW];
-    __shared__ uint32_t key[NMAX];
-    __shared__ uint16_t idx[NMAX];
+    __shared__ uint16_t ord[NMAX];
     __shared__ float tbs[LT][2 * NB];
     __shared__ float4 nsp[LT];
+    __shared__ typename BlockSort::storage_type sort_storage;
     const KdNodeRef nd = kd_node_at(ntiles, L0, blockIdx.x);
     if (!nd.valid) return;
     const uint32_t P0 = nd.t0 * kCullTile, T = nd.T;
     const uint32_t cnt = min(T * kCullTile, n > P0 ? n - P0 : 0u);
     const uint32_t tid = threadIdx.x;
-    for (uint32_t e = tid; e < cnt * (RW / 4); e += blockDim.x)
+    for (uint32_t e = tid; e < cnt * (RW / 4); e += BS)
         reinterpret_cast<float4 *>(rows)[e] = reinterpret_cast<const float4 *>(W + (size_t)P0 * RW)[e];
-    uint32_t N2 = 1;
-    while (N2 < T * kCullTile) N2 <<= 1;
-    for (uint32_t e = tid; e < N2; e += blockDim.x) idx[e] = (uint16_t)e;
+    for (uint32_t e = tid; e < NMAX; e += BS) ord[e] = (uint16_t)e;
     __syncthreads();
-    const int lanes = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int l = 0; L0 + l < depth && T > 1; ++l) {
         // 1. tile boxes of the current order (a wave per tile)
-        for (uint32_t t = wave; t < T; t += blockDim.x / 64) {
-            const uint32_t e = t * kCullTile + lanes;
+        for (uint32_t t = wave; t < T; t += BS / 64) {
+            const uint32_t e = t * kCullTile + lane;
             const bool in = e < cnt;
-            const float *r = rows + (size_t)idx[in ? e : 0] * RW;
+            const float *r = rows + (size_t)ord[in ? e : 0] * RW;
 #pragma unroll
             for (int d = 0; d < NB; ++d) {
                 float lo = in ? r[d] : __builtin_inff(), hi = in ? r[d] : -__builtin_inff();
@@ -2051,7 +2087,7 @@ __global__ __launch_bounds__(256) void kd_lds_finish_kernel(const float *__restr
                     lo = fminf(lo, __shfl_xor(lo, o));
                     hi = fmaxf(hi, __shfl_xor(hi, o));
                 }
-                if (lanes == 0) {
+                if (lane == 0) {
                     tbs[t][d] = lo;
                     tbs[t][NB + d] = hi;
                 }
@@ -2060,7 +2096,7 @@ __global__ __launch_bounds__(256) void kd_lds_finish_kernel(const float *__restr
         __syncthreads();
         // 2. widest coordinate of every sub-node that splits at this sub-level
         const uint32_t nsub = 1u << l;
-        for (uint32_t sp = tid; sp < nsub; sp += blockDim.x) {
+        for (uint32_t sp = tid; sp < nsub; sp += BS) {
             const KdNodeRef sn = kd_node_at(T, l, sp);
             if (!sn.valid || sn.T <= 1) continue;
             int bd = 0;
@@ -2080,9 +2116,12 @@ __global__ __launch_bounds__(256) void kd_lds_finish_kernel(const float *__restr
             nsp[sp] = make_float4(__uint_as_float((uint32_t)bd), blo, be > 0.f ? (float)kKdQ / be : 0.f, 0.f);
         }
         __syncthreads();
-        // 3. keys of the current order
-        for (uint32_t e = tid; e < N2; e += blockDim.x) {
-            uint32_t kk = 0xFFFFFFFFu;
+        // 3. packed keys of the current order (blocked: thread tid holds positions tid * IPT + i)
+        uint32_t kw[IPT];
+#pragma unroll
+        for (uint32_t i = 0; i < IPT; ++i) {
+            const uint32_t e = tid * IPT + i;
+            uint32_t kk = (1u << (32 - kKdIdxBits)) - 1u;  // padding: the largest key
             if (e < cnt) {
                 const uint32_t t = e / kCullTile;
                 uint32_t t0 = 0, TT = T, path = 0;
@@ -2101,48 +2140,34 @@ __global__ __launch_bounds__(256) void kd_lds_finish_kernel(const float *__restr
                 uint32_t q = 0;
                 if (ll == l && TT > 1) {
                     const float4 ns = nsp[path];
-                    q = kd_quant(rows[(size_t)idx[e] * RW + (int)__float_as_uint(ns.x)], ns);
+                    q = kd_quant(rows[(size_t)ord[e] * RW + (int)__float_as_uint(ns.x)], ns);
                 } else {
                     path <<= (l - ll);
                 }
                 kk = (path << kKdQBits) | q;
             }
-            key[e] = kk;
+            kw[i] = (kk << kKdIdxBits) | (e < NMAX ? (uint32_t)ord[e] : 0u);
         }
+        // 4. block radix sort on the key bits (sub-path bits <= 4, so key < 2^17 - 1 = padding)
+        BlockSort().sort(kw, sort_storage, kKdIdxBits, 32);
         __syncthreads();
-        // 4. bitonic sort of (key, idx) over N2 slots (ties: any order — boxes come from contents)
-        for (uint32_t k = 2; k <= N2; k <<= 1)
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t e = tid; e < N2; e += blockDim.x) {
-                    const uint32_t o = e ^ j;
-                    if (o > e) {
-                        const bool up = (e & k) == 0;
-                        const uint32_t ka = key[e], kb = key[o];
-                        if ((ka > kb) == up) {
-                            key[e] = kb;
-                            key[o] = ka;
-                            const uint16_t ia = idx[e];
-                            idx[e] = idx[o];
-                            idx[o] = ia;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
+#pragma unroll
+        for (uint32_t i = 0; i < IPT; ++i) ord[tid * IPT + i] = (uint16_t)(kw[i] & ((1u << kKdIdxBits) - 1u));
+        __syncthreads();
         // 5. node records of the sub-level (pre-order index = the node's + the relative one)
-        for (uint32_t sp = tid; sp < nsub; sp += blockDim.x) {
+        for (uint32_t sp = tid; sp < nsub; sp += BS) {
             const KdNodeRef sn = kd_node_at(T, l, sp);
             if (!sn.valid || sn.T <= 1) continue;
             const uint32_t tl = sn.T >> 1, e = (sn.t0 + tl) * kCullTile;
             const int d = (int)__float_as_uint(nsp[sp].x);
-            const float split = e < cnt ? rows[(size_t)idx[e] * RW + d] : __builtin_inff();
+            const float split = e < cnt ? rows[(size_t)ord[e] * RW + d] : __builtin_inff();
             const uint32_t pidx = nd.pidx + sn.pidx;
             nodes[pidx] = KdNode{(uint32_t)d, split, tl, pidx + tl};
         }
         __syncthreads();
     }
-    for (uint32_t e = tid; e < cnt; e += blockDim.x) {
-        const float4 *src = reinterpret_cast<const float4 *>(rows + (size_t)idx[e] * RW);
+    for (uint32_t e = tid; e < cnt; e += BS) {
+        const float4 *src = reinterpret_cast<const float4 *>(rows + (size_t)ord[e] * RW);
         float4 *dst = reinterpret_cast<float4 *>(Wout + (size_t)(P0 + e) * RW);
 #pragma unroll
         for (int c = 0; c < RW / 4; ++c) dst[c] = src[c];
@@ -2333,8 +2358,12 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
         hipLaunchKernelGGL((kd_row_tile_boxes_kernel<SP, F>), dim3((main_tiles + 3) / 4), b256, 0, st, W0, n_live,
                            main_tiles, tb);
     for (int level = 0; level < Lg; ++level) {
-        hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F>), dim3(1u << level), b256, 0, st, tb, main_tiles, level,
-                           nsplit);
+        if ((main_tiles >> level) > 4096u)  // few large nodes: wider blocks read their tile boxes
+            hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F, 1024>), dim3(1u << level), dim3(1024), 0, st, tb,
+                               main_tiles, level, nsplit);
+        else
+            hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F, 256>), dim3(1u << level), b256, 0, st, tb, main_tiles,
+                               level, nsplit);
         hipLaunchKernelGGL((kd_row_keys_kernel<SP, F>), dim3((nl + 255) / 256), b256, 0, st, W0, n_live, main_tiles,
                            level, nsplit, k0, vals);
         tb_bytes = std::max(tmp_sel, tmp_sort);
@@ -2348,8 +2377,8 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
                            main_tiles, level, nsplit, s->nodes);
     }
     if (Lg < depth) {  // every node of level Lg finishes its subtree in LDS
-        hipLaunchKernelGGL((kd_lds_finish_kernel<SP, F>), dim3(1u << Lg), b256, 0, st, W0, W1, n_live, main_tiles, Lg,
-                           depth, s->nodes);
+        hipLaunchKernelGGL((kd_lds_finish_kernel<SP, F>), dim3(1u << Lg), dim3(kd_lds_block<SP, F>()), 0, st, W0, W1,
+                           n_live, main_tiles, Lg, depth, s->nodes);
         std::swap(W0, W1);
     }
     if ((e = hipMemsetAsync(s->inv, 0xFF, 4ull * s->cap_inv, st)) != hipSuccess) return e;
