@@ -850,7 +850,12 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 // The store is split in chunks along grid.y; the certificate merges the chunk lists.
 constexpr int kWaveGroup = 8;
 
-template <int F, int K2, int G>
+// ORD 0: links in the reference's order, the wave-wide exit tested after links 4 and 8; ORD 1:
+// outermost links first (|P_i(a) - P_i(b)| grows with i, so the partial sum nears the distance
+// sooner) and the exit tested after every pair.  Summing in another order is inside the screen's
+// error bound (screen_error<KCHAIN>: (n + 1) u of the sum covers any order of n non-negative
+// terms); the certificate recomputes every candidate in the reference's order.
+template <int F, int K2, int G, int ORD>
 __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__restrict__ f32, uint64_t cap,
                                                              uint64_t n_end, const float *__restrict__ q32,
                                                              uint32_t nq, uint32_t chunk_len, float link, int nlinks,
@@ -866,35 +871,28 @@ __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__rest
     }
     __syncthreads();
     uint32_t qoff = 0;  // re-read the wave-uniform query rows from LDS per tile (see knn32_group_kernel)
-    float Ld[G];
-    uint32_t Li[G];
+    uint64_t Lk[G];     // packed (distance, id) entries, as knn32_group_kernel
     float td[G];
-    uint32_t ti[G];
+    uint64_t tk[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        Ld[g] = __builtin_inff();
-        Li[g] = kNoId;
+        Lk[g] = kMaxKey;
         td[g] = g0 + g < nq ? __builtin_inff() : -__builtin_inff();
-        ti[g] = kNoId;
+        tk[g] = g0 + g < nq ? kMaxKey : 0ull;
     }
     auto offer = [&](int g, float d, uint32_t id) {
         uint64_t bm = __ballot(d < td[g]);
+        const uint64_t mk = kpack(d, id);
         while (bm) {
             const int l = __builtin_ctzll(bm);
             bm &= bm - 1;
-            const float cd = readlane_f(d, l);
-            const uint32_t ci = readlane_u(id, l);
-            if (cd < td[g] || (cd == td[g] && ci < ti[g])) {
-                const float pv = shr1_f(Ld[g], -__builtin_inff());
-                const uint32_t pv_i = shr1_u(Li[g], 0u);
-                const bool lt_cur = cd < Ld[g] || (cd == Ld[g] && ci < Li[g]);
-                const bool lt_prev = lane > 0 && (cd < pv || (cd == pv && ci < pv_i));
-                const float nd = lt_prev ? pv : (lt_cur ? cd : Ld[g]);
-                const uint32_t ni = lt_prev ? pv_i : (lt_cur ? ci : Li[g]);
-                Ld[g] = nd;
-                Li[g] = ni;
-                td[g] = readlane_f(Ld[g], K2 - 1);
-                ti[g] = readlane_u(Li[g], K2 - 1);
+            const uint64_t ck = readlane_k(mk, l);
+            if (ck < tk[g]) {
+                const uint64_t pv = shr1_k(Lk[g], 0ull);
+                const bool lt_prev = lane > 0 && ck < pv;
+                Lk[g] = lt_prev ? pv : (ck < Lk[g] ? ck : Lk[g]);
+                tk[g] = readlane_k(Lk[g], K2 - 1);
+                td[g] = kdist(tk[g]);
             }
         }
     };
@@ -915,18 +913,18 @@ __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__rest
         asm volatile("" : "+s"(qoff));
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            // link * sum_i |P_i(a) - P_i(b)| (joint positions) with a wave-wide early exit: the partial sums only grow (fp32 addition
-            // of non-negative terms is monotone, so is the final * link), so once no lane's
-            // partial distance is below the threshold no lane's full distance is either, and
-            // the query's list could not change
-            // Two links per step on packed fp32 (v_pk_add / v_pk_mul / v_pk_fma: per element the
-            // same operations as fmaf(dy, dy, dx * dx), so the same bits); the sum stays in link order.
+            // link * sum_i |P_i(a) - P_i(b)| (joint positions) with a wave-wide early exit: the
+            // partial sums only grow (fp32 addition of non-negative terms is monotone, so is the
+            // final * link), so once no lane's partial distance is below the threshold no lane's
+            // full distance is either, and the query's list could not change.  Two links per step
+            // on packed fp32 (v_pk_add / v_pk_mul / v_pk_fma).
             const float *qq = &qrow[qoff + g * F];
             float acc = 0.f;
             bool alive = true;
             static_assert(NM % 2 == 0, "joint positions come in link pairs");
 #pragma unroll
-            for (int i = 0; i < NM; i += 2) {
+            for (int s = 0; s < NM; s += 2) {
+                const int i = ORD ? NM - 2 - s : s;
                 if (i < nlinks) {
                     const f2 dx = f2{x[i], x[i + 1]} - f2{qq[i], qq[i + 1]};
                     const f2 dy = f2{x[NM + i], x[NM + i + 1]} - f2{qq[NM + i], qq[NM + i + 1]};
@@ -934,7 +932,8 @@ __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__rest
                     acc += __builtin_amdgcn_sqrtf(s2.x);
                     if (i + 1 < nlinks) acc += __builtin_amdgcn_sqrtf(s2.y);
                 }
-                if ((i & 3) == 2 && i + 2 < NM && i + 2 < nlinks && !__ballot(acc * link < td[g])) {
+                const bool check = ORD ? (s + 2 < NM) : ((i & 3) == 2 && i + 2 < NM && i + 2 < nlinks);
+                if (check && !__ballot(acc * link < td[g])) {
                     alive = false;
                     break;
                 }
@@ -950,8 +949,8 @@ __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__rest
     for (int g = 0; g < G; ++g)
         if (g0 + g < nq && lane < K2) {
             const size_t o = ((size_t)blockIdx.y * nq + g0 + g) * K2 + lane;
-            pd[o] = Ld[g];
-            pi[o] = Li[g];
+            pd[o] = kdist(Lk[g]);
+            pi[o] = (uint32_t)Lk[g];
         }
 }
 
@@ -1463,8 +1462,20 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     if (p.cull && !walked) return hipErrorInvalidValue;
     if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
         timer_begin(st, "knn32_wave_scan_kernel");
-        hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup>), dim3((nq + kWaveGroup - 1) / kWaveGroup, p.chunks),
-                           dim3(64), 0, st, f32, cap, n_end, q32, nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
+        // link order of the screen (knn32_wave_scan_kernel ORD); OMPL_GPU_CHAIN_ORDER=0 restores the
+        // reference order with two exit tests (A/B)
+        static const int ord = [] {
+            const char *v = std::getenv("OMPL_GPU_CHAIN_ORDER");
+            return v ? std::atoi(v) : 1;
+        }();
+        if (ord == 0)
+            hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 0>),
+                               dim3((nq + kWaveGroup - 1) / kWaveGroup, p.chunks), dim3(64), 0, st, f32, cap, n_end, q32,
+                               nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
+        else
+            hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 1>),
+                               dim3((nq + kWaveGroup - 1) / kWaveGroup, p.chunks), dim3(64), 0, st, f32, cap, n_end, q32,
+                               nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
         timer_end(st);
         walked = true;
     }
