@@ -536,9 +536,11 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
             dmax = 2.0 * h->absmax * std::sqrt((double)h->sp.dim);
         }
         dmax = std::max(dmax * 1.0001, 1e-30);
+        const size_t wsb = knn_large_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus);
+        if (wsb) HIP_OR_FAIL(h->ws.ensure(wsb));
         HIP_OR_FAIL(launch_knn_large(h->sp, h->g, h->feat, h->feat32, h->cap, n_end, d_qf, (uint32_t)nq, k,
                                      (float)h->absmax * (1.0f + 1e-6f), (float)dmax, d_dist, d_ids,
-                                     size_t(4) << 30, h->num_cus, h->stream));
+                                     size_t(4) << 30, h->num_cus, h->stream, wsb ? h->ws.p : nullptr, h->ws.bytes));
         return OMPL_GPU_OK;
     }
     if (h->fast && screen_safe(h) && fast_k2(h->sp, k, (uint32_t)nq, h->cull) > 0) {

@@ -161,11 +161,16 @@ hipError_t launch_knn_stream32(const DevSpace &sp, const FeatGeom &g, const floa
 // ---- large k (k > 32; RRT* k ~ 6e3): histogram threshold + candidate sort (knn_large.hip)
 // dmax: bound of the distances between stored states (the histogram's range; larger
 // distances fall into an overflow bin and are still handled exactly).
+// k <= 8,192 with a workspace of knn_large_workspace_bytes(): sampled thresholds, one fill pass,
+// a block-per-query radix select + sort, all on the device (asynchronous); larger k: the
+// count / host offsets / fill / segmented sort form (synchronous).
 bool large_k_supported(const DevSpace &sp);
+size_t knn_large_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k, uint64_t n_end,
+                                 int num_cus);
 hipError_t launch_knn_large(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32,
                             uint64_t cap, uint64_t n_end, const double *qfeat64, uint32_t nq, uint32_t k, float absmax,
                             float dmax, double *out_d, uint32_t *out_i, size_t mem_budget, int num_cus,
-                            hipStream_t st);
+                            hipStream_t st, void *ws = nullptr, size_t ws_bytes = 0);
 hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t first, uint64_t n, float *feat32,
                           hipStream_t st);
 // exact re-run of the fast path's uncertified queries, with no host round trip: list[0..*d_nlist)

@@ -855,21 +855,28 @@ constexpr int kWaveGroup = 8;
 // sooner) and the exit tested after every pair.  Summing in another order is inside the screen's
 // error bound (screen_error<KCHAIN>: (n + 1) u of the sum covers any order of n non-negative
 // terms); the certificate recomputes every candidate in the reference's order.
-template <int F, int K2, int G, int ORD>
-__global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__restrict__ f32, uint64_t cap,
-                                                             uint64_t n_end, const float *__restrict__ q32,
-                                                             uint32_t nq, uint32_t chunk_len, float link, int nlinks,
-                                                             float *__restrict__ pd, uint32_t *__restrict__ pi) {
+// WPB waves per block share every tile: the block stages it once in LDS (double-buffered, the
+// next tile's global loads in flight while the current one is scanned), so the store is read
+// once per WPB * G queries instead of once per G (measured: 8 queries per read moved ~98 GB per
+// 8,192-milestone batch).
+template <int F, int K2, int G, int ORD, int WPB>
+__global__ __launch_bounds__(64 * WPB) void knn32_wave_scan_kernel(const float *__restrict__ f32, uint64_t cap,
+                                                                   uint64_t n_end, const float *__restrict__ q32,
+                                                                   uint32_t nq, uint32_t chunk_len, float link,
+                                                                   int nlinks, float *__restrict__ pd,
+                                                                   uint32_t *__restrict__ pi) {
     constexpr int NM = F / 2;
+    constexpr int NT = 64 * WPB;                 // threads
+    constexpr int PER = (F * 64 + NT - 1) / NT;  // tile floats staged per thread
     static_assert(K2 <= 64, "lists are spread over one wave");
-    __shared__ __attribute__((aligned(16))) float qrow[G * F];
-    const int lane = threadIdx.x;
-    const uint32_t g0 = blockIdx.x * G;
+    __shared__ __attribute__((aligned(16))) float qrow[WPB][G * F];
+    __shared__ float tile[2][F][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t g0 = (blockIdx.x * WPB + wv) * G;
     for (int t = lane; t < G * F; t += 64) {
         const uint32_t qi = g0 + t / F;
-        qrow[t] = qi < nq ? q32[(size_t)qi * F + t % F] : __builtin_nanf("");
+        qrow[wv][t] = qi < nq ? q32[(size_t)qi * F + t % F] : __builtin_nanf("");
     }
-    __syncthreads();
     uint32_t qoff = 0;  // re-read the wave-uniform query rows from LDS per tile (see knn32_group_kernel)
     uint64_t Lk[G];     // packed (distance, id) entries, as knn32_group_kernel
     float td[G];
@@ -898,17 +905,34 @@ __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__rest
     };
     const uint64_t c0 = (uint64_t)blockIdx.y * chunk_len;
     const uint64_t c1 = min(c0 + chunk_len, n_end);
-    float x[F], xn[F];
-    if (c0 < c1) {
+    // staging: thread t moves floats t, t + NT, ... of the F x 64 tile (row f = index / 64)
+    float pre[PER];
+    auto fetch = [&](uint64_t base) {
 #pragma unroll
-        for (int f = 0; f < F; ++f) x[f] = f32[(uint64_t)f * cap + c0 + lane];
+        for (int u = 0; u < PER; ++u) {
+            const int v = (int)threadIdx.x + u * NT;
+            if (v < F * 64) pre[u] = f32[(uint64_t)(v >> 6) * cap + base + (v & 63)];
+        }
+    };
+    auto stage = [&](int b) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int v = (int)threadIdx.x + u * NT;
+            if (v < F * 64) tile[b][v >> 6][v & 63] = pre[u];
+        }
+    };
+    int cur = 0;
+    if (c0 < c1) {
+        fetch(c0);
+        stage(0);
     }
+    __syncthreads();
     for (uint64_t base = c0; base < c1; base += 64) {
         const bool more = base + 64 < c1;
-        if (more) {  // prefetch the next tile while this one is scanned
+        if (more) fetch(base + 64);  // in flight while this tile is scanned
+        float x[F];
 #pragma unroll
-            for (int f = 0; f < F; ++f) xn[f] = f32[(uint64_t)f * cap + base + 64 + lane];
-        }
+        for (int f = 0; f < F; ++f) x[f] = tile[cur][f][lane];
         const uint32_t id = (uint32_t)(base + lane);
         asm volatile("" : "+s"(qoff));
 #pragma unroll
@@ -918,7 +942,7 @@ __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__rest
             // final * link), so once no lane's partial distance is below the threshold no lane's
             // full distance is either, and the query's list could not change.  Two links per step
             // on packed fp32 (v_pk_add / v_pk_mul / v_pk_fma).
-            const float *qq = &qrow[qoff + g * F];
+            const float *qq = &qrow[wv][qoff + g * F];
             float acc = 0.f;
             bool alive = true;
             static_assert(NM % 2 == 0, "joint positions come in link pairs");
@@ -940,10 +964,9 @@ __global__ __launch_bounds__(64) void knn32_wave_scan_kernel(const float *__rest
             }
             if (alive) offer(g, acc * link, id);
         }
-        if (more) {
-#pragma unroll
-            for (int f = 0; f < F; ++f) x[f] = xn[f];
-        }
+        if (more) stage(cur ^ 1);  // the other buffer: every wave left it at the last barrier
+        __syncthreads();
+        cur ^= 1;
     }
 #pragma unroll
     for (int g = 0; g < G; ++g)
@@ -1370,8 +1393,8 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
     }
     const uint64_t tiles = std::max<uint64_t>(n_end / kTile, 1);
     if (sp.kind == OMPL_GPU_SPACE_KCHAIN) {  // wave scan: ~8 waves per SIMD
-        const uint64_t groups = (nq + kWaveGroup - 1) / kWaveGroup;
-        const uint64_t target = (uint64_t)num_cus * 32;
+        const uint64_t groups = (nq + 4 * kWaveGroup - 1) / (4 * kWaveGroup);  // blocks of 4 waves
+        const uint64_t target = (uint64_t)num_cus * 8;
         const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>((target + groups - 1) / groups, tiles));
         const uint64_t per = (tiles + S - 1) / S;
         p.chunk_len = (uint32_t)(per * kTile);
@@ -1462,20 +1485,28 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     if (p.cull && !walked) return hipErrorInvalidValue;
     if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
         timer_begin(st, "knn32_wave_scan_kernel");
-        // link order of the screen (knn32_wave_scan_kernel ORD); OMPL_GPU_CHAIN_ORDER=0 restores the
-        // reference order with two exit tests (A/B)
+        // link order of the screen (knn32_wave_scan_kernel ORD) and waves sharing each staged tile
+        // (WPB); OMPL_GPU_CHAIN_ORDER=0 restores the reference order with two exit tests and
+        // OMPL_GPU_CHAIN_WPB=1 one wave per block (A/B)
         static const int ord = [] {
             const char *v = std::getenv("OMPL_GPU_CHAIN_ORDER");
             return v ? std::atoi(v) : 1;
         }();
+        static const int wpb = [] {
+            const char *v = std::getenv("OMPL_GPU_CHAIN_WPB");
+            return v ? std::atoi(v) : 4;
+        }();
+        const uint32_t qpb = (uint32_t)(kWaveGroup * (wpb == 1 ? 1 : 4));
+        const dim3 grid((nq + qpb - 1) / qpb, p.chunks);
         if (ord == 0)
-            hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 0>),
-                               dim3((nq + kWaveGroup - 1) / kWaveGroup, p.chunks), dim3(64), 0, st, f32, cap, n_end, q32,
-                               nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
+            hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 0, 4>), grid, dim3(256), 0, st, f32, cap,
+                               n_end, q32, nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
+        else if (wpb == 1)
+            hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 1, 1>), grid, dim3(64), 0, st, f32, cap,
+                               n_end, q32, nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
         else
-            hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 1>),
-                               dim3((nq + kWaveGroup - 1) / kWaveGroup, p.chunks), dim3(64), 0, st, f32, cap, n_end, q32,
-                               nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
+            hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 1, 4>), grid, dim3(256), 0, st, f32, cap,
+                               n_end, q32, nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
         timer_end(st);
         walked = true;
     }

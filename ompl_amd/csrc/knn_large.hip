@@ -14,6 +14,7 @@
 //      of each query's segment are the answer (exact, as the reference's ascending list).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/rocprim.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -395,6 +396,411 @@ hipError_t run_large(const DevSpace &sp, const double *f64, const float *f32, ui
     return hipGetLastError();
 }
 
+// ---- device-decided select (k <= kLargeSelMaxK): no host round trip -------------------------
+// 1. two sampled histograms of the fp32 screen (every kSampleA-th / kSampleB-th 256-state tile):
+//    A over [0, dmax) sets each query's range, B over that range (64 bins) gives a radius r whose
+//    estimated population is k plus six standard deviations of the sampling error;
+// 2. one pass over the store: every state with d32 <= r + 2e gets its exact fp64 distance and is
+//    written to the query's slab for that chunk (fixed capacity, in id order), and the states with
+//    d32 <= r are counted — at least k of them prove that the exact k-th distance is <= r + e, so
+//    every true neighbour (d32 <= d64 + e) is a candidate;
+// 3. a block per query radix-selects the k-th smallest (distance, id) among its candidates, packs the
+//    k selected in id order into LDS and block-radix-sorts them by distance (stable: (distance, id));
+// 4. a query whose slab overflowed or whose count fell short (sampling outlier, heavy ties) is
+//    answered by the exact fallback: a block per query, the same select over every stored state.
+constexpr uint32_t kSampleA = 64, kSampleB = 8;
+constexpr uint32_t kLargeSelMaxK = 8192;  // selected entries sorted in LDS
+constexpr int kSelBlock = 1024, kSelItems = kLargeSelMaxK / kSelBlock;
+
+template <int SP, int F>
+__global__ __launch_bounds__(256) void hist_sample_kernel(const float *__restrict__ f32, uint64_t cap,
+                                                          uint64_t n_end, const float *__restrict__ q32, uint32_t nq,
+                                                          uint32_t chunk_len, uint32_t stride, float w0, float w1,
+                                                          int nl, const float *__restrict__ inv_bin_q,
+                                                          float inv_bin, unsigned int *__restrict__ hist) {
+    constexpr int FS = Row<SP, F>::FS;
+    __shared__ __attribute__((aligned(16))) float tile[kTile * FS];
+    __shared__ unsigned int h[kTile * kBinStride];
+    for (int b = 0; b < kBins; ++b) h[threadIdx.x * kBinStride + b] = 0;
+    const uint32_t q = blockIdx.x * kTile + threadIdx.x;
+    float qf[FS];
+#pragma unroll
+    for (int f = 0; f < FS; ++f) qf[f] = q < nq ? q32[(size_t)q * FS + f] : __builtin_nanf("");
+    const float ib = inv_bin_q ? (q < nq ? inv_bin_q[q] : 0.f) : inv_bin;
+    const uint64_t c0 = (uint64_t)blockIdx.y * chunk_len, c1 = min(c0 + chunk_len, n_end);
+    for (uint64_t base = c0; base < c1; base += (uint64_t)kTile * stride) {
+        stage_tile<SP, FS>(tile, f32, cap, base + threadIdx.x);
+        __syncthreads();
+        for (int s = 0; s < kTile; ++s) {
+            const float d = d32<SP, FS>(&tile[s * FS], qf, w0, w1, nl);
+            const float x = d * ib;
+            if (x < (float)kBins) h[threadIdx.x * kBinStride + (int)x] += 1u;  // NaN / beyond the range: not counted
+        }
+        __syncthreads();
+    }
+    if (q >= nq) return;
+    for (int b = 0; b < kBins; ++b) {
+        const unsigned int c = h[threadIdx.x * kBinStride + b];
+        if (c) atomicAdd(&hist[(size_t)q * kBins + b], c);
+    }
+}
+
+// from sampled histogram A (over [0, dmax)): each query's range for B — the first bin whose
+// scaled count passes 1.5 k + 64 (or dmax) — as 64 / range
+__global__ void sel_range_kernel(const unsigned int *__restrict__ hist, uint32_t nq, uint32_t k, float bin_w,
+                                 float *__restrict__ inv_bin_q) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const double need = (1.5 * k + 64.0) / kSampleA;
+    double cum = 0;
+    int b = 0;
+    for (; b < kBins; ++b) {
+        cum += hist[(size_t)q * kBins + b];
+        if (cum >= need) break;
+    }
+    const float range = (float)(b + 1) * bin_w * 1.0001f;
+    inv_bin_q[q] = (float)kBins / range;
+}
+
+// from sampled histogram B: r (the counting radius) and r + 2e (the collecting radius)
+template <int SP, int F>
+__global__ void sel_radius_kernel(const unsigned int *__restrict__ hist, const float *__restrict__ inv_bin_q,
+                                  const double *__restrict__ qf64, uint32_t nq, uint32_t k, float absmax, DevSpace sp,
+                                  float *__restrict__ r_count, float *__restrict__ r_fill) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const double need = ((double)k + 6.0 * sqrt((double)kSampleB * k) + 2.0 * kSampleB) / kSampleB;
+    double cum = 0;
+    int b = 0;
+    for (; b < kBins - 1; ++b) {
+        cum += hist[(size_t)q * kBins + b];
+        if (cum >= need) break;
+    }
+    const double r = (double)(b + 1) / (double)inv_bin_q[q] * (1.0 + 1e-5);
+    double B = absmax;
+    const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_REALVECTOR ? F : 0);
+    for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qf64[(size_t)q * F + c]));
+    const double e = screen_err<SP>(sp, B, r + 1.0);
+    r_count[q] = (float)r;
+    r_fill[q] = (float)((r + 2.0 * e) * (1.0 + 16.0 * kU));
+}
+
+// one pass: candidates d32 <= r_fill of (query, chunk) into that slab (ascending id), exact fp64
+// distance; counts of d32 <= r_count per query.  slab_cnt may exceed `slab` (overflow).
+template <int SP, int F>
+__global__ __launch_bounds__(256) void sel_fill_kernel(const float *__restrict__ f32, const double *__restrict__ f64,
+                                                       uint64_t cap, uint64_t n_end, const float *__restrict__ q32,
+                                                       const double *__restrict__ qf64, uint32_t nq,
+                                                       uint32_t chunk_len, uint32_t chunks, DevSpace sp,
+                                                       const float *__restrict__ r_count,
+                                                       const float *__restrict__ r_fill, uint32_t slab,
+                                                       double *__restrict__ cd, uint32_t *__restrict__ ci,
+                                                       uint32_t *__restrict__ slab_cnt,
+                                                       unsigned int *__restrict__ count_r) {
+    constexpr int FS = Row<SP, F>::FS;
+    __shared__ __attribute__((aligned(16))) float tile[kTile * FS];
+    const uint32_t q = blockIdx.x * kTile + threadIdx.x;
+    const bool live = q < nq;
+    float qf[FS];
+#pragma unroll
+    for (int f = 0; f < FS; ++f) qf[f] = live ? q32[(size_t)q * FS + f] : __builtin_nanf("");
+    double qv[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qv[f] = live ? qf64[(size_t)q * F + f] : 0.0;
+    const float rc = live ? r_count[q] : -1.f, rf = live ? r_fill[q] : -1.f;
+    const uint64_t c0 = (uint64_t)blockIdx.y * chunk_len, c1 = min(c0 + chunk_len, n_end);
+    const size_t sbase = ((size_t)q * chunks + blockIdx.y) * slab;
+    uint32_t cnt = 0, cr = 0;
+    for (uint64_t base = c0; base < c1; base += kTile) {
+        stage_tile<SP, FS>(tile, f32, cap, base + threadIdx.x);
+        __syncthreads();
+        for (int s = 0; s < kTile; ++s) {
+            const float d = SP == OMPL_GPU_SPACE_KCHAIN ? d32<SP, FS>(&tile[s * FS], qf, (float)sp.link, 0.f, sp.dim)
+                                                        : d32<SP, FS>(&tile[s * FS], qf, (float)sp.w0, (float)sp.w1, 0);
+            cr += d <= rc ? 1u : 0u;
+            if (d <= rf) {
+                if (cnt < slab) {
+                    const uint32_t id = (uint32_t)(base + s);
+                    double sv[F];
+#pragma unroll
+                    for (int f = 0; f < F; ++f) sv[f] = f64[(uint64_t)f * cap + id];
+                    cd[sbase + cnt] = feat_dist<SP, F, SP == OMPL_GPU_SPACE_KCHAIN ? F / 2 : 0>(sv, qv, sp);
+                    ci[sbase + cnt] = id;
+                }
+                ++cnt;
+            }
+        }
+        __syncthreads();
+    }
+    if (!live) return;
+    slab_cnt[(size_t)q * chunks + blockIdx.y] = cnt;
+    if (cr) atomicAdd(&count_r[q], cr);
+}
+
+// (distance, id) as a 96-bit key, ordered: distances are >= 0 so their bits order as integers
+struct SelKey {
+    uint64_t d;
+    uint32_t i;
+};
+__device__ __forceinline__ bool sel_le(uint64_t d, uint32_t i, uint64_t Td, uint32_t Ti) {
+    return d < Td || (d == Td && i <= Ti);
+}
+
+// Block-wide selection over a candidate source: `count` candidates indexed 0..count-1 in id
+// order, get(e, d_bits, id) fetching one (valid == false: skip).  Finds the k-th smallest
+// (distance, id) by radix select (8-bit digits: 64 bits of the distance, then 32 of the id),
+// packs the k selected (id order) into LDS, sorts them stably by distance and writes row q.
+template <class Get>
+__device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t q, double *__restrict__ out_d,
+                                  uint32_t *__restrict__ out_i) {
+    using BlockSort = rocprim::block_radix_sort<uint64_t, kSelBlock, kSelItems, uint32_t>;
+    using BlockScan = rocprim::block_scan<uint32_t, kSelBlock>;
+    __shared__ union {
+        struct {
+            uint64_t d[kLargeSelMaxK];
+            uint32_t i[kLargeSelMaxK];
+        } stage;
+        typename BlockSort::storage_type sort;
+    } sh;
+    __shared__ typename BlockScan::storage_type scan_storage;
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh_digit, sh_need;
+    const uint32_t tid = threadIdx.x;
+    // radix select: prefix (Td, Ti) of the k-th key, 12 digits most significant first
+    uint64_t Td = 0;
+    uint32_t Ti = 0;
+    uint32_t need = min(k, count);
+    for (int dg = 0; dg < 12; ++dg) {
+        const bool on_d = dg < 8;
+        const int shift = on_d ? 56 - 8 * dg : 24 - 8 * (dg - 8);
+        // keys matching the prefix so far: the bits above `shift` (distance), then id bits above it
+        for (uint32_t b = tid; b < 256; b += kSelBlock) hist[b] = 0;
+        __syncthreads();
+        for (uint32_t e = tid; e < count; e += kSelBlock) {
+            uint64_t d;
+            uint32_t i;
+            if (!get(e, d, i)) continue;
+            bool match;
+            uint32_t digit;
+            if (on_d) {
+                match = dg == 0 || (d >> (shift + 8)) == (Td >> (shift + 8));
+                digit = (uint32_t)(d >> shift) & 255u;
+            } else {
+                match = d == Td && (dg == 8 || (i >> (shift + 8)) == (Ti >> (shift + 8)));
+                digit = (i >> shift) & 255u;
+            }
+            if (match) atomicAdd(&hist[digit], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t cum = 0, dgt = 255;
+            for (uint32_t b = 0; b < 256; ++b) {
+                if (cum + hist[b] >= need) {
+                    dgt = b;
+                    break;
+                }
+                cum += hist[b];
+            }
+            sh_digit = dgt;
+            sh_need = need - cum;
+        }
+        __syncthreads();
+        if (on_d)
+            Td |= (uint64_t)sh_digit << shift;
+        else
+            Ti |= sh_digit << shift;
+        need = sh_need;
+        __syncthreads();
+    }
+    // pack the selected keys (<= (Td, Ti)) in id order: block prefix sums over chunks of the source
+    uint32_t base = 0;
+    for (uint32_t e0 = 0; e0 < count; e0 += kSelBlock) {
+        const uint32_t e = e0 + tid;
+        uint64_t d = 0;
+        uint32_t i = 0;
+        const bool take = e < count && get(e, d, i) && sel_le(d, i, Td, Ti);
+        uint32_t pos = 0, tot = 0;
+        BlockScan().exclusive_scan(take ? 1u : 0u, pos, 0u, tot, scan_storage);
+        if (take && base + pos < kLargeSelMaxK) {
+            sh.stage.d[base + pos] = d;
+            sh.stage.i[base + pos] = i;
+        }
+        base += tot;
+        __syncthreads();
+    }
+    const uint32_t sel = min(min(base, k), kLargeSelMaxK);  // k, or every live state when fewer
+    for (uint32_t e = sel + tid; e < kLargeSelMaxK; e += kSelBlock) {
+        sh.stage.d[e] = ~0ull;
+        sh.stage.i[e] = kNoId;
+    }
+    __syncthreads();
+    uint64_t kd[kSelItems];
+    uint32_t ki[kSelItems];
+#pragma unroll
+    for (int j = 0; j < kSelItems; ++j) {
+        kd[j] = sh.stage.d[tid * kSelItems + j];
+        ki[j] = sh.stage.i[tid * kSelItems + j];
+    }
+    __syncthreads();
+    BlockSort().sort(kd, ki, sh.sort);  // stable: equal distances keep id order
+#pragma unroll
+    for (int j = 0; j < kSelItems; ++j) {
+        const uint32_t r = tid * kSelItems + j;
+        if (r < k) {
+            out_d[(size_t)q * k + r] = r < sel ? __longlong_as_double((long long)kd[j]) : __builtin_inf();
+            out_i[(size_t)q * k + r] = r < sel ? ki[j] : kNoId;
+        }
+    }
+}
+
+// a block per query: select + sort over its slabs, or put it on the fallback list
+__global__ __launch_bounds__(kSelBlock) void sel_sort_kernel(const double *__restrict__ cd,
+                                                             const uint32_t *__restrict__ ci,
+                                                             const uint32_t *__restrict__ slab_cnt,
+                                                             const unsigned int *__restrict__ count_r, uint32_t nq,
+                                                             uint32_t chunks, uint32_t slab, uint32_t k,
+                                                             double *__restrict__ out_d, uint32_t *__restrict__ out_i,
+                                                             uint32_t *__restrict__ fb_count,
+                                                             uint32_t *__restrict__ fb_list) {
+    const uint32_t q = blockIdx.x;
+    if (q >= nq) return;
+    __shared__ uint32_t sh_bad;
+    if (threadIdx.x == 0) sh_bad = count_r[q] < k ? 1u : 0u;
+    __syncthreads();
+    const uint32_t *cnt = slab_cnt + (size_t)q * chunks;
+    for (uint32_t c = threadIdx.x; c < chunks; c += blockDim.x)
+        if (cnt[c] > slab) sh_bad = 1u;  // benign race: every writer stores 1
+    __syncthreads();
+    if (sh_bad) {
+        if (threadIdx.x == 0) fb_list[atomicAdd(fb_count, 1u)] = q;
+        return;
+    }
+    const size_t base = (size_t)q * chunks * slab;
+    auto get = [&](uint32_t e, uint64_t &d, uint32_t &i) -> bool {
+        const uint32_t c = e / slab, j = e - c * slab;
+        if (j >= cnt[c]) return false;
+        d = (uint64_t)__double_as_longlong(cd[base + e]);
+        i = ci[base + e];
+        return true;
+    };
+    block_select_sort(get, chunks * slab, k, q, out_d, out_i);
+}
+
+// exact fallback: a block per listed query, the same select over every stored state (each
+// radix pass recomputes the exact distances) — slow, for sampling outliers and heavy ties
+template <int SP, int F>
+__global__ __launch_bounds__(kSelBlock) void sel_fallback_kernel(const double *__restrict__ f64, uint64_t cap,
+                                                                 uint64_t n_end, const double *__restrict__ qf64,
+                                                                 DevSpace sp, uint32_t k,
+                                                                 const uint32_t *__restrict__ fb_count,
+                                                                 const uint32_t *__restrict__ fb_list,
+                                                                 double *__restrict__ out_d,
+                                                                 uint32_t *__restrict__ out_i) {
+    const uint32_t n_fb = *fb_count;
+    for (uint32_t f = blockIdx.x; f < n_fb; f += gridDim.x) {
+        const uint32_t q = fb_list[f];
+        double qv[F];
+#pragma unroll
+        for (int c = 0; c < F; ++c) qv[c] = qf64[(size_t)q * F + c];
+        auto get = [&](uint32_t e, uint64_t &d, uint32_t &i) -> bool {
+            double sv[F];
+#pragma unroll
+            for (int c = 0; c < F; ++c) sv[c] = f64[(uint64_t)c * cap + e];
+            const double x = feat_dist<SP, F, SP == OMPL_GPU_SPACE_KCHAIN ? F / 2 : 0>(sv, qv, sp);
+            if (!(x == x)) return false;  // unused / removed slot
+            d = (uint64_t)__double_as_longlong(x);
+            i = e;
+            return true;
+        };
+        // live states only: count them once (NaN slots are skipped by get)
+        block_select_sort(get, (uint32_t)n_end, k, q, out_d, out_i);
+        __syncthreads();
+    }
+}
+
+struct SelLayout {
+    size_t q32, hist, inv, rc, rf, cntr, scnt, fb, cd, ci, total;
+    uint32_t chunks, chunk_len, slab, qb;
+};
+
+inline size_t sel_align(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// queries per batch and slab capacity: the slabs of a batch hold about 1.25 (k + 8 sqrt(8k) +
+// 1024) candidates per query spread over the chunks, plus slack for the spread between chunks
+SelLayout sel_layout(int FS, uint32_t nq, uint32_t k, uint64_t n_end, int num_cus) {
+    SelLayout L{};
+    const Plan p = plan(std::min<uint32_t>(nq, 4096u), n_end, num_cus);
+    L.chunks = p.chunks;
+    L.chunk_len = p.chunk_len;
+    const double est = (double)k + 8.0 * std::sqrt(8.0 * k) + 1024.0;
+    const double per = 1.25 * est / L.chunks;
+    L.slab = (uint32_t)std::ceil(per + 6.0 * std::sqrt(per) + 16.0);
+    L.qb = std::min<uint32_t>(nq, 4096u);
+    size_t off = 0;
+    auto take = [&](size_t b) {
+        const size_t o = off;
+        off += sel_align(b);
+        return o;
+    };
+    L.q32 = take(4ull * nq * FS);
+    L.hist = take(4ull * L.qb * kBins);
+    L.inv = take(4ull * L.qb);
+    L.rc = take(4ull * L.qb);
+    L.rf = take(4ull * L.qb);
+    L.cntr = take(4ull * L.qb);
+    L.scnt = take(4ull * L.qb * L.chunks);
+    L.fb = take(4ull * (L.qb + 1));
+    L.cd = take(8ull * L.qb * L.chunks * L.slab);
+    L.ci = take(4ull * L.qb * L.chunks * L.slab);
+    L.total = off;
+    return L;
+}
+
+template <int SP, int F>
+hipError_t run_large_select(const DevSpace &sp, const double *f64, const float *f32, uint64_t cap, uint64_t n_end,
+                            const double *qf64, uint32_t nq, uint32_t k, float absmax, float dmax, double *out_d,
+                            uint32_t *out_i, void *ws, size_t ws_bytes, int num_cus, hipStream_t st) {
+    constexpr int FS = Row<SP, F>::FS;
+    const SelLayout L = sel_layout(FS, nq, k, n_end, num_cus);
+    if (ws_bytes < L.total) return hipErrorInvalidValue;
+    char *w = (char *)ws;
+    float *q32 = (float *)(w + L.q32), *inv = (float *)(w + L.inv), *rc = (float *)(w + L.rc), *rf = (float *)(w + L.rf);
+    unsigned int *hist = (unsigned int *)(w + L.hist), *cntr = (unsigned int *)(w + L.cntr);
+    uint32_t *scnt = (uint32_t *)(w + L.scnt), *fb = (uint32_t *)(w + L.fb);
+    double *cd = (double *)(w + L.cd);
+    uint32_t *ci = (uint32_t *)(w + L.ci);
+    const float w0 = SP == OMPL_GPU_SPACE_KCHAIN ? (float)sp.link : (float)sp.w0;
+    const float bin_a = dmax / (float)kBins;
+    hipLaunchKernelGGL((rows32_kernel<SP, F>), dim3((nq + 255) / 256), dim3(256), 0, st, qf64, nq, q32);
+    hipError_t e;
+    for (uint32_t q0 = 0; q0 < nq; q0 += L.qb) {
+        const uint32_t nb = std::min(L.qb, nq - q0);
+        const float *bq32 = q32 + (size_t)q0 * FS;
+        const double *bqf = qf64 + (size_t)q0 * F;
+        const dim3 grid((nb + kTile - 1) / kTile, L.chunks);
+        if ((e = hipMemsetAsync(hist, 0, 4ull * nb * kBins, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL((hist_sample_kernel<SP, F>), grid, dim3(kTile), 0, st, f32, cap, n_end, bq32, nb,
+                           L.chunk_len, kSampleA, w0, (float)sp.w1, sp.dim, (const float *)nullptr, 1.f / bin_a, hist);
+        hipLaunchKernelGGL(sel_range_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, hist, nb, k, bin_a, inv);
+        if ((e = hipMemsetAsync(hist, 0, 4ull * nb * kBins, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL((hist_sample_kernel<SP, F>), grid, dim3(kTile), 0, st, f32, cap, n_end, bq32, nb,
+                           L.chunk_len, kSampleB, w0, (float)sp.w1, sp.dim, (const float *)inv, 0.f, hist);
+        hipLaunchKernelGGL((sel_radius_kernel<SP, F>), dim3((nb + 255) / 256), dim3(256), 0, st, hist, inv, bqf, nb, k,
+                           absmax, sp, rc, rf);
+        if ((e = hipMemsetAsync(cntr, 0, 4ull * nb, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(fb, 0, 4, st)) != hipSuccess) return e;
+        if (q0 == 0) timer_begin(st, "sel_fill_kernel");
+        hipLaunchKernelGGL((sel_fill_kernel<SP, F>), grid, dim3(kTile), 0, st, f32, f64, cap, n_end, bq32, bqf, nb,
+                           L.chunk_len, L.chunks, sp, rc, rf, L.slab, cd, ci, scnt, cntr);
+        if (q0 == 0) timer_end(st);
+        hipLaunchKernelGGL(sel_sort_kernel, dim3(nb), dim3(kSelBlock), 0, st, cd, ci, scnt, cntr, nb, L.chunks, L.slab,
+                           k, out_d + (size_t)q0 * k, out_i + (size_t)q0 * k, fb, fb + 1);
+        hipLaunchKernelGGL((sel_fallback_kernel<SP, F>), dim3((unsigned)std::max(num_cus, 1)), dim3(kSelBlock), 0, st,
+                           f64, cap, n_end, bqf, sp, k, fb, fb + 1, out_d + (size_t)q0 * k, out_i + (size_t)q0 * k);
+    }
+    return hipGetLastError();
+}
+
 }  // namespace
 
 bool large_k_supported(const DevSpace &sp) {
@@ -402,39 +808,42 @@ bool large_k_supported(const DevSpace &sp) {
            sp.kind == OMPL_GPU_SPACE_KCHAIN;
 }
 
+size_t knn_large_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k, uint64_t n_end,
+                                 int num_cus) {
+    if (nq == 0 || k == 0 || k > kLargeSelMaxK) return 0;
+    const int FS = sp.kind == OMPL_GPU_SPACE_SE3 ? 8 : g.F;
+    return sel_layout(FS, nq, k, n_end, num_cus).total;
+}
+
 hipError_t launch_knn_large(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32,
                             uint64_t cap, uint64_t n_end, const double *qfeat64, uint32_t nq, uint32_t k, float absmax,
                             float dmax, double *out_d, uint32_t *out_i, size_t mem_budget, int num_cus,
-                            hipStream_t st) {
+                            hipStream_t st, void *ws, size_t ws_bytes) {
     if (nq == 0 || k == 0) return hipSuccess;
+    // k <= kLargeSelMaxK: the device-decided select (asynchronous); larger k: count, host offsets, fill
+    const bool sel = k <= kLargeSelMaxK && ws && ws_bytes >= knn_large_workspace_bytes(sp, g, nq, k, n_end, num_cus);
+#define OMPL_AMD_LARGE(SPK, FK)                                                                                    \
+    return sel ? run_large_select<SPK, FK>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, dmax, out_d,    \
+                                           out_i, ws, ws_bytes, num_cus, st)                                       \
+               : run_large<SPK, FK>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, dmax, out_d, out_i,    \
+                                    mem_budget, num_cus, st)
     switch (sp.kind) {
     case OMPL_GPU_SPACE_SE3:
-        return run_large<OMPL_GPU_SPACE_SE3, 7>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, dmax, out_d,
-                                                 out_i, mem_budget, num_cus, st);
+        OMPL_AMD_LARGE(OMPL_GPU_SPACE_SE3, 7);
     case OMPL_GPU_SPACE_SO3:
-        return run_large<OMPL_GPU_SPACE_SO3, 4>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, dmax, out_d,
-                                                 out_i, mem_budget, num_cus, st);
+        OMPL_AMD_LARGE(OMPL_GPU_SPACE_SO3, 4);
     case OMPL_GPU_SPACE_REALVECTOR:
-        if (g.F == 4)
-            return run_large<OMPL_GPU_SPACE_REALVECTOR, 4>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax,
-                                                            dmax, out_d, out_i, mem_budget, num_cus, st);
-        if (g.F == 8)
-            return run_large<OMPL_GPU_SPACE_REALVECTOR, 8>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax,
-                                                            dmax, out_d, out_i, mem_budget, num_cus, st);
-        return run_large<OMPL_GPU_SPACE_REALVECTOR, 16>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, dmax,
-                                                         out_d, out_i, mem_budget, num_cus, st);
+        if (g.F == 4) OMPL_AMD_LARGE(OMPL_GPU_SPACE_REALVECTOR, 4);
+        if (g.F == 8) OMPL_AMD_LARGE(OMPL_GPU_SPACE_REALVECTOR, 8);
+        OMPL_AMD_LARGE(OMPL_GPU_SPACE_REALVECTOR, 16);
     case OMPL_GPU_SPACE_KCHAIN:  // features: cos / sin of the cumulative angles, nmax links each
-#define OMPL_AMD_LARGE_CHAIN(NMX)                                                                                  \
-    if (g.nmax == NMX)                                                                                             \
-        return run_large<OMPL_GPU_SPACE_KCHAIN, 2 * NMX>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, dmax, \
-                                                         out_d, out_i, mem_budget, num_cus, st);
-        OMPL_AMD_LARGE_CHAIN(4)
-        OMPL_AMD_LARGE_CHAIN(8)
-        OMPL_AMD_LARGE_CHAIN(12)
-        OMPL_AMD_LARGE_CHAIN(16)
-#undef OMPL_AMD_LARGE_CHAIN
+        if (g.nmax == 4) OMPL_AMD_LARGE(OMPL_GPU_SPACE_KCHAIN, 8);
+        if (g.nmax == 8) OMPL_AMD_LARGE(OMPL_GPU_SPACE_KCHAIN, 16);
+        if (g.nmax == 12) OMPL_AMD_LARGE(OMPL_GPU_SPACE_KCHAIN, 24);
+        if (g.nmax == 16) OMPL_AMD_LARGE(OMPL_GPU_SPACE_KCHAIN, 32);
         return hipErrorInvalidValue;
     }
+#undef OMPL_AMD_LARGE
     return hipErrorInvalidValue;
 }
 

@@ -74,3 +74,22 @@ def test_large_k_se3_rrtstar_1e6(gpu):
     assert (cnt == k_rrt).all()
     oi, od, _ = O.knn(sp, data, q, k_rrt + 8)
     assert_knn_parity(ids, d, oi, od, k_rrt)
+
+
+def test_large_k_heavy_ties_take_the_exact_fallback(gpu):
+    """50 distinct states, each stored 200 times in a row: whole chunks of the store are exact
+    ties, so the fill pass's per-(query, chunk) slabs overflow and the queries are answered by
+    the exact fallback kernel — still (distance, id) order, the lowest ids of a tie class first."""
+    rng = np.random.default_rng(81)
+    sp = SE3StateSpace()
+    base = W.uniform_se3(rng, 50)
+    data = np.repeat(base, 200, axis=0)
+    q = np.concatenate([W.uniform_se3(rng, 40), base[:3]])
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    for k in (1000, 4321):
+        ids, d, cnt = nn.nearestKBatch(q, k)
+        assert (cnt == k).all()
+        oi, od, _ = O.knn(sp, data, q, k)
+        np.testing.assert_array_equal(ids.astype(np.int64), oi.astype(np.int64))  # ties: ids ascending
+        assert_knn_parity(ids, d, oi, od, k)
