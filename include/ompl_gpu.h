@@ -38,6 +38,7 @@
  *                          src/ompl/geometric/planners/rrt/src/RRT.cpp:137-146
  *   ompl_gpu_rrt_grow_device  the RRT loop itself                 RRT.cpp:128-192
  *   ompl_gpu_prm_add_milestones  PRM* causal roadmap batches      prm/src/PRM.cpp:562-596
+ *   ompl_gpu_knn_merge_device  per-shard nearestK lists -> global top k (tree-sharded mode)
  *   ompl_gpu_nn_edges_device  the edges PRM / BIT* check after a neighbour query
  *                          prm/src/PRM.cpp:577-582, informedtrees/src/BITstar.cpp:815
  *
@@ -318,6 +319,14 @@ ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const
  * d_nearest / d_added are 0xFFFFFFFF).  Otherwise the added state strictly closest to the goal
  * is the approximate solution: *approx_id / *approx_dist (0xFFFFFFFF / +inf if nothing was
  * added).  goal: host, dim reals.  Output pointers may be NULL. */
+/* Tree-sharded nearestK (SURVEY §8e "state set sharded, queries broadcast"): every shard's
+ * [nq][k] result of the same queries — ids already global, each list sorted by (distance, id),
+ * missing entries (+inf, 0xFFFFFFFF) — stacked as d_dist / d_ids [lists][nq][k] (the layout an
+ * all_gather produces), merged into the global top k by (distance, id): the order of
+ * NearestNeighborsGNAT::nearestK over the union (NearestNeighborsGNAT.h:222-233).  Device
+ * pointers, asynchronous on `stream` (a hipStream_t; NULL = the null stream).  lists <= 64. */
+ompl_gpu_status ompl_gpu_knn_merge_device(const double *d_dist, const uint32_t *d_ids, uint32_t lists, size_t nq,
+                                          uint32_t k, double *d_out_dist, uint32_t *d_out_ids, void *stream);
 /* Persistent RRT runs that gave up and were re-run in the two-launch form (diagnostics). */
 ompl_gpu_status ompl_gpu_rrt_aborts(const ompl_gpu_nn *nn, uint64_t *aborts);
 ompl_gpu_status ompl_gpu_rrt_solve_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const double *d_samples, size_t ns,

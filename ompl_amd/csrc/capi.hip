@@ -1604,6 +1604,15 @@ ompl_gpu_status rrt_run(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples
 }
 }  // namespace
 
+ompl_gpu_status ompl_gpu_knn_merge_device(const double *d_dist, const uint32_t *d_ids, uint32_t lists, size_t nq,
+                                          uint32_t k, double *d_out_dist, uint32_t *d_out_ids, void *stream) {
+    if (nq && k && (!d_dist || !d_ids || !d_out_dist || !d_out_ids)) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (lists == 0 || lists > 64) return fail(OMPL_GPU_ERR_INVALID_ARG, "lists must be in [1, 64]");
+    if (nq > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many queries in one call");
+    HIP_OR_FAIL(launch_topk_merge(d_dist, d_ids, lists, (uint32_t)nq, k, d_out_dist, d_out_ids, (hipStream_t)stream));
+    return OMPL_GPU_OK;
+}
+
 ompl_gpu_status ompl_gpu_rrt_aborts(const ompl_gpu_nn *h, uint64_t *aborts) {
     if (!h || !aborts) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
     *aborts = h->rrt_aborts;

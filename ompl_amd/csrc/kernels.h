@@ -276,6 +276,9 @@ hipError_t launch_features(const DevSpace &sp, const FeatGeom &g, const double *
 // scatter AoS features of n new states into SoA storage at [first, first+n)
 hipError_t launch_store_soa(const double *aos, uint32_t n, int width, double *soa, uint64_t cap, uint64_t first,
                             hipStream_t st);
+// tree-sharded kNN: merge `lists` per-shard [nq][k] lists (each sorted by (distance, id)) into one
+hipError_t launch_topk_merge(const double *d, const uint32_t *ids, uint32_t lists, uint32_t nq, uint32_t k, double *od,
+                             uint32_t *oi, hipStream_t st);
 // RRT steer: from = raw[nearest], to = q or interpolate(from, q, maxd/d)
 hipError_t launch_steer(const DevSpace &sp, const double *raw_soa, uint64_t cap, const double *q, uint32_t nq,
                         const uint32_t *nearest, uint32_t stride, double maxd, double *from, double *to,

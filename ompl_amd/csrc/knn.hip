@@ -870,6 +870,45 @@ hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uin
     return hipGetLastError();
 }
 
+// tree-sharded kNN: the per-shard lists of every query (lists x nq x k, each sorted by
+// (distance, id), missing = (+inf, kNoId)) merged into the global top k by (distance, id) — a
+// thread per query, a lists-way merge of heads
+__global__ void topk_merge_kernel(const double *__restrict__ d, const uint32_t *__restrict__ ids, uint32_t lists,
+                                  uint32_t nq, uint32_t k, double *__restrict__ od, uint32_t *__restrict__ oi) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    constexpr uint32_t kMaxLists = 64;
+    uint32_t head[kMaxLists];
+    for (uint32_t l = 0; l < lists; ++l) head[l] = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+        uint32_t best = kMaxLists;
+        double bd = __builtin_inf();
+        uint32_t bi = kNoId;
+        for (uint32_t l = 0; l < lists; ++l) {
+            if (head[l] >= k) continue;
+            const size_t o = ((size_t)l * nq + q) * k + head[l];
+            const double x = d[o];
+            const uint32_t xi = ids[o];
+            if (xi != kNoId && (x < bd || (x == bd && xi < bi))) {
+                bd = x;
+                bi = xi;
+                best = l;
+            }
+        }
+        if (best != kMaxLists) ++head[best];
+        od[(size_t)q * k + j] = bd;
+        oi[(size_t)q * k + j] = bi;
+    }
+}
+
+hipError_t launch_topk_merge(const double *d, const uint32_t *ids, uint32_t lists, uint32_t nq, uint32_t k, double *od,
+                             uint32_t *oi, hipStream_t st) {
+    if (nq == 0 || k == 0) return hipSuccess;
+    if (lists == 0 || lists > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(topk_merge_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, d, ids, lists, nq, k, od, oi);
+    return hipGetLastError();
+}
+
 hipError_t launch_steer(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
                         const uint32_t *nearest, uint32_t stride, double maxd, double *from, double *to,
                         hipStream_t st) {

@@ -428,7 +428,10 @@ __global__ __launch_bounds__(256) void hist_sample_kernel(const float *__restric
     for (int f = 0; f < FS; ++f) qf[f] = q < nq ? q32[(size_t)q * FS + f] : __builtin_nanf("");
     const float ib = inv_bin_q ? (q < nq ? inv_bin_q[q] : 0.f) : inv_bin;
     const uint64_t c0 = (uint64_t)blockIdx.y * chunk_len, c1 = min(c0 + chunk_len, n_end);
-    for (uint64_t base = c0; base < c1; base += (uint64_t)kTile * stride) {
+    // the sample is every stride-th 256-state tile of the whole store (global tile index), so the
+    // sampled fraction is 1 / stride whatever the chunk length (chunks start on tile boundaries)
+    const uint64_t t0 = (c0 / kTile + stride - 1) / stride * stride;
+    for (uint64_t base = t0 * kTile; base < c1; base += (uint64_t)kTile * stride) {
         stage_tile<SP, FS>(tile, f32, cap, base + threadIdx.x);
         __syncthreads();
         for (int s = 0; s < kTile; ++s) {
@@ -576,20 +579,32 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
         // keys matching the prefix so far: the bits above `shift` (distance), then id bits above it
         for (uint32_t b = tid; b < 256; b += kSelBlock) hist[b] = 0;
         __syncthreads();
-        for (uint32_t e = tid; e < count; e += kSelBlock) {
-            uint64_t d;
-            uint32_t i;
-            if (!get(e, d, i)) continue;
-            bool match;
+        const int lane = threadIdx.x & 63;
+        for (uint32_t e0 = 0; e0 < count; e0 += kSelBlock) {  // uniform trip count: the ballots below
+            const uint32_t e = e0 + tid;
+            uint64_t d = 0;
+            uint32_t i = 0;
+            bool part = e < count && get(e, d, i);
             uint32_t digit;
             if (on_d) {
-                match = dg == 0 || (d >> (shift + 8)) == (Td >> (shift + 8));
+                part = part && (dg == 0 || (d >> (shift + 8)) == (Td >> (shift + 8)));
                 digit = (uint32_t)(d >> shift) & 255u;
             } else {
-                match = d == Td && (dg == 8 || (i >> (shift + 8)) == (Ti >> (shift + 8)));
+                part = part && d == Td && (dg == 8 || (i >> (shift + 8)) == (Ti >> (shift + 8)));
                 digit = (i >> shift) & 255u;
             }
-            if (match) atomicAdd(&hist[digit], 1u);
+            // the leading digits are mostly equal across a wave (the distances' exponent): one
+            // atomic with the wave's count then, instead of 64 serialised on one LDS address
+            const uint64_t pm = __ballot(part);
+            if (pm) {
+                const int leader = __builtin_ctzll(pm);
+                const uint32_t ld = (uint32_t)__shfl((int)digit, leader);
+                if (__ballot(part && digit == ld) == pm) {
+                    if (lane == leader) atomicAdd(&hist[ld], (uint32_t)__popcll(pm));
+                } else if (part) {
+                    atomicAdd(&hist[digit], 1u);
+                }
+            }
         }
         __syncthreads();
         if (tid == 0) {
