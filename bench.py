@@ -86,12 +86,18 @@ def parse():
     ap.add_argument("--rrt-iters", type=int, default=2000, help="device RRT iterations after the bench (0 = skip)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra measurements (index maintenance, sphere checker, RRT* k) after the timed steps")
+    ap.add_argument("--partition", default="replicated", choices=["replicated", "tree"],
+                    help="cfg3: replicated tree + sharded samples (default, weak scaling), or the tree sharded over "
+                         "the ranks with every sample answered by every shard and the per-shard top-k lists merged "
+                         "(all_gather over RCCL + the library's merge kernel; strong scaling)")
     ap.add_argument("--bitstar-knn", action="store_true",
                     help="cfg5: BIT*'s default kNN neighbourhood (useKNearest_, bitstar/ImplicitGraph.h:463), "
                          "k = ceil(1.1 (e + e/6) ln n) = 57 at 10^7, instead of the radius mode")
     ap.add_argument("--rrt-star-queries", type=int, default=1000,
                     help="cfg3: batch of RRT* neighbourhood queries at k = 6,169 (0 = skip)")
     a = ap.parse_args()
+    if a.partition == "tree" and a.workload != "cfg3":
+        ap.error("--partition tree is implemented for --workload cfg3")
     t, q, k = DEFAULTS[a.workload]
     a.tree = t if a.tree is None else a.tree
     a.queries = q if a.queries is None else a.queries
@@ -204,8 +210,10 @@ def _cpu_prm_causal(sp, ck, tree, milestones, k_cap, budget_s, T):
     """PRM*'s causal insertion on the GNAT restatement (PRM.cpp:562-596, KStarStrategy
     ConnectionStrategy.h:124-156): milestone i queries its k_i = ceil((e + e/d) ln(i + 1)) nearest
     among every vertex before it, is inserted, and its edges checkMotion(state[n], state[m]) are
-    checked.  Causal, so one thread (the reference's roadmap construction is sequential); the
-    edges are also timed on T threads."""
+    checked.  1 thread: exactly that sequential loop.  T threads: the decomposition the GPU uses
+    for a batch — the batch's kNN over the stored roadmap as const queries on T threads, then its
+    edges on T threads (the in-batch causal candidates, < 1 % of the neighbours, are left out of the
+    threaded sample, which favours the CPU).  `value` is the T-thread figure."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
 
@@ -215,32 +223,47 @@ def _cpu_prm_causal(sp, ck, tree, milestones, k_cap, budget_s, T):
     build_s = time.perf_counter() - t0
     kc = math.e + math.e / sp.dim
     n0 = len(tree)
+    # T threads over the stored roadmap (queries before any insert: every milestone sees the n0 states)
+    kq = min(int(math.ceil(kc * math.log(n0 + 1))), k_cap)
+    t0 = time.perf_counter()
+    g.knn(milestones[:16 * T], kq, T)
+    per = (time.perf_counter() - t0) / (16 * T)
+    nT = int(min(len(milestones), max(16 * T, 0.3 * budget_s / max(per, 1e-9))))
+    t0 = time.perf_counter()
+    idsT, _, cntT = g.knn(milestones[:nT], kq, T)
+    t_nnT = time.perf_counter() - t0
+    s1T = tree[idsT[:, :kq].reshape(-1).astype(np.int64)]
+    s2T = np.repeat(milestones[:nT], kq, axis=0)
+    mpsT, repsT = _motion_rate(sp, ck, s1T, s2T, 0.15 * budget_s, T)
+    mT = len(s1T)
+    # 1 thread: the sequential causal loop
     s1, s2, nq = [], [], 0
     t_nn = 0.0
     for i, q in enumerate(milestones):
-        kq = min(int(math.ceil(kc * math.log(n0 + i + 1))), k_cap)
+        kq1 = min(int(math.ceil(kc * math.log(n0 + i + 1))), k_cap)
         t0 = time.perf_counter()
-        ids, _, cnt = g.knn(q, kq)
+        ids, _, cnt = g.knn(q, kq1)
         g.add(q)
         t_nn += time.perf_counter() - t0
         nq += 1
         for j in ids[0, :cnt[0]].astype(np.int64):
             s1.append(tree[j] if j < n0 else milestones[j - n0])
             s2.append(q)
-        if t_nn > 0.6 * budget_s:
+        if t_nn > 0.3 * budget_s:
             break
     s1, s2 = np.asarray(s1), np.asarray(s2)
-    mps1, reps = _motion_rate(sp, ck, s1, s2, 0.2 * budget_s, 1)
-    mpsT, _ = _motion_rate(sp, ck, s1, s2, 0.2 * budget_s, T)
+    mps1, reps = _motion_rate(sp, ck, s1, s2, 0.15 * budget_s, 1)
     m = len(s1)
-    return {"value": (nq + m) / (t_nn + m / mps1), "unit": UNIT, "cores": 1, "kind": "port",
-            "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same {n0}-vertex "
-                       f"roadmap: the first {nq} milestones of the run inserted causally (k_i nearest, then add), "
-                       f"then their {m} checkMotion edges x{reps} with the oracle DiscreteMotionValidator, on 1 "
-                       f"thread; index build {build_s:.1f} s excluded"),
-            "nn_queries_per_s": nq / t_nn, "motion_checks_per_s": mps1, "gnat_build_s": build_s,
-            "threads": {"cores": T, "motion_checks_per_s": mpsT,
-                        "note": "causal inserts are sequential; only the edge checks use the threads"}}
+    return {"value": (nT + mT) / (t_nnT + mT / mpsT), "unit": UNIT, "cores": T, "kind": "port",
+            "sample": (f"GNAT restatement (oracle/gnat.cpp, degree 8/4/12, 50/leaf) over the same {n0}-vertex roadmap: "
+                       f"{nT} milestones' nearestK(k={kq}) over the roadmap as const queries on {T} threads, then their "
+                       f"{mT} checkMotion edges x{repsT} with the oracle DiscreteMotionValidator on {T} threads; index "
+                       f"build {build_s:.1f} s excluded"),
+            "nn_queries_per_s": nT / t_nnT, "motion_checks_per_s": mpsT, "gnat_build_s": build_s,
+            "single_thread": {"value": (nq + m) / (t_nn + m / mps1), "nn_queries_per_s": nq / t_nn,
+                              "motion_checks_per_s": mps1,
+                              "sample": f"the first {nq} milestones inserted causally (k_i nearest, then add), "
+                                        f"their {m} edges x{reps}"}}
 
 
 def _cpu_bitstar_radius(sp, ck, tree, queries, radius, budget_s, T, k=0):
@@ -468,9 +491,11 @@ class Runner:
         self.args, self.torch, self.dev = args, torch, dev
         wl, nq, k = args.workload, args.queries, args.k
         self.radius = None
+        self.tree_mode = args.partition == "tree"
         if wl == "cfg3":
             self.sp, self.ck = SE3StateSpace(0.0, 1.0), HypercubeChecker(3, 0.1)
-            self.tree, q = reference_inputs(self.sp, args.tree, nq, rank)
+            # tree mode: one global batch of samples for every rank (the rank-0 slice of the stream)
+            self.tree, q = reference_inputs(self.sp, args.tree, nq, 0 if self.tree_mode else rank)
         elif wl == "cfg2":
             self.sp, self.ck = RealVectorStateSpace(6), HypercubeChecker(6, 0.1)
             self.tree, q = reference_inputs(self.sp, args.tree, nq, rank)
@@ -508,7 +533,15 @@ class Runner:
         self.queries = torch.from_numpy(q).to(dev)
         self.nn = NearestNeighborsGPU(self.sp, local)
         self.nn.set_exact(args.exact)
-        self.nn.add(self.tree)
+        if self.tree_mode:  # this rank's contiguous slice of the ids (ompl_amd/shard.py)
+            from ompl_amd.shard import shard_bounds
+
+            self.world = int(os.environ.get("WORLD_SIZE", "1"))
+            self.rank = rank
+            self.lo, self.hi = shard_bounds(len(self.tree), rank, self.world)
+            self.nn.add(self.tree[self.lo:self.hi])
+        else:
+            self.nn.add(self.tree)
         self.nn.set_stream(stream.cuda_stream)
         self.mv.set_stream(stream.cuda_stream)
         dim = self.sp.dim
@@ -544,6 +577,9 @@ class Runner:
                 for j in (1, 2, 3):
                     e[j].record(self.stream)
             return
+        if self.tree_mode:
+            self.step_tree(e)
+            return
         if e:
             e[0].record(self.stream)
         if a.workload == "cfg5" and not self.k:
@@ -572,7 +608,47 @@ class Runner:
         if e:
             e[3].record(self.stream)
 
+    def step_tree(self, e=None):
+        """Tree-sharded step: every rank answers the whole batch on its shard, the per-shard top-k
+        lists (global ids) are exchanged with an all_gather over RCCL and merged by the library's
+        kernel (ompl_gpu_knn_merge_device); the rank that owns a sample's nearest state steers and
+        checks that sample's motion on its own store (RRT.cpp:137-148), so no state rows travel."""
+        import torch
+
+        from ompl_amd.shard import allgather_merge, merge_topk_device
+
+        nn, mv, q = self.nn, self.mv, self.queries
+        with torch.cuda.stream(self.stream):
+            if e:
+                e[0].record(self.stream)
+            nn.knn_device(q.data_ptr(), self.nq, self.k, self.ids.data_ptr(), self.dd.data_ptr())
+            if e:
+                e[1].record(self.stream)
+            gid = torch.where(self.ids >= 0, self.ids + self.lo, -1)
+            if self.world > 1:
+                md, mi = allgather_merge(self.dd, gid, self.k)
+            else:
+                md, mi = merge_topk_device(self.dd[None], gid[None].to(torch.int32), self.k,
+                                           stream=self.stream.cuda_stream)
+            near = mi[:, 0].to(torch.int64)
+            mine = torch.nonzero((near >= self.lo) & (near < self.hi)).flatten()
+            self.m = int(mine.numel())
+            qs = q[mine].contiguous()
+            nl = (near[mine] - self.lo).to(torch.int32).contiguous()
+            self._keep = (qs, nl)
+            if self.m:
+                nn.steer_device(qs.data_ptr(), self.m, nl.data_ptr(), 1, self.maxd, self.s_from.data_ptr(),
+                                self.s_to.data_ptr())
+            if e:
+                e[2].record(self.stream)
+            if self.m:
+                mv.check_device(self.s_from.data_ptr(), self.s_to.data_ptr(), self.m, self.valid.data_ptr())
+            if e:
+                e[3].record(self.stream)
+
     def units_per_step(self):
+        if self.tree_mode:  # the batch's queries once (rank 0), the motion checks of every rank
+            return (self.nq if self.rank == 0 else 0) + self.m
         """NN queries + motion checks one step issues on this rank."""
         if self.args.workload == "cfg2":
             return self.nq
@@ -593,6 +669,12 @@ class Runner:
         a = self.args
         base = {"tree_states": a.tree, "queries_per_gpu": self.nq,
                 "parallelism": f"queries sharded over {world} GPU(s), tree replicated"}
+        if self.tree_mode:
+            base.update(queries_per_gpu=None, queries_per_step=self.nq, partition="tree",
+                        parallelism=(f"tree sharded over {world} GPU(s) ({a.tree // world} states each), every sample "
+                                     f"answered on every shard, per-shard top-{self.k} lists all_gathered (RCCL) and "
+                                     f"merged on the device; the owner of each nearest state steers + checks it"),
+                        exchange_bytes_per_rank=self.nq * self.k * 12)
         if a.workload == "cfg3":
             base.update(workload="configs[2]: SE(3) RRT*-style batch — nearestK(k=10) + steer + checkMotion "
                                  "(HypercubeBenchmark predicate on translation, edgeWidth 0.1, resolution 0.01)",
@@ -797,7 +879,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if run.tree_mode else "weak",
             "vs_baseline": None,
             "dtype": "f32 screen + f64 certify" if screen else "f64",
             "data": ("synthetic: the reference's RNG streams — RNG::setSeed(42), then a tree sampler and a query "

@@ -507,9 +507,6 @@ __global__ __launch_bounds__(256) void sel_fill_kernel(const float *__restrict__
     float qf[FS];
 #pragma unroll
     for (int f = 0; f < FS; ++f) qf[f] = live ? q32[(size_t)q * FS + f] : __builtin_nanf("");
-    double qv[F];
-#pragma unroll
-    for (int f = 0; f < F; ++f) qv[f] = live ? qf64[(size_t)q * F + f] : 0.0;
     const float rc = live ? r_count[q] : -1.f, rf = live ? r_fill[q] : -1.f;
     const uint64_t c0 = (uint64_t)blockIdx.y * chunk_len, c1 = min(c0 + chunk_len, n_end);
     const size_t sbase = ((size_t)q * chunks + blockIdx.y) * slab;
@@ -521,15 +518,9 @@ __global__ __launch_bounds__(256) void sel_fill_kernel(const float *__restrict__
             const float d = SP == OMPL_GPU_SPACE_KCHAIN ? d32<SP, FS>(&tile[s * FS], qf, (float)sp.link, 0.f, sp.dim)
                                                         : d32<SP, FS>(&tile[s * FS], qf, (float)sp.w0, (float)sp.w1, 0);
             cr += d <= rc ? 1u : 0u;
-            if (d <= rf) {
-                if (cnt < slab) {
-                    const uint32_t id = (uint32_t)(base + s);
-                    double sv[F];
-#pragma unroll
-                    for (int f = 0; f < F; ++f) sv[f] = f64[(uint64_t)f * cap + id];
-                    cd[sbase + cnt] = feat_dist<SP, F, SP == OMPL_GPU_SPACE_KCHAIN ? F / 2 : 0>(sv, qv, sp);
-                    ci[sbase + cnt] = id;
-                }
+            if (d <= rf) {  // the exact distance comes later, densely (sel_exact_kernel): here it
+                            // would run for the whole wave whenever one lane has a candidate
+                if (cnt < slab) ci[sbase + cnt] = (uint32_t)(base + s);
                 ++cnt;
             }
         }
@@ -538,6 +529,30 @@ __global__ __launch_bounds__(256) void sel_fill_kernel(const float *__restrict__
     if (!live) return;
     slab_cnt[(size_t)q * chunks + blockIdx.y] = cnt;
     if (cr) atomicAdd(&count_r[q], cr);
+}
+
+// exact fp64 distances of the slab entries (a thread per entry, the query's row from LDS-free
+// global reads, the stored state's features by id)
+template <int SP, int F>
+__global__ void sel_exact_kernel(const double *__restrict__ f64, uint64_t cap, const double *__restrict__ qf64,
+                                 uint32_t nq, uint32_t chunks, uint32_t slab, DevSpace sp,
+                                 const uint32_t *__restrict__ slab_cnt, const uint32_t *__restrict__ ci,
+                                 double *__restrict__ cd) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t per_q = (uint64_t)chunks * slab;
+    if (t >= per_q * nq) return;
+    const uint32_t q = (uint32_t)(t / per_q);
+    const uint64_t r = t - (uint64_t)q * per_q;
+    const uint32_t c = (uint32_t)(r / slab), j = (uint32_t)(r - (uint64_t)c * slab);
+    if (j >= slab_cnt[(size_t)q * chunks + c]) return;
+    const uint32_t id = ci[t];
+    double qv[F], sv[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+        qv[f] = qf64[(size_t)q * F + f];
+        sv[f] = f64[(uint64_t)f * cap + id];
+    }
+    cd[t] = feat_dist<SP, F, SP == OMPL_GPU_SPACE_KCHAIN ? F / 2 : 0>(sv, qv, sp);
 }
 
 // (distance, id) as a 96-bit key, ordered: distances are >= 0 so their bits order as integers
@@ -808,6 +823,9 @@ hipError_t run_large_select(const DevSpace &sp, const double *f64, const float *
         hipLaunchKernelGGL((sel_fill_kernel<SP, F>), grid, dim3(kTile), 0, st, f32, f64, cap, n_end, bq32, bqf, nb,
                            L.chunk_len, L.chunks, sp, rc, rf, L.slab, cd, ci, scnt, cntr);
         if (q0 == 0) timer_end(st);
+        const uint64_t ne = (uint64_t)nb * L.chunks * L.slab;
+        hipLaunchKernelGGL((sel_exact_kernel<SP, F>), dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, f64, cap,
+                           bqf, nb, L.chunks, L.slab, sp, scnt, ci, cd);
         hipLaunchKernelGGL(sel_sort_kernel, dim3(nb), dim3(kSelBlock), 0, st, cd, ci, scnt, cntr, nb, L.chunks, L.slab,
                            k, out_d + (size_t)q0 * k, out_i + (size_t)q0 * k, fb, fb + 1);
         hipLaunchKernelGGL((sel_fallback_kernel<SP, F>), dim3((unsigned)std::max(num_cus, 1)), dim3(kSelBlock), 0, st,

@@ -38,11 +38,43 @@ def merge_topk(d: torch.Tensor, ids: torch.Tensor, k: int):
     return torch.gather(d1, 1, o2), torch.gather(i1, 1, o2)
 
 
+def merge_topk_device(d_stack: torch.Tensor, ids_stack: torch.Tensor, k: int, stream=None):
+    """The per-shard lists as an all_gather leaves them — d_stack [W, Q, k] fp64, ids_stack
+    [W, Q, k] int32 (global ids, missing = -1, i.e. 0xFFFFFFFF) on the GPU — merged by the
+    library's HIP kernel (ompl_gpu_knn_merge_device) into the global [Q, k] top k by
+    (distance, id).  Returns (distances fp64, ids int32)."""
+    import ctypes as C
+
+    from . import abi
+
+    W, Q, kk = d_stack.shape
+    d_stack = d_stack.contiguous()
+    ids_stack = ids_stack.to(torch.int32).contiguous()
+    od = torch.empty((Q, k), dtype=torch.float64, device=d_stack.device)
+    oi = torch.empty((Q, k), dtype=torch.int32, device=d_stack.device)
+    if kk != k:
+        raise ValueError("every shard list must hold k entries")
+    st = stream if stream is not None else torch.cuda.current_stream(d_stack.device).cuda_stream
+    abi.check(abi.lib.ompl_gpu_knn_merge_device(C.c_void_p(d_stack.data_ptr()), C.c_void_p(ids_stack.data_ptr()),
+                                                int(W), int(Q), int(k), C.c_void_p(od.data_ptr()),
+                                                C.c_void_p(oi.data_ptr()), C.c_void_p(st)))
+    return od, oi
+
+
 def allgather_merge(d_local: torch.Tensor, ids_global: torch.Tensor, k: int, group=None):
-    """Exchange per-rank [Q, k] candidate lists (global ids) and merge to the global top-k."""
+    """Exchange per-rank [Q, k] candidate lists (global ids, missing = -1) and merge to the global
+    top-k.  GPU tensors (RCCL): one all_gather per array into a [W, Q, k] stack, merged by the HIP
+    kernel (merge_topk_device); CPU tensors (gloo tests): the same merge with torch sorts."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
+    if d_local.is_cuda:
+        ds = torch.empty((world,) + tuple(d_local.shape), dtype=d_local.dtype, device=d_local.device)
+        ii = torch.empty((world,) + tuple(ids_global.shape), dtype=torch.int32, device=d_local.device)
+        dist.all_gather_into_tensor(ds, d_local.contiguous(), group=group)
+        dist.all_gather_into_tensor(ii, ids_global.to(torch.int32).contiguous(), group=group)
+        od, oi = merge_topk_device(ds, ii, k)
+        return od, oi.to(torch.int64)
     ds = [torch.empty_like(d_local) for _ in range(world)]
     ii = [torch.empty_like(ids_global) for _ in range(world)]
     dist.all_gather(ds, d_local.contiguous(), group=group)

@@ -131,6 +131,16 @@ def _exchange_worker(rank, world, port, result_dir, use_gpu):
         off, ri, rd = O.radius(sp, data[lo:hi], q, r)
     gid = torch.from_numpy(np.where(li >= 0, li + lo, -1))
     d, i = allgather_merge(torch.from_numpy(ld), gid, 12)
+    if use_gpu:  # the device merge kernel on the gathered stack gives the same lists
+        from ompl_amd.shard import merge_topk_device
+
+        ws = [torch.empty_like(torch.from_numpy(ld)) for _ in range(world)]
+        wi = [torch.empty_like(gid) for _ in range(world)]
+        dist.all_gather(ws, torch.from_numpy(ld))
+        dist.all_gather(wi, gid)
+        dd, di = merge_topk_device(torch.stack(ws).cuda(), torch.stack(wi).to(torch.int32).cuda(), 12)
+        torch.cuda.synchronize()
+        assert torch.equal(dd.cpu(), d) and torch.equal(di.cpu().to(torch.int64), i)
     goff, gi, gd = allgather_radius(torch.from_numpy(off.astype(np.int64)),
                                     torch.from_numpy(ri.astype(np.int64) + lo), torch.from_numpy(rd))
     # a batch of new states: rank r contributes r + 3 of them; every rank gets all, rank order
