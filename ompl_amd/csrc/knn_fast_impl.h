@@ -570,7 +570,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
     const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
     uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi,
-    unsigned long long *__restrict__ counters, int bulk, int k2) {
+    unsigned long long *__restrict__ counters, int bulk, int k2, int recheck) {
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
     constexpr int GH = G / 2;
     static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
@@ -746,33 +746,49 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     uint32_t base = s0 > 0 ? s0 - 1 : 0;
     uint64_t sm = (s0 > 0 ? 7ull : 3ull) & ((nsuper - base >= 64) ? ~0ull : ((1ull << (nsuper - base)) - 1));
     uint32_t sb = 0;
+    // the round's super-tile bounds (lane l: super-tile base + l, one per query): a super-tile
+    // popped later is skipped when the thresholds have tightened past all of its bounds since
+    // its round, before its 32 tile boxes are loaded and tested
+    float slb[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) slb[g] = -__builtin_inff();  // the neighbourhood's three: always visited
     auto next_super = [&]() -> int {  // next super-tile to visit, -1 when done
-        while (!sm) {
-            if (sb >= nsuper) return -1;
-            relaunder();
+        for (;;) {
+            while (!sm) {
+                if (sb >= nsuper) return -1;
+                relaunder();
 #ifdef OMPL_AMD_PROBE
-            ++pr_rounds;
+                ++pr_rounds;
 #endif
-            const uint32_t s = sb + lane;
-            bool need = false;
-            if (s < nsuper && (s + 1 < s0 || s > s0 + 1)) {
-                float bx[BW];
-                const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
+                const uint32_t s = sb + lane;
+                bool need = false;
 #pragma unroll
-                for (int c = 0; c < BW / 4; ++c) {
-                    const float4 v = b4[c];
-                    bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
+                for (int g = 0; g < G; ++g) slb[g] = __builtin_inff();
+                if (s < nsuper && (s + 1 < s0 || s > s0 + 1)) {
+                    float bx[BW];
+                    const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
+#pragma unroll
+                    for (int c = 0; c < BW / 4; ++c) {
+                        const float4 v = b4[c];
+                        bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
+                    }
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        slb[g] = box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1);
+                        need |= slb[g] < td[g];
+                    }
                 }
-#pragma unroll
-                for (int g = 0; g < G; ++g) need |= box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1) < td[g];
+                sm = __ballot(need);
+                base = sb;
+                sb += 64;
             }
-            sm = __ballot(need);
-            base = sb;
-            sb += 64;
+            const int l = __builtin_ctzll(sm);
+            sm &= sm - 1;
+            bool still = !recheck;
+#pragma unroll
+            for (int g = 0; g < G; ++g) still |= readlane_f(slb[g], l) < td[g];
+            if (still) return (int)(base + l);
         }
-        const int l = __builtin_ctzll(sm);
-        sm &= sm - 1;
-        return (int)(base + l);
     };
     // Software pipeline: the tile boxes of the next super-tile are loaded while the current
     // one is scanned, and the first tile of a super-tile is fetched before those boxes, so
@@ -1474,10 +1490,14 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             constexpr int G = group_queries<SP>();
+            static const int recheck = [] {  // A/B switch of the popped super-tile re-check
+                const char *v = std::getenv("OMPL_GPU_SUPER_RECHECK");
+                return v ? std::atoi(v) : 1;
+            }();
             hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
                                ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0,
                                q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, kBulkThreshold,
-                               p.k2);
+                               p.k2, recheck);
             timer_end(st);
             walked = true;
         }

@@ -15,3 +15,10 @@ f="$out/rrtstar.json"
 timeout -k 10 300 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --single-query-reps 0 --rrt-iters 0 > "$f" 2> "$f.err"
 rc=$?; if fatal $rc; then echo "rrtstar rc=$rc"; tail -3 "$f.err"; exit 1; fi
 python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('rrt_star_knn', d.get('rrt_star_knn'))" "$f"
+args="--steps 6 --warmup 2 --no-cpu-baseline --no-extras --single-query-reps 0 --rrt-iters 0"
+for r in 1 2; do for v in 1 0; do
+  f="$out/rc$v.$r.json"
+  OMPL_GPU_SUPER_RECHECK=$v timeout -k 10 300 python -u bench.py $args > "$f" 2> "$f.err"
+  rc=$?; if fatal $rc; then echo "rc=$rc"; tail -3 "$f.err"; exit 1; fi
+  python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[1].split('/')[-1], round(d['value']/1e6,2), 'step_ms', round(d['ms_per_step'],4), 'walk_ms', round(r['kernel_ms'],4), 'pairs', r['algorithmic'][:10])" "$f"
+done; done
