@@ -518,7 +518,7 @@ __global__ __launch_bounds__(256) void sel_fill_kernel(const float *__restrict__
             const float d = SP == OMPL_GPU_SPACE_KCHAIN ? d32<SP, FS>(&tile[s * FS], qf, (float)sp.link, 0.f, sp.dim)
                                                         : d32<SP, FS>(&tile[s * FS], qf, (float)sp.w0, (float)sp.w1, 0);
             cr += d <= rc ? 1u : 0u;
-            if (d <= rf) {  // the exact distance comes later, densely (sel_exact_kernel): here it
+            if (d <= rf) {  // the exact distance comes later, densely (sel_sort_kernel): here it
                             // would run for the whole wave whenever one lane has a candidate
                 if (cnt < slab) ci[sbase + cnt] = (uint32_t)(base + s);
                 ++cnt;
@@ -529,30 +529,6 @@ __global__ __launch_bounds__(256) void sel_fill_kernel(const float *__restrict__
     if (!live) return;
     slab_cnt[(size_t)q * chunks + blockIdx.y] = cnt;
     if (cr) atomicAdd(&count_r[q], cr);
-}
-
-// exact fp64 distances of the slab entries (a thread per entry, the query's row from LDS-free
-// global reads, the stored state's features by id)
-template <int SP, int F>
-__global__ void sel_exact_kernel(const double *__restrict__ f64, uint64_t cap, const double *__restrict__ qf64,
-                                 uint32_t nq, uint32_t chunks, uint32_t slab, DevSpace sp,
-                                 const uint32_t *__restrict__ slab_cnt, const uint32_t *__restrict__ ci,
-                                 double *__restrict__ cd) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t per_q = (uint64_t)chunks * slab;
-    if (t >= per_q * nq) return;
-    const uint32_t q = (uint32_t)(t / per_q);
-    const uint64_t r = t - (uint64_t)q * per_q;
-    const uint32_t c = (uint32_t)(r / slab), j = (uint32_t)(r - (uint64_t)c * slab);
-    if (j >= slab_cnt[(size_t)q * chunks + c]) return;
-    const uint32_t id = ci[t];
-    double qv[F], sv[F];
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-        qv[f] = qf64[(size_t)q * F + f];
-        sv[f] = f64[(uint64_t)f * cap + id];
-    }
-    cd[t] = feat_dist<SP, F, SP == OMPL_GPU_SPACE_KCHAIN ? F / 2 : 0>(sv, qv, sp);
 }
 
 // (distance, id) as a 96-bit key, ordered: distances are >= 0 so their bits order as integers
@@ -573,6 +549,7 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
                                   uint32_t *__restrict__ out_i) {
     using BlockSort = rocprim::block_radix_sort<uint64_t, kSelBlock, kSelItems, uint32_t>;
     using BlockScan = rocprim::block_scan<uint32_t, kSelBlock>;
+    constexpr int kDigit = 11, kRadix = 1 << kDigit;
     __shared__ union {
         struct {
             uint64_t d[kLargeSelMaxK];
@@ -581,20 +558,27 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
         typename BlockSort::storage_type sort;
     } sh;
     __shared__ typename BlockScan::storage_type scan_storage;
-    __shared__ uint32_t hist[256];
+    __shared__ uint32_t hist[kRadix];
     __shared__ uint32_t sh_digit, sh_need;
     const uint32_t tid = threadIdx.x;
-    // radix select: prefix (Td, Ti) of the k-th key, 12 digits most significant first
+    const int lane = threadIdx.x & 63;
+    // radix select of the k-th smallest (distance bits, id): 11-bit digits, most significant
+    // first — 64 distance bits in 6 digits (11, 11, 11, 11, 11, 9), then 32 id bits in 3
+    constexpr int kShift[9] = {53, 42, 31, 20, 9, 0, 21, 10, 0};
+    constexpr int kBits[9] = {11, 11, 11, 11, 11, 9, 11, 11, 10};
     uint64_t Td = 0;
     uint32_t Ti = 0;
     uint32_t need = min(k, count);
-    for (int dg = 0; dg < 12; ++dg) {
-        const bool on_d = dg < 8;
-        const int shift = on_d ? 56 - 8 * dg : 24 - 8 * (dg - 8);
-        // keys matching the prefix so far: the bits above `shift` (distance), then id bits above it
-        for (uint32_t b = tid; b < 256; b += kSelBlock) hist[b] = 0;
+    for (int dg = 0; dg < 9; ++dg) {
+        const bool on_d = dg < 6;
+        const int shift = kShift[dg], bits = kBits[dg];
+        const uint32_t dmask = (1u << bits) - 1u;
+        for (uint32_t b = tid; b < kRadix; b += kSelBlock) hist[b] = 0;
+        if (tid == 0) {  // defaults: nothing left to select (need == 0) takes the whole digit range
+            sh_digit = dmask;
+            sh_need = 0;
+        }
         __syncthreads();
-        const int lane = threadIdx.x & 63;
         for (uint32_t e0 = 0; e0 < count; e0 += kSelBlock) {  // uniform trip count: the ballots below
             const uint32_t e = e0 + tid;
             uint64_t d = 0;
@@ -602,11 +586,11 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
             bool part = e < count && get(e, d, i);
             uint32_t digit;
             if (on_d) {
-                part = part && (dg == 0 || (d >> (shift + 8)) == (Td >> (shift + 8)));
-                digit = (uint32_t)(d >> shift) & 255u;
+                part = part && (dg == 0 || (d >> (shift + bits)) == (Td >> (shift + bits)));
+                digit = (uint32_t)(d >> shift) & dmask;
             } else {
-                part = part && d == Td && (dg == 8 || (i >> (shift + 8)) == (Ti >> (shift + 8)));
-                digit = (i >> shift) & 255u;
+                part = part && d == Td && (dg == 6 || (i >> (shift + bits)) == (Ti >> (shift + bits)));
+                digit = (i >> shift) & dmask;
             }
             // the leading digits are mostly equal across a wave (the distances' exponent): one
             // atomic with the wave's count then, instead of 64 serialised on one LDS address
@@ -622,19 +606,17 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
             }
         }
         __syncthreads();
-        if (tid == 0) {
-            uint32_t cum = 0, dgt = 255;
-            for (uint32_t b = 0; b < 256; ++b) {
-                if (cum + hist[b] >= need) {
-                    dgt = b;
-                    break;
-                }
-                cum += hist[b];
-            }
-            sh_digit = dgt;
-            sh_need = need - cum;
+        // the digit where the running count reaches `need`: block scan of the 2,048 counts
+        uint32_t c0 = hist[2 * tid], c1 = hist[2 * tid + 1], pre = 0, tot = 0;
+        BlockScan().exclusive_scan(c0 + c1, pre, 0u, tot, scan_storage);
+        if (pre < need && pre + c0 >= need) {
+            sh_digit = 2 * tid;
+            sh_need = need - pre;
+        } else if (pre + c0 < need && pre + c0 + c1 >= need) {
+            sh_digit = 2 * tid + 1;
+            sh_need = need - pre - c0;
         }
-        __syncthreads();
+        __syncthreads();  // (fewer candidates than k: the defaults take them all)
         if (on_d)
             Td |= (uint64_t)sh_digit << shift;
         else
@@ -642,7 +624,7 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
         need = sh_need;
         __syncthreads();
     }
-    // pack the selected keys (<= (Td, Ti)) in id order: block prefix sums over chunks of the source
+    // pack the selected keys (<= (Td, Ti)) in source order (id order): block prefix sums
     uint32_t base = 0;
     for (uint32_t e0 = 0; e0 < count; e0 += kSelBlock) {
         const uint32_t e = e0 + tid;
@@ -683,37 +665,72 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
     }
 }
 
-// a block per query: select + sort over its slabs, or put it on the fallback list
-__global__ __launch_bounds__(kSelBlock) void sel_sort_kernel(const double *__restrict__ cd,
+// a block per query: its candidates' exact fp64 distances computed densely (id order: chunk
+// by chunk, slot by slot) into dd / di, then the select + sort over them; or, on a slab
+// overflow or a short count, the query goes to the fallback list
+template <int SP, int F>
+__global__ __launch_bounds__(kSelBlock) void sel_sort_kernel(const double *__restrict__ f64, uint64_t cap,
+                                                             const double *__restrict__ qf64, DevSpace sp,
                                                              const uint32_t *__restrict__ ci,
                                                              const uint32_t *__restrict__ slab_cnt,
                                                              const unsigned int *__restrict__ count_r, uint32_t nq,
                                                              uint32_t chunks, uint32_t slab, uint32_t k,
+                                                             double *__restrict__ dd, uint32_t *__restrict__ di,
                                                              double *__restrict__ out_d, uint32_t *__restrict__ out_i,
                                                              uint32_t *__restrict__ fb_count,
                                                              uint32_t *__restrict__ fb_list) {
+    using BlockScan = rocprim::block_scan<uint32_t, kSelBlock>;
+    __shared__ typename BlockScan::storage_type scan_storage;
+    __shared__ uint32_t coff[kSelBlock + 1];  // chunk offsets of the dense order (chunks <= kSelBlock)
+    __shared__ uint32_t sh_bad;
     const uint32_t q = blockIdx.x;
     if (q >= nq) return;
-    __shared__ uint32_t sh_bad;
-    if (threadIdx.x == 0) sh_bad = count_r[q] < k ? 1u : 0u;
-    __syncthreads();
+    const uint32_t tid = threadIdx.x;
     const uint32_t *cnt = slab_cnt + (size_t)q * chunks;
-    for (uint32_t c = threadIdx.x; c < chunks; c += blockDim.x)
-        if (cnt[c] > slab) sh_bad = 1u;  // benign race: every writer stores 1
+    const uint32_t c = tid < chunks ? cnt[tid] : 0u;
+    uint32_t pre = 0, tot = 0;
+    BlockScan().exclusive_scan(c, pre, 0u, tot, scan_storage);
+    if (tid == 0) sh_bad = count_r[q] < k ? 1u : 0u;
+    __syncthreads();
+    if (tid < chunks) {
+        coff[tid] = pre;
+        if (c > slab) sh_bad = 1u;  // benign race: every writer stores 1
+    }
+    if (tid == 0) coff[chunks] = tot;
     __syncthreads();
     if (sh_bad) {
-        if (threadIdx.x == 0) fb_list[atomicAdd(fb_count, 1u)] = q;
+        if (tid == 0) fb_list[atomicAdd(fb_count, 1u)] = q;
         return;
     }
-    const size_t base = (size_t)q * chunks * slab;
+    double qv[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qv[f] = qf64[(size_t)q * F + f];
+    const size_t sbase = (size_t)q * chunks * slab;
+    double *qd = dd + sbase;
+    uint32_t *qi = di + sbase;
+    for (uint32_t e = tid; e < tot; e += kSelBlock) {
+        uint32_t lo = 0, hi = chunks;  // the chunk holding dense position e: coff[lo] <= e < coff[lo + 1]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (coff[mid] <= e)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        const uint32_t id = ci[sbase + (size_t)lo * slab + (e - coff[lo])];
+        double sv[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) sv[f] = f64[(uint64_t)f * cap + id];
+        qd[e] = feat_dist<SP, F, SP == OMPL_GPU_SPACE_KCHAIN ? F / 2 : 0>(sv, qv, sp);
+        qi[e] = id;
+    }
+    __syncthreads();
     auto get = [&](uint32_t e, uint64_t &d, uint32_t &i) -> bool {
-        const uint32_t c = e / slab, j = e - c * slab;
-        if (j >= cnt[c]) return false;
-        d = (uint64_t)__double_as_longlong(cd[base + e]);
-        i = ci[base + e];
+        d = (uint64_t)__double_as_longlong(qd[e]);
+        i = qi[e];
         return true;
     };
-    block_select_sort(get, chunks * slab, k, q, out_d, out_i);
+    block_select_sort(get, tot, k, q, out_d, out_i);
 }
 
 // exact fallback: a block per listed query, the same select over every stored state (each
@@ -749,7 +766,7 @@ __global__ __launch_bounds__(kSelBlock) void sel_fallback_kernel(const double *_
 }
 
 struct SelLayout {
-    size_t q32, hist, inv, rc, rf, cntr, scnt, fb, cd, ci, total;
+    size_t q32, hist, inv, rc, rf, cntr, scnt, fb, cd, ci, di, total;
     uint32_t chunks, chunk_len, slab, qb;
 };
 
@@ -759,7 +776,12 @@ inline size_t sel_align(size_t x) { return (x + 255) & ~(size_t)255; }
 // 1024) candidates per query spread over the chunks, plus slack for the spread between chunks
 SelLayout sel_layout(int FS, uint32_t nq, uint32_t k, uint64_t n_end, int num_cus) {
     SelLayout L{};
-    const Plan p = plan(std::min<uint32_t>(nq, 4096u), n_end, num_cus);
+    Plan p = plan(std::min<uint32_t>(nq, 4096u), n_end, num_cus);
+    if (p.chunks > (uint32_t)kSelBlock) {  // sel_sort_kernel scans one chunk count per thread
+        const uint64_t tiles = (n_end + kTile - 1) / kTile, per = (tiles + kSelBlock - 1) / kSelBlock;
+        p.chunk_len = (uint32_t)(per * kTile);
+        p.chunks = (uint32_t)((n_end + p.chunk_len - 1) / p.chunk_len);
+    }
     L.chunks = p.chunks;
     L.chunk_len = p.chunk_len;
     const double est = (double)k + 8.0 * std::sqrt(8.0 * k) + 1024.0;
@@ -782,6 +804,7 @@ SelLayout sel_layout(int FS, uint32_t nq, uint32_t k, uint64_t n_end, int num_cu
     L.fb = take(4ull * (L.qb + 1));
     L.cd = take(8ull * L.qb * L.chunks * L.slab);
     L.ci = take(4ull * L.qb * L.chunks * L.slab);
+    L.di = take(4ull * L.qb * L.chunks * L.slab);
     L.total = off;
     return L;
 }
@@ -797,8 +820,8 @@ hipError_t run_large_select(const DevSpace &sp, const double *f64, const float *
     float *q32 = (float *)(w + L.q32), *inv = (float *)(w + L.inv), *rc = (float *)(w + L.rc), *rf = (float *)(w + L.rf);
     unsigned int *hist = (unsigned int *)(w + L.hist), *cntr = (unsigned int *)(w + L.cntr);
     uint32_t *scnt = (uint32_t *)(w + L.scnt), *fb = (uint32_t *)(w + L.fb);
-    double *cd = (double *)(w + L.cd);
-    uint32_t *ci = (uint32_t *)(w + L.ci);
+    double *cd = (double *)(w + L.cd);  // the dense exact distances of each query's candidates
+    uint32_t *ci = (uint32_t *)(w + L.ci), *di = (uint32_t *)(w + L.di);
     const float w0 = SP == OMPL_GPU_SPACE_KCHAIN ? (float)sp.link : (float)sp.w0;
     const float bin_a = dmax / (float)kBins;
     hipLaunchKernelGGL((rows32_kernel<SP, F>), dim3((nq + 255) / 256), dim3(256), 0, st, qf64, nq, q32);
@@ -823,11 +846,9 @@ hipError_t run_large_select(const DevSpace &sp, const double *f64, const float *
         hipLaunchKernelGGL((sel_fill_kernel<SP, F>), grid, dim3(kTile), 0, st, f32, f64, cap, n_end, bq32, bqf, nb,
                            L.chunk_len, L.chunks, sp, rc, rf, L.slab, cd, ci, scnt, cntr);
         if (q0 == 0) timer_end(st);
-        const uint64_t ne = (uint64_t)nb * L.chunks * L.slab;
-        hipLaunchKernelGGL((sel_exact_kernel<SP, F>), dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, f64, cap,
-                           bqf, nb, L.chunks, L.slab, sp, scnt, ci, cd);
-        hipLaunchKernelGGL(sel_sort_kernel, dim3(nb), dim3(kSelBlock), 0, st, cd, ci, scnt, cntr, nb, L.chunks, L.slab,
-                           k, out_d + (size_t)q0 * k, out_i + (size_t)q0 * k, fb, fb + 1);
+        hipLaunchKernelGGL((sel_sort_kernel<SP, F>), dim3(nb), dim3(kSelBlock), 0, st, f64, cap, bqf, sp, ci, scnt,
+                           cntr, nb, L.chunks, L.slab, k, cd, di, out_d + (size_t)q0 * k, out_i + (size_t)q0 * k, fb,
+                           fb + 1);
         hipLaunchKernelGGL((sel_fallback_kernel<SP, F>), dim3((unsigned)std::max(num_cus, 1)), dim3(kSelBlock), 0, st,
                            f64, cap, n_end, bqf, sp, k, fb, fb + 1, out_d + (size_t)q0 * k, out_i + (size_t)q0 * k);
     }
