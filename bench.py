@@ -340,7 +340,7 @@ def single_query_scan(torch, nn, dev, reps, n_tree, note=None):
     wall = time.perf_counter() - t0
     ms1, n1, name = nn.kernel_time()
     kern_ms = (ms1 - ms0) / max(n1 - n0, 1)
-    b = B_SE3["f32"] if "stream32" in name else B_SE3["f64"]
+    b = B_SE3["f64"] if name == "knn_stream_kernel" else B_SE3["f32"]  # the fp64 stream reads 56 B per state
     achieved = n_tree * b / (kern_ms * 1e-3) / 1e9
     return {"queries_per_s": reps / wall, "kernel": name, "kernel_us": kern_ms * 1e3, "tree_states": n_tree,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

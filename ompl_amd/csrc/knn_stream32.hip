@@ -20,6 +20,7 @@ namespace ompl_amd {
 namespace {
 
 constexpr int kS32Threads = 256;
+constexpr uint32_t g_stream1_blocks = 1024;  // knn_stream1_kernel blocks over the batch (4 per CU)
 
 #if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 1 || OMPL_AMD_VARIANT == 3)
 __device__ __forceinline__ float4 load_row4(const float *p) {  // A/B build: non-temporal stream
@@ -155,6 +156,136 @@ __global__ __launch_bounds__(256) void knn_stream32_merge_kernel(const double *_
     }
 }
 
+// k = 1 (RRT's nearest, RRT.cpp:137): a persistent form.  Each block streams one long
+// contiguous range (n / P states, P ~ 4 blocks per CU over the batch), its row loads two float4
+// groups ahead of the arithmetic, and every thread keeps only its two smallest d32.  Then, as
+// above with K = 1, thr = (m + E)(1 + 32u) from the block's fp32 minimum m: the block's exact
+// nearest has d32 <= thr; a thread's smallest is refined in fp64 when <= thr, and a thread whose
+// second smallest is <= thr too rescans its positions (rare).  One selection per range instead
+// of two per 1,024 states, so the loads keep streaming.
+
+template <int SP, int F>
+__global__ __launch_bounds__(kS32Threads) void knn_stream1_kernel(const float *__restrict__ feat32,
+                                                                  const double *__restrict__ feat64, uint64_t cap,
+                                                                  uint64_t n_end, uint64_t range,
+                                                                  const double *__restrict__ qfeat, DevSpace sp,
+                                                                  float absmax, float qeta,
+                                                                  double *__restrict__ part_d,
+                                                                  uint32_t *__restrict__ part_i) {
+    constexpr int FS = Geo<SP, F>::FS;
+    __shared__ double lds_d[4];
+    __shared__ uint32_t lds_i[4];
+    __shared__ float lds_f[4];
+    const uint32_t q = blockIdx.y;
+    double qv[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qv[f] = qfeat[(size_t)q * F + f];
+    float q32[FS];
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) q32[c] = (float)qv[c];
+        q32[3] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) q32[4 + c] = (float)qv[3 + c];
+    } else {
+#pragma unroll
+        for (int f = 0; f < F; ++f) q32[f] = (float)qv[f];
+    }
+    const float w0 = (float)sp.w0, w1 = (float)sp.w1;
+    const uint64_t b0 = (uint64_t)blockIdx.x * range, b1 = min(b0 + range, n_end);
+    const float nan4 = __builtin_nanf("");
+    float m1 = __builtin_inff(), m2 = __builtin_inff();
+    uint32_t i1 = kNoId;
+    auto screen = [&](const float4 (&x)[F], uint64_t p) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float s[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) s[f] = u == 0 ? x[f].x : u == 1 ? x[f].y : u == 2 ? x[f].z : x[f].w;
+            const float d = state_dist32<SP, F>(s, q32, w0, w1);  // NaN: unused / removed slot
+            if (d < m1) {
+                m2 = m1;
+                m1 = d;
+                i1 = (uint32_t)(p + u);
+            } else if (d < m2) {
+                m2 = d;
+            }
+        }
+    };
+    auto load = [&](float4 (&x)[F], uint64_t p) {
+#pragma unroll
+        for (int f = 0; f < F; ++f)
+            x[f] = p < b1 ? load_row4(feat32 + (uint64_t)f * cap + p) : make_float4(nan4, nan4, nan4, nan4);
+    };
+    // thread t covers positions b0 + 4t + 1024 j (a wave reads 1 KB per row per load)
+    float4 xa[F], xb[F];
+    uint64_t p = b0 + 4 * threadIdx.x;
+    load(xa, p);
+    load(xb, p + 4 * kS32Threads);
+    for (; p < b1; p += 2 * 4 * kS32Threads) {
+        screen(xa, p);
+        load(xa, p + 2 * 4 * kS32Threads);
+        screen(xb, p + 4 * kS32Threads);
+        load(xb, p + 3 * 4 * kS32Threads);
+    }
+    // the block's fp32 minimum and the refinement threshold
+    float m = m1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) lds_f[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fminf(fminf(lds_f[0], lds_f[1]), fminf(lds_f[2], lds_f[3]));
+    double B = absmax;
+    const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : F;
+    for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qv[c]));
+    const double t = (double)m;  // +inf: no live state in the range (nothing passes below)
+    const double thr = (t + screen_error<SP>(sp, B, t, (double)qeta + query_eta<SP>(qv))) * (1.0 + 32.0 * kU);
+    // exact fp64 distances of this thread's candidates (reference operation order)
+    double bd = __builtin_inf();
+    uint32_t bi = kNoId;
+    auto refine = [&](uint64_t id) {
+        double sv[F];
+#pragma unroll
+        for (int f = 0; f < F; ++f) sv[f] = feat64[(uint64_t)f * cap + id];
+        const double x = feat_dist<SP, F, 0>(sv, qv, sp);
+        if (lex_less(x, (uint32_t)id, bd, bi)) {
+            bd = x;
+            bi = (uint32_t)id;
+        }
+    };
+    if ((double)m2 <= thr) {  // two or more candidates here: rescan this thread's positions
+        for (uint64_t pp = b0 + 4 * threadIdx.x; pp < b1; pp += 4 * kS32Threads) {
+            float4 x[F];
+            load(x, pp);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                float s[F];
+#pragma unroll
+                for (int f = 0; f < F; ++f) s[f] = u == 0 ? x[f].x : u == 1 ? x[f].y : u == 2 ? x[f].z : x[f].w;
+                if ((double)state_dist32<SP, F>(s, q32, w0, w1) <= thr) refine(pp + u);
+            }
+        }
+    } else if ((double)m1 <= thr) {
+        refine(i1);
+    }
+    wave_argmin(bd, bi);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        lds_d[threadIdx.x >> 6] = bd;
+        lds_i[threadIdx.x >> 6] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w)
+            if (lex_less(lds_d[w], lds_i[w], bd, bi)) {
+                bd = lds_d[w];
+                bi = lds_i[w];
+            }
+        part_d[(size_t)q * gridDim.x + blockIdx.x] = bd;
+        part_i[(size_t)q * gridDim.x + blockIdx.x] = bi;
+    }
+}
+
 template <int SP, int F, int K, int ITEMS>
 hipError_t run_stream32(const DevSpace &sp, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_end,
                         const double *qfeat, uint32_t nq, uint32_t k, float absmax, float qeta, double *out_d,
@@ -188,9 +319,22 @@ template <int SP, int F>
 hipError_t stream32_k(const DevSpace &sp, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_end,
                       const double *qfeat, uint32_t nq, uint32_t k, float absmax, float qeta, double *out_d,
                       uint32_t *out_i, void *ws, size_t ws_bytes, hipStream_t st) {
-    if (k <= 1)
-        return stream32_items<SP, F, 1>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
-                                        ws_bytes, st);
+    if (k <= 1) {  // the persistent form: ~4 blocks per CU over the batch
+        const uint64_t groups = (n_end + 1023) / 1024;  // 1,024-state steps (a block's stride)
+        const uint64_t P = std::max<uint64_t>(1, std::min<uint64_t>(groups, (uint64_t)g_stream1_blocks / nq + 1));
+        const uint64_t range = (groups + P - 1) / P * 1024;
+        const uint32_t Pb = (uint32_t)((n_end + range - 1) / range);
+        const size_t need = (size_t)nq * Pb * (sizeof(double) + sizeof(uint32_t));
+        if (ws_bytes < need) return hipErrorInvalidValue;
+        double *pd = (double *)ws;
+        uint32_t *pi = (uint32_t *)(pd + (size_t)nq * Pb);
+        timer_begin(st, "knn_stream1_kernel");
+        hipLaunchKernelGGL((knn_stream1_kernel<SP, F>), dim3(Pb, nq), dim3(kS32Threads), 0, st, feat32, feat64, cap,
+                           n_end, range, qfeat, sp, absmax, qeta, pd, pi);
+        timer_end(st);
+        hipLaunchKernelGGL((knn_stream32_merge_kernel<1>), dim3(nq), dim3(256), 0, st, pd, pi, Pb, out_d, out_i, k);
+        return hipGetLastError();
+    }
     if (k <= 4)
         return stream32_items<SP, F, 4>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
                                         ws_bytes, st);
