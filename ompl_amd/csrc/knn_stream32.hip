@@ -20,7 +20,15 @@ namespace ompl_amd {
 namespace {
 
 constexpr int kS32Threads = 256;
-constexpr uint32_t g_stream1_blocks = 1024;  // knn_stream1_kernel blocks over the batch (4 per CU)
+// knn_stream1_kernel blocks over the batch; OMPL_GPU_S1_BLOCKS overrides (A/B), 0 selects the
+// chunked form for k = 1 too
+inline uint32_t stream1_blocks() {
+    static const uint32_t b = [] {
+        const char *v = std::getenv("OMPL_GPU_S1_BLOCKS");
+        return v ? (uint32_t)std::atoi(v) : 1024u;
+    }();
+    return b;
+}
 
 #if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 1 || OMPL_AMD_VARIANT == 3)
 __device__ __forceinline__ float4 load_row4(const float *p) {  // A/B build: non-temporal stream
@@ -319,9 +327,9 @@ template <int SP, int F>
 hipError_t stream32_k(const DevSpace &sp, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_end,
                       const double *qfeat, uint32_t nq, uint32_t k, float absmax, float qeta, double *out_d,
                       uint32_t *out_i, void *ws, size_t ws_bytes, hipStream_t st) {
-    if (k <= 1) {  // the persistent form: ~4 blocks per CU over the batch
+    if (k <= 1 && stream1_blocks() > 0) {  // the persistent form: ~4 blocks per CU over the batch
         const uint64_t groups = (n_end + 1023) / 1024;  // 1,024-state steps (a block's stride)
-        const uint64_t P = std::max<uint64_t>(1, std::min<uint64_t>(groups, (uint64_t)g_stream1_blocks / nq + 1));
+        const uint64_t P = std::max<uint64_t>(1, std::min<uint64_t>(groups, (uint64_t)stream1_blocks() / nq + 1));
         const uint64_t range = (groups + P - 1) / P * 1024;
         const uint32_t Pb = (uint32_t)((n_end + range - 1) / range);
         const size_t need = (size_t)nq * Pb * (sizeof(double) + sizeof(uint32_t));
