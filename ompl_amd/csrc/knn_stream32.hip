@@ -200,7 +200,12 @@ __global__ __launch_bounds__(kS32Threads) void knn_stream1_kernel(const float *_
         for (int f = 0; f < F; ++f) q32[f] = (float)qv[f];
     }
     const float w0 = (float)sp.w0, w1 = (float)sp.w1;
-    const uint64_t b0 = (uint64_t)blockIdx.x * range, b1 = min(b0 + range, n_end);
+    // grid-stride over 1,024-state groups (group g = blockIdx.x + j gridDim.x): at any moment the
+    // blocks stream neighbouring groups of every row, as a one-shot grid would (a contiguous range
+    // per block streamed 5-10 % slower at 10^7 states)
+    (void)range;
+    const uint64_t gstride = (uint64_t)gridDim.x * 4 * kS32Threads;
+    const uint64_t b0 = (uint64_t)blockIdx.x * 4 * kS32Threads, b1 = n_end;
     const float nan4 = __builtin_nanf("");
     float m1 = __builtin_inff(), m2 = __builtin_inff();
     uint32_t i1 = kNoId;
@@ -229,12 +234,12 @@ __global__ __launch_bounds__(kS32Threads) void knn_stream1_kernel(const float *_
     float4 xa[F], xb[F];
     uint64_t p = b0 + 4 * threadIdx.x;
     load(xa, p);
-    load(xb, p + 4 * kS32Threads);
-    for (; p < b1; p += 2 * 4 * kS32Threads) {
+    load(xb, p + gstride);
+    for (; p < b1; p += 2 * gstride) {
         screen(xa, p);
-        load(xa, p + 2 * 4 * kS32Threads);
-        screen(xb, p + 4 * kS32Threads);
-        load(xb, p + 3 * 4 * kS32Threads);
+        load(xa, p + 2 * gstride);
+        screen(xb, p + gstride);
+        load(xb, p + 3 * gstride);
     }
     // the block's fp32 minimum and the refinement threshold
     float m = m1;
@@ -262,7 +267,7 @@ __global__ __launch_bounds__(kS32Threads) void knn_stream1_kernel(const float *_
         }
     };
     if ((double)m2 <= thr) {  // two or more candidates here: rescan this thread's positions
-        for (uint64_t pp = b0 + 4 * threadIdx.x; pp < b1; pp += 4 * kS32Threads) {
+        for (uint64_t pp = b0 + 4 * threadIdx.x; pp < b1; pp += gstride) {
             float4 x[F];
             load(x, pp);
 #pragma unroll
