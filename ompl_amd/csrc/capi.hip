@@ -464,7 +464,7 @@ static bool screen_safe(const ompl_gpu_nn *h) {
 }
 
 #ifdef OMPL_AMD_PROBE
-constexpr int kCullCounters = 10;  // + walk event counters of the probe build (tools/probe)
+constexpr int kCullCounters = 12;  // + walk event counters of the probe build (tools/probe)
 #else
 constexpr int kCullCounters = 5;
 #endif

@@ -609,7 +609,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     }
     uint32_t visited = 0, qscans = 0;  // tiles fetched; (tile, query) scans
 #ifdef OMPL_AMD_PROBE
-    uint32_t pr_offers = 0, pr_bulk = 0, pr_ins = 0, pr_supers = 0, pr_rounds = 0;
+    uint32_t pr_offers = 0, pr_bulk = 0, pr_ins = 0, pr_supers = 0, pr_rounds = 0, pr_empty = 0, pr_skip = 0;
 #endif
 
     // tiles of super-tile s some query may still need; lb[j]: this lane's bound for tile
@@ -788,6 +788,9 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 #pragma unroll
             for (int g = 0; g < G; ++g) still |= readlane_f(slb[g], l) < td[g];
             if (still) return (int)(base + l);
+#ifdef OMPL_AMD_PROBE
+            ++pr_skip;
+#endif
         }
     };
     // Software pipeline: the tile boxes of the next super-tile are loaded while the current
@@ -802,6 +805,9 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         float lb[GH];
         uint32_t m = tile_mask(bx, lb);
         if ((uint32_t)s == th / kSuperTiles) m &= ~(1u << (th % kSuperTiles));  // scanned first
+#ifdef OMPL_AMD_PROBE
+        if (!m) ++pr_empty;
+#endif
         const int sn = next_super();
         float x[R], xn[R];
         uint32_t id = kNoId, idn = kNoId;
@@ -846,6 +852,8 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         atomicAdd(&cs[7], (unsigned long long)pr_ins);
         atomicAdd(&cs[8], (unsigned long long)pr_supers);
         atomicAdd(&cs[9], (unsigned long long)pr_rounds);
+        atomicAdd(&cs[10], (unsigned long long)pr_empty);
+        atomicAdd(&cs[11], (unsigned long long)pr_skip);
 #endif
     }
 #pragma unroll

@@ -39,12 +39,12 @@ def main():
     nn.knn_device(dq.data_ptr(), a.queries, a.k, ids.data_ptr(), dd.data_ptr())
     nn.sync()
     f = getattr(abi.lib, "ompl_gpu_probe_counters", None)
-    cnt = (C.c_uint64 * 10)()
+    cnt = (C.c_uint64 * 12)()
 
     def counters():
         if f is None:
-            return [0] * 10
-        f(nn._h, cnt, 10)
+            return [0] * 12
+        f(nn._h, cnt, 12)
         return list(cnt)
 
     c0 = counters()
@@ -57,7 +57,7 @@ def main():
     c1 = counters()
     per = [(y - x) / a.reps for x, y in zip(c0, c1)]
     keys = ["tiles", "tiles_bruteforce", "qscans", "radius_tiles", "radius_qscans", "offers", "bulk_merges",
-            "insertions", "supertile_masks", "super_rounds"]
+            "insertions", "supertile_masks", "super_rounds", "empty_masks", "recheck_skips"]
     out = {"lib": os.path.basename(abi.LIB_PATH), "kernel": name, "kernel_ms": (ms1 - ms0) / max(n1 - n0, 1),
            "per_query": {k: v / a.queries for k, v in zip(keys, per) if v}, "reruns": nn.stats()[1]}
     # spot parity against the exact path on a few queries
