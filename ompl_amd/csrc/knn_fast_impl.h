@@ -644,6 +644,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         for (int j = 0; j < GH; ++j) {
             lb[j] = box_lb<SP, F>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
             need |= lb[j] < (half ? td[GH + j] : td[j]);
+            __builtin_amdgcn_sched_barrier(0);  // one bound at a time (temporaries)
         }
         return fold_tiles(__ballot(need));
     };
@@ -746,51 +747,61 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     uint32_t base = s0 > 0 ? s0 - 1 : 0;
     uint64_t sm = (s0 > 0 ? 7ull : 3ull) & ((nsuper - base >= 64) ? ~0ull : ((1ull << (nsuper - base)) - 1));
     uint32_t sb = 0;
-    // the round's super-tile bounds (lane l: super-tile base + l, one per query): a super-tile
+    // the round's super-tile bounds (slb[g][l]: super-tile base + l, query g): a super-tile
     // popped later is skipped when the thresholds have tightened past all of its bounds since
-    // its round, before its 32 tile boxes are loaded and tested
-    float slb[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) slb[g] = -__builtin_inff();  // the neighbourhood's three: always visited
+    // its round, before its 32 tile boxes are loaded and tested.  Kept in LDS, not VGPRs: G
+    // values live across the whole walk cost 29 VGPRs (69 -> 98, 7 -> 5 waves per SIMD)
+    __shared__ float slb[G][64];
+    bool first_round = true;  // the neighbourhood's three are always visited
     auto next_super = [&]() -> int {  // next super-tile to visit, -1 when done
         for (;;) {
-            while (!sm) {
-                if (sb >= nsuper) return -1;
-                relaunder();
+            if (sm && recheck && !first_round) {  // drop what the tightened thresholds exclude
+                bool keep = false;
+#pragma unroll
+                for (int g = 0; g < G; ++g) keep |= slb[g][lane] < td[g];
 #ifdef OMPL_AMD_PROBE
-                ++pr_rounds;
+                pr_skip += __popcll(sm & ~__ballot(keep));
 #endif
-                const uint32_t s = sb + lane;
-                bool need = false;
-#pragma unroll
-                for (int g = 0; g < G; ++g) slb[g] = __builtin_inff();
-                if (s < nsuper && (s + 1 < s0 || s > s0 + 1)) {
-                    float bx[BW];
-                    const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
-#pragma unroll
-                    for (int c = 0; c < BW / 4; ++c) {
-                        const float4 v = b4[c];
-                        bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
-                    }
-#pragma unroll
-                    for (int g = 0; g < G; ++g) {
-                        slb[g] = box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1);
-                        need |= slb[g] < td[g];
-                    }
-                }
-                sm = __ballot(need);
-                base = sb;
-                sb += 64;
+                sm &= __ballot(keep);
             }
-            const int l = __builtin_ctzll(sm);
-            sm &= sm - 1;
-            bool still = !recheck;
-#pragma unroll
-            for (int g = 0; g < G; ++g) still |= readlane_f(slb[g], l) < td[g];
-            if (still) return (int)(base + l);
+            if (sm) {
+                const int l = __builtin_ctzll(sm);
+                sm &= sm - 1;
+                return (int)(base + l);
+            }
+            if (sb >= nsuper) return -1;
+            relaunder();
 #ifdef OMPL_AMD_PROBE
-            ++pr_skip;
+            ++pr_rounds;
 #endif
+            const uint32_t s = sb + lane;
+            bool need = false;
+            float lbs[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) lbs[g] = __builtin_inff();
+            if (s < nsuper && (s + 1 < s0 || s > s0 + 1)) {
+                float bx[BW];
+                const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
+#pragma unroll
+                for (int c = 0; c < BW / 4; ++c) {
+                    const float4 v = b4[c];
+                    bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    lbs[g] = box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1);
+                    need |= lbs[g] < td[g];
+                    // one query's bound at a time: interleaving the G bounds needs ~40 temporaries
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) slb[g][lane] = lbs[g];
+            __builtin_amdgcn_wave_barrier();  // one wave: its LDS ops complete in order
+            first_round = false;
+            sm = __ballot(need);
+            base = sb;
+            sb += 64;
         }
     };
     // Software pipeline: the tile boxes of the next super-tile are loaded while the current
@@ -798,6 +809,77 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     // a wave keeps its next round trips in flight instead of serialising box -> tile ->
     // box.  The next super-tile's mask is computed on arrival with the thresholds of that
     // moment; every tile is re-checked against the current thresholds before it is scanned.
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 1
+    // Cross-super-tile pipeline: on the last tile of super-tile s the next non-empty
+    // super-tile's mask is computed (its boxes were loaded when s began) and its first tile is
+    // fetched before that last tile is scanned, so no tile fetch waits behind a box bound; the
+    // super-tile after it is popped (a round's box loads included) only after the scan.
+    float bx[BW];
+    const uint32_t home_s = th / kSuperTiles;
+    auto mask_of = [&](int sv, float (&l)[GH]) -> uint32_t {
+        uint32_t mm = tile_mask(bx, l);
+        if ((uint32_t)sv == home_s) mm &= ~(1u << (th % kSuperTiles));  // scanned first
+#ifdef OMPL_AMD_PROBE
+        if (!mm) ++pr_empty;
+#endif
+        return mm;
+    };
+    float lb[GH];
+    float x[R], xn[R];
+    uint32_t id = kNoId, idn = kNoId, m = 0;
+    int t = 0, tn = 0, s = -1;
+    bool have = false;  // x holds a fetched tile of s
+    int sn = next_super();
+    if (sn >= 0) load_tbox((uint32_t)sn, bx);
+    // one site each for the mask, the fetch, the scan and next_super (every inlined copy of
+    // next_super's round adds its box-bound temporaries to the live set of its site)
+    for (;;) {
+        // fetch the next tile (xn) while x is scanned: the next of s, or else the first tile of
+        // sn (bx holds its boxes) when its mask is not empty
+        bool got = false, cross = false, consumed = false;
+        uint32_t mn = 0;
+        float lbn[GH];
+        if (!m && sn >= 0) {
+            mn = mask_of(sn, lbn);
+            consumed = true;
+            cross = mn != 0;
+        }
+        uint32_t &mf = cross ? mn : m;
+        if (mf) {
+            tn = __builtin_ctz(mf);
+            mf &= mf - 1;
+            load_state((uint32_t)(cross ? sn : s) * kSuperTiles + tn, xn, idn);
+            got = true;
+        }
+        if (have) {
+            scan_state(x, id, t, lb);
+            ++visited;
+        }
+        if (cross) {
+            s = sn;
+            m = mn;
+#pragma unroll
+            for (int j = 0; j < GH; ++j) lb[j] = lbn[j];
+        }
+        if (consumed) {  // after the scan: a round's box loads wait behind it, not before
+            sn = next_super();
+            if (sn >= 0) load_tbox((uint32_t)sn, bx);
+        }
+        bool still = false;  // drop the tiles of s that the tightened thresholds exclude
+#pragma unroll
+        for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
+        m &= fold_tiles(__ballot(still));
+        have = got;
+        if (got) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) x[r] = xn[r];
+            id = idn;
+            t = tn;
+        } else if (sn < 0 && !m) {
+            break;
+        }
+    }
+#else
     float bx[BW];
     int s = next_super();
     if (s >= 0) load_tbox((uint32_t)s, bx);
@@ -841,6 +923,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         }
         s = sn;
     }
+#endif
     if (counters && lane == 0) {
         unsigned long long *cs = counters + (blockIdx.x % kCounterSlots) * kCounterStride;
         atomicAdd(&cs[0], (unsigned long long)visited);  // tiles scanned
@@ -1228,7 +1311,9 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
         qrow[t] = qi < nq ? q32[(size_t)qi * FS + t % FS] : __builtin_nanf("");
     }
     __syncthreads();
-    double qv[G][F];
+    // the exact query rows live in LDS (read on a hit, a broadcast): G x F doubles held in
+    // VGPRs for the whole walk cost 2 G F registers (56 for SE3, G = 4)
+    __shared__ double qv[G][F];
     uint32_t qo[G];
     float thr[G];
     uint64_t cur[G];
@@ -1236,119 +1321,180 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
     for (int g = 0; g < G; ++g) {
         const bool live = g0 + g < nq;
         qo[g] = live ? perm[g0 + g] : 0u;
+        double qd[F];
 #pragma unroll
-        for (int f = 0; f < F; ++f) qv[g][f] = live ? qf64[(size_t)qo[g] * F + f] : 0.0;
+        for (int f = 0; f < F; ++f) qd[f] = live ? qf64[(size_t)qo[g] * F + f] : 0.0;
+        if (lane < F) qv[g][lane] = qd[lane < F ? lane : 0];
         double B = absmax;
         const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : F;
-        for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qv[g][c]));
+        for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qd[c]));
         // every element with d <= r has d32 <= r + e; rounding to fp32 is covered by the 16 u
-        const double t = (r + screen_error<SP>(sp, B, r, (double)qeta + query_eta<SP>(qv[g]))) * (1.0 + 16.0 * kU);
+        const double t = (r + screen_error<SP>(sp, B, r, (double)qeta + query_eta<SP>(qd))) * (1.0 + 16.0 * kU);
         thr[g] = live ? (float)t : -__builtin_inff();
         cur[g] = (FILL && live) ? offsets[qo[g]] : 0ull;
     }
+    __syncthreads();
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     uint64_t cnt[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) cnt[g] = 0;
     uint32_t visited = 0, qscans = 0;
-    for (uint32_t sb = 0; sb < nsuper; sb += 64) {
-        const uint32_t s = sb + lane;
-        bool need = false;
-        if (s < nsuper) {
-            float bx[BW];
-            const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
-#pragma unroll
-            for (int c = 0; c < BW / 4; ++c) {
-                const float4 v = b4[c];
-                bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
-            }
-#pragma unroll
-            for (int g = 0; g < G; ++g) need |= box_lb<SP, F>(bx, &qrow[g * FS], w0, w1) <= thr[g];
-        }
-        uint64_t sm = __ballot(need);
-        while (sm) {
-            const uint32_t ss = sb + (uint32_t)__builtin_ctzll(sm);
-            sm &= sm - 1;
-            // this lane's tile (lane & 31) of super-tile ss, bounds for queries half * GH + j
-            const uint32_t tt = ss * kSuperTiles + (lane & 31);
-            float lb[GH];
-            bool tneed = false;
-            if (tt < ntiles) {
+    // re-read the wave-uniform query rows from LDS at every use through an offset the compiler
+    // cannot see through, instead of letting it hoist them into VGPRs for the whole walk
+    uint32_t qoff = 0;
+    // super-tiles whose box comes within some query's bound, 64 box tests per round
+    uint32_t sb = 0, base = 0;
+    uint64_t sm = 0;
+    auto next_super = [&]() -> int {
+        while (!sm) {
+            if (sb >= nsuper) return -1;
+            asm volatile("" : "+s"(qoff));
+            const uint32_t s = sb + lane;
+            bool need = false;
+            if (s < nsuper) {
                 float bx[BW];
-                const float4 *b4 = reinterpret_cast<const float4 *>(tbox + (size_t)tt * BW);
+                const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
 #pragma unroll
                 for (int c = 0; c < BW / 4; ++c) {
                     const float4 v = b4[c];
                     bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
                 }
 #pragma unroll
-                for (int j = 0; j < GH; ++j) {
-                    lb[j] = box_lb<SP, F>(bx, &qrow[(half * GH + j) * FS], w0, w1);
-                    tneed |= lb[j] <= (half ? thr[GH + j] : thr[j]);
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < GH; ++j) lb[j] = __builtin_inff();
-            }
-            uint32_t m = fold_tiles(__ballot(tneed));
-            while (m) {
-                const int t = __builtin_ctz(m);
-                m &= m - 1;
-                const uint64_t p = (uint64_t)(ss * kSuperTiles + t) * kCullTile + lane;
-                float x[R];
-#pragma unroll
-                for (int rr = 0; rr < R; ++rr) x[rr] = rows[(uint64_t)rr * n_pad + p];
-                const uint32_t id = ids[p];
-                ++visited;
-#pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    if (!(readlane_f(lb[g % GH], t + (g < GH ? 0 : 32)) <= thr[g])) continue;
-                    ++qscans;
-                    bool hit;  // NaN never hits
-                    if constexpr (SP == OMPL_GPU_SPACE_SE3) {  // chord bound first, as in the kNN walk
-                        const float *qq = &qrow[g * FS];
-                        const float dx = x[0] - qq[0], dy = x[1] - qq[1], dz = x[2] - qq[2];
-                        float tt = dx * dx;
-                        tt = fmaf(dy, dy, tt);
-                        tt = fmaf(dz, dz, tt);
-                        const float c2 = chord2(x + 3, qq + 4);
-                        const float c = __builtin_amdgcn_sqrtf(c2), wt = w0 * __builtin_amdgcn_sqrtf(tt);
-                        hit = __ballot(fmaf(w1, c, wt) <= thr[g]) && fmaf(w1, chord_theta(c, c2), wt) <= thr[g];
-                    } else {
-                        hit = state_dist32<SP, F>(x, &qrow[g * FS], w0, w1) <= thr[g];
-                    }
-                    double dd = 0.0;
-                    if (hit) {  // exact decision from the sorted fp64 row (coalesced over the tile)
-                        constexpr int FA = (F + 3) & ~3;
-                        double sv[F];
-                        const double2 *r2 = reinterpret_cast<const double2 *>(rows64 + p * FA);
-#pragma unroll
-                        for (int c = 0; c < FA / 2; ++c) {
-                            const double2 v = r2[c];
-                            if (2 * c < F) sv[2 * c] = v.x;
-                            if (2 * c + 1 < F) sv[2 * c + 1] = v.y;
-                        }
-                        dd = feat_dist<SP, F, 0>(sv, qv[g], sp);
-                        hit = dd <= r;
-                    }
-                    const uint64_t bm = __ballot(hit);
-                    if (FILL && hit) {
-                        const uint64_t pos = cur[g] + (uint64_t)__popcll(bm & lt);
-                        out_i[pos] = id;
-                        out_d[pos] = dd;
-                    }
-                    if (SLAB && hit) {
-                        const uint64_t j = cnt[g] + (uint64_t)__popcll(bm & lt);
-                        if (j < slab) {
-                            out_i[(uint64_t)qo[g] * slab + j] = id;
-                            out_d[(uint64_t)qo[g] * slab + j] = dd;
-                        }
-                    }
-                    cur[g] += (uint64_t)__popcll(bm);
-                    cnt[g] += (uint64_t)__popcll(bm);
+                    need |= box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1) <= thr[g];
+                    __builtin_amdgcn_sched_barrier(0);  // one bound at a time (temporaries)
                 }
             }
+            sm = __ballot(need);
+            base = sb;
+            sb += 64;
         }
+        const int l = __builtin_ctzll(sm);
+        sm &= sm - 1;
+        return (int)(base + l);
+    };
+    // this lane's row of super-tile ss's tile boxes (tile ss * 32 + (lane & 31)); rows past the
+    // last tile read as empty boxes (bound +inf)
+    auto load_tbox = [&](uint32_t ss, float (&bx)[BW]) {
+        const uint32_t tt = ss * kSuperTiles + (lane & 31);
+        if (tt < ntiles) {
+            const float4 *b4 = reinterpret_cast<const float4 *>(tbox + (size_t)tt * BW);
+#pragma unroll
+            for (int c = 0; c < BW / 4; ++c) {
+                const float4 v = b4[c];
+                bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < BW; ++c) bx[c] = c < Geo<SP, F>::NB ? __builtin_inff() : -__builtin_inff();
+            if constexpr (SP == OMPL_GPU_SPACE_SE3) bx[2 * Geo<SP, F>::NB] = bx[2 * Geo<SP, F>::NB + 1] = 0.f;
+        }
+    };
+    auto load_tile = [&](uint32_t ss, int t, float (&x)[R], uint32_t &id) {
+        const uint64_t p = (uint64_t)(ss * kSuperTiles + t) * kCullTile + lane;
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) x[rr] = rows[(uint64_t)rr * n_pad + p];
+        id = ids[p];
+    };
+    auto scan_tile = [&](uint32_t ss, int t, const float (&x)[R], uint32_t id, const float (&lb)[GH]) {
+        asm volatile("" : "+s"(qoff));
+        const uint64_t p = (uint64_t)(ss * kSuperTiles + t) * kCullTile + lane;
+        ++visited;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            if (!(readlane_f(lb[g % GH], t + (g < GH ? 0 : 32)) <= thr[g])) continue;
+            ++qscans;
+            bool hit;  // NaN never hits
+            if constexpr (SP == OMPL_GPU_SPACE_SE3) {  // chord bound first, as in the kNN walk
+                const float *qq = &qrow[qoff + g * FS];
+                const float dx = x[0] - qq[0], dy = x[1] - qq[1], dz = x[2] - qq[2];
+                float tt = dx * dx;
+                tt = fmaf(dy, dy, tt);
+                tt = fmaf(dz, dz, tt);
+                const float c2 = chord2(x + 3, qq + 4);
+                const float c = __builtin_amdgcn_sqrtf(c2), wt = w0 * __builtin_amdgcn_sqrtf(tt);
+                hit = __ballot(fmaf(w1, c, wt) <= thr[g]) && fmaf(w1, chord_theta(c, c2), wt) <= thr[g];
+            } else {
+                hit = state_dist32<SP, F>(x, &qrow[qoff + g * FS], w0, w1) <= thr[g];
+            }
+            double dd = 0.0;
+            if (hit) {  // exact decision from the sorted fp64 row (coalesced over the tile)
+                constexpr int FA = (F + 3) & ~3;
+                double sv[F];
+                const double2 *r2 = reinterpret_cast<const double2 *>(rows64 + p * FA);
+#pragma unroll
+                for (int c = 0; c < FA / 2; ++c) {
+                    const double2 v = r2[c];
+                    if (2 * c < F) sv[2 * c] = v.x;
+                    if (2 * c + 1 < F) sv[2 * c + 1] = v.y;
+                }
+                double qd[F];
+#pragma unroll
+                for (int f = 0; f < F; ++f) qd[f] = (&qv[0][0])[qoff + g * F + f];
+                dd = feat_dist<SP, F, 0>(sv, qd, sp);
+                hit = dd <= r;
+            }
+            const uint64_t bm = __ballot(hit);
+            if (FILL && hit) {
+                const uint64_t pos = cur[g] + (uint64_t)__popcll(bm & lt);
+                out_i[pos] = id;
+                out_d[pos] = dd;
+            }
+            if (SLAB && hit) {
+                const uint64_t j = cnt[g] + (uint64_t)__popcll(bm & lt);
+                if (j < slab) {
+                    out_i[(uint64_t)qo[g] * slab + j] = id;
+                    out_d[(uint64_t)qo[g] * slab + j] = dd;
+                }
+            }
+            cur[g] += (uint64_t)__popcll(bm);
+            cnt[g] += (uint64_t)__popcll(bm);
+        }
+    };
+    // Software pipeline (the bound is fixed, so nothing waits on a result): the next tile is
+    // fetched while the current one is scanned, and the next super-tile's tile boxes while the
+    // current super-tile's tiles are; tiles are visited in the same order as before, so FILL
+    // writes each CSR segment in tile order.
+    float bx[BW];
+    int ss = next_super();
+    if (ss >= 0) load_tbox((uint32_t)ss, bx);
+    while (ss >= 0) {
+        float lb[GH];
+        bool tneed = false;
+        asm volatile("" : "+s"(qoff));
+#pragma unroll
+        for (int j = 0; j < GH; ++j) {
+            lb[j] = box_lb<SP, F>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
+            tneed |= lb[j] <= (half ? thr[GH + j] : thr[j]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        uint32_t m = fold_tiles(__ballot(tneed));
+        float x[R], xn[R];
+        uint32_t id = 0, idn = 0;
+        int t = 0, tn = 0;
+        const bool have = m != 0;
+        if (have) {
+            t = __builtin_ctz(m);
+            m &= m - 1;
+            load_tile((uint32_t)ss, t, x, id);
+        }
+        const int ssn = next_super();
+        if (ssn >= 0) load_tbox((uint32_t)ssn, bx);
+        while (have) {
+            const bool more = m != 0;
+            if (more) {
+                tn = __builtin_ctz(m);
+                m &= m - 1;
+                load_tile((uint32_t)ss, tn, xn, idn);
+            }
+            scan_tile((uint32_t)ss, t, x, id, lb);
+            if (!more) break;
+#pragma unroll
+            for (int rr = 0; rr < R; ++rr) x[rr] = xn[rr];
+            id = idn;
+            t = tn;
+        }
+        ss = ssn;
     }
     if (lane == 0) {
         if (!FILL) {
