@@ -718,6 +718,13 @@ class Runner:
             dt = "f32"
             what = (f"{pairs:.4g} (query, state) fp32 distance evaluations per launch x {flop} flop (SURVEY §8d); "
                     f"the culled walk scanned {pairs / (float(nq) * n):.4%} of the {nq} x {n} pairs")
+        elif kern_name == "knn32_chain_cull_kernel":
+            pairs = (after["kq"] - before["kq"]) * 64 / launches
+            flop, dt = F_CHAIN, "f32"
+            what = (f"{pairs:.4g} (query, state) fp32 chain distances per launch x {F_CHAIN} flop (SURVEY §8d); the "
+                    f"culled chain scan evaluated {pairs / (float(nq) * n):.4%} of the {nq} x {n} pairs, each counted "
+                    "at the full 84 flop although a wave leaves a pair's remaining links once no lane's partial sum is "
+                    "below its threshold (an upper bound of the work done)")
         else:  # brute-force scans (exact fp64 tiled kernel, or the chunked fp32 screen)
             pairs = float(nq) * n
             flop = {"cfg3": F_SE3, "cfg2": F_L2_6, "cfg4": F_CHAIN, "cfg5": F_SE3}[wl]

@@ -666,7 +666,7 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
         HIP_OR_FAIL(hipMemsetAsync(d_qoff, 0, sizeof(uint64_t) * (nq + 1), h->stream));
         return OMPL_GPU_OK;
     }
-    if (h->fast && h->cull && cull_supported(h->sp) && nq <= 0x7FFFFFFFull && screen_safe(h) && r < kScreenMaxAbs) {
+    if (h->fast && h->cull && radius_cull_supported(h->sp) && nq <= 0x7FFFFFFFull && screen_safe(h) && r < kScreenMaxAbs) {
         // culled walk over the Morton-sorted copy (knn_fast_impl.h)
         ompl_gpu_status s = ensure_sorted(h);
         if (s != OMPL_GPU_OK) return s;
@@ -694,8 +694,8 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
         *total = tm[0];
         if (tm[0] == 0) return OMPL_GPU_OK;
         if (tm[0] > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "radius result above 2^31 entries");
-        const uint64_t tot = tm[0];
         if (tm[1] <= slab) {  // every segment is complete in its slab: sort into the CSR result
+            const uint64_t tot = tm[0];
             h->radius_one_pass += 1;
             HIP_OR_FAIL(h->sorted_ids.ensure(sizeof(uint32_t) * tot));
             HIP_OR_FAIL(h->sorted_d.ensure(sizeof(double) * tot));
@@ -707,6 +707,17 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
             *res_d = sd;
             return OMPL_GPU_OK;
         }
+        // a slab overflowed: its query's count is a candidate count (the exact decisions run on
+        // the slab), so recount exactly with the count walk before the fill walk
+        HIP_OR_FAIL(launch_radius_fast(h->sp, h->g, h->feat, h->cap, &h->sorted, d_qf, (uint32_t)nq, r, b, h->ws.p,
+                                       h->ws.bytes, 0, &d_off, nullptr, nullptr, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(tm, d_off + nq, sizeof(tm), hipMemcpyDeviceToHost, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(d_qoff, d_off, sizeof(uint64_t) * (nq + 1), hipMemcpyDeviceToDevice, h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+        *total = tm[0];
+        if (tm[0] == 0) return OMPL_GPU_OK;
+        if (tm[0] > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "radius result above 2^31 entries");
+        const uint64_t tot = tm[0];
         uint32_t grow = 16;
         while (grow < tm[1] && grow < kRankSortMax) grow <<= 1;
         h->radius_slab = grow;  // the next call's slab holds this call's longest segment

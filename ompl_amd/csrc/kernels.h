@@ -122,6 +122,7 @@ struct SortedStore {
     unsigned long long *counters = nullptr;
 };
 bool cull_supported(const DevSpace &sp);
+bool radius_cull_supported(const DevSpace &sp);  // the culled radius walk (SE3, R^n)
 // full device build of the sorted copy over the live ids of [0, n_total) (live[id] != 0, n_live
 // of them); asynchronous on st
 hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, const double *feat64,

@@ -12,7 +12,7 @@ namespace ompl_amd {
 int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq, bool cull) {
     if (nq < kStreamMaxQ || k == 0) return 0;
     const int K = k_bucket(k);
-    if (cull && cull_supported(sp)) {
+    if (cull && cull_supported(sp) && sp.kind != OMPL_GPU_SPACE_KCHAIN) {
         if (K == 0 || k + 3 > 64) return 0;
         const int K2 = k_bucket(k + 3);
         return K2 < 16 ? 16 : K2;
@@ -33,7 +33,12 @@ hipError_t launch_rows32(const DevSpace &sp, const FeatGeom &g, const double *fe
     return launch_to_fp32(feat64, cap, g.F, first, n, feat32, st);
 }
 
+// spaces with a k-d sorted store: the SE3 / R^n group walks (kNN and radius) and the
+// KinematicChain culled scan (kNN only: radius_cull_supported)
 bool cull_supported(const DevSpace &sp) {
+    return sp.kind == OMPL_GPU_SPACE_SE3 || sp.kind == OMPL_GPU_SPACE_REALVECTOR || sp.kind == OMPL_GPU_SPACE_KCHAIN;
+}
+bool radius_cull_supported(const DevSpace &sp) {
     return sp.kind == OMPL_GPU_SPACE_SE3 || sp.kind == OMPL_GPU_SPACE_REALVECTOR;
 }
 
@@ -64,6 +69,7 @@ hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float
     switch (sp.kind) {
     case OMPL_GPU_SPACE_SE3: return fast_se3_build(g, feat32, feat64, cap, n_total, n_live, live, s, st);
     case OMPL_GPU_SPACE_REALVECTOR: return fast_rv_build(g, feat32, feat64, cap, n_total, n_live, live, s, st);
+    case OMPL_GPU_SPACE_KCHAIN: return fast_chain_build(g, feat32, feat64, cap, n_total, n_live, live, s, st);
     }
     return hipErrorInvalidValue;
 }
@@ -74,6 +80,7 @@ hipError_t append_sorted_store(const DevSpace &sp, const FeatGeom &g, const floa
     switch (sp.kind) {
     case OMPL_GPU_SPACE_SE3: return fast_se3_append(g, feat32, feat64, cap, n_total, b, s, st, fits);
     case OMPL_GPU_SPACE_REALVECTOR: return fast_rv_append(g, feat32, feat64, cap, n_total, b, s, st, fits);
+    case OMPL_GPU_SPACE_KCHAIN: return fast_chain_append(g, feat32, feat64, cap, n_total, b, s, st, fits);
     }
     *fits = false;
     return hipErrorInvalidValue;
@@ -101,7 +108,7 @@ hipError_t launch_knn_fast(const DevSpace &sp, const FeatGeom &g, const double *
         return fast_rv(sp, g, feat64, feat32, cap, n_end, sorted, qfeat64, nq, k, b, out_d, out_i, ws, ws_bytes,
                        num_cus, st, fail_count, fail_list);
     case OMPL_GPU_SPACE_KCHAIN:
-        return fast_chain(sp, g, feat64, feat32, cap, n_end, nullptr, qfeat64, nq, k, b, out_d, out_i, ws, ws_bytes,
+        return fast_chain(sp, g, feat64, feat32, cap, n_end, sorted, qfeat64, nq, k, b, out_d, out_i, ws, ws_bytes,
                           num_cus, st, fail_count, fail_list);
     }
     return hipErrorInvalidValue;

@@ -7,11 +7,11 @@
 namespace ompl_amd {
 
 hipError_t fast_chain(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32, uint64_t cap,
-                      uint64_t n_end, const SortedStore *, const double *qfeat64, uint32_t nq, uint32_t k,
+                      uint64_t n_end, const SortedStore *sorted, const double *qfeat64, uint32_t nq, uint32_t k,
                       const FastBounds &b, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes, int num_cus,
                       hipStream_t st, uint32_t **fail_count, uint32_t **fail_list) {
 #define OMPL_AMD_CHAIN(FF)                                                                                      \
-    return fast_entry<OMPL_GPU_SPACE_KCHAIN, FF>(sp, g, feat64, feat32, cap, n_end, nullptr, qfeat64, nq, k, b, \
+    return fast_entry<OMPL_GPU_SPACE_KCHAIN, FF>(sp, g, feat64, feat32, cap, n_end, sorted, qfeat64, nq, k, b,  \
                                                  out_d, out_i, ws, ws_bytes, num_cus, st, fail_count, fail_list)
     if (g.F == 8) OMPL_AMD_CHAIN(8);
     if (g.F == 16) OMPL_AMD_CHAIN(16);
@@ -20,9 +20,27 @@ hipError_t fast_chain(const DevSpace &sp, const FeatGeom &g, const double *feat6
 #undef OMPL_AMD_CHAIN
 }
 
-hipError_t fast_chain_build(const FeatGeom &, const float *, uint64_t, uint32_t, const FastBounds &, SortedStore *,
-                            hipStream_t) {
-    return hipErrorInvalidValue;
+// k-d sorted store of the joint positions (the culled chain scan, knn32_chain_cull_kernel)
+hipError_t fast_chain_build(const FeatGeom &g, const float *feat32, const double *feat64, uint64_t cap,
+                            uint64_t n_total, uint32_t n_live, const uint8_t *live, SortedStore *s, hipStream_t st) {
+#define OMPL_AMD_CHAIN_B(FF) \
+    return build_sorted<OMPL_GPU_SPACE_KCHAIN, FF>(feat32, feat64, cap, n_total, n_live, live, s, st)
+    if (g.F == 8) OMPL_AMD_CHAIN_B(8);
+    if (g.F == 16) OMPL_AMD_CHAIN_B(16);
+    if (g.F == 24) OMPL_AMD_CHAIN_B(24);
+    OMPL_AMD_CHAIN_B(32);
+#undef OMPL_AMD_CHAIN_B
+}
+
+hipError_t fast_chain_append(const FeatGeom &g, const float *feat32, const double *feat64, uint64_t cap,
+                             uint64_t n_total, const FastBounds &b, SortedStore *s, hipStream_t st, bool *fits) {
+#define OMPL_AMD_CHAIN_A(FF) \
+    return append_sorted<OMPL_GPU_SPACE_KCHAIN, FF>(feat32, feat64, cap, n_total, b, s, st, fits)
+    if (g.F == 8) OMPL_AMD_CHAIN_A(8);
+    if (g.F == 16) OMPL_AMD_CHAIN_A(16);
+    if (g.F == 24) OMPL_AMD_CHAIN_A(24);
+    OMPL_AMD_CHAIN_A(32);
+#undef OMPL_AMD_CHAIN_A
 }
 
 hipError_t fast_chain_radius(const DevSpace &, const FeatGeom &, const double *, uint64_t, const SortedStore *,

@@ -164,8 +164,8 @@ __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, Fa
         for (int d = 0; d < b.nkey; ++d) x[d] = o[d];
     }
     for (int f = 0; f < FS; ++f) q32u[(size_t)i * FS + f] = o[f];
-    if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
-        keys[i] = 0u;  // no spatial order for the chain metric (no culled walk)
+    if (SP == OMPL_GPU_SPACE_KCHAIN && !(nodes && ntiles > 1)) {
+        keys[i] = 0u;  // no sorted store: the brute-force wave scan needs no order
     } else if (nodes && ntiles > 1) {
         // order by home leaf: the box coordinates, quaternion sign-canonical as in the store
         float c[Geo<SP, F>::NB];
@@ -414,7 +414,9 @@ __global__ __launch_bounds__(256) void knn32_screen_kernel(const float *__restri
 // 20% slower for the radius walk, whose register allocation it upsets.)
 __device__ __forceinline__ float gap(float a, float b) { return fmaxf(fmaxf(a, b), 0.f); }
 
-template <int SP, int F>
+// SCHED: translation and rotation gaps as two scheduling regions (fewer live temporaries: the
+// kNN walk's pipelined loop stays at 7 waves per SIMD; the radius walk is faster without)
+template <int SP, int F, bool SCHED = false>
 __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w0, float w1) {
     constexpr int NB = Geo<SP, F>::NB;
     if constexpr (SP == OMPL_GPU_SPACE_SE3) {
@@ -424,6 +426,7 @@ __device__ __forceinline__ float box_lb(const float *bx, const float *q, float w
             const float g = gap(bx[c] - q[c], q[c] - bx[NB + c]);
             tg = fmaf(g, g, tg);
         }
+        if constexpr (SCHED) __builtin_amdgcn_sched_barrier(0);
         // rotation: the screened 2 asin(c / 2) >= c = min(|p - q|, |p + q|) >= the distance
         // from q or from -q to the box (state_dist32)
         float rp = 0.f, rm = 0.f;
@@ -642,7 +645,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         bool need = false;
 #pragma unroll
         for (int j = 0; j < GH; ++j) {
-            lb[j] = box_lb<SP, F>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
+            lb[j] = box_lb<SP, F, true>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
             need |= lb[j] < (half ? td[GH + j] : td[j]);
             __builtin_amdgcn_sched_barrier(0);  // one bound at a time (temporaries)
         }
@@ -789,7 +792,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
                 }
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    lbs[g] = box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1);
+                    lbs[g] = box_lb<SP, F, true>(bx, &qrow[qoff + g * FS], w0, w1);
                     need |= lbs[g] < td[g];
                     // one query's bound at a time: interleaving the G bounds needs ~40 temporaries
                     __builtin_amdgcn_sched_barrier(0);
@@ -804,16 +807,13 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             sb += 64;
         }
     };
-    // Software pipeline: the tile boxes of the next super-tile are loaded while the current
-    // one is scanned, and the first tile of a super-tile is fetched before those boxes, so
-    // a wave keeps its next round trips in flight instead of serialising box -> tile ->
-    // box.  The next super-tile's mask is computed on arrival with the thresholds of that
-    // moment; every tile is re-checked against the current thresholds before it is scanned.
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 1
-    // Cross-super-tile pipeline: on the last tile of super-tile s the next non-empty
-    // super-tile's mask is computed (its boxes were loaded when s began) and its first tile is
-    // fetched before that last tile is scanned, so no tile fetch waits behind a box bound; the
-    // super-tile after it is popped (a round's box loads included) only after the scan.
+    // Software pipeline: the tile boxes of the next super-tile sn are loaded while the tiles
+    // of s are scanned, and the next tile is always fetched before the current one is scanned
+    // — within s, and across the boundary: on the last tile of s, sn's mask is computed (its
+    // boxes arrived meanwhile) and its first tile fetched, so no tile fetch waits behind a box
+    // bound; the super-tile after sn is popped (a round's box loads included) only after that
+    // scan.  Masks use the thresholds of their moment; every tile is re-checked against the
+    // current thresholds before it is scanned.  (Measured: 1.27-1.29 -> 1.25-1.26 ms on cfg3.)
     float bx[BW];
     const uint32_t home_s = th / kSuperTiles;
     auto mask_of = [&](int sv, float (&l)[GH]) -> uint32_t {
@@ -851,8 +851,8 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             load_state((uint32_t)(cross ? sn : s) * kSuperTiles + tn, xn, idn);
             got = true;
         }
-        if (have) {
-            scan_state(x, id, t, lb);
+        if (have) {  // the list ids are sorted positions: recomputed, not carried in a VGPR
+            scan_state(x, ((uint32_t)s * kSuperTiles + (uint32_t)t) * kCullTile + (uint32_t)lane, t, lb);
             ++visited;
         }
         if (cross) {
@@ -879,51 +879,6 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             break;
         }
     }
-#else
-    float bx[BW];
-    int s = next_super();
-    if (s >= 0) load_tbox((uint32_t)s, bx);
-    while (s >= 0) {
-        float lb[GH];
-        uint32_t m = tile_mask(bx, lb);
-        if ((uint32_t)s == th / kSuperTiles) m &= ~(1u << (th % kSuperTiles));  // scanned first
-#ifdef OMPL_AMD_PROBE
-        if (!m) ++pr_empty;
-#endif
-        const int sn = next_super();
-        float x[R], xn[R];
-        uint32_t id = kNoId, idn = kNoId;
-        int t = 0, tn = 0;
-        const bool have = m != 0;
-        if (have) {
-            t = __builtin_ctz(m);
-            m &= m - 1;
-            load_state((uint32_t)s * kSuperTiles + t, x, id);
-        }
-        if (sn >= 0) load_tbox((uint32_t)sn, bx);  // prefetch: bx is dead once lb / m exist
-        while (have) {
-            const bool more = m != 0;
-            if (more) {  // prefetch the next tile while this one is scanned
-                tn = __builtin_ctz(m);
-                m &= m - 1;
-                load_state((uint32_t)s * kSuperTiles + tn, xn, idn);
-            }
-            scan_state(x, id, t, lb);
-            ++visited;
-            // drop the remaining tiles that the tightened thresholds exclude
-            bool still = false;
-#pragma unroll
-            for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
-            m &= fold_tiles(__ballot(still));
-            if (!more) break;
-#pragma unroll
-            for (int r = 0; r < R; ++r) x[r] = xn[r];
-            id = idn;
-            t = tn;
-        }
-        s = sn;
-    }
-#endif
     if (counters && lane == 0) {
         unsigned long long *cs = counters + (blockIdx.x % kCounterSlots) * kCounterStride;
         atomicAdd(&cs[0], (unsigned long long)visited);  // tiles scanned
@@ -956,6 +911,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 // positions, chain_positions), and query g's K2-list lives across the wave (lane j = entry j).
 // The store is split in chunks along grid.y; the certificate merges the chunk lists.
 constexpr int kWaveGroup = 8;
+constexpr int kChainCullG = 8;  // queries per wave of the culled chain scan
 
 // ORD 0: links in the reference's order, the wave-wide exit tested after links 4 and 8; ORD 1:
 // outermost links first (|P_i(a) - P_i(b)| grows with i, so the partial sum nears the distance
@@ -1091,6 +1047,217 @@ __global__ __launch_bounds__(64 * WPB) void knn32_wave_scan_kernel(const float *
 constexpr double kFltMin = 1.1754943508222875e-38;
 
 // eta: |norm^2 - 1| of the stored quaternions (largest) plus the query's (SE3)
+// Merge of the S chunk lists of a query (each sorted, K2 <= 64 entries) into one list of the
+// K2 best by (distance, id), written over chunk 0's slots: a wave per query, one bitonic merge
+// per further chunk (wave_merge_sorted_k).  The culled chain scan's lists then take the wave
+// certificate (a lane per candidate) instead of the thread-per-query one.
+template <int K2>
+__global__ __launch_bounds__(256) void knn_chunk_merge_kernel(float *__restrict__ pd, uint32_t *__restrict__ pi,
+                                                              uint32_t S, uint32_t nq) {
+    const uint32_t qs = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (qs >= nq) return;  // uniform over the wave
+    auto entry = [&](uint32_t c) -> uint64_t {
+        if (lane >= K2) return kMaxKey;
+        const size_t o = ((size_t)c * nq + qs) * K2 + lane;
+        const uint32_t id = pi[o];
+        return id == kNoId ? kMaxKey : kpack(pd[o], id);
+    };
+    uint64_t L = entry(0);
+    for (uint32_t c = 1; c < S; ++c) wave_merge_sorted_k(L, entry(c), lane);
+    if (lane < K2) {
+        const size_t o = (size_t)qs * K2 + lane;
+        pd[o] = L == kMaxKey ? __builtin_inff() : kdist(L);
+        pi[o] = L == kMaxKey ? kNoId : (uint32_t)L;
+    }
+}
+
+// ---- culled KinematicChain scan --------------------------------------------------------------
+// PRM*'s kNN on the chain metric (demos/KinematicChain.h:105-124 = link * sum_i |P_i(a) - P_i(b)|
+// over the joint positions P_i; ConnectionStrategy.h:145-149 sets k) over the k-d sorted store of
+// joint positions (the same device build as SE3 / R^n, boxes over all 2 NM position
+// coordinates).  A tile's box bounds the distance of each of its states from below by
+// link * sum_i dist(P_i(q), box_i) (each term is >= the distance from P_i(q) to the 2-D box of
+// the P_i), so a tile whose bound is not below a query's threshold cannot change its list.
+// One wave serves G queries adjacent in k-d order (sorted by home tile) over one chunk of tiles
+// (grid.y; the certificate merges the chunk lists, as for the brute-force wave scan):
+//   1. threshold: the G queries scan the 4 tiles around the middle query's home tile; each
+//      query's tau = the K2-th smallest screened distance there.  At least K2 stored states
+//      have d32 <= tau, so the K2 best of all stored states have d32 <= tau: every chunk keeps
+//      only keys <= (tau, max id) and the merged lists are still the exact K2 best (those home
+//      tiles belong to some chunk, so the merge is full).  The lists are then emptied.
+//   2. the chunk's tiles in blocks of 64 (lane = tile): box bounds of the G queries, one ballot
+//      per query; the passing tiles are fetched (lane = state) and scanned for every query whose
+//      own bound is still below its threshold, with the wave scan's outer-links-first partial
+//      sums and wave-wide early exit.
+// Lists hold original ids (the chunked certificate reads the fp64 features by id).
+template <int F, int K2, int G>
+__global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
+    const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
+    const float *__restrict__ tbox, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys, uint32_t nq,
+    uint32_t chunk_tiles, float link, int nlinks, float *__restrict__ pd, uint32_t *__restrict__ pi,
+    unsigned long long *__restrict__ counters) {
+    constexpr int NM = F / 2;
+    static_assert(K2 <= 64 && NM % 2 == 0, "chain cull shape");
+    __shared__ __attribute__((aligned(16))) float qrow[G * F];
+    const int lane = threadIdx.x;
+    const uint32_t g0 = blockIdx.x * G;
+    for (int t = lane; t < G * F; t += 64) {
+        const uint32_t qi = g0 + t / F;
+        qrow[t] = qi < nq ? q32[(size_t)qi * F + t % F] : __builtin_nanf("");
+    }
+    __syncthreads();
+    uint32_t qoff = 0;  // re-read the wave-uniform query rows from LDS (see knn32_group_kernel)
+    uint64_t Lk[G];
+    float td[G];
+    uint64_t tk[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        Lk[g] = kMaxKey;
+        td[g] = g0 + g < nq ? __builtin_inff() : -__builtin_inff();
+        tk[g] = g0 + g < nq ? kMaxKey : 0ull;
+    }
+    uint64_t tauk[G];  // the chunk-independent key bound (phase 1)
+    auto offer = [&](int g, float d, uint32_t id) {
+        uint64_t bm = __ballot(d < td[g]);
+        const uint64_t mk = kpack(d, id);
+        while (bm) {
+            const int l = __builtin_ctzll(bm);
+            bm &= bm - 1;
+            const uint64_t ck = readlane_k(mk, l);
+            if (ck < tk[g]) {
+                const uint64_t pv = shr1_k(Lk[g], 0ull);
+                const bool lt_prev = lane > 0 && ck < pv;
+                Lk[g] = lt_prev ? pv : (ck < Lk[g] ? ck : Lk[g]);
+                const uint64_t lk = readlane_k(Lk[g], K2 - 1);
+                if (lk < tk[g]) {
+                    tk[g] = lk;
+                    td[g] = kdist(lk);
+                }
+            }
+        }
+    };
+    uint32_t visited = 0, qscans = 0;
+    auto load_tile = [&](uint32_t t, float (&x)[F]) {
+        const uint64_t p = (uint64_t)t * kCullTile + lane;
+#pragma unroll
+        for (int f = 0; f < F; ++f) x[f] = rows[(uint64_t)f * n_pad + p];
+    };
+    // query g against the lane's state x, outermost links first (|P_i(a) - P_i(b)| grows with
+    // i), the wave leaving as soon as no lane's partial sum is below the threshold
+    auto scan = [&](int g, const float (&x)[F], uint32_t id) {
+        ++qscans;
+        const float *qq = &qrow[qoff + g * F];
+        float acc = 0.f;
+#pragma unroll
+        for (int s = 0; s < NM; s += 2) {
+            const int i = NM - 2 - s;
+            if (i < nlinks) {
+                const f2 dx = f2{x[i], x[i + 1]} - f2{qq[i], qq[i + 1]};
+                const f2 dy = f2{x[NM + i], x[NM + i + 1]} - f2{qq[NM + i], qq[NM + i + 1]};
+                const f2 s2 = pk_fma(dy, dy, dx * dx);
+                acc += __builtin_amdgcn_sqrtf(s2.x);
+                if (i + 1 < nlinks) acc += __builtin_amdgcn_sqrtf(s2.y);
+            }
+            if (s + 2 < NM && !__ballot(acc * link < td[g])) return;
+        }
+        offer(g, acc * link, id);
+    };
+    // 1. thresholds from the home neighbourhood
+    {
+        const uint32_t key = qkeys[min(g0 + G / 2, nq - 1)];
+        const uint32_t h = min(key, ntiles - 1);
+        const uint32_t t0 = h > 0 ? h - 1 : 0, t1 = min(t0 + 4, ntiles);
+        for (uint32_t t = t0; t < t1; ++t) {
+            float x[F];
+            load_tile(t, x);
+            const uint32_t id = ids[(uint64_t)t * kCullTile + lane];
+            asm volatile("" : "+s"(qoff));
+#pragma unroll
+            for (int g = 0; g < G; ++g) scan(g, x, id);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            // tau = the K2-th screened distance (+inf when fewer live states): keys <= (tau, max)
+            const float tau = kdist(readlane_k(Lk[g], K2 - 1));
+            tauk[g] = g0 + g < nq ? kpack(tau, 0xFFFFFFFFu) : 0ull;
+            Lk[g] = kMaxKey;
+            tk[g] = tauk[g];
+            // the next float above tau (tau >= 0 or +inf): a distance equal to tau still passes
+            const float up = tau < __builtin_inff() ? __uint_as_float(__float_as_uint(tau) + 1u) : tau;
+            td[g] = g0 + g < nq ? up : -__builtin_inff();
+        }
+    }
+    // 2. the chunk's tiles
+    const uint32_t c0 = blockIdx.y * chunk_tiles, c1 = min(c0 + chunk_tiles, ntiles);
+    for (uint32_t tb = c0; tb < c1; tb += 64) {
+        const uint32_t t = tb + lane;
+        float lb[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) lb[g] = t < c1 ? 0.f : __builtin_inff();
+        asm volatile("" : "+s"(qoff));
+        if (t < c1) {
+            const float *bx = tbox + (size_t)t * (2 * F);
+#pragma unroll
+            for (int i = 0; i < NM; i += 2) {
+                if (i < nlinks) {
+                    const float2 lx = *reinterpret_cast<const float2 *>(bx + i);
+                    const float2 ly = *reinterpret_cast<const float2 *>(bx + NM + i);
+                    const float2 hx = *reinterpret_cast<const float2 *>(bx + F + i);
+                    const float2 hy = *reinterpret_cast<const float2 *>(bx + F + NM + i);
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        const float *qq = &qrow[qoff + g * F];
+                        const float ax = gap(lx.x - qq[i], qq[i] - hx.x), ay = gap(ly.x - qq[NM + i], qq[NM + i] - hy.x);
+                        lb[g] += __builtin_amdgcn_sqrtf(fmaf(ay, ay, ax * ax));
+                        if (i + 1 < nlinks) {
+                            const float bx2 = gap(lx.y - qq[i + 1], qq[i + 1] - hx.y);
+                            const float by2 = gap(ly.y - qq[NM + i + 1], qq[NM + i + 1] - hy.y);
+                            lb[g] += __builtin_amdgcn_sqrtf(fmaf(by2, by2, bx2 * bx2));
+                        }
+                    }
+                }
+            }
+            // the sum of the per-link bounds rounds like the distance's own sum (monotone in its
+            // terms): shave (n + 2) u off so that the bound stays below every screened distance
+#pragma unroll
+            for (int g = 0; g < G; ++g) lb[g] = lb[g] * link * (1.f - 4e-6f);
+        }
+        uint64_t need = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) need |= __ballot(lb[g] < td[g]);
+        while (need) {
+            const int l = __builtin_ctzll(need);
+            need &= need - 1;
+            float x[F];
+            load_tile(tb + (uint32_t)l, x);
+            const uint32_t id = ids[(uint64_t)(tb + l) * kCullTile + lane];
+            ++visited;
+            asm volatile("" : "+s"(qoff));
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                if (readlane_f(lb[g], l) < td[g]) scan(g, x, id);
+            uint64_t still = 0;  // drop the tiles the tightened thresholds now exclude
+#pragma unroll
+            for (int g = 0; g < G; ++g) still |= __ballot(lb[g] < td[g]);
+            need &= still;
+        }
+    }
+    if (counters && lane == 0) {
+        unsigned long long *cs = counters + (blockIdx.x % kCounterSlots) * kCounterStride;
+        atomicAdd(&cs[0], (unsigned long long)visited);
+        atomicAdd(&cs[1], (unsigned long long)(c1 > c0 ? c1 - c0 : 0));
+        atomicAdd(&cs[2], (unsigned long long)qscans);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+        if (g0 + g < nq && lane < K2) {
+            const size_t o = ((size_t)blockIdx.y * nq + g0 + g) * K2 + lane;
+            pd[o] = kdist(Lk[g]);
+            pi[o] = (uint32_t)Lk[g];
+        }
+}
+
 template <int SP>
 __device__ __forceinline__ double screen_error(const DevSpace &sp, double B, double L, double eta = 0.0) {
     double e = 0.0;
@@ -1417,6 +1584,18 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
             } else {
                 hit = state_dist32<SP, F>(x, &qrow[qoff + g * FS], w0, w1) <= thr[g];
             }
+            if constexpr (SLAB) {
+                // the screen's candidates go to the slab as sorted positions; their exact fp64
+                // decisions run afterwards (radius_slab_exact_kernel), off the walk: no fp64
+                // registers or dependent row loads here
+                const uint64_t bm = __ballot(hit);
+                if (hit) {
+                    const uint64_t j = cnt[g] + (uint64_t)__popcll(bm & lt);
+                    if (j < slab) out_i[(uint64_t)qo[g] * slab + j] = (uint32_t)p;
+                }
+                cnt[g] += (uint64_t)__popcll(bm);
+                continue;
+            }
             double dd = 0.0;
             if (hit) {  // exact decision from the sorted fp64 row (coalesced over the tile)
                 constexpr int FA = (F + 3) & ~3;
@@ -1439,13 +1618,6 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
                 const uint64_t pos = cur[g] + (uint64_t)__popcll(bm & lt);
                 out_i[pos] = id;
                 out_d[pos] = dd;
-            }
-            if (SLAB && hit) {
-                const uint64_t j = cnt[g] + (uint64_t)__popcll(bm & lt);
-                if (j < slab) {
-                    out_i[(uint64_t)qo[g] * slab + j] = id;
-                    out_d[(uint64_t)qo[g] * slab + j] = dd;
-                }
             }
             cur[g] += (uint64_t)__popcll(bm);
             cnt[g] += (uint64_t)__popcll(bm);
@@ -1510,6 +1682,61 @@ __global__ __launch_bounds__(64) void radius32_group_kernel(
     }
 }
 
+// Exact decisions of the one-walk radius pass (MODE 2): query q's slab holds the sorted positions
+// of its screen candidates (d32 <= r + e, counts[q] of them); a wave per query recomputes each
+// candidate's fp64 distance from the sorted fp64 rows in the reference's operation order, keeps
+// d <= r (Linear :135-142, inclusive) and compacts the hits in place as (id, d), in candidate
+// order.  counts[q] becomes the hit count; a query whose candidates overflowed its slab keeps its
+// candidate count (> slab), which sends the call to the two-walk path (exact counts, then fill).
+template <int SP, int F>
+__global__ __launch_bounds__(64) void radius_slab_exact_kernel(const double *__restrict__ rows64,
+                                                               const uint32_t *__restrict__ ids,
+                                                               const double *__restrict__ qf64, DevSpace sp, double r,
+                                                               uint32_t slab, uint64_t *__restrict__ counts,
+                                                               uint32_t *__restrict__ slab_i,
+                                                               double *__restrict__ slab_d) {
+    constexpr int FA = (F + 3) & ~3;
+    const uint32_t q = blockIdx.x, lane = threadIdx.x;
+    const uint64_t c = counts[q];
+    if (c > slab) return;
+    double qv[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) qv[f] = qf64[(size_t)q * F + f];
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const size_t base = (size_t)q * slab;
+    uint32_t hits = 0;
+    for (uint32_t j0 = 0; j0 < (uint32_t)c; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        bool hit = false;
+        double d = 0.0;
+        uint32_t id = kNoId;
+        if (j < c) {
+            const uint32_t p = slab_i[base + j];
+            double sv[F];
+            const double2 *r2 = reinterpret_cast<const double2 *>(rows64 + (size_t)p * FA);
+#pragma unroll
+            for (int cc = 0; cc < FA / 2; ++cc) {
+                const double2 v = r2[cc];
+                if (2 * cc < F) sv[2 * cc] = v.x;
+                if (2 * cc + 1 < F) sv[2 * cc + 1] = v.y;
+            }
+            d = feat_dist<SP, F, 0>(sv, qv, sp);
+            hit = d <= r;
+            id = ids[p];
+        }
+        // every lane has read its entry (the ballot depends on it) before any write below;
+        // writes land at or below the positions read
+        const uint64_t bm = __ballot(hit);
+        if (hit) {
+            const uint32_t o = hits + (uint32_t)__popcll(bm & lt);
+            slab_i[base + o] = id;
+            slab_d[base + o] = d;
+        }
+        hits += (uint32_t)__popcll(bm);
+    }
+    if (lane == 0) counts[q] = hits;
+}
+
 __global__ void to_fp32_kernel(const double *__restrict__ f64, uint64_t cap, int rows, uint64_t first, uint64_t n,
                                float *__restrict__ f32) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1550,6 +1777,19 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
     p.K = k_bucket(k);
     p.k2 = p.K2;
     p.cull = cull;
+    if (cull && sp.kind == OMPL_GPU_SPACE_KCHAIN) {
+        // culled chain scan: full K2 lists per chunk (the chunked certificate's proof takes the
+        // merged list's K2-th entry), chunks along grid.y for ~24 waves per CU
+        p.K2 = k_bucket(k + 6) < 16 ? 16 : k_bucket(k + 6);
+        p.k2 = p.K2;
+        const uint64_t ntile = std::max<uint64_t>(1, (n_end + kCullTile - 1) / kCullTile);
+        const uint64_t groups = (nq + kChainCullG - 1) / kChainCullG;
+        const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)num_cus * 24 + groups - 1) / groups, 64));
+        const uint64_t per = (ntile + S - 1) / S;
+        p.chunk_len = (uint32_t)per;  // tiles per chunk
+        p.chunks = (uint32_t)((ntile + per - 1) / per);
+        return p;
+    }
     if (cull) {  // group walk: one list per query, k + 3 entries in the smallest slot bucket
         // k + 3: measured on cfg3 (SE3 10^6, k = 10, 10^5 queries), k + 2 left 250 of 10^5
         // queries uncertified (a 90 us bounded re-run), k + 3 none, for +0.01 ms of walk
@@ -1656,8 +1896,22 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             walked = true;
         }
     }
-    if (p.cull && !walked) return hipErrorInvalidValue;
     if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+        if (p.cull) {
+            if (!ss || !ss->built) return hipErrorInvalidValue;
+            // the plan's chunk count sized the lists; the store's tiles (main + tail) set their length
+            const uint32_t per = (ss->ntiles + p.chunks - 1) / p.chunks;
+            timer_begin(st, "knn32_chain_cull_kernel");
+            hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG>),
+                               dim3((nq + kChainCullG - 1) / kChainCullG, p.chunks), dim3(64), 0, st, ss->rows,
+                               ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per, (float)sp.link, sp.dim,
+                               pd, pi, ss->counters);
+            timer_end(st);
+            walked = true;
+        }
+    }
+    if (p.cull && !walked) return hipErrorInvalidValue;
+    if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) if (!p.cull) {
         timer_begin(st, "knn32_wave_scan_kernel");
         // link order of the screen (knn32_wave_scan_kernel ORD) and waves sharing each staged tile
         // (WPB); OMPL_GPU_CHAIN_ORDER=0 restores the reference order with two exit tests and
@@ -1691,7 +1945,15 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
                            st, f32, cap, n_end, q32, nq, p.chunk_len, w0, (float)sp.w1, sp.dim, pd, pi);
         timer_end(st);
     }
-    if (p.chunks == 1) {
+    if (SP == OMPL_GPU_SPACE_KCHAIN && p.cull) {
+        // the culled chain scan: merge its chunk lists, then the wave certificate (ids, SoA rows)
+        if (p.chunks > 1)
+            hipLaunchKernelGGL((knn_chunk_merge_kernel<K2>), dim3((nq + 3) / 4), b256, 0, st, pd, pi, p.chunks, nq);
+        constexpr uint32_t QPB = 256 / K2;
+        hipLaunchKernelGGL((knn_certify_wave_kernel<SP, F, K2>), dim3((nq + QPB - 1) / QPB), b256, 0, st, pd, pi, nq,
+                           perm, f64, cap, nullptr, nullptr, qf64, sp, b.absmax, b.qeta, b.n_live, (uint32_t)K2, od,
+                           oi, k, fail, fail + 1);
+    } else if (p.chunks == 1) {
         constexpr uint32_t QPB = 256 / K2;
         // the group walk's lists hold positions in the sorted store (rows64 / ids map them)
         const bool pos = walked && p.cull;
@@ -1749,6 +2011,13 @@ hipError_t run_fast_space(const DevSpace &sp, const FastPlan &p, const FastLayou
 // the last one zero) and the offsets their exclusive scan gives (nq + 2: [nq] = total,
 // [nq + 1] = longest segment)
 constexpr int kRadiusGroup = 4;  // 10^7-state radius pass: G=2 2.37 ms, G=4 2.27 ms (tiles shared by more queries)
+// the one-walk (slab) pass holds no fp64 state, so a group can be wider: each fetched tile serves
+// more queries (A/B build: OMPL_AMD_VARIANT 2 -> 8)
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 2
+constexpr int kRadiusSlabGroup = 8;
+#else
+constexpr int kRadiusSlabGroup = 4;
+#endif
 
 struct RadiusLayout {
     size_t keys, keys2, idx, perm, cub, q32u, q32, counts, off, scan, red, total;
@@ -1815,10 +2084,13 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
         if ((e = hipMemsetAsync(counts + nq, 0, 8, st)) != hipSuccess) return e;
         if (phase == 2) {
             timer_begin(st, "radius32_group_kernel");
-            hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 2>), grid, b64, 0, st, ss->rows, ss->n_pad,
+            hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusSlabGroup, 2>),
+                               dim3((nq + kRadiusSlabGroup - 1) / kRadiusSlabGroup), b64, 0, st, ss->rows, ss->n_pad,
                                ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64,
                                sp, b.absmax, b.qeta, r, counts, nullptr, out_i, out_d, ss->counters, b.slab);
             timer_end(st);
+            hipLaunchKernelGGL((radius_slab_exact_kernel<SP, F>), dim3(nq), b64, 0, st, ss->rows64, ss->ids, qf64, sp,
+                               r, b.slab, counts, out_i, out_d);
         } else {
             hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 0>), grid, b64, 0, st, ss->rows, ss->n_pad,
                                ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64,
@@ -1909,7 +2181,8 @@ __global__ void sorted_gather_kernel(const float *__restrict__ f32, uint64_t cap
 
 template <int SP, int F>
 __global__ void tail_keys_kernel(const float *__restrict__ f32, uint64_t cap, uint64_t first, uint32_t n, FastBounds b,
-                                 uint32_t *__restrict__ keys, uint32_t *__restrict__ idx) {
+                                 const KdNode *__restrict__ nodes, uint32_t kd_tiles, uint32_t *__restrict__ keys,
+                                 uint32_t *__restrict__ idx) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t id = (uint32_t)(first + i);
@@ -1917,9 +2190,15 @@ __global__ void tail_keys_kernel(const float *__restrict__ f32, uint64_t cap, ui
     float x[R > kKeyDims + 1 ? R : kKeyDims + 1];
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = f32[(uint64_t)r * cap + id];
-    float c[kKeyDims];
-    key_coords<SP>(x, c, b.nkey);
-    keys[i] = morton_key(c, b);
+    if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+        // the chain's 2 NM position coordinates have no Morton order worth the name: order the
+        // tail by the k-d home tile of the main part, so that tail tiles are compact too
+        keys[i] = (nodes && kd_tiles > 1) ? kd_home_tile(x, nodes, kd_tiles) : 0u;
+    } else {
+        float c[kKeyDims];
+        key_coords<SP>(x, c, b.nkey);
+        keys[i] = morton_key(c, b);
+    }
     idx[i] = id;
 }
 
@@ -2574,8 +2853,10 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
         hipLaunchKernelGGL((kd_row_tile_boxes_kernel<SP, F>), dim3((main_tiles + 3) / 4), b256, 0, st, W0, n_live,
                            main_tiles, tb);
     for (int level = 0; level < Lg; ++level) {
-        if ((main_tiles >> level) > 4096u)  // few large nodes: wider blocks read their tile boxes
-            hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F, 1024>), dim3(1u << level), dim3(1024), 0, st, tb,
+        // few large nodes: wider blocks read their tile boxes (LDS: 2 NB floats per thread)
+        constexpr int BSL = NB * 8 * 1024 <= 150 * 1024 ? 1024 : 256;
+        if ((main_tiles >> level) > 4096u && BSL == 1024)
+            hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F, BSL>), dim3(1u << level), dim3(BSL), 0, st, tb,
                                main_tiles, level, nsplit);
         else
             hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F, 256>), dim3(1u << level), b256, 0, st, tb, main_tiles,
@@ -2671,7 +2952,7 @@ hipError_t append_sorted(const float *f32, const double *f64, uint64_t cap, uint
     uint32_t *i0 = (uint32_t *)(w + o_i0), *i1 = (uint32_t *)(w + o_i1);
     const dim3 b256(256);
     hipLaunchKernelGGL((tail_keys_kernel<SP, F>), dim3((n_tail + 255) / 256), b256, 0, st, f32, cap, s->main_covered,
-                       n_tail, b, k0, i0);
+                       n_tail, b, s->nodes, s->kd_tiles, k0, i0);
     if ((e = hipcub::DeviceRadixSort::SortPairs(w + o_cub, cub, k0, k1, i0, i1, (int)n_tail, 0, 32, st)) != hipSuccess)
         return e;
     const uint32_t tiles = (n_tail + kCullTile - 1) / kCullTile;

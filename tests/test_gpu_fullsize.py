@@ -132,3 +132,42 @@ def test_random_access_pattern(gpu):
     builds, appends = nn.index_stats()
     assert builds >= 2 and appends >= 1  # removals forced rebuilds; adds went to the tail
     nn.close()
+
+
+def test_cfg4_chain_culled_scan_1e6(gpu):
+    """cfg4: PRM*'s stored-part kNN on the KinematicChain space at the bench's
+    size — 10^6 reference-stream states, k = 41 (ConnectionStrategy.h:145-149) — through the
+    culled chain scan over the k-d sorted joint-position store; 64 of 8,192 milestones checked
+    against the oracle's brute force, then again after a tail append (a PRM* batch's 8,192 new
+    milestones) and 500 removals."""
+    import bench
+    from ompl_amd.spaces import KinematicChainSpace
+
+    sp = KinematicChainSpace(12, 1.0 / 12)
+    tree, q = bench.reference_inputs(sp, 1_000_000, 8_192, 0)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(tree)
+    before = nn.cull_stats()[2]
+    ids, d, cnt = nn.nearestKBatch(q, 41)
+    assert nn.cull_stats()[2] > before, "the batch did not take the culled chain scan"
+    assert (cnt == 41).all()
+    pick = np.random.default_rng(5).choice(len(q), 64, replace=False)
+    oi, od = oracle_knn_mt(O, sp, tree, q[pick], 41)
+    np.testing.assert_array_equal(d[pick], od)  # the chain metric is bit-exact (fp64, reference order)
+    np.testing.assert_array_equal(ids[pick].astype(np.int64), oi.astype(np.int64))
+    # a PRM* batch later: the milestones join the store (tail tiles), some states go away
+    nn.add(q)
+    gone = np.random.default_rng(6).choice(len(tree), 500, replace=False)
+    for i in gone:
+        nn.remove(int(i))
+    q2 = bench.reference_inputs(sp, 0, 2 * 8_192, 0)[1][8_192:]
+    ids2, d2, _ = nn.nearestKBatch(q2, 41)
+    keep = np.ones(len(tree) + len(q), dtype=bool)
+    keep[gone] = False
+    store = np.concatenate([tree, q])
+    live_ids = np.flatnonzero(keep)
+    pick2 = np.random.default_rng(7).choice(len(q2), 64, replace=False)
+    oi2, od2 = oracle_knn_mt(O, sp, store[live_ids], q2[pick2], 41)
+    np.testing.assert_array_equal(d2[pick2], od2)
+    np.testing.assert_array_equal(ids2[pick2].astype(np.int64), live_ids[oi2.astype(np.int64)])
+    nn.close()
