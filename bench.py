@@ -45,7 +45,7 @@ HBM_PEAK_GBS = 8000.0                       # HBM3E spec
 # flops per distance evaluation (SURVEY.md §8d constants; sqrt and acos counted as 1 each)
 F_SE3, F_L2_6, F_CHAIN = 21, 18, 84
 B_SE3 = {"f32": 28, "f64": 56}              # bytes per stored SE(3) state streamed by a scan
-PMC_PROFILES = {"cfg3": "r2_cfg3", "cfg2": "r2_cfg2", "cfg4": "r2_cfg4", "cfg5": "r2_cfg5"}
+PMC_PROFILES = {"cfg3": "r3_cfg3", "cfg2": "r3_cfg2", "cfg4": "r3_cfg4", "cfg5": "r3_cfg5"}
 DEFAULTS = {  # tree states, queries (samples / milestones / vertices) per GPU per step, k
     "cfg3": (1_000_000, 100_000, 10),
     "cfg2": (100_000, 100_000, 10),
