@@ -826,7 +826,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     };
     float lb[GH];
     float x[R], xn[R];
-    uint32_t id = kNoId, idn = kNoId, m = 0;
+    uint32_t idn = kNoId, m = 0;  // (the scan recomputes the position ids)
     int t = 0, tn = 0, s = -1;
     bool have = false;  // x holds a fetched tile of s
     int sn = next_super();
@@ -873,7 +873,6 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         if (got) {
 #pragma unroll
             for (int r = 0; r < R; ++r) x[r] = xn[r];
-            id = idn;
             t = tn;
         } else if (sn < 0 && !m) {
             break;
@@ -2616,7 +2615,7 @@ __global__ __launch_bounds__(1024) void kd_lds_finish_kernel(
 #pragma unroll
         for (uint32_t i = 0; i < IPT; ++i) {
             const uint32_t e = tid * IPT + i;
-            uint32_t kk = (1u << (32 - kKdIdxBits)) - 1u;  // padding: the largest key
+            uint32_t kk = 1u << (kKdQBits + l);  // padding: above every (l-bit path, q) key
             if (e < cnt) {
                 const uint32_t t = e / kCullTile;
                 uint32_t t0 = 0, TT = T, path = 0;
@@ -2643,8 +2642,9 @@ __global__ __launch_bounds__(1024) void kd_lds_finish_kernel(
             }
             kw[i] = (kk << kKdIdxBits) | (e < NMAX ? (uint32_t)ord[e] : 0u);
         }
-        // 4. block radix sort on the key bits (sub-path bits <= 4, so key < 2^17 - 1 = padding)
-        BlockSort().sort(kw, sort_storage, kKdIdxBits, 32);
+        // 4. block radix sort on the key bits only: l path bits + 12 coordinate bits + the padding
+        //    bit (13 + l <= 17 bits instead of all 21 above the row index: fewer digit passes)
+        BlockSort().sort(kw, sort_storage, kKdIdxBits, kKdIdxBits + kKdQBits + l + 1);
         __syncthreads();
 #pragma unroll
         for (uint32_t i = 0; i < IPT; ++i) ord[tid * IPT + i] = (uint16_t)(kw[i] & ((1u << kKdIdxBits) - 1u));

@@ -95,3 +95,27 @@ def test_stream32_large_store_equals_exact(gpu):
             np.testing.assert_array_equal(ids, ei)
             np.testing.assert_array_equal(d, ed)
     assert fast.nearest(data[4_499_999]) == 4_499_999
+
+
+@pytest.mark.parametrize("copies", [3_000, 70_000])
+def test_stream32_split_batch_and_overflow(gpu, copies):
+    """The split form (n >= 4M: screen-only stream, candidates per chunk, multi-block refine):
+    a batch of queries at k = 1 / 4 / 16 buckets, and a store holding 3,000 copies of one state
+    next to the queries, so that whole chunks tie at the same screened distance and overflow
+    their candidate lists (the refine kernel rescans them; with 70,000 copies more chunks
+    overflow than its list holds, so it rescans every chunk under the threshold): ids and
+    distances equal the exact fp64 stream."""
+    rng = np.random.default_rng(78)
+    sp = SE3StateSpace()
+    data = W.uniform_se3(rng, 4_300_000)
+    data[1_000_000:1_000_000 + copies] = data[5]
+    fast, exact = _pair(sp, gpu, data)
+    q = np.concatenate([W.uniform_se3(rng, 5), data[[5]], data[[2_000_000]]])
+    q[6, :3] += 1e-7
+    for k in (1, 3, 12):
+        ids, d, _ = fast.nearestKBatch(q, k)
+        ei, ed, _ = exact.nearestKBatch(q, k)
+        np.testing.assert_array_equal(ids, ei)
+        np.testing.assert_array_equal(d, ed)
+    ids, _, _ = fast.nearestKBatch(q[5:6], 12)
+    np.testing.assert_array_equal(ids[0], np.concatenate([[5], np.arange(1_000_000, 1_000_011)]))
