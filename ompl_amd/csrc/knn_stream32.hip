@@ -31,6 +31,16 @@ inline bool stream_split() {
     }();
     return b;
 }
+// smallest store the split form serves (OMPL_GPU_SPLIT_MIN overrides).  Measured at 10^6 (k = 1,
+// Infinity-Cache resident): split 9.1 us / 5.6e4 queries/s against the persistent
+// knn_stream1_kernel's 14.3 us / 4.7e4; at 10^7 49 us / 1.6e4 against 54.5 us / 1.37e4
+inline uint64_t stream_split_min() {
+    static const uint64_t m = [] {
+        const char *v = std::getenv("OMPL_GPU_SPLIT_MIN");
+        return v ? (uint64_t)std::atoll(v) : 0ull;
+    }();
+    return m;
+}
 inline uint32_t stream1_blocks() {
     static const uint32_t b = [] {
         const char *v = std::getenv("OMPL_GPU_S1_BLOCKS");
@@ -596,13 +606,12 @@ template <int SP, int F, int K>
 hipError_t stream32_items(const DevSpace &sp, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_end,
                           const double *qfeat, uint32_t nq, uint32_t k, float absmax, float qeta, double *out_d,
                           uint32_t *out_i, void *ws, size_t ws_bytes, hipStream_t st) {
-    if (n_end >= (4ull << 20)) {
-        if (stream_split())
-            return run_stream32_split<SP, F, K, kS32LargeItems>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax,
-                                                                qeta, out_d, out_i, ws, ws_bytes, st);
+    if (stream_split() && n_end >= stream_split_min())
+        return run_stream32_split<SP, F, K, kS32LargeItems>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax,
+                                                            qeta, out_d, out_i, ws, ws_bytes, st);
+    if (n_end >= (4ull << 20))
         return run_stream32<SP, F, K, kS32LargeItems>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
                                          ws_bytes, st);
-    }
     return run_stream32<SP, F, K, 4>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
                                      ws_bytes, st);
 }
@@ -615,7 +624,7 @@ hipError_t stream32_k(const DevSpace &sp, const float *feat32, const double *fea
     // form, the merge of 1,024 instead of 977 x 4 partials included); from 4 M states up the
     // chunked form streams faster (10^7: 56.6 us against 60 us at its best, 2,048 blocks — the
     // persistent grid ends with every block selecting at once, while HBM idles)
-    if (k <= 1 && (n_end >= (4ull << 20) || stream1_blocks() == 0))
+    if (k <= 1 && (n_end >= (4ull << 20) || stream1_blocks() == 0 || (stream_split() && n_end >= stream_split_min())))
         return stream32_items<SP, F, 1>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
                                         ws_bytes, st);
     if (k <= 1) {  // the persistent form: ~8 blocks per CU over the batch

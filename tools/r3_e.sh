@@ -12,7 +12,7 @@ rc=$?; tail -2 "$out/pytest_p.log"; if [ $rc != 0 ]; then echo "pytest rc=$rc"; 
 a="--steps 1 --warmup 1 --no-cpu-baseline --single-query-reps 200 --rrt-iters 0 --rrt-star-queries 0"
 for r in 1 2; do for v in 1 0; do
   f="$out/sq_split$v.$r.json"
-  OMPL_GPU_STREAM_SPLIT=$v timeout -k 10 300 python -u bench.py $a > "$f" 2> "$f.err"
+  OMPL_GPU_SPLIT_MIN=${SPLIT_MIN:-4194304} OMPL_GPU_STREAM_SPLIT=$v timeout -k 10 300 python -u bench.py $a > "$f" 2> "$f.err"
   rc=$?; if fatal $rc; then echo "sq rc=$rc"; tail -3 "$f.err"; exit 1; fi
-  python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1].split('/')[-1], json.dumps(d.get('single_query_1e7'))[:260])" "$f"
+  python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1].split('/')[-1], json.dumps(d.get('single_query'))[:200], json.dumps(d.get('single_query_1e7'))[:200])" "$f"
 done; done
