@@ -1792,7 +1792,11 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
         p.k2 = p.K2;
         const uint64_t ntile = std::max<uint64_t>(1, (n_end + kCullTile - 1) / kCullTile);
         const uint64_t groups = (nq + kChainCullG - 1) / kChainCullG;
-        const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)num_cus * 24 + groups - 1) / groups, 64));
+        static const uint64_t wpc = [] {  // waves per CU the chunks aim at (OMPL_GPU_CHAIN_WPC: A/B)
+            const char *v = std::getenv("OMPL_GPU_CHAIN_WPC");
+            return v ? (uint64_t)std::max(1, std::atoi(v)) : (uint64_t)96;
+        }();
+        const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)num_cus * wpc + groups - 1) / groups, 64));
         const uint64_t per = (ntile + S - 1) / S;
         p.chunk_len = (uint32_t)per;  // tiles per chunk
         p.chunks = (uint32_t)((ntile + per - 1) / per);
@@ -2530,6 +2534,289 @@ __global__ void kd_row_split_kernel(const float *__restrict__ W, uint32_t n, uin
     nodes[nd.pidx] = KdNode{(uint32_t)d, split, tl, nd.pidx + tl};
 }
 
+// ---- global levels as a median partition (no sort) -----------------------------------------
+// A level only has to put the floor(T/2) * 64 states with the smallest quantised split coordinate
+// of every node on its left; their order inside each child is free.  So instead of a radix sort of
+// (path, q) keys (2-3 digit passes over keys and values, then a row gather) a level is: a
+// histogram of q per node (kd_part_hist_kernel, which keeps q), the median bin b* and how many of
+// its states go left (kd_part_select_kernel, which also writes the node record), per-chunk counts
+// of q < b* / q == b* (kd_part_count_kernel), and one stable scatter of the rows
+// (kd_part_scatter_kernel: q < b* left, q > b* right, the first `need` states of bin b* in the
+// current order left) that also reduces both children's boxes, from which the next level's split
+// coordinates follow (kd_part_split_dim_kernel) without a tile-box pass.  Deterministic (the
+// histogram's atomics only count); every tile / super-tile box is still computed from the states
+// it ends up holding.
+constexpr uint32_t kPartChunk = 4096;  // states per block of the per-level passes (64 tiles)
+constexpr uint32_t kPartBins = kKdQ + 1;
+
+struct KdPartRange {
+    uint32_t P0, c0, c1, L;
+    bool ok;
+};
+__device__ __forceinline__ KdPartRange kd_part_range(const KdNodeRef &nd, uint32_t n, uint32_t chunk) {
+    KdPartRange r{nd.t0 * kCullTile, 0u, 0u, (nd.T >> 1) * kCullTile, false};
+    const uint32_t pend = min((nd.t0 + nd.T) * kCullTile, n);
+    r.c0 = r.P0 + chunk * kPartChunk;
+    r.c1 = min(r.c0 + kPartChunk, pend);
+    r.ok = nd.valid && nd.T > 1 && r.c0 < pend;
+    return r;
+}
+
+template <int SP, int F>
+__global__ __launch_bounds__(256) void kd_part_hist_kernel(const float *__restrict__ W, uint32_t n, uint32_t ntiles,
+                                                           int level, const float4 *__restrict__ nsplit,
+                                                           uint16_t *__restrict__ Q, uint32_t *__restrict__ H) {
+    constexpr int RW = KdRow<SP, F>::W;
+    __shared__ uint32_t h[kPartBins];
+    const uint32_t node = blockIdx.y;
+    const KdPartRange r = kd_part_range(kd_node_at(ntiles, level, node), n, blockIdx.x);
+    if (!r.ok) return;
+    for (uint32_t b = threadIdx.x; b < kPartBins; b += 256) h[b] = 0;
+    __syncthreads();
+    const float4 ns = nsplit[node];
+    const int d = (int)__float_as_uint(ns.x);
+    for (uint32_t p = r.c0 + threadIdx.x; p < r.c1; p += 256) {
+        const uint32_t q = kd_quant(W[(size_t)p * RW + d], ns);
+        Q[p] = (uint16_t)q;
+        atomicAdd(&h[q], 1u);
+    }
+    __syncthreads();
+    uint32_t *hn = H + (size_t)node * kPartBins;
+    for (uint32_t b = threadIdx.x; b < kPartBins; b += 256)
+        if (h[b]) atomicAdd(&hn[b], h[b]);
+}
+
+// block-wide exclusive scan of one flag per thread (256 threads); returns the prefix, `total` the sum
+__device__ __forceinline__ uint32_t block_flag_scan(bool f, uint32_t *wsum, uint32_t &total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t m = __ballot(f);
+    const uint32_t pre = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t v = wsum[w];
+        before += w < wave ? v : 0u;
+        total += v;
+    }
+    __syncthreads();
+    return pre + before;
+}
+
+// one block per node: the median bin b* (the first whose cumulative count reaches L) and the
+// number of its states that go left; the node record (split: the lower edge of bin b*, which
+// routes the home-tile descent of a query — only a heuristic, never a bound)
+template <int SP, int F>
+__global__ __launch_bounds__(256) void kd_part_select_kernel(const uint32_t *__restrict__ H, uint32_t n,
+                                                             uint32_t ntiles, int level,
+                                                             const float4 *__restrict__ nsplit,
+                                                             uint2 *__restrict__ sel, KdNode *__restrict__ nodes) {
+    constexpr uint32_t PER = (kPartBins + 255) / 256;
+    __shared__ uint32_t part[256];
+    const uint32_t node = blockIdx.x;
+    const KdNodeRef nd = kd_node_at(ntiles, level, node);
+    const KdPartRange r = kd_part_range(nd, n, 0);
+    if (!r.ok) return;
+    const uint32_t *hn = H + (size_t)node * kPartBins;
+    const uint32_t b0 = threadIdx.x * PER;
+    uint32_t sum = 0;
+    for (uint32_t i = 0; i < PER; ++i)
+        if (b0 + i < kPartBins) sum += hn[b0 + i];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive Hillis-Steele scan
+        const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    const uint32_t incl = part[threadIdx.x], excl = incl - sum;
+    if (excl < r.L && r.L <= incl) {  // exactly one thread: L >= 1 and the total covers L
+        uint32_t c = excl, b = b0;
+        for (uint32_t i = 0; i < PER && b0 + i < kPartBins; ++i) {
+            const uint32_t v = hn[b0 + i];
+            if (c + v >= r.L) {
+                b = b0 + i;
+                break;
+            }
+            c += v;
+        }
+        sel[node] = make_uint2(b, r.L - c);
+        const float4 ns = nsplit[node];
+        const uint32_t tl = nd.T >> 1;
+        const float split = ns.z > 0.f ? ns.y + (float)b / ns.z : ns.y;
+        nodes[nd.pidx] = KdNode{__float_as_uint(ns.x), split, tl, nd.pidx + tl};
+    }
+}
+
+// per (node, chunk): states with q < b* and with q == b*
+__global__ __launch_bounds__(256) void kd_part_count_kernel(const uint16_t *__restrict__ Q, uint32_t n,
+                                                            uint32_t ntiles, int level,
+                                                            const uint2 *__restrict__ sel, uint32_t cpn,
+                                                            uint2 *__restrict__ cnt) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t node = blockIdx.y;
+    const KdPartRange r = kd_part_range(kd_node_at(ntiles, level, node), n, blockIdx.x);
+    if (!r.ok) return;
+    const uint32_t b = sel[node].x;
+    uint32_t lt = 0, eq = 0;
+    for (uint32_t p = r.c0 + threadIdx.x; p < r.c1; p += 256) {
+        const uint32_t q = Q[p];
+        lt += q < b ? 1u : 0u;
+        eq += q == b ? 1u : 0u;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lt += (uint32_t)__shfl_xor((int)lt, o);
+        eq += (uint32_t)__shfl_xor((int)eq, o);
+    }
+    __shared__ uint32_t esum[4];
+    if ((threadIdx.x & 63) == 0) {
+        wsum[threadIdx.x >> 6] = lt;
+        esum[threadIdx.x >> 6] = eq;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        cnt[(size_t)node * cpn + blockIdx.x] =
+            make_uint2(wsum[0] + wsum[1] + wsum[2] + wsum[3], esum[0] + esum[1] + esum[2] + esum[3]);
+}
+
+// ordered-integer image of a float (min of images = image of the min), for the box atomics
+__device__ __forceinline__ uint32_t kd_fenc(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float kd_fdec(uint32_t e) {
+    return __uint_as_float((e & 0x80000000u) ? (e & 0x7FFFFFFFu) : ~e);
+}
+
+// the stable scatter of one chunk; cbox[child path][2 NB]: images of min v and of min -v
+// (both minima, so one 0xFF fill initialises them)
+template <int SP, int F>
+__global__ __launch_bounds__(256) void kd_part_scatter_kernel(const float *__restrict__ W, float *__restrict__ W2,
+                                                              uint32_t n, uint32_t ntiles, int level,
+                                                              const uint16_t *__restrict__ Q,
+                                                              const uint2 *__restrict__ sel,
+                                                              const uint2 *__restrict__ cnt, uint32_t cpn,
+                                                              uint32_t *__restrict__ cbox) {
+    constexpr int NB = KdRow<SP, F>::NB, RW = KdRow<SP, F>::W;
+    __shared__ uint32_t wsum[4], red[2][2 * NB];
+    const uint32_t node = blockIdx.y;
+    const KdPartRange r = kd_part_range(kd_node_at(ntiles, level, node), n, blockIdx.x);
+    if (!r.ok) return;
+    const uint2 sv = sel[node];
+    const uint32_t b = sv.x, need = sv.y;
+    // states of this node before the chunk: q < b* and q == b* (the chunks' counts)
+    uint32_t lt = 0, eq = 0;
+    for (uint32_t c = threadIdx.x; c < blockIdx.x; c += 256) {
+        const uint2 v = cnt[(size_t)node * cpn + c];
+        lt += v.x;
+        eq += v.y;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lt += (uint32_t)__shfl_xor((int)lt, o);
+        eq += (uint32_t)__shfl_xor((int)eq, o);
+    }
+    for (uint32_t i = threadIdx.x; i < 2 * 2 * NB; i += 256) (&red[0][0])[i] = 0xFFFFFFFFu;
+    __shared__ uint32_t lts[4], eqs[4];
+    if ((threadIdx.x & 63) == 0) {
+        lts[threadIdx.x >> 6] = lt;
+        eqs[threadIdx.x >> 6] = eq;
+    }
+    __syncthreads();
+    uint32_t eq_before = eqs[0] + eqs[1] + eqs[2] + eqs[3];
+    uint32_t left_before = lts[0] + lts[1] + lts[2] + lts[3] + min(eq_before, need);
+    uint32_t right_before = (r.c0 - r.P0) - left_before;
+    float lo[2][NB], nhi[2][NB];  // per side: min v, min -v
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd)
+#pragma unroll
+        for (int d = 0; d < NB; ++d) lo[sd][d] = nhi[sd][d] = __builtin_inff();
+    for (uint32_t base = r.c0; base < r.c1; base += 256) {
+        const uint32_t p = base + threadIdx.x;
+        const bool in = p < r.c1;
+        const uint32_t q = in ? (uint32_t)Q[p] : 0xFFFFFFFFu;
+        uint32_t te, tl;
+        const uint32_t er = block_flag_scan(in && q == b, wsum, te);
+        const bool take = in && (q < b || (q == b && eq_before + er < need));
+        const uint32_t lr = block_flag_scan(take, wsum, tl);
+        if (in) {
+            const uint32_t dst = take ? r.P0 + left_before + lr : r.P0 + r.L + right_before + (threadIdx.x - lr);
+            const float4 *src4 = reinterpret_cast<const float4 *>(W + (size_t)p * RW);
+            float4 *dst4 = reinterpret_cast<float4 *>(W2 + (size_t)dst * RW);
+            float row[RW];
+#pragma unroll
+            for (int c = 0; c < RW / 4; ++c) {
+                const float4 v = src4[c];
+                dst4[c] = v;
+                row[4 * c] = v.x; row[4 * c + 1] = v.y; row[4 * c + 2] = v.z; row[4 * c + 3] = v.w;
+            }
+            const int sd = take ? 0 : 1;
+#pragma unroll
+            for (int d = 0; d < NB; ++d) {
+                if (sd == 0) {
+                    lo[0][d] = fminf(lo[0][d], row[d]);
+                    nhi[0][d] = fminf(nhi[0][d], -row[d]);
+                } else {
+                    lo[1][d] = fminf(lo[1][d], row[d]);
+                    nhi[1][d] = fminf(nhi[1][d], -row[d]);
+                }
+            }
+        }
+        const uint32_t cnt_step = min(256u, r.c1 - base);
+        eq_before += te;
+        left_before += tl;
+        right_before += cnt_step - tl;
+    }
+    // children's boxes: wave minima, then LDS atomics, then one global atomic per value
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd)
+#pragma unroll
+        for (int d = 0; d < NB; ++d) {
+            float a = lo[sd][d], c = nhi[sd][d];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                a = fminf(a, __shfl_xor(a, o));
+                c = fminf(c, __shfl_xor(c, o));
+            }
+            if ((threadIdx.x & 63) == 0) {
+                if (a < __builtin_inff()) atomicMin(&red[sd][d], kd_fenc(a));
+                if (c < __builtin_inff()) atomicMin(&red[sd][NB + d], kd_fenc(c));
+            }
+        }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 2 * 2 * NB; i += 256) {
+        const uint32_t sd = i / (2 * NB), j = i % (2 * NB);
+        const uint32_t v = red[sd][j];
+        if (v != 0xFFFFFFFFu) atomicMin(&cbox[(size_t)(2 * node + sd) * 2 * NB + j], v);
+    }
+}
+
+// split coordinates of the nodes of `level` (>= 1) from the boxes the previous scatter reduced
+template <int SP, int F>
+__global__ void kd_part_split_dim_kernel(const uint32_t *__restrict__ cbox, uint32_t ntiles, int level,
+                                         float4 *__restrict__ nsplit) {
+    constexpr int NB = KdRow<SP, F>::NB;
+    const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;
+    if (path >= (1u << level)) return;
+    const KdNodeRef nd = kd_node_at(ntiles, level, path);
+    if (!nd.valid || nd.T <= 1) return;
+    const uint32_t *cb = cbox + (size_t)path * 2 * NB;
+    int bd = 0;
+    float be = -1.f, blo = 0.f;
+    for (int d = 0; d < NB; ++d) {
+        const float lo = kd_fdec(cb[d]), hi = -kd_fdec(cb[NB + d]);
+        const float e = hi - lo;
+        if (e > be) {  // first widest, as kd_node_split_dim_kernel
+            be = e;
+            bd = d;
+            blo = lo;
+        }
+    }
+    nsplit[path] = make_float4(__uint_as_float((uint32_t)bd), blo, be > 0.f ? (float)kKdQ / be : 0.f, 0.f);
+}
+
 // The deep levels in LDS: one block per node of level L0 (at most kd_lds_tiles<SP, F>() tiles,
 // so its rows fit in LDS) splits its whole subtree there — per sub-level the same steps as the
 // global loop (tile boxes of the current order, the widest coordinate of every splitting
@@ -2797,6 +3084,15 @@ hipError_t sorted_alloc(SortedStore *s, uint32_t pad_tiles, uint32_t max_nodes, 
 }
 
 // Full build over ids [0, n_total) whose live flag is set (n_live of them), on `st`, no sync.
+// the global k-d levels as median partitions (OMPL_GPU_KD_PART=0: one radix sort per level, A/B)
+inline bool kd_partition() {
+    static const bool b = [] {
+        const char *v = std::getenv("OMPL_GPU_KD_PART");
+        return v ? std::atoi(v) != 0 : true;
+    }();
+    return b;
+}
+
 template <int SP, int F>
 hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint64_t n_total, uint32_t n_live,
                         const uint8_t *live, SortedStore *s, hipStream_t st) {
@@ -2839,6 +3135,11 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
     const size_t o_flags = take(n), o_sel = take(4 * n), o_k0 = take(4ull * nl), o_k1 = take(4ull * nl),
                  o_v0 = take(4ull * nl), o_w = take(2 * row_bytes), o_tb = take(4ull * main_tiles * 2 * NB),
                  o_ns = take(16ull * main_tiles + 16), o_cnt = take(8), o_tmp = take(std::max(tmp_sel, tmp_sort));
+    // median partition: bin counts per node of the deepest global level, children's boxes,
+    // per-node selections, per-chunk counts (Q, the quantised coordinates, reuses k0)
+    const size_t nodes_max = Lg > 0 ? (size_t)1 << (Lg - 1) : 1;
+    const size_t o_h = take(4ull * kPartBins * nodes_max), o_cb = take(4ull * 2 * NB * 2 * nodes_max),
+                 o_ps = take(8ull * nodes_max), o_pc = take(8ull * (nodes_max + main_tiles / (kPartChunk / kCullTile) + 2));
     if ((e = scratch_ensure(s, off)) != hipSuccess) return e;
     char *w = (char *)s->scratch;
     uint8_t *flags = (uint8_t *)(w + o_flags);
@@ -2847,6 +3148,9 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
     float *W0 = (float *)(w + o_w), *W1 = (float *)(w + o_w + row_bytes);
     float *tb = (float *)(w + o_tb);
     float4 *nsplit = (float4 *)(w + o_ns);
+    uint32_t *H = (uint32_t *)(w + o_h), *cbox = (uint32_t *)(w + o_cb);
+    uint2 *psel = (uint2 *)(w + o_ps), *pcnt = (uint2 *)(w + o_pc);
+    uint16_t *Qp = (uint16_t *)k0;
     const dim3 b256(256);
     if (n_total)
         hipLaunchKernelGGL(kd_live_flags_kernel, dim3((unsigned)((n_total + 255) / 256)), b256, 0, st, live, n_total,
@@ -2858,7 +3162,34 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
     if (Lg > 0)
         hipLaunchKernelGGL((kd_row_tile_boxes_kernel<SP, F>), dim3((main_tiles + 3) / 4), b256, 0, st, W0, n_live,
                            main_tiles, tb);
-    for (int level = 0; level < Lg; ++level) {
+    for (int level = 0; level < Lg && kd_partition(); ++level) {  // the median partition levels
+        constexpr int BSL = NB * 8 * 1024 <= 150 * 1024 ? 1024 : 256;
+        if (level == 0) {
+            if ((main_tiles >> level) > 4096u && BSL == 1024)
+                hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F, BSL>), dim3(1), dim3(BSL), 0, st, tb, main_tiles,
+                                   0, nsplit);
+            else
+                hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F, 256>), dim3(1), b256, 0, st, tb, main_tiles, 0,
+                                   nsplit);
+        } else {
+            hipLaunchKernelGGL((kd_part_split_dim_kernel<SP, F>), dim3(((1u << level) + 255) / 256), b256, 0, st, cbox,
+                               main_tiles, level, nsplit);
+        }
+        const uint32_t nodes_l = 1u << level;
+        const uint32_t tmax = (main_tiles + nodes_l - 1) >> level;
+        const uint32_t cpn = (tmax * kCullTile + kPartChunk - 1) / kPartChunk;
+        const dim3 grid(cpn, nodes_l);
+        if ((e = hipMemsetAsync(H, 0, 4ull * kPartBins * nodes_l, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL((kd_part_hist_kernel<SP, F>), grid, b256, 0, st, W0, n_live, main_tiles, level, nsplit, Qp, H);
+        hipLaunchKernelGGL((kd_part_select_kernel<SP, F>), dim3(nodes_l), b256, 0, st, H, n_live, main_tiles, level,
+                           nsplit, psel, s->nodes);
+        hipLaunchKernelGGL(kd_part_count_kernel, grid, b256, 0, st, Qp, n_live, main_tiles, level, psel, cpn, pcnt);
+        if ((e = hipMemsetAsync(cbox, 0xFF, 4ull * 2 * NB * 2 * nodes_l, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL((kd_part_scatter_kernel<SP, F>), grid, b256, 0, st, W0, W1, n_live, main_tiles, level, Qp,
+                           psel, pcnt, cpn, cbox);
+        std::swap(W0, W1);
+    }
+    for (int level = 0; level < Lg && !kd_partition(); ++level) {  // the radix-sort levels (A/B)
         // few large nodes: wider blocks read their tile boxes (LDS: 2 NB floats per thread)
         constexpr int BSL = NB * 8 * 1024 <= 150 * 1024 ? 1024 : 256;
         if ((main_tiles >> level) > 4096u && BSL == 1024)
