@@ -13,7 +13,7 @@ for v in 1 0; do
   OMPL_GPU_KD_PART=$v timeout -k 10 200 python -u tools/build_probe.py > "$out/build_part$v.json" 2> "$out/build_part$v.err"
   rc=$?; echo "part=$v $(cat $out/build_part$v.json)"; if [ $rc != 0 ]; then echo "build rc=$rc"; tail -3 "$out/build_part$v.err"; exit 1; fi
 done
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python3 -u tools/build_probe.py 10000000 > "$out/prof.log" 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run --output-format csv -- python3 -u tools/build_probe.py 10000000 > "$out/prof.log" 2>&1
 rc=$?; echo "prof rc=$rc"
 f=$(find "$out/prof" -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cp "$f" "$out/trace_kernel_stats.csv"
 exit $rc
