@@ -1461,8 +1461,17 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
 // query's CSR segment in tile order; the caller sorts each segment by (distance, id).
 // MODE 2 (SLAB) counts like MODE 0 and also writes the first `slab` hits of each query to its
 // fixed-size slab, so that one walk suffices when no query has more hits than that.
+// (A/B builds: variants 5 / 6 ask the compiler for 7 / 8 waves per SIMD — 72 / 64 VGPRs with
+// 24 / 68 B of scratch spills — against the default's 80 VGPRs, 6 waves)
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 5
+#define OMPL_RADIUS_LB __launch_bounds__(64, 7)
+#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 6
+#define OMPL_RADIUS_LB __launch_bounds__(64, 8)
+#else
+#define OMPL_RADIUS_LB __launch_bounds__(64)
+#endif
 template <int SP, int F, int G, int MODE>
-__global__ __launch_bounds__(64) void radius32_group_kernel(
+__global__ OMPL_RADIUS_LB void radius32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ q32,
     const uint32_t *__restrict__ perm, uint32_t nq, const double *__restrict__ rows64,
