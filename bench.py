@@ -95,6 +95,10 @@ def parse():
                          "k = ceil(1.1 (e + e/6) ln n) = 57 at 10^7, instead of the radius mode")
     ap.add_argument("--rrt-star-queries", type=int, default=1000,
                     help="cfg3: batch of RRT* neighbourhood queries at k = 6,169 (0 = skip)")
+    ap.add_argument("--workloads", default="auto",
+                    help="configs measured after the headline into the line's `workloads` record: 'auto' = "
+                         f"{','.join(SUB_WORKLOADS)} when the headline is cfg3 replicated, 'none', or a comma list")
+    ap.add_argument("--sub-cpu-seconds", type=float, default=6.0, help="CPU baseline budget of each sub-workload")
     a = ap.parse_args()
     if a.partition == "tree" and a.workload != "cfg3":
         ap.error("--partition tree is implemented for --workload cfg3")
@@ -110,17 +114,55 @@ def reference_inputs(sp, n_tree, nq, rank, valid=None):
     (space->allocStateSampler() twice, RandomNumbers.cpp:53-279, StateSpace.cpp:800-806).  The
     tree is identical on every rank; rank r takes queries [r*nq, (r+1)*nq) of the query stream.
     With `valid`, only valid states are kept, in stream order (UniformValidStateSampler)."""
+    tree, q = _stream_inputs(sp, n_tree, nq * (rank + 1), valid)
+    return tree, np.ascontiguousarray(q[rank * nq:])
+
+
+def _stream_inputs(sp, n_tree, n_q, valid=None):
+    """(tree, the first n_q states of the query stream) — see reference_inputs."""
     from ompl_amd import sampling as S
     from ompl_amd import workloads as W
 
     S.set_seed(42)
     ts, qs = S.StateSampler(sp), S.StateSampler(sp)
-    need = nq * (rank + 1)
     if valid is None:
-        return ts.sample_uniform(n_tree), np.ascontiguousarray(qs.sample_uniform(need)[rank * nq:])
+        return ts.sample_uniform(n_tree), qs.sample_uniform(n_q)
     tree, _ = W.reference_valid_states(sp, n_tree, valid, sampler=ts, chunk=min(2_000_000, max(4 * n_tree, 4096)))
-    q, _ = W.reference_valid_states(sp, need, valid, sampler=qs, chunk=min(2_000_000, max(4 * need, 4096)))
-    return tree, np.ascontiguousarray(q[rank * nq:])
+    q, _ = W.reference_valid_states(sp, n_q, valid, sampler=qs, chunk=min(2_000_000, max(4 * n_q, 4096)))
+    return tree, q
+
+
+_INPUTS = {}  # (space, checker, n_tree, n_q) -> (tree, queries): cfg5's radius and kNN lines share one sample set
+
+
+def shared_inputs(key, sp, n_tree, n_q, valid, dist, dev):
+    """The tree and the first n_q query-stream states, drawn once per process and, with several
+    ranks, drawn on rank 0 only and broadcast over RCCL (the replicas are identical by
+    construction; at N = 8 this keeps eight ranks from re-sampling 10^7 valid states on the same
+    host cores)."""
+    k = (key, n_tree, n_q)
+    if k in _INPUTS:
+        return _INPUTS[k]
+    if dist is None:
+        out = _stream_inputs(sp, n_tree, n_q, valid)
+    else:
+        import torch
+
+        root = dist.get_rank() == 0
+        arrs = _stream_inputs(sp, n_tree, n_q, valid) if root else None
+        meta = [[a.shape for a in arrs] if root else None]
+        dist.broadcast_object_list(meta, src=0, device=dev)
+        out = []
+        for i, shape in enumerate(meta[0]):
+            t = (torch.from_numpy(np.ascontiguousarray(arrs[i])).to(dev) if root
+                 else torch.empty(shape, dtype=torch.float64, device=dev))
+            dist.broadcast(t, src=0)
+            out.append(t.cpu().numpy())
+            del t
+        out = tuple(out)
+    _INPUTS.clear()  # keep one set: the next workload either reuses it or needs another
+    _INPUTS[k] = out
+    return out
 
 
 CPU_THREADS = 8  # SURVEY §8d protocol: 1 core and all 8 cores of the reference container
@@ -482,7 +524,7 @@ def rrt_device(torch, nn, mv, sp, dev, iters):
 class Runner:
     """One workload: builds the inputs, the step, and the roofline of its dominant kernel."""
 
-    def __init__(self, args, torch, dev, local, rank, stream):
+    def __init__(self, args, torch, dev, local, rank, stream, dist=None):
         from ompl_amd import DiscreteMotionValidatorGPU, NearestNeighborsGPU
         from ompl_amd import workloads as W
         from ompl_amd.checkers import HypercubeChecker, KinematicChainChecker, SpheresChecker
@@ -492,18 +534,16 @@ class Runner:
         wl, nq, k = args.workload, args.queries, args.k
         self.radius = None
         self.tree_mode = args.partition == "tree"
+        world = int(os.environ.get("WORLD_SIZE", "1"))
         if wl == "cfg3":
             self.sp, self.ck = SE3StateSpace(0.0, 1.0), HypercubeChecker(3, 0.1)
-            # tree mode: one global batch of samples for every rank (the rank-0 slice of the stream)
-            self.tree, q = reference_inputs(self.sp, args.tree, nq, 0 if self.tree_mode else rank)
         elif wl == "cfg2":
             self.sp, self.ck = RealVectorStateSpace(6), HypercubeChecker(6, 0.1)
-            self.tree, q = reference_inputs(self.sp, args.tree, nq, rank)
         elif wl == "cfg4":
             self.sp = KinematicChainSpace(12, 1.0 / 12)                   # KinematicChainBenchmark.cpp:48-49
             self.ck = KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))
             self.kc = math.e + math.e / 12.0                              # KStarStrategy (ConnectionStrategy.h:141)
-            last = args.tree + nq * (args.warmup + args.steps) * int(os.environ.get("WORLD_SIZE", "1"))
+            last = args.tree + nq * (args.warmup + args.steps) * world
             self.k = int(math.ceil(self.kc * math.log(last)))           # k_cap: the largest k_i of the run
         else:
             self.sp = SE3StateSpace(0.0, 1.0)
@@ -516,14 +556,20 @@ class Runner:
             # BIT* kNN mode: k = ceil(1.1 (e + e/d) ln n) (bitstar/src/ImplicitGraph.cpp:313-316, 1383-1387)
             self.k = int(math.ceil(1.1 * (math.e + math.e / 6.0) * math.log(args.tree))) if args.bitstar_knn else 0
         self.mv = DiscreteMotionValidatorGPU(self.sp, self.ck, local)
-        if wl == "cfg5":  # sample sets hold valid states (ImplicitGraph.cpp:981)
-            self.tree, q = reference_inputs(self.sp, args.tree, nq, rank, valid=self.mv.isValid)
-        elif wl == "cfg4":  # roadmap + the milestones of every step: valid states (PRM.cpp:356-378)
+        if wl in ("cfg3", "cfg2"):
+            # tree mode: one global batch of samples for every rank (the rank-0 slice of the stream)
+            tree, qa = shared_inputs(wl, self.sp, args.tree, nq * world, None, dist, dev)
+            r0 = 0 if self.tree_mode else rank
+            self.tree, q = tree, np.ascontiguousarray(qa[r0 * nq:(r0 + 1) * nq])
+        elif wl == "cfg5":  # sample sets hold valid states (ImplicitGraph.cpp:981)
+            self.tree, qa = shared_inputs("cfg5", self.sp, args.tree, nq * world, self.mv.isValid, dist, dev)
+            q = np.ascontiguousarray(qa[rank * nq:(rank + 1) * nq])
+        else:  # cfg4: roadmap + the milestones of every step: valid states (PRM.cpp:356-378)
             # one causal batch per step holds world * nq milestones of the query stream; every rank
             # inserts the whole batch (replicas stay identical) and computes the neighbours and edges
             # of its slice [rank * nq, (rank + 1) * nq) — no collective in the data path
-            nsteps, world = args.warmup + args.steps, int(os.environ.get("WORLD_SIZE", "1"))
-            self.tree, q = reference_inputs(self.sp, args.tree, nq * world * nsteps, 0, valid=self.mv.isValid)
+            nsteps = args.warmup + args.steps
+            self.tree, q = shared_inputs("cfg4", self.sp, args.tree, nq * world * nsteps, self.mv.isValid, dist, dev)
             self.milestones = [q[i * nq * world:(i + 1) * nq * world] for i in range(nsteps)]
             self.slice = (rank * nq, (rank + 1) * nq)
             self.step_i = 0
@@ -741,6 +787,11 @@ class Runner:
                 "brute_force_equivalent_tflops": float(nq) * n * flop / (kern_ms * 1e-3) / 1e12,
                 "traffic_source": traffic["source"] if traffic else None}
 
+    def close(self):
+        """release the library handles (the next workload gets the HBM back)"""
+        for h in (self.nn, self.mv):
+            h.close()
+
     def counters(self):
         k = self.nn.cull_stats()
         r = self.nn.radius_cull_stats()
@@ -777,6 +828,118 @@ def spawn_ranks(n):
     sys.exit(rc)
 
 
+SUB_WORKLOADS = {  # the default line's `workloads` record: every other config, same steps / warmup
+    "cfg2": {"workload": "cfg2"},
+    "cfg4": {"workload": "cfg4"},
+    "cfg5": {"workload": "cfg5"},
+    "cfg5k": {"workload": "cfg5", "bitstar_knn": True},
+}
+
+
+def sub_args(args, spec):
+    """args for one sub-workload: its own defaults (DEFAULTS), the headline's steps / warmup."""
+    a = argparse.Namespace(**vars(args))
+    a.workload = spec["workload"]
+    a.bitstar_knn = spec.get("bitstar_knn", False)
+    a.partition = "replicated"
+    a.tree, a.queries, a.k = DEFAULTS[a.workload]
+    a.exact = False
+    return a
+
+
+def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
+    """Run one workload: warmup, exactly args.steps timed steps bracketed by a barrier +
+    synchronize on both sides (max over ranks), then the line's common fields.  Returns
+    (line or None on ranks > 0, the Runner, the phase-valid fraction)."""
+    run = Runner(args, torch, dev, local, rank, stream, dist)
+    run.stream = stream
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    for _ in range(args.warmup):
+        run.step()
+    torch.cuda.synchronize(dev)
+    run.nn.profile(True)
+    run.nn.kernel_time()
+    scr0, fb0 = run.nn.stats()
+    c0 = run.counters()
+    units = 0
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        run.step(ev[s])
+        units += run.units_per_step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms_total, kern_n, kern_name = run.nn.kernel_time()
+    kern_ms = kern_ms_total / max(kern_n, 1)
+    run.nn.profile(False)
+    scr1, fb1 = run.nn.stats()
+    c1 = run.counters()
+    nn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    edge_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    mv_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
+    t = torch.tensor([elapsed, nn_ms, edge_ms, mv_ms, kern_ms], dtype=torch.float64, device=dev)
+    u = torch.tensor([units], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+    elapsed, nn_ms, edge_ms, mv_ms, kern_ms = t.tolist()
+    total_units = float(u.item())
+    if args.workload == "cfg4":  # edge validity of the last batch: row r holds cnt[r] edges
+        cols = torch.arange(run.k, device=dev).unsqueeze(0)
+        live = cols < run.cnt.unsqueeze(1)
+        valid_frac = float(run.evalid[live].float().mean().item()) if bool(live.any()) else None
+    elif args.workload != "cfg2":
+        valid_frac = float(run.valid[: max(run.m, 1)].float().mean().item())
+    else:
+        valid_frac = None
+    if rank != 0:
+        return None, run
+    metric, unit = run.metric()
+    screen = kern_name.startswith(("knn32", "radius32"))
+    line = {
+        "metric": metric,
+        "value": total_units / elapsed,
+        "unit": unit,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong" if run.tree_mode else "weak",
+        "vs_baseline": None,
+        "dtype": "f32 screen + f64 certify" if screen else "f64",
+        "config": run.config(world),
+        "nn_queries_per_s": run.nq * world / (nn_ms * 1e-3),
+        "phase_ms": {"nn": nn_ms, "steer_or_edges": edge_ms, "motion": mv_ms},
+        "fast_path": {"screened": scr1 - scr0, "exact_reruns": fb1 - fb0},
+        "roofline": run.roofline(kern_ms, kern_name, c0, c1, max(args.steps, 1)),
+    }
+    if args.workload == "cfg4":  # one synchronous call per step: kNN, causal scan, edges and insert together
+        line["phase_ms"] = {"prm_batch": nn_ms}
+        line["edges_checked_per_s"] = run.m * world / (nn_ms * 1e-3)
+        line["motion_valid_fraction"] = valid_frac
+        line["roadmap_vertices"] = run.nn.size()
+    elif args.workload != "cfg2":
+        line["motion_checks_per_s"] = run.m * world / (mv_ms * 1e-3)
+        line["motion_valid_fraction"] = valid_frac
+    return line, run
+
+
+def attach_cpu_baseline(line, run, args, rank, world, budget):
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        t0 = time.perf_counter()
+        line["cpu_baseline"] = cpu_baseline(args.workload, run.sp, run.ck, run.tree, run.q_host, run.k, budget,
+                                            run.radius)
+        line["cpu_baseline"]["wall_s"] = time.perf_counter() - t0
+    else:
+        line["cpu_baseline"] = None
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -808,52 +971,8 @@ def main():
 
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(dev)  # a real (non-null) stream shared by torch events and the library
-    run = Runner(args, torch, dev, local, rank, stream)
-    run.stream = stream
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-
-    for _ in range(args.warmup):
-        run.step()
-    torch.cuda.synchronize(dev)
-    run.nn.profile(True)
-    run.nn.kernel_time()
-    scr0, fb0 = run.nn.stats()
-    c0 = run.counters()
-    units = 0
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        run.step(ev[s])
-        units += run.units_per_step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    kern_ms_total, kern_n, kern_name = run.nn.kernel_time()
-    kern_ms = kern_ms_total / max(kern_n, 1)
-    scr1, fb1 = run.nn.stats()
-    c1 = run.counters()
-    nn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    edge_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
-    mv_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
-    t = torch.tensor([elapsed, nn_ms, edge_ms, mv_ms, kern_ms], dtype=torch.float64, device=dev)
-    u = torch.tensor([units], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(u, op=dist.ReduceOp.SUM)
-    elapsed, nn_ms, edge_ms, mv_ms, kern_ms = t.tolist()
-    total_units = float(u.item())
-    if args.workload == "cfg4":  # edge validity of the last batch: row r holds cnt[r] edges
-        cols = torch.arange(run.k, device=dev).unsqueeze(0)
-        live = cols < run.cnt.unsqueeze(1)
-        valid_frac = float(run.evalid[live].float().mean().item()) if bool(live.any()) else None
-    elif args.workload != "cfg2":
-        valid_frac = float(run.valid[: max(run.m, 1)].float().mean().item())
-    else:
-        valid_frac = None
+    wall0 = time.perf_counter()
+    line, run = measure(args, torch, dev, local, rank, world, dist, stream, args.cpu_seconds)
 
     single = single_large = rrt = spheres = rrt_star = index = None
     if rank == 0 and args.workload in ("cfg3", "cfg2") and not args.no_extras:
@@ -867,45 +986,34 @@ def main():
                                    "the 28 MB of fp32 rows stay Infinity-Cache resident across back-to-back scans")
         if not args.no_extras:
             single_large = single_query_large(torch, dev, args.single_query_reps)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.workload, run.sp, run.ck, run.tree, run.q_host, run.k, args.cpu_seconds, run.radius)
+    if rank == 0:
+        attach_cpu_baseline(line, run, args, rank, world, args.cpu_seconds)
     if rank == 0 and args.workload == "cfg3" and args.rrt_iters > 0:
         rrt = rrt_device(torch, run.nn, run.mv, run.sp, dev, args.rrt_iters)
+    run.close()
+    del run
+
+    subs = {}
+    names = [] if args.workloads == "none" else (
+        list(SUB_WORKLOADS) if args.workloads == "auto" else [w for w in args.workloads.split(",") if w])
+    if args.workload != "cfg3" or args.partition != "replicated":
+        names = [] if args.workloads == "auto" else names
+    for name in names:
+        t0 = time.perf_counter()
+        sa = sub_args(args, SUB_WORKLOADS[name])
+        sline, srun = measure(sa, torch, dev, local, rank, world, dist, stream, args.sub_cpu_seconds)
+        if rank == 0:
+            attach_cpu_baseline(sline, srun, sa, rank, world, args.sub_cpu_seconds)
+            sline["wall_s"] = time.perf_counter() - t0
+            subs[name] = sline
+        srun.close()
+        del srun
+        torch.cuda.synchronize(dev)
 
     if rank == 0:
-        metric, unit = run.metric()
-        screen = kern_name.startswith(("knn32", "radius32"))
-        line = {
-            "metric": metric,
-            "value": total_units / elapsed,
-            "unit": unit,
-            "n_gpus": world,
-            "rccl_ranks": rccl_ranks,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "strong" if run.tree_mode else "weak",
-            "vs_baseline": None,
-            "dtype": "f32 screen + f64 certify" if screen else "f64",
-            "data": ("synthetic: the reference's RNG streams — RNG::setSeed(42), then a tree sampler and a query "
-                     "sampler (allocStateSampler x2); rank r takes queries [r*Q, (r+1)*Q)"),
-            "config": run.config(world),
-            "nn_queries_per_s": run.nq * world / (nn_ms * 1e-3),
-            "phase_ms": {"nn": nn_ms, "steer_or_edges": edge_ms, "motion": mv_ms},
-            "fast_path": {"screened": scr1 - scr0, "exact_reruns": fb1 - fb0},
-            "roofline": run.roofline(kern_ms, kern_name, c0, c1, max(args.steps, 1)),
-            "cpu_baseline": cpu,
-        }
-        if args.workload == "cfg4":  # one synchronous call per step: kNN, causal scan, edges and insert together
-            line["phase_ms"] = {"prm_batch": nn_ms}
-            line["edges_checked_per_s"] = run.m * world / (nn_ms * 1e-3)
-            line["motion_valid_fraction"] = valid_frac
-            line["roadmap_vertices"] = run.nn.size()
-        elif args.workload != "cfg2":
-            line["motion_checks_per_s"] = run.m * world / (mv_ms * 1e-3)
-            line["motion_valid_fraction"] = valid_frac
+        line["rccl_ranks"] = rccl_ranks
+        line["data"] = ("synthetic: the reference's RNG streams — RNG::setSeed(42), then a tree sampler and a query "
+                        "sampler (allocStateSampler x2); rank r takes queries [r*Q, (r+1)*Q)")
         if index:
             line["index"] = index
         if spheres:
@@ -918,6 +1026,9 @@ def main():
             line["single_query_1e7"] = single_large
         if rrt:
             line["rrt_device"] = rrt
+        if subs:
+            line["workloads"] = subs
+        line["wall_s"] = time.perf_counter() - wall0
         print(json.dumps(line), flush=True)
     # release every library handle while the HIP runtime (and a profiler attached to it) is up
     torch.cuda.synchronize(dev)

@@ -271,6 +271,15 @@ ompl_gpu_status ompl_gpu_mv_motion_states(ompl_gpu_mv *h, const double *s1, cons
                                           uint32_t count, int endpoints, double *out);
 ompl_gpu_status ompl_gpu_mv_motion_states_device(ompl_gpu_mv *h, const double *d_s1, const double *d_s2, size_t m,
                                                  uint32_t count, int endpoints, double *d_out);
+/* StateSpace::distance(a[i], b[i]) (t == NULL: out[m]) or StateSpace::interpolate(a[i], b[i], t[i])
+ * (out[m][dim], AoS) for m pairs, evaluated by the device fp64 code the kernels use — the
+ * reference's virtuals RealVectorStateSpace.cpp:230-265, SO3StateSpace.cpp:254-318 (arcLength,
+ * slerp), CompoundStateSpace StateSpace.cpp:1068-1116 (SE3), KinematicChain.h:105-175.  Host AoS
+ * (synchronous) / device-resident (asynchronous on the handle's stream) variants. */
+ompl_gpu_status ompl_gpu_mv_space_pairs(ompl_gpu_mv *h, const double *a, const double *b, const double *t, size_t m,
+                                        double *out);
+ompl_gpu_status ompl_gpu_mv_space_pairs_device(ompl_gpu_mv *h, const double *d_a, const double *d_b, const double *d_t,
+                                               size_t m, double *d_out);
 
 /* ---- PRM* roadmap construction, causal batches ------------------------------------
  * PRM::addMilestone (geometric/planners/prm/src/PRM.cpp:562-596) with KStarStrategy

@@ -130,6 +130,8 @@ SIGNATURES = {
     "ompl_gpu_sampler_local_seeds": (C.c_int, [_P, _U32, C.POINTER(C.c_int)]),
     "ompl_gpu_mv_motion_states": (C.c_int, [_P, _D, _D, C.c_size_t, C.c_uint32, C.c_int, _D]),
     "ompl_gpu_mv_motion_states_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_uint32, C.c_int, _P]),
+    "ompl_gpu_mv_space_pairs": (C.c_int, [_P, _D, _D, _D, C.c_size_t, _D]),
+    "ompl_gpu_mv_space_pairs_device": (C.c_int, [_P, _P, _P, _P, C.c_size_t, _P]),
 }
 
 

@@ -1325,6 +1325,40 @@ ompl_gpu_status ompl_gpu_mv_motion_states(ompl_gpu_mv *h, const double *s1, cons
     return OMPL_GPU_OK;
 }
 
+// StateSpace::distance / interpolate per pair on the device (see ompl_gpu.h)
+ompl_gpu_status ompl_gpu_mv_space_pairs_device(ompl_gpu_mv *h, const double *d_a, const double *d_b, const double *d_t,
+                                               size_t m, double *d_out) {
+    if (!h || (m && (!d_a || !d_b || !d_out))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (m > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many pairs in one call");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (m == 0) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    HIP_OR_FAIL(launch_space_pairs(h->sp, d_a, d_b, d_t, (uint32_t)m, d_out, h->stream));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_mv_space_pairs(ompl_gpu_mv *h, const double *a, const double *b, const double *t, size_t m,
+                                        double *out) {
+    if (!h || (m && (!a || !b || !out))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (m > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many pairs in one call");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (m == 0) return OMPL_GPU_OK;
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    const size_t sb = sizeof(double) * m * h->sp.dim, ob = t ? sb : sizeof(double) * m;
+    HIP_OR_FAIL(h->s1.ensure(sb));
+    HIP_OR_FAIL(h->s2.ensure(sb));
+    HIP_OR_FAIL(h->ms.ensure(ob + (t ? sizeof(double) * m : 0)));
+    double *dout = (double *)h->ms.p, *dt = t ? dout + (ob / sizeof(double)) : nullptr;
+    HIP_OR_FAIL(hipMemcpyAsync(h->s1.p, a, sb, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(h->s2.p, b, sb, hipMemcpyHostToDevice, h->stream));
+    if (t) HIP_OR_FAIL(hipMemcpyAsync(dt, t, sizeof(double) * m, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(launch_space_pairs(h->sp, (const double *)h->s1.p, (const double *)h->s2.p, dt, (uint32_t)m, dout,
+                                   h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(out, dout, ob, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return OMPL_GPU_OK;
+}
+
 // ------------------------------------------------------------------------------ PRM*
 
 namespace {

@@ -296,5 +296,8 @@ hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const do
 inline uint64_t motion_states_per(uint32_t count, int endpoints) { return (uint64_t)count + (endpoints ? 2u : 0u); }
 hipError_t launch_motion_states(const DevSpace &sp, const double *s1, const double *s2, uint32_t m, uint32_t count,
                                 int endpoints, double *out, hipStream_t st);
+// StateSpace::distance (t == NULL: out[m]) or StateSpace::interpolate at t[i] (out[m][dim]) per pair
+hipError_t launch_space_pairs(const DevSpace &sp, const double *a, const double *b, const double *t, uint32_t m,
+                              double *out, hipStream_t st);
 
 }  // namespace ompl_amd

@@ -720,7 +720,18 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
                 float t = dx * dx;
                 t = fmaf(dy, dy, t);
                 t = fmaf(dz, dz, t);
+#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 7 || OMPL_AMD_VARIANT == 9)
+                // square-root-free rejects first: d >= w0 |t| + w1 c and (a + b)^2 >= a^2 + b^2, so
+                // a lane with w0^2 t (+ w1^2 c^2) >= td^2 (1 + 1e-4) has d > td after any fp32
+                // rounding (the slack is far above it): no lane below -> the wave skips the
+                // chord and both square roots (8-cycle issues each)
+                const float td2 = td[g] * td[g] * 1.0001f;
+                if (!__ballot(w0 * w0 * t < td2)) continue;
                 const float c2 = chord2(x + 3, qq + 4);
+                if (!__ballot(fmaf(w1 * w1, c2, w0 * w0 * t) < td2)) continue;
+#else
+                const float c2 = chord2(x + 3, qq + 4);
+#endif
                 const float c = __builtin_amdgcn_sqrtf(c2), wt = w0 * __builtin_amdgcn_sqrtf(t);
                 if (!__ballot(fmaf(w1, c, wt) < td[g])) continue;
                 offer(g, fmaf(w1, chord_theta(c, c2), wt), id);

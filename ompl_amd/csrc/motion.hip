@@ -211,6 +211,35 @@ hipError_t launch_motion_states(const DevSpace &sp, const double *s1, const doub
     return hipGetLastError();
 }
 
+// StateSpace::distance / StateSpace::interpolate per pair (the reference's virtuals:
+// RealVectorStateSpace.cpp:230-265, SO3StateSpace.cpp:254-318, StateSpace.cpp:1068-1116,
+// KinematicChain.h:105-175) with the device fp64 code the kernels use: thread per pair; t per pair
+// (interpolate) or NULL (distance -> out[m]).  Not a hot path: the state-space known-answer tests
+// (tests/base/StateSpaceTest.h) and planners that need single distances on device data.
+__global__ __launch_bounds__(256) void space_pairs_kernel(DevSpace sp, const double *__restrict__ a,
+                                                          const double *__restrict__ b, const double *__restrict__ t,
+                                                          uint32_t m, double *__restrict__ out) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const int dim = sp.dim;
+    double x[kChainMaxLinks], y[kChainMaxLinks], r[kChainMaxLinks];
+    load_state<0>(a + (size_t)e * dim, dim, x);
+    load_state<0>(b + (size_t)e * dim, dim, y);
+    if (!t) {
+        out[e] = raw_distance(sp, x, y);
+        return;
+    }
+    interpolate(sp, x, y, t[e], r);
+    for (int c = 0; c < dim; ++c) out[(size_t)e * dim + c] = r[c];
+}
+
+hipError_t launch_space_pairs(const DevSpace &sp, const double *a, const double *b, const double *t, uint32_t m,
+                              double *out, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(space_pairs_kernel, dim3((m + 255) / 256), dim3(256), 0, st, sp, a, b, t, m, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const double *s, uint32_t m, uint8_t *valid,
                               hipStream_t st) {
     if (m == 0) return hipSuccess;

@@ -97,6 +97,30 @@ class DiscreteMotionValidatorGPU(abi.Handle):
                                                     int(bool(endpoints)), abi.dptr(out)))
         return out
 
+    def distance(self, a, b) -> np.ndarray:
+        """StateSpace::distance(a[i], b[i]) per pair, evaluated on the device (RealVectorStateSpace.cpp:230-242,
+        SO3StateSpace.cpp:254-262, StateSpace.cpp:1068-1076, KinematicChain.h:105-124)."""
+        x, y = abi.as_states(a, self.dim), abi.as_states(b, self.dim)
+        if x.shape != y.shape:
+            raise ValueError("a and b must have the same shape")
+        out = np.zeros(x.shape[0])
+        abi.check(abi.lib.ompl_gpu_mv_space_pairs(self._h, abi.dptr(x), abi.dptr(y), None, x.shape[0],
+                                                  abi.dptr(out)))
+        return out
+
+    def interpolate(self, a, b, t) -> np.ndarray:
+        """StateSpace::interpolate(a[i], b[i], t[i]) per pair, evaluated on the device
+        (RealVectorStateSpace.cpp:257-265, SO3StateSpace.cpp:289-318, StateSpace.cpp:1109-1116,
+        KinematicChain.h:150-175); t is a scalar or one fraction per pair."""
+        x, y = abi.as_states(a, self.dim), abi.as_states(b, self.dim)
+        if x.shape != y.shape:
+            raise ValueError("a and b must have the same shape")
+        tt = np.ascontiguousarray(np.broadcast_to(np.asarray(t, dtype=np.float64), (x.shape[0],)))
+        out = np.zeros_like(x)
+        abi.check(abi.lib.ompl_gpu_mv_space_pairs(self._h, abi.dptr(x), abi.dptr(y), abi.dptr(tt), x.shape[0],
+                                                  abi.dptr(out)))
+        return out
+
     # device-resident
     def set_stream(self, stream_ptr: int | None) -> None:
         abi.check(abi.lib.ompl_gpu_mv_set_stream(self._h, C.c_void_p(stream_ptr or 0)))

@@ -4,6 +4,8 @@ port of the reference's randomAccessPatternTest (tests/datastructures/nearestnei
 
 * cfg3: the 10^6-state SE(3) tree, 10^5 queries through the culled group walk
   at k = 10, 128 of them checked against the oracle's brute force.
+* cfg2 (M1): the 10^5-state R^6 store, 10^5 queries through the culled group walk at k = 10,
+  128 of them checked against the oracle's brute force (bit-exact distances).
 * cfg5 (M4): the 10^7 valid-sample SE(3) set, 10^5 vertices through the radius walk at BIT*'s
   r = 0.1528, 32 CSR segments checked against the oracle's brute force.
 """
@@ -49,6 +51,30 @@ def test_cfg3_reference_tree_k10(gpu):
     pick = np.concatenate([np.arange(64), np.random.default_rng(3).choice(np.arange(64, len(q)), 64, replace=False)])
     oi, od = oracle_knn_mt(O, sp, tree, q[pick], 16)
     assert_knn_parity(ids[pick], d[pick], oi, od, 10)
+    nn.close()
+
+
+def test_cfg2_reference_store_k10(gpu):
+    """cfg2: RealVectorStateSpace(6) over [0,1]^6, the bench's reference-stream
+    10^5-state store and 10^5 queries, nearestK(k = 10) through the culled group walk; 128 queries
+    (the first 64 and 64 random) against the oracle's brute force: identical ids (ties aside) and
+    bit-identical fp64 distances (the R^n metric is exact in the reference's operation order)."""
+    import bench
+    from ompl_amd.spaces import RealVectorStateSpace
+
+    sp = RealVectorStateSpace(6)
+    tree, q = bench.reference_inputs(sp, 100_000, 100_000, 0)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(tree)
+    before = nn.cull_stats()[2]
+    ids, d, cnt = nn.nearestKBatch(q, 10)
+    assert nn.cull_stats()[2] > before, "the batch did not take the culled group walk"
+    assert (cnt == 10).all()
+    pick = np.concatenate([np.arange(64), np.random.default_rng(8).choice(np.arange(64, len(q)), 64, replace=False)])
+    oi, od = oracle_knn_mt(O, sp, tree, q[pick], 16)
+    np.testing.assert_array_equal(d[pick], od[:, :10])
+    assert_knn_parity(ids[pick], d[pick], oi, od, 10)
+    assert bool(np.all(np.diff(d, axis=1) >= 0)), "every list sorted ascending"
     nn.close()
 
 

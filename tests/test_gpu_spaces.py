@@ -1,0 +1,118 @@
+"""The reference's state-space known answers run on the DEVICE distance / interpolate code
+(ompl_gpu_mv_space_pairs, the same device functions the kNN certificate, steer, motion and
+getMotionStates kernels use), not only on the oracle (test_oracle.py):
+
+  StateSpaceTest::testDistance / testInterpolation   tests/base/StateSpaceTest.h:72-116
+      (n = 1000 random pairs, eps = 1e-12 as SO3_Simple / RealVector_Simple pass it,
+       tests/base/state_spaces.cpp:203, :278)
+  SO3_Simple: extent pi/2, getMotionStates(s1, s2, 100, endpoints) -> 102 states of unit norm
+      within 1e-15                                   tests/base/state_spaces.cpp:197-240
+  RealVector_Simple: d(s0, s0) = 0, interpolate(s0, s0, 0.6) = s0, interpolate(s0, (0,0,1), 0.5)[2] = 0.5
+                                                     tests/base/state_spaces.cpp:266-300
+
+The spaces are the ones on the hot path: R^3 / R^6, SO3, SE3 and the 12-link KinematicChain.
+Random states come from the reference's sampler streams (RNG::setSeed(42)).  Beside the
+properties, every device distance is compared with the oracle restatement: bit-identical for
+R^n and the chain, within 4 ulp for SO3 / SE3 (acos / sin differ between libms)."""
+import math
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+from ompl_amd import DiscreteMotionValidatorGPU
+from ompl_amd import sampling as S
+from ompl_amd.checkers import AllValidChecker
+from ompl_amd.spaces import KinematicChainSpace, RealVectorStateSpace, SE3StateSpace, SO3StateSpace
+
+pytestmark = pytest.mark.gpu
+
+N, EPS = 1000, 1e-12
+SPACES = {
+    "r3": lambda: RealVectorStateSpace(3),
+    "r6": lambda: RealVectorStateSpace(6),
+    "so3": SO3StateSpace,
+    "se3": SE3StateSpace,
+    "chain12": lambda: KinematicChainSpace(12, 1.0 / 12),
+}
+
+
+def _setup(name, gpu):
+    sp = SPACES[name]()
+    S.set_seed(42)
+    smp = S.StateSampler(sp)
+    return sp, DiscreteMotionValidatorGPU(sp, AllValidChecker(), gpu), smp
+
+
+def _ulps(a, b):
+    return np.abs(a - b) / np.spacing(np.maximum(np.abs(a), np.abs(b)))
+
+
+@pytest.mark.parametrize("name", list(SPACES))
+def test_state_space_test_distance(gpu, name):
+    """testDistance (StateSpaceTest.h:72-90): d(s1,s1) ~ 0, d12 > 0, d12 ~ d21, on the device."""
+    sp, mv, smp = _setup(name, gpu)
+    s1, s2 = smp.sample_uniform(N), smp.sample_uniform(N)
+    d11 = mv.distance(s1, s1)
+    d12, d21 = mv.distance(s1, s2), mv.distance(s2, s1)
+    assert np.all(np.abs(d11) < EPS)
+    differ = np.any(s1 != s2, axis=1)
+    assert np.all(d12[differ] > 0.0)
+    assert np.all(np.abs(d12 - d21)[differ] < EPS)
+    # the device metric against the oracle restatement (the reference's operation order)
+    od = np.array([O.distance(sp, a, b) for a, b in zip(s1, s2)])
+    if name in ("r3", "r6", "chain12"):
+        assert np.array_equal(d12, od)
+    else:
+        assert np.all(_ulps(d12, od) <= 4)
+
+
+@pytest.mark.parametrize("name", list(SPACES))
+def test_state_space_test_interpolation(gpu, name):
+    """testInterpolation (StateSpaceTest.h:93-116), every interpolate and distance on the device."""
+    sp, mv, smp = _setup(name, gpu)
+    s1, s2 = smp.sample_uniform(N), smp.sample_uniform(N)
+    s3 = mv.interpolate(s1, s2, 0.0)
+    assert np.all(mv.distance(s1, s3) < EPS)
+    s3 = mv.interpolate(s1, s2, 1.0)
+    assert np.all(mv.distance(s2, s3) < EPS)
+    s3 = mv.interpolate(s1, s2, 0.5)
+    tri = mv.distance(s1, s3) + mv.distance(s3, s2) - mv.distance(s1, s2)
+    assert np.all(np.abs(tri) < EPS)
+    s3 = mv.interpolate(s3, s2, 0.5)           # interpolate(s3, s2, 0.5, s3)
+    s2b = mv.interpolate(s1, s2, 0.75)          # interpolate(s1, s2, 0.75, s2)
+    assert np.all(mv.distance(s2b, s3) < EPS)
+    # per-pair fractions and the oracle restatement of interpolate
+    t = np.linspace(0.0, 1.0, N)
+    si = mv.interpolate(s1, s2, t)
+    oi = np.array([O.interpolate(sp, a, b, x) for a, b, x in zip(s1, s2, t)])
+    if name in ("r3", "r6", "chain12"):
+        assert np.array_equal(si, oi)
+    else:
+        np.testing.assert_allclose(si, oi, rtol=0, atol=1e-15)
+
+
+def test_so3_simple_known_answers(gpu):
+    """SO3_Simple (state_spaces.cpp:197-240): extent pi/2; d(s1, s1) ~ 0 within 1e-3; the 102
+    states of getMotionStates(s1, s2, 100, endpoints) — here from the device kernel — have unit
+    norm within 1e-15."""
+    sp, mv, smp = _setup("so3", gpu)
+    assert sp.getMaximumExtent() == 0.5 * math.pi
+    s = smp.sample_uniform(64)
+    assert np.all(np.abs(mv.distance(s[:32], s[:32])) < 1e-3)
+    ms = mv.getMotionStates(s[:32], s[32:], 100, True)
+    assert ms.shape == (32, 102, 4)
+    np.testing.assert_array_equal(ms[:, 0], s[:32])
+    np.testing.assert_array_equal(ms[:, -1], s[32:])
+    nrm = np.sqrt(np.sum(ms * ms, axis=2))
+    assert np.all(np.abs(nrm - 1.0) <= 1e-15 * 4)   # norm() of the state, reference eps 1e-15 (+ our sqrt rounding)
+
+
+def test_realvector_simple_known_answers(gpu):
+    """RealVector_Simple (state_spaces.cpp:266-300) on the device."""
+    sp, mv, _ = _setup("r3", gpu)
+    assert abs(sp.getMaximumExtent() - math.sqrt(3.0)) < 1e-3
+    s0, s1 = np.zeros((1, 3)), np.array([[0.0, 0.0, 1.0]])
+    assert abs(mv.distance(s0, s0)[0]) < 1e-3
+    np.testing.assert_array_equal(mv.interpolate(s0, s0, 0.6), s0)
+    assert abs(mv.interpolate(s0, s1, 0.5)[0, 2] - 0.5) < 1e-3
