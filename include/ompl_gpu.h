@@ -187,6 +187,11 @@ ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint
  * store for all uncertified queries, keeping d <= the certificate's exact k-th distance)
  * exceeded its candidate cap and took the full exact scan. */
 ompl_gpu_status ompl_gpu_nn_rerun_stats(const ompl_gpu_nn *h, uint64_t *full);
+/* Large-k select (k > 61 on SE3 / R^n, RRT*'s k = 6,169): queries whose candidates overflowed a
+ * per-chunk slab into the query's pool (a store whose id order follows space), and queries the
+ * select could not answer (sampling short-count, pool overflow) and re-ran on the exact fallback,
+ * summed over calls.  Synchronises the handle's stream. */
+ompl_gpu_status ompl_gpu_nn_large_stats(ompl_gpu_nn *h, uint64_t *spilled, uint64_t *exact);
 /* Bring the culled walks' sorted copy up to date now (a device k-d build, or placing the states
  * added since the last call in its tail) instead of at the next batched query; asynchronous on
  * the handle's stream.  No-op for spaces without a culled walk (SO3, KCHAIN). */

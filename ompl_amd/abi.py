@@ -87,6 +87,7 @@ SIGNATURES = {
     "ompl_gpu_nn_set_exact": (C.c_int, [_P, C.c_int]),
     "ompl_gpu_nn_stats": (C.c_int, [_P, _U64, _U64]),
     "ompl_gpu_nn_rerun_stats": (C.c_int, [_P, _U64]),
+    "ompl_gpu_nn_large_stats": (C.c_int, [_P, _U64, _U64]),
     "ompl_gpu_nn_index_stats": (C.c_int, [_P, _U64, _U64]),
     "ompl_gpu_nn_build_index": (C.c_int, [_P]),
     "ompl_gpu_nn_profile": (C.c_int, [_P, C.c_int]),

@@ -119,6 +119,7 @@ struct ompl_gpu_nn {
     // its Morton-ordered tail, removals are tombstoned in place (kernels.h SortedStore)
     SortedStore sorted;
     DevBuf raw_aos;         // [n_total][da] fp64 raw states by id (edge endpoints), appended lazily
+    DevBuf large_counter;   // large-k select: queries that spilled to the pool, queries re-run exactly
     DevBuf edge_q;          // per-edge CSR segment (query) of ompl_gpu_nn_edges_device
     uint64_t aos_n = 0;     // ids [0, aos_n) converted
     uint64_t sorted_builds = 0, sorted_appends = 0;  // device k-d builds / tail appends
@@ -496,6 +497,9 @@ static ompl_gpu_status ensure_sorted(ompl_gpu_nn *h) {
     return OMPL_GPU_OK;
 }
 
+static int aos_width(const ompl_gpu_nn *h);
+static ompl_gpu_status ensure_aos(ompl_gpu_nn *h);
+
 // knn on device-resident features (queries already converted); caller holds the lock
 static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, size_t nq, uint32_t k, uint32_t *d_ids,
                                            double *d_dist) {
@@ -536,11 +540,26 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
             dmax = 2.0 * h->absmax * std::sqrt((double)h->sp.dim);
         }
         dmax = std::max(dmax * 1.0001, 1e-30);
-        const size_t wsb = knn_large_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus);
-        if (wsb) HIP_OR_FAIL(h->ws.ensure(wsb));
-        HIP_OR_FAIL(launch_knn_large(h->sp, h->g, h->feat, h->feat32, h->cap, n_end, d_qf, (uint32_t)nq, k,
-                                     (float)h->absmax * (1.0f + 1e-6f), (float)dmax, d_dist, d_ids,
-                                     size_t(4) << 30, h->num_cus, h->stream, wsb ? h->ws.p : nullptr, h->ws.bytes));
+        size_t wsb = knn_large_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus);
+        if (wsb && h->ws.ensure(wsb) != hipSuccess) {  // no room for the select's slabs: the
+            (void)hipGetLastError();                    // count / fill / sort form still answers
+            wsb = 0;
+        }
+        if (!h->large_counter.p) {
+            HIP_OR_FAIL(h->large_counter.ensure(2 * sizeof(unsigned long long)));
+            HIP_OR_FAIL(hipMemsetAsync(h->large_counter.p, 0, 2 * sizeof(unsigned long long), h->stream));
+        }
+        const bool raw_rows = h->sp.kind != OMPL_GPU_SPACE_KCHAIN;  // features = raw coordinates
+        if (raw_rows) {
+            ompl_gpu_status s = ensure_aos(h);
+            if (s != OMPL_GPU_OK) return s;
+        }
+        HIP_OR_FAIL(launch_knn_large(h->sp, h->g, h->feat, h->feat32, h->cap, n_end,
+                                     raw_rows ? (const double *)h->raw_aos.p : nullptr, aos_width(h), d_qf,
+                                     (uint32_t)nq, k, (float)h->absmax * (1.0f + 1e-6f), (float)h->qeta * 1.01f,
+                                     (float)dmax, d_dist, d_ids, size_t(4) << 30, h->num_cus, h->stream,
+                                     wsb ? h->ws.p : nullptr, wsb ? h->ws.bytes : 0,
+                                     (unsigned long long *)h->large_counter.p));
         return OMPL_GPU_OK;
     }
     if (h->fast && screen_safe(h) && fast_k2(h->sp, k, (uint32_t)nq, h->cull) > 0) {
@@ -1063,6 +1082,20 @@ ompl_gpu_status ompl_gpu_nn_stats(const ompl_gpu_nn *h, uint64_t *screened, uint
     if (s != OMPL_GPU_OK) return s;
     if (screened) *screened = h->fast_queries;
     if (fallbacks) *fallbacks = c[0];
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_large_stats(ompl_gpu_nn *h, uint64_t *spilled, uint64_t *exact) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    unsigned long long c[2] = {0, 0};
+    if (h->large_counter.p) {
+        HIP_OR_FAIL(hipSetDevice(h->device));
+        HIP_OR_FAIL(hipMemcpyAsync(c, h->large_counter.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    }
+    if (spilled) *spilled = c[0];
+    if (exact) *exact = c[1];
     return OMPL_GPU_OK;
 }
 

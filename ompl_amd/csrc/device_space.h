@@ -286,6 +286,43 @@ __host__ __device__ inline bool is_valid(const DevSpace &sp, const DevChecker &c
     }
 }
 
+// KinematicChain isValid (demos/KinematicChain.h:200-276) for a compile-time link count NL: the
+// joint positions and every segment pair unrolled, so the 2 (NL + 2) positions stay in registers
+// (chain_valid's runtime loops index them dynamically, which puts them in scratch).  The same
+// arithmetic in the same order, so the bit is identical.
+template <int NL>
+__device__ __forceinline__ bool chain_valid_fixed(const double *s, double link, const double *env, int nenv) {
+    double px[NL + 2], py[NL + 2];  // segment i = (p[i], p[i+1])
+    double theta = 0., x = 0., y = 0.;
+    px[0] = 0.;
+    py[0] = 0.;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        theta += s[i];
+        const double xN = x + cos(theta) * link;
+        const double yN = y + sin(theta) * link;
+        px[i + 1] = xN;
+        py[i + 1] = yN;
+        x = xN;
+        y = yN;
+    }
+    px[NL + 1] = x + cos(theta) * 0.001;
+    py[NL + 1] = y + sin(theta) * 0.001;
+    constexpr int ns = NL + 1;
+#pragma unroll
+    for (int i = 0; i < ns; ++i)
+#pragma unroll
+        for (int j = i + 1; j < ns; ++j)
+            if (seg_intersect(px[i], py[i], px[i + 1], py[i + 1], px[j], py[j], px[j + 1], py[j + 1])) return false;
+#pragma unroll
+    for (int i = 0; i < ns; ++i)
+        for (int j = 0; j < nenv; ++j)
+            if (seg_intersect(px[i], py[i], px[i + 1], py[i + 1], env[4 * j], env[4 * j + 1], env[4 * j + 2],
+                              env[4 * j + 3]))
+                return false;
+    return true;
+}
+
 // Does the checker read the SO3 part of an SE3 state?  (None of the closed set does.)
 __host__ __device__ inline bool checker_reads_rotation(int kind) { return false; }
 
@@ -351,6 +388,17 @@ __device__ __forceinline__ bool valid_t(const DevSpace &sp, const DevChecker &ck
         }
     } else {
         return is_valid(sp, ck, s);
+    }
+}
+
+// valid_t with the space kind: the KinematicChain space at a fixed link count gets its unrolled
+// checker; every other specialisation is valid_t
+template <int SP, int DIM>
+__device__ __forceinline__ bool valid_sp(const DevSpace &sp, const DevChecker &ck, const double *s) {
+    if constexpr (SP == OMPL_GPU_SPACE_KCHAIN && DIM > 0) {
+        return ck.kind == OMPL_GPU_CHECK_KCHAIN ? chain_valid_fixed<DIM>(s, sp.link, ck.data, ck.count) : true;
+    } else {
+        return valid_t<DIM>(sp, ck, s);
     }
 }
 

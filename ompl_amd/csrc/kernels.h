@@ -168,10 +168,15 @@ hipError_t launch_knn_stream32(const DevSpace &sp, const FeatGeom &g, const floa
 bool large_k_supported(const DevSpace &sp);
 size_t knn_large_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t nq, uint32_t k, uint64_t n_end,
                                  int num_cus);
+// aos / da: the raw states by id as AoS rows of da doubles (SE3 / SO3 / R^n: the features), read
+// one row per candidate by the exact-distance step (NULL: the SoA features); seta: the store's
+// largest |norm^2 - 1| of a quaternion (SE3 fp32 screen bound); stats (device, 2 counters, may be
+// NULL): += queries whose candidates spilled to the pool, += queries sent to the exact fallback
 hipError_t launch_knn_large(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32,
-                            uint64_t cap, uint64_t n_end, const double *qfeat64, uint32_t nq, uint32_t k, float absmax,
-                            float dmax, double *out_d, uint32_t *out_i, size_t mem_budget, int num_cus,
-                            hipStream_t st, void *ws = nullptr, size_t ws_bytes = 0);
+                            uint64_t cap, uint64_t n_end, const double *aos, int da, const double *qfeat64, uint32_t nq,
+                            uint32_t k, float absmax, float seta, float dmax, double *out_d, uint32_t *out_i,
+                            size_t mem_budget, int num_cus, hipStream_t st, void *ws = nullptr, size_t ws_bytes = 0,
+                            unsigned long long *stats = nullptr);
 hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t first, uint64_t n, float *feat32,
                           hipStream_t st);
 // exact re-run of the fast path's uncertified queries, with no host round trip: list[0..*d_nlist)

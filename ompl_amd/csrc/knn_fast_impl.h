@@ -218,44 +218,6 @@ __device__ __forceinline__ float acos01(float x) {
     return __builtin_amdgcn_sqrtf(1.f - x) * p;
 }
 
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-
-// squared chord c^2 = min(|p - q|^2, |p + q|^2) of two quaternions, both sums on packed fp32
-// (one v_pk_add / v_pk_fma per component gives both)
-__device__ __forceinline__ float chord2(const float *p, const float *q) {
-    f2 a = f2{p[0], p[0]} + f2{-q[0], q[0]};
-    f2 c2 = a * a;
-    a = f2{p[1], p[1]} + f2{-q[1], q[1]};
-    c2 = pk_fma(a, a, c2);
-    a = f2{p[2], p[2]} + f2{-q[2], q[2]};
-    c2 = pk_fma(a, a, c2);
-    a = f2{p[3], p[3]} + f2{-q[3], q[3]};
-    c2 = pk_fma(a, a, c2);
-    return fminf(c2.x, c2.y);
-}
-
-// theta = 2 asin(c / 2) from the chord c and c^2: theta = c (1 + x R(x)), x = c^2 / 4 in
-// [0, 0.5], R a degree-5 fit of (asin(h) / h - 1) / h^2 (|error on theta| <= 1.1e-7, fp32
-// evaluation <= 1.8e-7 over the whole range; tools/fit_asin.py).  x R(x) >= 0, so the fp32
-// result is never below c: c is a lower bound of the screened angle, bit for bit.
-__device__ __forceinline__ float chord_theta(float c, float c2) {
-    const float x = 0.25f * c2;
-    float r = 0.11142297f;
-    r = fmaf(r, x, -0.07120271f);
-    r = fmaf(r, x, 0.070305005f);
-    r = fmaf(r, x, 0.036311187f);
-    r = fmaf(r, x, 0.07580938f);
-    r = fmaf(r, x, 0.16663891f);
-    return fmaf(c, x * r, c);
-}
-
-__device__ __forceinline__ float chord_angle(const float *p, const float *q) {
-    const float c2 = chord2(p, q);
-    return chord_theta(__builtin_amdgcn_sqrtf(c2), c2);
-}
-
 // Rotation pre-reject threshold: an element with |dot| <= cos(tau/w1 + 1e-5) has
 // acos(|dot|) > tau/w1 even after every fp32 error, hence distance > tau: skip it without
 // the square root and the arc cosine.  ctau < 0 rejects nothing.
@@ -586,6 +548,11 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
     constexpr int GH = G / 2;
     static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
+#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 8 || OMPL_AMD_VARIANT == 9)
+    constexpr bool kDyn = true;
+#else
+    constexpr bool kDyn = false;
+#endif
     __shared__ __attribute__((aligned(16))) float qrow[G * FS];
     const int lane = threadIdx.x;
     const int half = lane >> 5;
@@ -646,17 +613,52 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     };
     // tiles of the super-tile whose boxes are in bx that some query may still need;
     // lb[j]: this lane's bound for its tile and query half * GH + j
-    auto tile_mask = [&](const float (&bx)[BW], float (&lb)[GH]) -> uint32_t {
+    // kDyn: the bounds are computed only for the queries whose own super-tile bound passes
+    // (`bits`, from the round's bounds in LDS): the needed queries are paired, pass p puts the
+    // (2p)-th on lanes 0-31 and the (2p+1)-th on lanes 32-63, and passes past the last needed
+    // pair are skipped wave-wide — otherwise every query costs its bound on every popped tile
+    // row.  A query's slot is (pass, half) = (rank / 2, rank % 2), rank = its index among the
+    // set bits.  Without kDyn lane half h always holds queries h*GH + j.
+    auto pair_of = [&](uint32_t bits, int p, int &qa, int &qb) {  // the needed pair of pass p
+        for (int i = 0; i < 2 * p; ++i) bits &= bits - 1;
+        qa = bits ? __builtin_ctz(bits) : -1;
+        bits &= bits - 1;
+        qb = bits ? __builtin_ctz(bits) : -1;
+    };
+    auto td_of = [&](int q) -> float {  // td[q] for a wave-uniform q (selects, no indexing)
+        float v = -__builtin_inff();
+#pragma unroll
+        for (int g = 0; g < G; ++g) v = q == g ? td[g] : v;
+        return v;
+    };
+    auto tile_mask = [&](const float (&bx)[BW], float (&lb)[GH], uint32_t bits) -> uint32_t {
         relaunder();
 #ifdef OMPL_AMD_PROBE
         ++pr_supers;
 #endif
         bool need = false;
+        if constexpr (kDyn) {
 #pragma unroll
-        for (int j = 0; j < GH; ++j) {
-            lb[j] = box_lb<SP, F, true>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
-            need |= lb[j] < (half ? td[GH + j] : td[j]);
-            __builtin_amdgcn_sched_barrier(0);  // one bound at a time (temporaries)
+            for (int p = 0; p < GH; ++p) {
+                lb[p] = __builtin_inff();
+                int qa, qb;
+                pair_of(bits, p, qa, qb);
+                if (qa < 0) continue;  // wave-uniform
+                const int qg = half ? qb : qa;
+                const float thr = half ? td_of(qb) : td_of(qa);
+                if (qg >= 0) {
+                    lb[p] = box_lb<SP, F, true>(bx, &qrow[qoff + qg * FS], w0, w1);
+                    need |= lb[p] < thr;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < GH; ++j) {
+                lb[j] = box_lb<SP, F, true>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
+                need |= lb[j] < (half ? td[GH + j] : td[j]);
+                __builtin_amdgcn_sched_barrier(0);  // one bound at a time (temporaries)
+            }
         }
         return fold_tiles(__ballot(need));
     };
@@ -705,11 +707,20 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
                 }
             }
     };
-    auto scan_state = [&](const float (&x)[R], uint32_t id, int tin, const float (&lb)[GH]) {
+    auto scan_state = [&](const float (&x)[R], uint32_t id, int tin, const float (&lb)[GH], uint32_t bits) {
         relaunder();
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            if (!(readlane_f(lb[g % GH], tin + (g < GH ? 0 : 32)) < td[g])) continue;
+            if constexpr (kDyn) {
+                if (!((bits >> g) & 1u)) continue;
+                const int rank = __builtin_popcount(bits & ((1u << g) - 1u));
+                float v = lb[0];
+#pragma unroll
+                for (int p = 1; p < GH; ++p) v = (rank >> 1) == p ? lb[p] : v;
+                if (!(readlane_f(v, tin + ((rank & 1) ? 32 : 0)) < td[g])) continue;
+            } else {
+                if (!(readlane_f(lb[g % GH], tin + (g < GH ? 0 : 32)) < td[g])) continue;
+            }
             ++qscans;
             if constexpr (SP == OMPL_GPU_SPACE_SE3) {
                 // screened d = fma(w1, theta, w0 |t|) with theta >= c: when no lane's chord
@@ -762,7 +773,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         float lbh[GH];
 #pragma unroll
         for (int j = 0; j < GH; ++j) lbh[j] = -__builtin_inff();
-        scan_state(x, id, 0, lbh);
+        scan_state(x, id, 0, lbh, (1u << G) - 1u);
         ++visited;
     }
     // visit order: s0 - 1, s0, s0 + 1 (the group's neighbourhood, which sets the thresholds),
@@ -776,6 +787,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     // values live across the whole walk cost 29 VGPRs (69 -> 98, 7 -> 5 waves per SIMD)
     __shared__ float slb[G][64];
     bool first_round = true;  // the neighbourhood's three are always visited
+    int pop_l = -1;           // round slot of the last popped super-tile (-1: the neighbourhood's)
     auto next_super = [&]() -> int {  // next super-tile to visit, -1 when done
         for (;;) {
             if (sm && recheck && !first_round) {  // drop what the tightened thresholds exclude
@@ -790,6 +802,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             if (sm) {
                 const int l = __builtin_ctzll(sm);
                 sm &= sm - 1;
+                pop_l = first_round ? -1 : l;
                 return (int)(base + l);
             }
             if (sb >= nsuper) return -1;
@@ -836,8 +849,18 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     // current thresholds before it is scanned.  (Measured: 1.27-1.29 -> 1.25-1.26 ms on cfg3.)
     float bx[BW];
     const uint32_t home_s = th / kSuperTiles;
-    auto mask_of = [&](int sv, float (&l)[GH]) -> uint32_t {
-        uint32_t mm = tile_mask(bx, l);
+    auto mask_of = [&](int sv, float (&l)[GH], uint32_t &bits) -> uint32_t {
+        bits = (1u << G) - 1u;
+        if constexpr (kDyn) {
+            if (pop_l >= 0) {
+                bits = 0;
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    if (__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(slb[g][pop_l]))) < td[g])
+                        bits |= 1u << g;
+            }
+        }
+        uint32_t mm = bits ? tile_mask(bx, l, bits) : 0u;
         if ((uint32_t)sv == home_s) mm &= ~(1u << (th % kSuperTiles));  // scanned first
 #ifdef OMPL_AMD_PROBE
         if (!mm) ++pr_empty;
@@ -847,6 +870,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     float lb[GH];
     float x[R], xn[R];
     uint32_t idn = kNoId, m = 0;  // (the scan recomputes the position ids)
+    uint32_t bits = (1u << G) - 1u;  // queries that need the current super-tile s (kDyn)
     int t = 0, tn = 0, s = -1;
     bool have = false;  // x holds a fetched tile of s
     int sn = next_super();
@@ -857,10 +881,10 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         // fetch the next tile (xn) while x is scanned: the next of s, or else the first tile of
         // sn (bx holds its boxes) when its mask is not empty
         bool got = false, cross = false, consumed = false;
-        uint32_t mn = 0;
+        uint32_t mn = 0, bitsn = 0;
         float lbn[GH];
         if (!m && sn >= 0) {
-            mn = mask_of(sn, lbn);
+            mn = mask_of(sn, lbn, bitsn);
             consumed = true;
             cross = mn != 0;
         }
@@ -872,12 +896,13 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             got = true;
         }
         if (have) {  // the list ids are sorted positions: recomputed, not carried in a VGPR
-            scan_state(x, ((uint32_t)s * kSuperTiles + (uint32_t)t) * kCullTile + (uint32_t)lane, t, lb);
+            scan_state(x, ((uint32_t)s * kSuperTiles + (uint32_t)t) * kCullTile + (uint32_t)lane, t, lb, bits);
             ++visited;
         }
         if (cross) {
             s = sn;
             m = mn;
+            bits = bitsn;
 #pragma unroll
             for (int j = 0; j < GH; ++j) lb[j] = lbn[j];
         }
@@ -886,8 +911,17 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             if (sn >= 0) load_tbox((uint32_t)sn, bx);
         }
         bool still = false;  // drop the tiles of s that the tightened thresholds exclude
+        if constexpr (kDyn) {
 #pragma unroll
-        for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
+            for (int p = 0; p < GH; ++p) {
+                int qa, qb;
+                pair_of(bits, p, qa, qb);
+                still |= lb[p] < (half ? td_of(qb) : td_of(qa));
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
+        }
         m &= fold_tiles(__ballot(still));
         have = got;
         if (got) {

@@ -62,11 +62,8 @@ __device__ __forceinline__ float d32(const float *s, const float *q, float w0, f
         float t = dx * dx;
         t = fmaf(dy, dy, t);
         t = fmaf(dz, dz, t);
-        float dot = s[4] * q[4];
-        dot = fmaf(s[5], q[5], dot);
-        dot = fmaf(s[6], q[6], dot);
-        dot = fmaf(s[7], q[7], dot);
-        return w0 * sqrtf(t) + w1 * acosf(abs1(dot));
+        // rotation by the chord, as the culled walks (knn_fast_impl.h header: error bound)
+        return fmaf(w1, chord_angle(s + 4, q + 4), w0 * __builtin_amdgcn_sqrtf(t));
     } else if constexpr (SP == OMPL_GPU_SPACE_SO3) {
         float dot = s[0] * q[0];
         dot = fmaf(s[1], q[1], dot);
@@ -158,11 +155,23 @@ __global__ __launch_bounds__(256) void hist_kernel(const float *__restrict__ f32
     }
 }
 
+// eta (SE3): the store's largest |norm^2 - 1| of a quaternion + the query's (the chord bound,
+// knn_fast_impl.h screen_error<SE3>)
 template <int SP>
-__device__ __forceinline__ double screen_err(const DevSpace &sp, double B, double L) {
+__device__ __forceinline__ double query_eta(const double *qv) {  // |norm^2 - 1| of an SE3 query's quaternion
+    if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+        const double n = qv[3] * qv[3] + qv[4] * qv[4] + qv[5] * qv[5] + qv[6] * qv[6];
+        return fabs(n - 1.0);
+    }
+    return 0.0;
+}
+
+template <int SP>
+__device__ __forceinline__ double screen_err(const DevSpace &sp, double B, double L, double eta) {
     double e;
     if constexpr (SP == OMPL_GPU_SPACE_SE3)
-        e = sp.w0 * (6.0 * 1.7320508075688772 * kU * B) + 6.0 * kU * L + sp.w1 * (1.1 * sqrt(12.0 * kU) + 1e-6 + 4.5e-5);
+        e = sp.w0 * (6.0 * 1.7320508075688772 * kU * B) + 6.0 * kU * L +
+            sp.w1 * (2.25 * sqrt(0.5 * eta + 1e-15) + 2e-6 + 4.5e-5) + sp.w0 * sqrt(3.0 * 1.1754943508222875e-38);
     else if constexpr (SP == OMPL_GPU_SPACE_SO3)
         e = 1.1 * sqrt(12.0 * kU) + 1e-6 + 4.5e-5;
     else if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {  // knn_fast_impl.h screen_error<KCHAIN>
@@ -177,7 +186,8 @@ __device__ __forceinline__ double screen_err(const DevSpace &sp, double B, doubl
 
 template <int SP, int F>
 __global__ void threshold_kernel(const unsigned int *__restrict__ hist, const double *__restrict__ qf64, uint32_t nq,
-                                 uint32_t k, float bin_w, float absmax, DevSpace sp, float *__restrict__ radius) {
+                                 uint32_t k, float bin_w, float absmax, float seta, DevSpace sp,
+                                 float *__restrict__ radius) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     unsigned long long cum = 0;
@@ -194,7 +204,7 @@ __global__ void threshold_kernel(const unsigned int *__restrict__ hist, const do
     double B = absmax;
     const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_REALVECTOR ? F : 0);
     for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qf64[(size_t)q * F + c]));
-    const double e = screen_err<SP>(sp, B, r_hi + 1.0);
+    const double e = screen_err<SP>(sp, B, r_hi + 1.0, (double)seta + query_eta<SP>(qf64 + (size_t)q * F));
     radius[q] = (float)((r_hi + 2.0 * e) * (1.0 + 16.0 * kU));
 }
 
@@ -283,8 +293,8 @@ Plan plan(uint32_t nq, uint64_t n_end, int num_cus) {
 
 template <int SP, int F>
 hipError_t run_large(const DevSpace &sp, const double *f64, const float *f32, uint64_t cap, uint64_t n_end,
-                     const double *qf64, uint32_t nq, uint32_t k, float absmax, float dmax, double *out_d,
-                     uint32_t *out_i, size_t mem_budget, int num_cus, hipStream_t st) {
+                     const double *qf64, uint32_t nq, uint32_t k, float absmax, float seta, float dmax,
+                     double *out_d, uint32_t *out_i, size_t mem_budget, int num_cus, hipStream_t st) {
     constexpr int FS = Row<SP, F>::FS;
     const Plan p = plan(nq, n_end, num_cus);
     const float bin_w = dmax / (float)(kBins - 1);
@@ -316,7 +326,7 @@ hipError_t run_large(const DevSpace &sp, const double *f64, const float *f32, ui
                        (float)sp.w1, sp.dim, 1.0f / bin_w, hist);
     timer_end(st);
     hipLaunchKernelGGL((threshold_kernel<SP, F>), dim3((nq + 255) / 256), dim3(256), 0, st, hist, qf64, nq, k, bin_w,
-                       absmax, sp, radius);
+                       absmax, seta, sp, radius);
     hipLaunchKernelGGL((select_kernel<SP, F, false>), grid, dim3(kTile), 0, st, f32, f64, cap, n_end, q32, qf64, 0u,
                        nq, p.chunk_len, p.chunks, sp, radius, counts, nullptr, nullptr, nullptr);
     std::vector<uint32_t> hc((size_t)nq * p.chunks);
@@ -468,8 +478,8 @@ __global__ void sel_range_kernel(const unsigned int *__restrict__ hist, uint32_t
 // from sampled histogram B: r (the counting radius) and r + 2e (the collecting radius)
 template <int SP, int F>
 __global__ void sel_radius_kernel(const unsigned int *__restrict__ hist, const float *__restrict__ inv_bin_q,
-                                  const double *__restrict__ qf64, uint32_t nq, uint32_t k, float absmax, DevSpace sp,
-                                  float *__restrict__ r_count, float *__restrict__ r_fill) {
+                                  const double *__restrict__ qf64, uint32_t nq, uint32_t k, float absmax, float seta,
+                                  DevSpace sp, float *__restrict__ r_count, float *__restrict__ r_fill) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     const double need = ((double)k + 6.0 * sqrt((double)kSampleB * k) + 2.0 * kSampleB) / kSampleB;
@@ -483,7 +493,7 @@ __global__ void sel_radius_kernel(const unsigned int *__restrict__ hist, const f
     double B = absmax;
     const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_REALVECTOR ? F : 0);
     for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qf64[(size_t)q * F + c]));
-    const double e = screen_err<SP>(sp, B, r + 1.0);
+    const double e = screen_err<SP>(sp, B, r + 1.0, (double)seta + query_eta<SP>(qf64 + (size_t)q * F));
     r_count[q] = (float)r;
     r_fill[q] = (float)((r + 2.0 * e) * (1.0 + 16.0 * kU));
 }
@@ -497,7 +507,8 @@ __global__ __launch_bounds__(256) void sel_fill_kernel(const float *__restrict__
                                                        uint32_t chunk_len, uint32_t chunks, DevSpace sp,
                                                        const float *__restrict__ r_count,
                                                        const float *__restrict__ r_fill, uint32_t slab,
-                                                       double *__restrict__ cd, uint32_t *__restrict__ ci,
+                                                       uint32_t ovcap, uint32_t *__restrict__ ci,
+                                                       uint32_t *__restrict__ ov, uint32_t *__restrict__ ov_cnt,
                                                        uint32_t *__restrict__ slab_cnt,
                                                        unsigned int *__restrict__ count_r) {
     constexpr int FS = Row<SP, F>::FS;
@@ -520,7 +531,14 @@ __global__ __launch_bounds__(256) void sel_fill_kernel(const float *__restrict__
             cr += d <= rc ? 1u : 0u;
             if (d <= rf) {  // the exact distance comes later, densely (sel_sort_kernel): here it
                             // would run for the whole wave whenever one lane has a candidate
-                if (cnt < slab) ci[sbase + cnt] = (uint32_t)(base + s);
+                if (cnt < slab) {
+                    ci[sbase + cnt] = (uint32_t)(base + s);
+                } else {  // a full slab spills to the query's pool (the ids whose chunk is dense:
+                          // a store whose id order follows space puts a query's whole
+                          // neighbourhood in a few chunks)
+                    const uint32_t p = atomicAdd(&ov_cnt[q], 1u);
+                    if (p < ovcap) ov[(size_t)q * ovcap + p] = (uint32_t)(base + s);
+                }
                 ++cnt;
             }
         }
@@ -544,10 +562,16 @@ __device__ __forceinline__ bool sel_le(uint64_t d, uint32_t i, uint64_t Td, uint
 // order, get(e, d_bits, id) fetching one (valid == false: skip).  Finds the k-th smallest
 // (distance, id) by radix select (8-bit digits: 64 bits of the distance, then 32 of the id),
 // packs the k selected (id order) into LDS, sorts them stably by distance and writes row q.
+// id_sort: the source is not in id order (slab spills): the k selected are sorted by id first, so
+// that the stable distance sort still orders equal distances by id.
+// A digit whose boundary bin is taken whole (its count equals what is still needed) ends the
+// select early: every key with that prefix is selected, whatever its lower bits — usually after
+// 3-4 of the 9 digits.
 template <class Get>
 __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t q, double *__restrict__ out_d,
-                                  uint32_t *__restrict__ out_i) {
+                                  uint32_t *__restrict__ out_i, bool id_sort = false) {
     using BlockSort = rocprim::block_radix_sort<uint64_t, kSelBlock, kSelItems, uint32_t>;
+    using IdSort = rocprim::block_radix_sort<uint32_t, kSelBlock, kSelItems, uint64_t>;
     using BlockScan = rocprim::block_scan<uint32_t, kSelBlock>;
     constexpr int kDigit = 11, kRadix = 1 << kDigit;
     __shared__ union {
@@ -556,10 +580,11 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
             uint32_t i[kLargeSelMaxK];
         } stage;
         typename BlockSort::storage_type sort;
+        typename IdSort::storage_type id_sort;
     } sh;
     __shared__ typename BlockScan::storage_type scan_storage;
     __shared__ uint32_t hist[kRadix];
-    __shared__ uint32_t sh_digit, sh_need;
+    __shared__ uint32_t sh_digit, sh_need, sh_full;
     const uint32_t tid = threadIdx.x;
     const int lane = threadIdx.x & 63;
     // radix select of the k-th smallest (distance bits, id): 11-bit digits, most significant
@@ -577,6 +602,7 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
         if (tid == 0) {  // defaults: nothing left to select (need == 0) takes the whole digit range
             sh_digit = dmask;
             sh_need = 0;
+            sh_full = 1;
         }
         __syncthreads();
         for (uint32_t e0 = 0; e0 < count; e0 += kSelBlock) {  // uniform trip count: the ballots below
@@ -612,9 +638,11 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
         if (pre < need && pre + c0 >= need) {
             sh_digit = 2 * tid;
             sh_need = need - pre;
+            sh_full = pre + c0 == need ? 1u : 0u;
         } else if (pre + c0 < need && pre + c0 + c1 >= need) {
             sh_digit = 2 * tid + 1;
             sh_need = need - pre - c0;
+            sh_full = pre + c0 + c1 == need ? 1u : 0u;
         }
         __syncthreads();  // (fewer candidates than k: the defaults take them all)
         if (on_d)
@@ -622,7 +650,17 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
         else
             Ti |= sh_digit << shift;
         need = sh_need;
+        const bool full = sh_full != 0;
         __syncthreads();
+        if (full) {  // the boundary bin is taken whole: every lower bit (and id) passes
+            if (on_d) {
+                Td |= shift ? ((1ull << shift) - 1ull) : 0ull;
+                Ti = 0xFFFFFFFFu;
+            } else {
+                Ti |= shift ? ((1u << shift) - 1u) : 0u;
+            }
+            break;
+        }
     }
     // pack the selected keys (<= (Td, Ti)) in source order (id order): block prefix sums
     uint32_t base = 0;
@@ -654,6 +692,10 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
         ki[j] = sh.stage.i[tid * kSelItems + j];
     }
     __syncthreads();
+    if (id_sort) {  // block-uniform
+        IdSort().sort(ki, kd, sh.id_sort);
+        __syncthreads();
+    }
     BlockSort().sort(kd, ki, sh.sort);  // stable: equal distances keep id order
 #pragma unroll
     for (int j = 0; j < kSelItems; ++j) {
@@ -670,15 +712,19 @@ __device__ void block_select_sort(Get get, uint32_t count, uint32_t k, uint32_t 
 // overflow or a short count, the query goes to the fallback list
 template <int SP, int F>
 __global__ __launch_bounds__(kSelBlock) void sel_sort_kernel(const double *__restrict__ f64, uint64_t cap,
+                                                             const double *__restrict__ aos, int da,
                                                              const double *__restrict__ qf64, DevSpace sp,
                                                              const uint32_t *__restrict__ ci,
+                                                             const uint32_t *__restrict__ ov,
+                                                             const uint32_t *__restrict__ ov_cnt, uint32_t ovcap,
                                                              const uint32_t *__restrict__ slab_cnt,
                                                              const unsigned int *__restrict__ count_r, uint32_t nq,
                                                              uint32_t chunks, uint32_t slab, uint32_t k,
                                                              double *__restrict__ dd, uint32_t *__restrict__ di,
                                                              double *__restrict__ out_d, uint32_t *__restrict__ out_i,
                                                              uint32_t *__restrict__ fb_count,
-                                                             uint32_t *__restrict__ fb_list) {
+                                                             uint32_t *__restrict__ fb_list,
+                                                             unsigned long long *__restrict__ stats) {
     using BlockScan = rocprim::block_scan<uint32_t, kSelBlock>;
     __shared__ typename BlockScan::storage_type scan_storage;
     __shared__ uint32_t coff[kSelBlock + 1];  // chunk offsets of the dense order (chunks <= kSelBlock)
@@ -687,17 +733,16 @@ __global__ __launch_bounds__(kSelBlock) void sel_sort_kernel(const double *__res
     if (q >= nq) return;
     const uint32_t tid = threadIdx.x;
     const uint32_t *cnt = slab_cnt + (size_t)q * chunks;
-    const uint32_t c = tid < chunks ? cnt[tid] : 0u;
+    const uint32_t c = tid < chunks ? min(cnt[tid], slab) : 0u;  // a slab's overflow is in the pool
     uint32_t pre = 0, tot = 0;
     BlockScan().exclusive_scan(c, pre, 0u, tot, scan_storage);
-    if (tid == 0) sh_bad = count_r[q] < k ? 1u : 0u;
+    const uint32_t nov = ov_cnt[q];
+    if (tid == 0) sh_bad = (count_r[q] < k || nov > ovcap) ? 1u : 0u;
     __syncthreads();
-    if (tid < chunks) {
-        coff[tid] = pre;
-        if (c > slab) sh_bad = 1u;  // benign race: every writer stores 1
-    }
+    if (tid < chunks) coff[tid] = pre;
     if (tid == 0) coff[chunks] = tot;
     __syncthreads();
+    if (stats && tid == 0) atomicAdd(&stats[sh_bad ? 1 : 0], sh_bad || nov > 0 ? 1ull : 0ull);
     if (sh_bad) {
         if (tid == 0) fb_list[atomicAdd(fb_count, 1u)] = q;
         return;
@@ -706,21 +751,33 @@ __global__ __launch_bounds__(kSelBlock) void sel_sort_kernel(const double *__res
 #pragma unroll
     for (int f = 0; f < F; ++f) qv[f] = qf64[(size_t)q * F + f];
     const size_t sbase = (size_t)q * chunks * slab;
-    double *qd = dd + sbase;
-    uint32_t *qi = di + sbase;
-    for (uint32_t e = tid; e < tot; e += kSelBlock) {
-        uint32_t lo = 0, hi = chunks;  // the chunk holding dense position e: coff[lo] <= e < coff[lo + 1]
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (coff[mid] <= e)
-                lo = mid;
-            else
-                hi = mid;
+    const size_t dbase = (size_t)q * ((size_t)chunks * slab + ovcap);
+    double *qd = dd + dbase;
+    uint32_t *qi = di + dbase;
+    const uint32_t all = tot + nov;  // dense order: the slabs chunk by chunk (id order), then the pool
+    for (uint32_t e = tid; e < all; e += kSelBlock) {
+        uint32_t id;
+        if (e < tot) {
+            uint32_t lo = 0, hi = chunks;  // the chunk holding dense position e: coff[lo] <= e < coff[lo + 1]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (coff[mid] <= e)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            id = ci[sbase + (size_t)lo * slab + (e - coff[lo])];
+        } else {
+            id = ov[(size_t)q * ovcap + (e - tot)];
         }
-        const uint32_t id = ci[sbase + (size_t)lo * slab + (e - coff[lo])];
         double sv[F];
+        if (aos) {  // one contiguous row per candidate (the raw AoS copy; features = raw coordinates)
 #pragma unroll
-        for (int f = 0; f < F; ++f) sv[f] = f64[(uint64_t)f * cap + id];
+            for (int f = 0; f < F; ++f) sv[f] = f < sp.dim ? aos[(size_t)id * da + f] : 0.0;
+        } else {
+#pragma unroll
+            for (int f = 0; f < F; ++f) sv[f] = f64[(uint64_t)f * cap + id];
+        }
         qd[e] = feat_dist<SP, F, SP == OMPL_GPU_SPACE_KCHAIN ? F / 2 : 0>(sv, qv, sp);
         qi[e] = id;
     }
@@ -730,7 +787,7 @@ __global__ __launch_bounds__(kSelBlock) void sel_sort_kernel(const double *__res
         i = qi[e];
         return true;
     };
-    block_select_sort(get, tot, k, q, out_d, out_i);
+    block_select_sort(get, all, k, q, out_d, out_i, nov > 0);
 }
 
 // exact fallback: a block per listed query, the same select over every stored state (each
@@ -766,14 +823,15 @@ __global__ __launch_bounds__(kSelBlock) void sel_fallback_kernel(const double *_
 }
 
 struct SelLayout {
-    size_t q32, hist, inv, rc, rf, cntr, scnt, fb, cd, ci, di, total;
-    uint32_t chunks, chunk_len, slab, qb;
+    size_t q32, hist, inv, rc, rf, cntr, scnt, fb, ovc, cd, ci, ov, di, total;
+    uint32_t chunks, chunk_len, slab, ovcap, qb;
 };
 
 inline size_t sel_align(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // queries per batch and slab capacity: the slabs of a batch hold about 1.25 (k + 8 sqrt(8k) +
-// 1024) candidates per query spread over the chunks, plus slack for the spread between chunks
+// 1024) candidates per query spread over the chunks, plus slack for the spread between chunks;
+// what a chunk holds beyond its slab goes to the query's pool (as many slots as the estimate)
 SelLayout sel_layout(int FS, uint32_t nq, uint32_t k, uint64_t n_end, int num_cus) {
     SelLayout L{};
     Plan p = plan(std::min<uint32_t>(nq, 4096u), n_end, num_cus);
@@ -786,7 +844,8 @@ SelLayout sel_layout(int FS, uint32_t nq, uint32_t k, uint64_t n_end, int num_cu
     L.chunk_len = p.chunk_len;
     const double est = (double)k + 8.0 * std::sqrt(8.0 * k) + 1024.0;
     const double per = 1.25 * est / L.chunks;
-    L.slab = (uint32_t)std::ceil(per + 6.0 * std::sqrt(per) + 16.0);
+    L.slab = (uint32_t)std::ceil(per + 3.0 * std::sqrt(per) + 8.0);
+    L.ovcap = (uint32_t)std::ceil(est);
     L.qb = std::min<uint32_t>(nq, 4096u);
     size_t off = 0;
     auto take = [&](size_t b) {
@@ -802,24 +861,29 @@ SelLayout sel_layout(int FS, uint32_t nq, uint32_t k, uint64_t n_end, int num_cu
     L.cntr = take(4ull * L.qb);
     L.scnt = take(4ull * L.qb * L.chunks);
     L.fb = take(4ull * (L.qb + 1));
-    L.cd = take(8ull * L.qb * L.chunks * L.slab);
+    L.ovc = take(4ull * L.qb);
+    const size_t dense = (size_t)L.qb * ((size_t)L.chunks * L.slab + L.ovcap);
+    L.cd = take(8ull * dense);
     L.ci = take(4ull * L.qb * L.chunks * L.slab);
-    L.di = take(4ull * L.qb * L.chunks * L.slab);
+    L.ov = take(4ull * L.qb * L.ovcap);
+    L.di = take(4ull * dense);
     L.total = off;
     return L;
 }
 
 template <int SP, int F>
 hipError_t run_large_select(const DevSpace &sp, const double *f64, const float *f32, uint64_t cap, uint64_t n_end,
-                            const double *qf64, uint32_t nq, uint32_t k, float absmax, float dmax, double *out_d,
-                            uint32_t *out_i, void *ws, size_t ws_bytes, int num_cus, hipStream_t st) {
+                            const double *aos, int da, const double *qf64, uint32_t nq, uint32_t k, float absmax,
+                            float seta, float dmax, double *out_d, uint32_t *out_i, void *ws, size_t ws_bytes,
+                            int num_cus, hipStream_t st, unsigned long long *stats) {
     constexpr int FS = Row<SP, F>::FS;
     const SelLayout L = sel_layout(FS, nq, k, n_end, num_cus);
     if (ws_bytes < L.total) return hipErrorInvalidValue;
     char *w = (char *)ws;
     float *q32 = (float *)(w + L.q32), *inv = (float *)(w + L.inv), *rc = (float *)(w + L.rc), *rf = (float *)(w + L.rf);
     unsigned int *hist = (unsigned int *)(w + L.hist), *cntr = (unsigned int *)(w + L.cntr);
-    uint32_t *scnt = (uint32_t *)(w + L.scnt), *fb = (uint32_t *)(w + L.fb);
+    uint32_t *scnt = (uint32_t *)(w + L.scnt), *fb = (uint32_t *)(w + L.fb), *ovc = (uint32_t *)(w + L.ovc);
+    uint32_t *ov = (uint32_t *)(w + L.ov);
     double *cd = (double *)(w + L.cd);  // the dense exact distances of each query's candidates
     uint32_t *ci = (uint32_t *)(w + L.ci), *di = (uint32_t *)(w + L.di);
     const float w0 = SP == OMPL_GPU_SPACE_KCHAIN ? (float)sp.link : (float)sp.w0;
@@ -839,16 +903,17 @@ hipError_t run_large_select(const DevSpace &sp, const double *f64, const float *
         hipLaunchKernelGGL((hist_sample_kernel<SP, F>), grid, dim3(kTile), 0, st, f32, cap, n_end, bq32, nb,
                            L.chunk_len, kSampleB, w0, (float)sp.w1, sp.dim, (const float *)inv, 0.f, hist);
         hipLaunchKernelGGL((sel_radius_kernel<SP, F>), dim3((nb + 255) / 256), dim3(256), 0, st, hist, inv, bqf, nb, k,
-                           absmax, sp, rc, rf);
+                           absmax, seta, sp, rc, rf);
         if ((e = hipMemsetAsync(cntr, 0, 4ull * nb, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(ovc, 0, 4ull * nb, st)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(fb, 0, 4, st)) != hipSuccess) return e;
         if (q0 == 0) timer_begin(st, "sel_fill_kernel");
         hipLaunchKernelGGL((sel_fill_kernel<SP, F>), grid, dim3(kTile), 0, st, f32, f64, cap, n_end, bq32, bqf, nb,
-                           L.chunk_len, L.chunks, sp, rc, rf, L.slab, cd, ci, scnt, cntr);
+                           L.chunk_len, L.chunks, sp, rc, rf, L.slab, L.ovcap, ci, ov, ovc, scnt, cntr);
         if (q0 == 0) timer_end(st);
-        hipLaunchKernelGGL((sel_sort_kernel<SP, F>), dim3(nb), dim3(kSelBlock), 0, st, f64, cap, bqf, sp, ci, scnt,
-                           cntr, nb, L.chunks, L.slab, k, cd, di, out_d + (size_t)q0 * k, out_i + (size_t)q0 * k, fb,
-                           fb + 1);
+        hipLaunchKernelGGL((sel_sort_kernel<SP, F>), dim3(nb), dim3(kSelBlock), 0, st, f64, cap, aos, da, bqf, sp, ci,
+                           ov, ovc, L.ovcap, scnt, cntr, nb, L.chunks, L.slab, k, cd, di, out_d + (size_t)q0 * k,
+                           out_i + (size_t)q0 * k, fb, fb + 1, stats);
         hipLaunchKernelGGL((sel_fallback_kernel<SP, F>), dim3((unsigned)std::max(num_cus, 1)), dim3(kSelBlock), 0, st,
                            f64, cap, n_end, bqf, sp, k, fb, fb + 1, out_d + (size_t)q0 * k, out_i + (size_t)q0 * k);
     }
@@ -870,17 +935,19 @@ size_t knn_large_workspace_bytes(const DevSpace &sp, const FeatGeom &g, uint32_t
 }
 
 hipError_t launch_knn_large(const DevSpace &sp, const FeatGeom &g, const double *feat64, const float *feat32,
-                            uint64_t cap, uint64_t n_end, const double *qfeat64, uint32_t nq, uint32_t k, float absmax,
-                            float dmax, double *out_d, uint32_t *out_i, size_t mem_budget, int num_cus,
-                            hipStream_t st, void *ws, size_t ws_bytes) {
+                            uint64_t cap, uint64_t n_end, const double *aos, int da, const double *qfeat64, uint32_t nq,
+                            uint32_t k, float absmax, float seta, float dmax, double *out_d, uint32_t *out_i,
+                            size_t mem_budget, int num_cus, hipStream_t st, void *ws, size_t ws_bytes,
+                            unsigned long long *stats) {
     if (nq == 0 || k == 0) return hipSuccess;
     // k <= kLargeSelMaxK: the device-decided select (asynchronous); larger k: count, host offsets, fill
     const bool sel = k <= kLargeSelMaxK && ws && ws_bytes >= knn_large_workspace_bytes(sp, g, nq, k, n_end, num_cus);
 #define OMPL_AMD_LARGE(SPK, FK)                                                                                    \
-    return sel ? run_large_select<SPK, FK>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, dmax, out_d,    \
-                                           out_i, ws, ws_bytes, num_cus, st)                                       \
-               : run_large<SPK, FK>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, dmax, out_d, out_i,    \
-                                    mem_budget, num_cus, st)
+    return sel ? run_large_select<SPK, FK>(sp, feat64, feat32, cap, n_end, SPK == OMPL_GPU_SPACE_KCHAIN ? nullptr \
+                                           : aos, da, qfeat64, nq, k, absmax, seta, dmax, out_d, out_i, ws,        \
+                                           ws_bytes, num_cus, st, stats)                                           \
+               : run_large<SPK, FK>(sp, feat64, feat32, cap, n_end, qfeat64, nq, k, absmax, seta, dmax, out_d,     \
+                                    out_i, mem_budget, num_cus, st)
     switch (sp.kind) {
     case OMPL_GPU_SPACE_SE3:
         OMPL_AMD_LARGE(OMPL_GPU_SPACE_SE3, 7);

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
         load_state<DIM>(s1 + (size_t)e * dim, dim, a);
         load_state<DIM>(s2 + (size_t)e * dim, dim, b);
         ++checks;
-        result = valid_t<DIM>(sp, ck, b);  // :96 — s2 first, as the reference
+        result = valid_sp<SP, DIM>(sp, ck, b);  // :96 — s2 first, as the reference
         // the segment count (an arc cosine for SE3) only when something reads it: the sweep of a
         // motion whose s2 is valid, the lastValid sweep, or the caller
         const int nd = (result || nd_out || fi_out) ? (int)valid_segment_count(sp, a, b) : 0;
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
                     const int mid = (lo + hi) / 2;
                     interpolate(sp, a, b, (double)mid / (double)nd, t, rot != 0);
                     ++checks;
-                    if (!valid_t<DIM>(sp, ck, t)) result = false;
+                    if (!valid_sp<SP, DIM>(sp, ck, t)) result = false;
                 }
             }
         }
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
                 // linear sweep :57-69, then s2 :73-79
                 for (int j = 1; j < nd; ++j) {
                     interpolate(sp, a, b, (double)j / (double)nd, t, rot != 0);
-                    if (!valid_t<DIM>(sp, ck, t)) {
+                    if (!valid_sp<SP, DIM>(sp, ck, t)) {
                         fi = j;
                         break;
                     }
@@ -123,11 +123,12 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void state_valid_kern
     if (i >= m) return;
     double a[Width<DIM>::N];
     load_state<DIM>(s + (size_t)i * sp.dim, sp.dim, a);
-    valid[i] = valid_t<DIM>(sp, ck, a) ? 1 : 0;
+    valid[i] = valid_sp<SP, DIM>(sp, ck, a) ? 1 : 0;
 }
 
 // the specialisations: SE3 (7 reals), SO3 (4), R^2 / R^3 / R^6 (the closed checker set's
-// spaces); everything else (other R^n, KinematicChain) takes the runtime-width form.  A
+// spaces), the 12-link KinematicChain; everything else (other R^n, other chains) takes the
+// runtime-width form.  A
 // hypercube over more coordinates than the fixed width, and the KinematicChain checker, never
 // take a fixed form.
 template <class F>
@@ -135,6 +136,12 @@ static hipError_t dispatch_width(const DevSpace &sp, const DevChecker &ck, F &&l
     const bool fixed_ok = (ck.kind == OMPL_GPU_CHECK_ALL_VALID || ck.kind == OMPL_GPU_CHECK_SPHERES ||
                            ck.kind == OMPL_GPU_CHECK_CIRCLES2D ||
                            (ck.kind == OMPL_GPU_CHECK_HYPERCUBE && ck.ndim <= sp.dim));
+    // the KinematicChain benchmark's 12 links (KinematicChainBenchmark.cpp:48): its checker or none
+#if !(defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 10)  // A/B build: the runtime-width form
+    if (sp.kind == OMPL_GPU_SPACE_KCHAIN && sp.dim == 12 &&
+        (ck.kind == OMPL_GPU_CHECK_KCHAIN || ck.kind == OMPL_GPU_CHECK_ALL_VALID))
+        return launch(std::integral_constant<int, OMPL_GPU_SPACE_KCHAIN>{}, std::integral_constant<int, 12>{});
+#endif
     if (fixed_ok) {
         if (sp.kind == OMPL_GPU_SPACE_SE3 && sp.dim == 7) return launch(std::integral_constant<int, OMPL_GPU_SPACE_SE3>{}, std::integral_constant<int, 7>{});
         if (sp.kind == OMPL_GPU_SPACE_SO3 && sp.dim == 4) return launch(std::integral_constant<int, OMPL_GPU_SPACE_SO3>{}, std::integral_constant<int, 4>{});

@@ -142,6 +142,13 @@ class NearestNeighborsGPU(abi.Handle):
         abi.check(abi.lib.ompl_gpu_nn_rerun_stats(self._h, C.byref(a)))
         return a.value
 
+    def large_stats(self) -> tuple[int, int]:
+        """Large-k select: (queries whose candidates spilled to the per-query pool, queries re-run
+        on the exact fallback), summed over calls."""
+        a, b = C.c_uint64(), C.c_uint64()
+        abi.check(abi.lib.ompl_gpu_nn_large_stats(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def build_index(self) -> None:
         """Bring the culled walks' sorted copy up to date now (asynchronous on the handle's stream)."""
         abi.check(abi.lib.ompl_gpu_nn_build_index(self._h))

@@ -93,3 +93,25 @@ def test_large_k_heavy_ties_take_the_exact_fallback(gpu):
         oi, od, _ = O.knn(sp, data, q, k)
         np.testing.assert_array_equal(ids.astype(np.int64), oi.astype(np.int64))  # ties: ids ascending
         assert_knn_parity(ids, d, oi, od, k)
+
+
+def test_large_k_spatially_sorted_store(gpu):
+    """A store whose id order follows space (states added in a sweep: sorted by x): a query's
+    ~k candidates sit in a few contiguous id chunks, so the fill pass's per-(query, chunk) slabs
+    overflow.  The overflow goes to the query's pool (ompl_gpu_nn_large_stats: spilled), not to the
+    exact fallback, and the answers still equal the oracle's, (distance, id) order included."""
+    rng = np.random.default_rng(82)
+    sp = SE3StateSpace()
+    data = W.uniform_se3(rng, 100_000)
+    data = data[np.argsort(data[:, 0], kind="stable")]
+    q = W.uniform_se3(rng, 64)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    k = W.rrt_star_k(len(data), 6)
+    ids, d, cnt = nn.nearestKBatch(q, k)
+    spilled, exact = nn.large_stats()
+    assert (cnt == k).all()
+    assert spilled > 0, "the sorted store should overflow the per-chunk slabs"
+    assert exact == 0, f"{exact} queries took the exact fallback"
+    oi, od, _ = O.knn(sp, data, q, k + 8)
+    assert_knn_parity(ids, d, oi, od, k)

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/r4a; mkdir -p "$out"
-timeout -k 10 300 python -u -m pytest tests/test_gpu_spaces.py -x -q --timeout 120 --timeout-method thread > "$out/spaces.log" 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests/test_gpu_spaces.py tests/test_gpu_large_k.py -x -q --timeout 120 --timeout-method thread > "$out/spaces.log" 2>&1; rc=$?
 tail -3 "$out/spaces.log"; case $rc in 124|134|137|139) exit 1;; esac
 s=$(date +%s)
 timeout -k 10 400 python -u bench.py --workload cfg5 --bitstar-knn --steps 10 --warmup 2 --cpu-seconds 8 \
@@ -15,4 +15,4 @@ s=$(date +%s)
 timeout -k 10 590 python -u bench.py --steps 20 --warmup 5 > "$out/default.json" 2> "$out/default.err" || { echo "default rc=$?"; tail -5 "$out/default.err"; exit 1; }
 echo "default wall $(( $(date +%s) - s )) s"
 bash tools/prof_workload.sh cfg5 r4_cfg5k --bitstar-knn || { echo "prof rc=$?"; exit 1; }
-bash tools/ab_bench.sh "cfg5" "5 6" 2 && bash tools/ab_bench.sh "cfg3" "7" 3
+
