@@ -100,8 +100,8 @@ def parse():
                          f"{','.join(SUB_WORKLOADS)} when the headline is cfg3 replicated, 'none', or a comma list")
     ap.add_argument("--sub-cpu-seconds", type=float, default=6.0, help="CPU baseline budget of each sub-workload")
     a = ap.parse_args()
-    if a.partition == "tree" and a.workload != "cfg3":
-        ap.error("--partition tree is implemented for --workload cfg3")
+    if a.partition == "tree" and (a.workload not in ("cfg3", "cfg5") or a.bitstar_knn):
+        ap.error("--partition tree is implemented for --workload cfg3 and the cfg5 radius mode")
     t, q, k = DEFAULTS[a.workload]
     a.tree = t if a.tree is None else a.tree
     a.queries = q if a.queries is None else a.queries
@@ -563,7 +563,8 @@ class Runner:
             self.tree, q = tree, np.ascontiguousarray(qa[r0 * nq:(r0 + 1) * nq])
         elif wl == "cfg5":  # sample sets hold valid states (ImplicitGraph.cpp:981)
             self.tree, qa = shared_inputs("cfg5", self.sp, args.tree, nq * world, self.mv.isValid, dist, dev)
-            q = np.ascontiguousarray(qa[rank * nq:(rank + 1) * nq])
+            r0 = 0 if self.tree_mode else rank  # tree mode: every shard answers the same vertices
+            q = np.ascontiguousarray(qa[r0 * nq:(r0 + 1) * nq])
         else:  # cfg4: roadmap + the milestones of every step: valid states (PRM.cpp:356-378)
             # one causal batch per step holds world * nq milestones of the query stream; every rank
             # inserts the whole batch (replicas stay identical) and computes the neighbours and edges
@@ -586,6 +587,7 @@ class Runner:
             self.rank = rank
             self.lo, self.hi = shard_bounds(len(self.tree), rank, self.world)
             self.nn.add(self.tree[self.lo:self.hi])
+            self.owned = torch.zeros((), dtype=torch.int64, device=dev)
         else:
             self.nn.add(self.tree)
         self.nn.set_stream(stream.cuda_stream)
@@ -624,7 +626,7 @@ class Runner:
                     e[j].record(self.stream)
             return
         if self.tree_mode:
-            self.step_tree(e)
+            (self.step_tree_radius if a.workload == "cfg5" else self.step_tree)(e)
             return
         if e:
             e[0].record(self.stream)
@@ -654,6 +656,39 @@ class Runner:
         if e:
             e[3].record(self.stream)
 
+    def step_tree_radius(self, e=None):
+        """Tree-sharded BIT* batch (cfg5 radius): every rank answers every vertex's nearestR on its
+        slice of the samples; the per-shard CSR results (global ids) are exchanged — a count
+        all_gather, then padded id / distance all_gathers over RCCL — and merged by the library's
+        kernel (ompl_gpu_csr_merge_device), so every rank holds each vertex's whole neighbourhood
+        (NearestNeighborsGNAT.h:236-245); each edge (vertex, sample) is checked by the rank that
+        stores the sample (BITstar.cpp:815), from its own rows, so no state rows travel."""
+        import torch
+
+        from ompl_amd.shard import allgather_radius, merge_csr_device
+
+        nn, mv, q = self.nn, self.mv, self.queries
+        with torch.cuda.stream(self.stream):
+            if e:
+                e[0].record(self.stream)
+            self.m = nn.radius_device(q.data_ptr(), self.nq, self.radius, self.off.data_ptr(), self.ids.data_ptr(),
+                                      self.dd.data_ptr(), self.cap)
+            gid = self.ids[: self.m].to(torch.int64) + self.lo
+            if self.world > 1:
+                self._merged = allgather_radius(self.off, gid, self.dd[: self.m])
+            else:
+                self._merged = merge_csr_device(self.off[None], gid[None].to(torch.int32), self.dd[None, : self.m],
+                                                self.m, stream=self.stream.cuda_stream)
+            if e:
+                e[1].record(self.stream)
+            nn.edges_device(q.data_ptr(), self.nq, self.off.data_ptr(), self.ids.data_ptr(), 0, self.m, True,
+                            self.s_from.data_ptr(), self.s_to.data_ptr())
+            if e:
+                e[2].record(self.stream)
+            mv.check_device(self.s_from.data_ptr(), self.s_to.data_ptr(), self.m, self.valid.data_ptr())
+            if e:
+                e[3].record(self.stream)
+
     def step_tree(self, e=None):
         """Tree-sharded step: every rank answers the whole batch on its shard, the per-shard top-k
         lists (global ids) are exchanged with an all_gather over RCCL and merged by the library's
@@ -677,25 +712,27 @@ class Runner:
                 md, mi = merge_topk_device(self.dd[None], gid[None].to(torch.int32), self.k,
                                            stream=self.stream.cuda_stream)
             near = mi[:, 0].to(torch.int64)
-            mine = torch.nonzero((near >= self.lo) & (near < self.hi)).flatten()
-            self.m = int(mine.numel())
-            qs = q[mine].contiguous()
-            nl = (near[mine] - self.lo).to(torch.int32).contiguous()
-            self._keep = (qs, nl)
-            if self.m:
-                nn.steer_device(qs.data_ptr(), self.m, nl.data_ptr(), 1, self.maxd, self.s_from.data_ptr(),
-                                self.s_to.data_ptr())
+            # no host round trip: every sample is steered, the ones whose nearest state another
+            # rank owns with a missing id (from = to = the sample: a zero-length motion, one
+            # isValid) — the owned count stays on the device until the timed loop is over
+            mine = (near >= self.lo) & (near < self.hi)
+            nl = torch.where(mine, near - self.lo, -1).to(torch.int32)
+            self.owned = self.owned + mine.sum()
+            self.last_owned = mine.sum()
+            self._keep = nl
+            nn.steer_device(q.data_ptr(), self.nq, nl.data_ptr(), 1, self.maxd, self.s_from.data_ptr(),
+                            self.s_to.data_ptr())
             if e:
                 e[2].record(self.stream)
-            if self.m:
-                mv.check_device(self.s_from.data_ptr(), self.s_to.data_ptr(), self.m, self.valid.data_ptr())
+            mv.check_device(self.s_from.data_ptr(), self.s_to.data_ptr(), self.nq, self.valid.data_ptr())
             if e:
                 e[3].record(self.stream)
 
     def units_per_step(self):
-        if self.tree_mode:  # the batch's queries once (rank 0), the motion checks of every rank
-            return (self.nq if self.rank == 0 else 0) + self.m
-        """NN queries + motion checks one step issues on this rank."""
+        """NN queries + motion checks one step issues on this rank (tree mode: the batch's queries
+        once, on rank 0; the owned motion checks are summed on the device, see owned_units)."""
+        if self.tree_mode:  # cfg5: each edge is checked by the rank storing its sample
+            return (self.nq if self.rank == 0 else 0) + (self.m if self.args.workload == "cfg5" else 0)
         if self.args.workload == "cfg2":
             return self.nq
         return self.nq + self.m
@@ -715,7 +752,14 @@ class Runner:
         a = self.args
         base = {"tree_states": a.tree, "queries_per_gpu": self.nq,
                 "parallelism": f"queries sharded over {world} GPU(s), tree replicated"}
-        if self.tree_mode:
+        if self.tree_mode and a.workload == "cfg5":
+            base.update(queries_per_gpu=None, queries_per_step=self.nq, partition="tree",
+                        parallelism=(f"sample set sharded over {world} GPU(s) ({a.tree // world} samples each), every "
+                                     f"vertex's nearestR answered on every shard, the per-shard CSR results exchanged "
+                                     f"(count all_gather + padded id / distance all_gathers over RCCL) and merged on "
+                                     f"the device; each edge checked by the rank storing its sample"),
+                        exchange_bytes_per_rank=(self.nq + 1) * 8 + self.m * 12)
+        elif self.tree_mode:
             base.update(queries_per_gpu=None, queries_per_step=self.nq, partition="tree",
                         parallelism=(f"tree sharded over {world} GPU(s) ({a.tree // world} states each), every sample "
                                      f"answered on every shard, per-shard top-{self.k} lists all_gathered (RCCL) and "
@@ -857,6 +901,8 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
     for _ in range(args.warmup):
         run.step()
     torch.cuda.synchronize(dev)
+    if run.tree_mode and args.workload == "cfg3":
+        run.owned = torch.zeros((), dtype=torch.int64, device=dev)
     run.nn.profile(True)
     run.nn.kernel_time()
     scr0, fb0 = run.nn.stats()
@@ -874,6 +920,9 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    if run.tree_mode and args.workload == "cfg3":  # motion checks of the samples whose nearest state this rank owns
+        units += int(run.owned.item())
+        run.m = int(run.last_owned.item())
     kern_ms_total, kern_n, kern_name = run.nn.kernel_time()
     kern_ms = kern_ms_total / max(kern_n, 1)
     run.nn.profile(False)

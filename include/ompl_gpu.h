@@ -39,6 +39,7 @@
  *   ompl_gpu_rrt_grow_device  the RRT loop itself                 RRT.cpp:128-192
  *   ompl_gpu_prm_add_milestones  PRM* causal roadmap batches      prm/src/PRM.cpp:562-596
  *   ompl_gpu_knn_merge_device  per-shard nearestK lists -> global top k (tree-sharded mode)
+ *   ompl_gpu_csr_merge_device  per-shard nearestR CSR results -> one CSR (tree-sharded mode)
  *   ompl_gpu_nn_edges_device  the edges PRM / BIT* check after a neighbour query
  *                          prm/src/PRM.cpp:577-582, informedtrees/src/BITstar.cpp:815
  *
@@ -235,7 +236,8 @@ ompl_gpu_status ompl_gpu_nn_edges_device(ompl_gpu_nn *h, const double *d_queries
                                          double *d_from, double *d_to);
 /* RRT extend on device: for each query q with nearest id nid[q*stride]:
  * from = state[nid]; to = q; if d(from,q) > max_distance, to = interpolate(from,
- * q, max_distance/d).  Writes AoS from/to rows (RRT.cpp:137-146). */
+ * q, max_distance/d).  Writes AoS from/to rows (RRT.cpp:137-146).  A missing id (0xFFFFFFFF)
+ * gives from = to = q (a motion of length 0: checkMotion then tests q alone). */
 ompl_gpu_status ompl_gpu_steer_device(ompl_gpu_nn *h, const double *d_queries, size_t nq,
                                       const uint32_t *d_nearest, uint32_t stride, double max_distance,
                                       double *d_from, double *d_to);
@@ -341,6 +343,15 @@ ompl_gpu_status ompl_gpu_rrt_grow_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const
  * pointers, asynchronous on `stream` (a hipStream_t; NULL = the null stream).  lists <= 64. */
 ompl_gpu_status ompl_gpu_knn_merge_device(const double *d_dist, const uint32_t *d_ids, uint32_t lists, size_t nq,
                                           uint32_t k, double *d_out_dist, uint32_t *d_out_ids, void *stream);
+/* Tree-sharded nearestR (SURVEY §8e "Radius search"): `lists` shards' CSR results of the same nq
+ * queries — shard l: offsets d_offsets[l * (nq + 1) + 0..nq] (uint64), ids (global, uint32) and
+ * distances at d_ids / d_dist + l * stride, each segment sorted by (distance, id) — merged into
+ * one CSR: d_out_offsets[nq + 1], segment q the union of the shards' segments in (distance, id)
+ * order (NearestNeighborsGNAT.h:236-245).  d_out_ids / d_out_dist hold sum_l d_offsets[l][nq]
+ * entries.  Device pointers, asynchronous on `stream`.  lists <= 1024. */
+ompl_gpu_status ompl_gpu_csr_merge_device(const uint64_t *d_offsets, uint32_t lists, size_t nq, const uint32_t *d_ids,
+                                          const double *d_dist, size_t stride, uint64_t *d_out_offsets,
+                                          uint32_t *d_out_ids, double *d_out_dist, void *stream);
 /* Persistent RRT runs that gave up and were re-run in the two-launch form (diagnostics). */
 ompl_gpu_status ompl_gpu_rrt_aborts(const ompl_gpu_nn *nn, uint64_t *aborts);
 ompl_gpu_status ompl_gpu_rrt_solve_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const double *d_samples, size_t ns,

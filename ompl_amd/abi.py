@@ -99,6 +99,7 @@ SIGNATURES = {
     "ompl_gpu_nn_edges_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P, C.c_uint32, C.c_size_t, C.c_int, _P, _P]),
     "ompl_gpu_rrt_grow_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, _P, _P]),
     "ompl_gpu_rrt_aborts": (C.c_int, [_P, _U64]),
+    "ompl_gpu_csr_merge_device": (C.c_int, [_P, C.c_uint32, C.c_size_t, _P, _P, C.c_size_t, _P, _P, _P, _P]),
     "ompl_gpu_knn_merge_device": (C.c_int, [_P, _P, C.c_uint32, C.c_size_t, C.c_uint32, _P, _P, _P]),
     "ompl_gpu_rrt_solve_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, _D, C.c_double, _P, _P, _U64,
                                             _U32, _D]),

@@ -1691,6 +1691,18 @@ ompl_gpu_status ompl_gpu_knn_merge_device(const double *d_dist, const uint32_t *
     return OMPL_GPU_OK;
 }
 
+ompl_gpu_status ompl_gpu_csr_merge_device(const uint64_t *d_offsets, uint32_t lists, size_t nq, const uint32_t *d_ids,
+                                          const double *d_dist, size_t stride, uint64_t *d_out_offsets,
+                                          uint32_t *d_out_ids, double *d_out_dist, void *stream) {
+    if (nq && (!d_offsets || !d_out_offsets || ((!d_ids || !d_dist) && stride) || !d_out_ids || !d_out_dist))
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (lists == 0 || lists > 1024) return fail(OMPL_GPU_ERR_INVALID_ARG, "lists must be in [1, 1024]");
+    if (nq > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many queries in one call");
+    HIP_OR_FAIL(launch_csr_merge(d_offsets, lists, (uint32_t)nq, d_ids, d_dist, stride, d_out_offsets, d_out_ids,
+                                 d_out_dist, (hipStream_t)stream));
+    return OMPL_GPU_OK;
+}
+
 ompl_gpu_status ompl_gpu_rrt_aborts(const ompl_gpu_nn *h, uint64_t *aborts) {
     if (!h || !aborts) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
     *aborts = h->rrt_aborts;

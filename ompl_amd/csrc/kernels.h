@@ -283,6 +283,8 @@ hipError_t launch_features(const DevSpace &sp, const FeatGeom &g, const double *
 hipError_t launch_store_soa(const double *aos, uint32_t n, int width, double *soa, uint64_t cap, uint64_t first,
                             hipStream_t st);
 // tree-sharded kNN: merge `lists` per-shard [nq][k] lists (each sorted by (distance, id)) into one
+hipError_t launch_csr_merge(const uint64_t *offs, uint32_t lists, uint32_t nq, const uint32_t *ids, const double *d,
+                            uint64_t stride, uint64_t *out_off, uint32_t *out_i, double *out_d, hipStream_t st);
 hipError_t launch_topk_merge(const double *d, const uint32_t *ids, uint32_t lists, uint32_t nq, uint32_t k, double *od,
                              uint32_t *oi, hipStream_t st);
 // RRT steer: from = raw[nearest], to = q or interpolate(from, q, maxd/d)

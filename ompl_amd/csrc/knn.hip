@@ -480,8 +480,8 @@ __global__ void steer_kernel(DevSpace sp_in, const double *__restrict__ raw, uin
     double a[Width<W>::N], b[Width<W>::N], o[Width<W>::N];
     const uint32_t nid = nearest[(size_t)i * stride];
     for (int c = 0; c < dim; ++c) {
-        a[c] = raw[(uint64_t)c * cap + nid];
         b[c] = q[(size_t)i * dim + c];
+        a[c] = nid < cap ? raw[(uint64_t)c * cap + nid] : b[c];  // a missing id (kNoId): from = to = q
     }
     const double d = raw_distance(sp, a, b);  // si_->distance(nmotion->state, rstate)  RRT.cpp:141
     if (d > maxd) {
@@ -870,34 +870,51 @@ hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uin
     return hipGetLastError();
 }
 
-// tree-sharded kNN: the per-shard lists of every query (lists x nq x k, each sorted by
-// (distance, id), missing = (+inf, kNoId)) merged into the global top k by (distance, id) — a
-// thread per query, a lists-way merge of heads
-__global__ void topk_merge_kernel(const double *__restrict__ d, const uint32_t *__restrict__ ids, uint32_t lists,
-                                  uint32_t nq, uint32_t k, double *__restrict__ od, uint32_t *__restrict__ oi) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= nq) return;
-    constexpr uint32_t kMaxLists = 64;
-    uint32_t head[kMaxLists];
-    for (uint32_t l = 0; l < lists; ++l) head[l] = 0;
-    for (uint32_t j = 0; j < k; ++j) {
-        uint32_t best = kMaxLists;
-        double bd = __builtin_inf();
-        uint32_t bi = kNoId;
-        for (uint32_t l = 0; l < lists; ++l) {
-            if (head[l] >= k) continue;
-            const size_t o = ((size_t)l * nq + q) * k + head[l];
-            const double x = d[o];
-            const uint32_t xi = ids[o];
-            if (xi != kNoId && (x < bd || (x == bd && xi < bi))) {
-                bd = x;
-                bi = xi;
-                best = l;
-            }
+// tree-sharded kNN / nearestR: per-shard results of the same queries merged by rank placement
+// (merge path): every element's place in the merged order is its index in its own sorted list
+// plus, for every other list, the number of that list's elements ordered before it (a binary
+// search) — no per-thread list heads, no data-dependent loop over the lists.  Keys are (distance,
+// id), ids are global and distinct across shards, so the places are a permutation.
+__device__ __forceinline__ uint32_t count_before(const double *__restrict__ d, const uint32_t *__restrict__ ids,
+                                                 uint64_t b, uint32_t L, double x, uint32_t xi) {
+    uint32_t lo = 0, hi = L;  // first position whose key is not below (x, xi)
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (lex_less(d[b + mid], ids[b + mid], x, xi))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// lists x nq x k, each sorted by (distance, id), missing = (+inf, kNoId) at the end: thread per
+// (query, list, entry)
+__global__ __launch_bounds__(256) void topk_merge_kernel(const double *__restrict__ d, const uint32_t *__restrict__ ids,
+                                                         uint32_t lists, uint32_t nq, uint32_t k,
+                                                         double *__restrict__ od, uint32_t *__restrict__ oi) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)nq * lists * k) return;
+    const uint32_t j = (uint32_t)(t % k), w = (uint32_t)((t / k) % lists), q = (uint32_t)(t / ((uint64_t)k * lists));
+    auto base = [&](uint32_t l) { return ((uint64_t)l * nq + q) * k; };
+    const double x = d[base(w) + j];
+    const uint32_t xi = ids[base(w) + j];
+    if (xi != kNoId) {
+        uint32_t rank = j;
+        for (uint32_t l = 0; l < lists; ++l)
+            if (l != w) rank += count_before(d, ids, base(l), k, x, xi);
+        if (rank < k) {
+            od[(size_t)q * k + rank] = x;
+            oi[(size_t)q * k + rank] = xi;
         }
-        if (best != kMaxLists) ++head[best];
-        od[(size_t)q * k + j] = bd;
-        oi[(size_t)q * k + j] = bi;
+    }
+    if (w == 0) {  // the entries past every list's valid ones are missing
+        uint32_t valid = 0;
+        for (uint32_t l = 0; l < lists; ++l) valid += count_before(d, ids, base(l), k, __builtin_inf(), kNoId);
+        if (j >= valid) {
+            od[(size_t)q * k + j] = __builtin_inf();
+            oi[(size_t)q * k + j] = kNoId;
+        }
     }
 }
 
@@ -905,7 +922,55 @@ hipError_t launch_topk_merge(const double *d, const uint32_t *ids, uint32_t list
                              uint32_t *oi, hipStream_t st) {
     if (nq == 0 || k == 0) return hipSuccess;
     if (lists == 0 || lists > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(topk_merge_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, d, ids, lists, nq, k, od, oi);
+    const uint64_t n = (uint64_t)nq * lists * k;
+    hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, ids, lists, nq, k, od,
+                       oi);
+    return hipGetLastError();
+}
+
+// lists CSR results of the same nq queries (list l: offsets offs[l][0..nq], payload ids / d at
+// l * stride, each segment sorted by (distance, id)) -> one CSR: out_off[q] = sum_l offs[l][q]
+// (the offsets are exclusive prefix sums), segment q holding the union in (distance, id) order.
+// Block per query.
+__global__ __launch_bounds__(64) void csr_merge_kernel(const uint64_t *__restrict__ offs, uint32_t lists, uint32_t nq,
+                                                       const uint32_t *__restrict__ ids, const double *__restrict__ d,
+                                                       uint64_t stride, uint64_t *__restrict__ out_off,
+                                                       uint32_t *__restrict__ out_i, double *__restrict__ out_d) {
+    const uint32_t q = blockIdx.x;
+    uint64_t ob = 0;
+    for (uint32_t l = 0; l < lists; ++l) ob += offs[(uint64_t)l * (nq + 1) + q];
+    if (threadIdx.x == 0) {
+        out_off[q] = ob;
+        if (q + 1 == nq) {
+            uint64_t e = 0;
+            for (uint32_t l = 0; l < lists; ++l) e += offs[(uint64_t)l * (nq + 1) + nq];
+            out_off[nq] = e;
+        }
+    }
+    for (uint32_t w = 0; w < lists; ++w) {
+        const uint64_t bw = offs[(uint64_t)w * (nq + 1) + q];
+        const uint32_t Lw = (uint32_t)(offs[(uint64_t)w * (nq + 1) + q + 1] - bw);
+        for (uint32_t j = threadIdx.x; j < Lw; j += blockDim.x) {
+            const double x = d[(uint64_t)w * stride + bw + j];
+            const uint32_t xi = ids[(uint64_t)w * stride + bw + j];
+            uint64_t rank = j;
+            for (uint32_t l = 0; l < lists; ++l) {
+                if (l == w) continue;
+                const uint64_t bl = offs[(uint64_t)l * (nq + 1) + q];
+                const uint32_t Ll = (uint32_t)(offs[(uint64_t)l * (nq + 1) + q + 1] - bl);
+                rank += count_before(d, ids, (uint64_t)l * stride + bl, Ll, x, xi);
+            }
+            out_d[ob + rank] = x;
+            out_i[ob + rank] = xi;
+        }
+    }
+}
+
+hipError_t launch_csr_merge(const uint64_t *offs, uint32_t lists, uint32_t nq, const uint32_t *ids, const double *d,
+                            uint64_t stride, uint64_t *out_off, uint32_t *out_i, double *out_d, hipStream_t st) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(csr_merge_kernel, dim3(nq), dim3(64), 0, st, offs, lists, nq, ids, d, stride, out_off, out_i,
+                       out_d);
     return hipGetLastError();
 }
 

@@ -61,6 +61,36 @@ def merge_topk_device(d_stack: torch.Tensor, ids_stack: torch.Tensor, k: int, st
     return od, oi
 
 
+def ids_int64(ids32: torch.Tensor) -> torch.Tensor:
+    """uint32 ids held in an int32 tensor -> int64 with the missing marker 0xFFFFFFFF as -1 (ids
+    at or above 2^31 stay positive: the library stores up to 2^32 - 16 states)."""
+    u = ids32.to(torch.int64) & 0xFFFFFFFF
+    return torch.where(u == 0xFFFFFFFF, torch.full_like(u, -1), u)
+
+
+def merge_csr_device(offs: torch.Tensor, ids: torch.Tensor, dists: torch.Tensor, total: int, stream=None):
+    """W shards' CSR results of the same queries on the GPU — offs [W, Q+1] int64, ids [W, S]
+    int32 (global ids), dists [W, S] fp64, as the padded all_gathers leave them — merged by the
+    library's HIP kernel (ompl_gpu_csr_merge_device).  Returns (offsets int64 [Q+1], ids int32,
+    distances fp64) with `total` = the sum of the shards' counts."""
+    import ctypes as C
+
+    from . import abi
+
+    W, Q1 = offs.shape
+    dev = offs.device
+    offs, ids, dists = offs.to(torch.int64).contiguous(), ids.to(torch.int32).contiguous(), dists.contiguous()
+    oo = torch.empty(Q1, dtype=torch.int64, device=dev)
+    oi = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+    od = torch.empty(max(total, 1), dtype=torch.float64, device=dev)
+    st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    abi.check(abi.lib.ompl_gpu_csr_merge_device(C.c_void_p(offs.data_ptr()), int(W), int(Q1 - 1),
+                                                C.c_void_p(ids.data_ptr()), C.c_void_p(dists.data_ptr()),
+                                                int(ids.shape[1]), C.c_void_p(oo.data_ptr()), C.c_void_p(oi.data_ptr()),
+                                                C.c_void_p(od.data_ptr()), C.c_void_p(st)))
+    return oo, oi[:total], od[:total]
+
+
 def allgather_merge(d_local: torch.Tensor, ids_global: torch.Tensor, k: int, group=None):
     """Exchange per-rank [Q, k] candidate lists (global ids, missing = -1) and merge to the global
     top-k.  GPU tensors (RCCL): one all_gather per array into a [W, Q, k] stack, merged by the HIP
@@ -74,7 +104,7 @@ def allgather_merge(d_local: torch.Tensor, ids_global: torch.Tensor, k: int, gro
         dist.all_gather_into_tensor(ds, d_local.contiguous(), group=group)
         dist.all_gather_into_tensor(ii, ids_global.to(torch.int32).contiguous(), group=group)
         od, oi = merge_topk_device(ds, ii, k)
-        return od, oi.to(torch.int64)
+        return od, ids_int64(oi)
     ds = [torch.empty_like(d_local) for _ in range(world)]
     ii = [torch.empty_like(ids_global) for _ in range(world)]
     dist.all_gather(ds, d_local.contiguous(), group=group)
@@ -139,6 +169,24 @@ def allgather_radius(offsets: torch.Tensor, ids_global: torch.Tensor, dists: tor
     all_gather followed by padded payload all_gathers, and merged on every rank."""
     tot = int(offsets[-1])
     ids_global, dists = ids_global[:tot], dists[:tot]
+    if offsets.is_cuda:  # RCCL: padded payload all_gathers, merged by the library's kernel
+        import torch.distributed as dist
+
+        world = dist.get_world_size(group)
+        offs = torch.empty((world, offsets.numel()), dtype=torch.int64, device=offsets.device)
+        dist.all_gather_into_tensor(offs, offsets.to(torch.int64).contiguous(), group=group)
+        counts = offs[:, -1].tolist()
+        m = max(max(counts), 1)
+        pi = torch.zeros(m, dtype=torch.int32, device=offsets.device)
+        pd = torch.zeros(m, dtype=torch.float64, device=offsets.device)
+        pi[:tot] = ids_global.to(torch.int32)
+        pd[:tot] = dists
+        ii = torch.empty((world, m), dtype=torch.int32, device=offsets.device)
+        dd = torch.empty((world, m), dtype=torch.float64, device=offsets.device)
+        dist.all_gather_into_tensor(ii, pi, group=group)
+        dist.all_gather_into_tensor(dd, pd, group=group)
+        oo, oi, od = merge_csr_device(offs, ii, dd, int(sum(counts)))
+        return oo, ids_int64(oi), od
     offs, _ = _allgather_varlen(offsets.to(torch.int64).contiguous(), group)
     ii, _ = _allgather_varlen(ids_global.to(torch.int64).contiguous(), group)
     dd, _ = _allgather_varlen(dists.contiguous(), group)

@@ -143,6 +143,18 @@ def _exchange_worker(rank, world, port, result_dir, use_gpu):
         assert torch.equal(dd.cpu(), d) and torch.equal(di.cpu().to(torch.int64), i)
     goff, gi, gd = allgather_radius(torch.from_numpy(off.astype(np.int64)),
                                     torch.from_numpy(ri.astype(np.int64) + lo), torch.from_numpy(rd))
+    if use_gpu:  # the device CSR merge kernel on the gathered (padded) shard results gives the same CSR
+        from ompl_amd.shard import _allgather_varlen, ids_int64, merge_csr_device
+
+        offs, _ = _allgather_varlen(torch.from_numpy(off.astype(np.int64)))
+        ii, cnt = _allgather_varlen(torch.from_numpy(ri.astype(np.int64) + lo))
+        dd2, _ = _allgather_varlen(torch.from_numpy(rd))
+        m = max(max(cnt), 1)
+        pi = torch.stack([torch.cat([x, torch.zeros(m - len(x), dtype=x.dtype)]) for x in ii]).to(torch.int32)
+        pd = torch.stack([torch.cat([x, torch.zeros(m - len(x), dtype=x.dtype)]) for x in dd2])
+        oo, oi2, od2 = merge_csr_device(torch.stack(offs).cuda(), pi.cuda(), pd.cuda(), int(sum(cnt)))
+        torch.cuda.synchronize()
+        assert torch.equal(oo.cpu(), goff) and torch.equal(ids_int64(oi2).cpu(), gi) and torch.equal(od2.cpu(), gd)
     # a batch of new states: rank r contributes r + 3 of them; every rank gets all, rank order
     mine = torch.full((rank + 3, 7), float(rank), dtype=torch.float64)
     batch = allgather_states(mine)
@@ -215,3 +227,53 @@ def test_bench_spawn_plumbing():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "--gpus 4 but WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.gpu
+def test_merge_kernels_random_lists(gpu):
+    """The merge-path kernels alone: W sorted shard lists with missing tails (top-k) and ragged
+    CSR segments (radius), global ids above 2^31 included, against a torch reference."""
+    from ompl_amd.shard import ids_int64, merge_csr_device, merge_topk, merge_topk_device
+
+    g = torch.Generator().manual_seed(5)
+    W, Q, k = 5, 300, 12
+    d = torch.rand((W, Q, k), generator=g, dtype=torch.float64)
+    d[:, :, 3] = d[:, :, 2]  # equal distances across lists: ids decide
+    ids = torch.randperm(W * Q * k, generator=g).reshape(W, Q, k).to(torch.int64) + (1 << 31)
+    valid = torch.rand((W, Q, k), generator=g) < 0.8
+    d = torch.where(valid, d, torch.full_like(d, float("inf")))
+    ids = torch.where(valid, ids, torch.full_like(ids, -1))
+    key = torch.where(ids < 0, torch.full_like(ids, 1 << 40), ids)
+    o = torch.argsort(key, dim=2, stable=True)
+    d, ids = torch.gather(d, 2, o), torch.gather(ids, 2, o)
+    o = torch.argsort(d, dim=2, stable=True)
+    d, ids = torch.gather(d, 2, o), torch.gather(ids, 2, o)
+    rd, ri = merge_topk(d.permute(1, 0, 2).reshape(Q, W * k), ids.permute(1, 0, 2).reshape(Q, W * k), k)
+    md, mi = merge_topk_device(d.cuda(), ids.to(torch.int32).cuda(), k)
+    torch.cuda.synchronize()
+    assert torch.equal(md.cpu(), rd) and torch.equal(ids_int64(mi).cpu(), ri)
+    # CSR: per shard, segment q = its valid entries of row q
+    cnt = valid.sum(dim=2)                                   # [W, Q]
+    offs = torch.zeros((W, Q + 1), dtype=torch.int64)
+    offs[:, 1:] = torch.cumsum(cnt, dim=1)
+    m = int(offs[:, -1].max())
+    pi = torch.zeros((W, m), dtype=torch.int32)
+    pd = torch.zeros((W, m), dtype=torch.float64)
+    for w in range(W):
+        sel = ids[w] >= 0
+        pi[w, : int(offs[w, -1])] = ids[w][sel].to(torch.int32)
+        pd[w, : int(offs[w, -1])] = d[w][sel]
+    oo, oi, od = merge_csr_device(offs.cuda(), pi.cuda(), pd.cuda(), int(offs[:, -1].sum()))
+    torch.cuda.synchronize()
+    tot = torch.zeros(Q + 1, dtype=torch.int64)
+    tot[1:] = torch.cumsum(cnt.sum(dim=0), 0)
+    assert torch.equal(oo.cpu(), tot)
+    for q in range(Q):
+        seg = slice(int(tot[q]), int(tot[q + 1]))
+        n = int(tot[q + 1] - tot[q])
+        assert torch.equal(od.cpu()[seg], rd[q, :n]) if n <= k else True
+        allv = torch.cat([d[w, q][ids[w, q] >= 0] for w in range(W)])
+        alli = torch.cat([ids[w, q][ids[w, q] >= 0] for w in range(W)])
+        o1 = torch.argsort(alli, stable=True)
+        o2 = torch.argsort(allv[o1], stable=True)
+        assert torch.equal(od.cpu()[seg], allv[o1][o2]) and torch.equal(ids_int64(oi).cpu()[seg], alli[o1][o2])
