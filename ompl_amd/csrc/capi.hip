@@ -106,6 +106,9 @@ struct ompl_gpu_nn {
     uint64_t radius_one_pass = 0;   // radius calls answered by the one-pass walk
     DevBuf rrt_n, rrt_pd, rrt_pi;  // device RRT growth: live size + barrier words, per-block partial minima
     int rrt_coop = -1;             // persistent RRT grid size (0: two-launch form), found on first use
+    int rrt_abort_streak = 0;      // consecutive aborted persistent grids (a device kept busy by others)
+    bool rrt_spin_read = false;    // OMPL_GPU_RRT_SPIN_LIMIT read (tests)
+    uint64_t rrt_spin_override = 0;
     void *rrt_sync = nullptr;      // its uncached synchronisation record
     DevBuf rrt_goal;               // goal record + goal reals of ompl_gpu_rrt_solve_device
     DevBuf rrt_save;               // motion-validator counters before a persistent run (restored on abort)
@@ -1616,15 +1619,20 @@ ompl_gpu_status rrt_run(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples
     if (h->sp.kind == OMPL_GPU_SPACE_SE3) h->qeta = std::max(h->qeta, 1e-12);
     // the persistent form screens in fp32 (rrt.hip): it needs the fp32 rows and screenable
     // coordinates, and starts from the store's bounds (words 7 = B, 28 = eta of its record)
-    const bool coop = h->rrt_sync && h->rows32 && screen_safe(h);
+    // after two aborts in a row the handle keeps the two-launch form: its device is shared with
+    // long kernels, and every further persistent try would spin up to kSpinLimit first
+    const bool coop = h->rrt_sync && h->rows32 && screen_safe(h) && h->rrt_abort_streak < 2;
     if (coop) {
-        // OMPL_GPU_RRT_SPIN_LIMIT (tests): a small spin limit forces the abort-and-re-run path
-        const char *lim = std::getenv("OMPL_GPU_RRT_SPIN_LIMIT");
-        if (lim && std::atoll(lim) > 0) {
-            const uint64_t v = (uint64_t)std::atoll(lim);
-            HIP_OR_FAIL(hipMemcpyAsync((uint64_t *)h->rrt_sync + 4, &v, sizeof(v), hipMemcpyHostToDevice, h->stream));
-            HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // v is a host local
+        // OMPL_GPU_RRT_SPIN_LIMIT (tests): a small spin limit forces the abort-and-re-run path;
+        // read once per handle and kept in it, so that the copy needs no synchronisation
+        if (!h->rrt_spin_read) {
+            const char *lim = std::getenv("OMPL_GPU_RRT_SPIN_LIMIT");
+            h->rrt_spin_override = (lim && std::atoll(lim) > 0) ? (uint64_t)std::atoll(lim) : 0ull;
+            h->rrt_spin_read = true;
         }
+        if (h->rrt_spin_override)
+            HIP_OR_FAIL(hipMemcpyAsync((uint64_t *)h->rrt_sync + 4, &h->rrt_spin_override, sizeof(uint64_t),
+                                       hipMemcpyHostToDevice, h->stream));
         const double B = h->absmax * (1.0 + 1e-6), eta = h->qeta * 1.01;
         HIP_OR_FAIL(hipMemcpyAsync((uint64_t *)h->rrt_sync + 7, &B, sizeof(double), hipMemcpyHostToDevice, h->stream));
         HIP_OR_FAIL(hipMemcpyAsync((uint64_t *)h->rrt_sync + 28, &eta, sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -1648,6 +1656,7 @@ ompl_gpu_status rrt_run(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples
     uint64_t bar_h[3] = {0, 0, 0};
     if (coop) HIP_OR_FAIL(hipMemcpyAsync(bar_h, h->rrt_sync, sizeof(bar_h), hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (coop) h->rrt_abort_streak = bar_h[2] ? h->rrt_abort_streak + 1 : 0;
     if (bar_h[2]) {  // aborted: restore and re-run the whole batch in the two-launch form
         h->rrt_aborts++;
         HIP_OR_FAIL(hipMemcpyAsync(mv->counters, h->rrt_save.p, 4 * sizeof(unsigned long long),

@@ -1144,12 +1144,27 @@ __global__ __launch_bounds__(256) void knn_chunk_merge_kernel(float *__restrict_
 //      own bound is still below its threshold, with the wave scan's outer-links-first partial
 //      sums and wave-wide early exit.
 // Lists hold original ids (the chunked certificate reads the fp64 features by id).
-template <int F, int K2, int G>
+//
+// MODE 0: as above.  MODE 1 / 2 (the default, two launches): the thresholds are shared across the
+// chunks.  Each chunk only sees 1/S of the store, so its own list converges to its chunk's K2-th
+// distance — for a chunk far from the query that is far above the store's — and culls little.
+// But the store's K2 best have keys <= every chunk's K2-th key (a chunk's K2-th key has K2 stored
+// states at or below it), so any chunk may drop what is above the smallest of them:
+//   MODE 1 (one wave per group, no chunks): phase 1 over kChainTauTiles tiles around the home
+//     tile; key[q] = (tau, max id) to global memory;
+//   MODE 2 (the chunk pass): starts from key[q], and after every 64-tile block publishes its own
+//     K2-th key (atomicMin, device scope) and takes the smallest published one — the chunk holding
+//     the query's neighbourhood tightens everybody's threshold.  The chunk's blocks are visited
+//     from the one holding the home tile on (wrapping), so that chunk publishes early.
+// The merge stays exact: a store state among the K2 best has a key <= every published key, and
+// fewer than K2 states of its own chunk are below it, so it is in its chunk's list.
+constexpr int kChainTauTiles = 16;
+template <int F, int K2, int G, int MODE>
 __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys, uint32_t nq,
     uint32_t chunk_tiles, float link, int nlinks, float *__restrict__ pd, uint32_t *__restrict__ pi,
-    unsigned long long *__restrict__ counters) {
+    unsigned long long *__restrict__ counters, unsigned long long *__restrict__ shared_key) {
     constexpr int NM = F / 2;
     static_assert(K2 <= 64 && NM % 2 == 0, "chain cull shape");
     __shared__ __attribute__((aligned(16))) float qrow[G * F];
@@ -1217,10 +1232,24 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
         offer(g, acc * link, id);
     };
     // 1. thresholds from the home neighbourhood
-    {
-        const uint32_t key = qkeys[min(g0 + G / 2, nq - 1)];
-        const uint32_t h = min(key, ntiles - 1);
-        const uint32_t t0 = h > 0 ? h - 1 : 0, t1 = min(t0 + 4, ntiles);
+    const uint32_t home = min(qkeys[min(g0 + G / 2, nq - 1)], ntiles - 1);
+    auto up_of = [](float tau) {  // the next float above tau (>= 0 or +inf): a distance equal to tau still passes
+        return tau < __builtin_inff() ? __uint_as_float(__float_as_uint(tau) + 1u) : tau;
+    };
+    if constexpr (MODE == 2) {  // the pre-pass's keys
+        uint64_t v = kMaxKey;
+        if (lane < G && g0 + lane < nq)
+            v = __hip_atomic_load(&shared_key[g0 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            tk[g] = g0 + g < nq ? readlane_k(v, g) : 0ull;
+            td[g] = g0 + g < nq ? up_of(kdist(tk[g])) : -__builtin_inff();
+        }
+    } else {
+        const uint32_t h = home;
+        const uint32_t span = MODE == 1 ? (uint32_t)kChainTauTiles : 4u;
+        const uint32_t t0 = h >= span / 2 - (MODE == 1 ? 0u : 1u) ? h - (span / 2 - (MODE == 1 ? 0u : 1u)) : 0u;
+        const uint32_t t1 = min(t0 + span, ntiles);
         for (uint32_t t = t0; t < t1; ++t) {
             float x[F];
             load_tile(t, x);
@@ -1236,14 +1265,40 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
             tauk[g] = g0 + g < nq ? kpack(tau, 0xFFFFFFFFu) : 0ull;
             Lk[g] = kMaxKey;
             tk[g] = tauk[g];
-            // the next float above tau (tau >= 0 or +inf): a distance equal to tau still passes
-            const float up = tau < __builtin_inff() ? __uint_as_float(__float_as_uint(tau) + 1u) : tau;
-            td[g] = g0 + g < nq ? up : -__builtin_inff();
+            td[g] = g0 + g < nq ? up_of(tau) : -__builtin_inff();
+        }
+        if constexpr (MODE == 1) {
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                if (lane == g && g0 + g < nq) shared_key[g0 + g] = tauk[g];
+            return;
         }
     }
-    // 2. the chunk's tiles
+    // 2. the chunk's tiles (MODE 2: from the home tile's block on, wrapping)
     const uint32_t c0 = blockIdx.y * chunk_tiles, c1 = min(c0 + chunk_tiles, ntiles);
-    for (uint32_t tb = c0; tb < c1; tb += 64) {
+    const uint32_t nblk = c1 > c0 ? (c1 - c0 + 63) / 64 : 0u;
+    const uint32_t sblk = (MODE == 2 && home >= c0 && home < c1) ? (home - c0) / 64 : 0u;
+    for (uint32_t bi = 0; bi < nblk; ++bi) {
+        const uint32_t tb = c0 + ((sblk + bi) % nblk) * 64;
+        if constexpr (MODE == 2) {  // share the thresholds: publish this chunk's K2-th keys, take the smallest
+            if (bi) {
+                uint64_t mine = kMaxKey;
+#pragma unroll
+                for (int g = 0; g < G; ++g) mine = lane == g ? tk[g] : mine;
+                uint64_t best = kMaxKey;
+                if (lane < G && g0 + lane < nq)
+                    best = __hip_atomic_fetch_min(&shared_key[g0 + lane], mine, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const uint64_t o = readlane_k(best, g);
+                    if (g0 + g < nq && o < tk[g]) {
+                        tk[g] = o;
+                        td[g] = up_of(kdist(o));
+                    }
+                }
+            }
+        }
         const uint32_t t = tb + lane;
         float lb[G];
 #pragma unroll
@@ -1889,7 +1944,7 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct FastLayout {
-    size_t keys, keys2, idx, perm, cub, q32u, q32, pd, pi, fail, total;
+    size_t keys, keys2, idx, perm, cub, q32u, q32, pd, pi, fail, tau, total;
     size_t cub_bytes;
 };
 
@@ -1916,6 +1971,7 @@ FastLayout fast_layout(const DevSpace &sp, const FeatGeom &g, const FastPlan &p,
     L.pd = take(4ull * p.chunks * nq * p.K2);
     L.pi = take(4ull * p.chunks * nq * p.K2);
     L.fail = take(4ull * (nq + 1));
+    L.tau = take(8ull * nq);  // the chain cull's shared threshold keys
     L.total = off;
     return L;
 }
@@ -1965,11 +2021,27 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             if (!ss || !ss->built) return hipErrorInvalidValue;
             // the plan's chunk count sized the lists; the store's tiles (main + tail) set their length
             const uint32_t per = (ss->ntiles + p.chunks - 1) / p.chunks;
+            // thresholds shared across the chunks (MODE 1 + 2); OMPL_GPU_CHAIN_SHARE=0: each chunk
+            // on its own (MODE 0, A/B)
+            static const int share = [] {
+                const char *v = std::getenv("OMPL_GPU_CHAIN_SHARE");
+                return v ? std::atoi(v) : 1;
+            }();
+            unsigned long long *skey = (unsigned long long *)(ws + L.tau);
+            const uint32_t ng = (nq + kChainCullG - 1) / kChainCullG;
+            if (share)
+                hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, 1>), dim3(ng, 1), dim3(64), 0, st,
+                                   ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,
+                                   (float)sp.link, sp.dim, pd, pi, nullptr, skey);
             timer_begin(st, "knn32_chain_cull_kernel");
-            hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG>),
-                               dim3((nq + kChainCullG - 1) / kChainCullG, p.chunks), dim3(64), 0, st, ss->rows,
-                               ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per, (float)sp.link, sp.dim,
-                               pd, pi, ss->counters);
+            if (share)
+                hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, 2>), dim3(ng, p.chunks), dim3(64), 0,
+                                   st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,
+                                   (float)sp.link, sp.dim, pd, pi, ss->counters, skey);
+            else
+                hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, 0>), dim3(ng, p.chunks), dim3(64), 0,
+                                   st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,
+                                   (float)sp.link, sp.dim, pd, pi, ss->counters, nullptr);
             timer_end(st);
             walked = true;
         }

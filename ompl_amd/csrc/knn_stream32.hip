@@ -620,10 +620,11 @@ template <int SP, int F>
 hipError_t stream32_k(const DevSpace &sp, const float *feat32, const double *feat64, uint64_t cap, uint64_t n_end,
                       const double *qfeat, uint32_t nq, uint32_t k, float absmax, float qeta, double *out_d,
                       uint32_t *out_i, void *ws, size_t ws_bytes, hipStream_t st) {
-    // k = 1: the persistent form below 4 M states (10^6: 14.2 us against 17.6 us for the chunked
-    // form, the merge of 1,024 instead of 977 x 4 partials included); from 4 M states up the
-    // chunked form streams faster (10^7: 56.6 us against 60 us at its best, 2,048 blocks — the
-    // persistent grid ends with every block selecting at once, while HBM idles)
+    // Default dispatch: every k, every store size takes the split form (stream32_items: the
+    // streaming kernel screens, one refine block per query decides; OMPL_GPU_SPLIT_MIN = 0).  The
+    // persistent k = 1 form below is kept only behind the A/B switches (OMPL_GPU_STREAM_SPLIT=0 or
+    // OMPL_GPU_SPLIT_MIN above the store size): measured at 10^6 it took 14.3 us against the split
+    // form's 9.1 us, at 10^7 54.5 against 49 us
     if (k <= 1 && (n_end >= (4ull << 20) || stream1_blocks() == 0 || (stream_split() && n_end >= stream_split_min())))
         return stream32_items<SP, F, 1>(sp, feat32, feat64, cap, n_end, qfeat, nq, k, absmax, qeta, out_d, out_i, ws,
                                         ws_bytes, st);
