@@ -113,6 +113,7 @@ struct SortedStore {
     uint32_t main_live = 0, tail_t0 = 0, tail_cap_tiles = 0;
     uint64_t main_covered = 0, covered = 0, removed = 0;
     size_t cap_pos = 0, cap_nodes = 0, cap_inv = 0;  // allocated positions / nodes / inv entries
+    uint32_t *qcount = nullptr;  // [pad_tiles + 1] per-tile query counts of the home-key counting sort
     void *scratch = nullptr;     // build / append workspace (grow-only)
     size_t scratch_bytes = 0;
     size_t bytes = 0;

@@ -44,7 +44,7 @@ bool radius_cull_supported(const DevSpace &sp) {
 
 void free_sorted_store(SortedStore *s) {
     for (void *x : {(void *)s->rows, (void *)s->ids, (void *)s->tbox, (void *)s->sbox, (void *)s->tkey0, (void *)s->nodes,
-                    (void *)s->rows64, (void *)s->inv, s->scratch})
+                    (void *)s->rows64, (void *)s->inv, (void *)s->qcount, s->scratch})
         if (x) (void)hipFree(x);
     *s = SortedStore{};
 }

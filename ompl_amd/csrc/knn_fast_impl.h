@@ -185,11 +185,57 @@ __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, Fa
     idx[i] = i;
 }
 
-// queries sorted by home tile (keys < 2^key_bits): a device radix sort over the keys' bits.
-// (Measured and rejected: a one-block LDS counting sort — one launch instead of ~10, but one
-// CU's atomics and scattered writes made the 10^5-query nn phase 1.41 -> 1.48 ms.)
+// queries sorted by home tile.  Home-tile keys (< bins = the k-d tiles) take a counting sort over
+// the whole grid — a count kernel whose atomicAdd also hands each query its slot inside its tile,
+// a one-block exclusive scan of the bins, a scatter: three launches; queries of one tile land in
+// any order, which only changes how the walk's groups are formed, never a result.  Morton keys
+// (32 bits, no k-d tree) take the library radix sort.  (Measured and rejected in round 3: a
+// one-block LDS counting sort, one CU doing every atomic and write: nn phase 1.41 -> 1.48 ms.)
+__global__ void home_count_kernel(const uint32_t *__restrict__ keys, uint32_t nq, uint32_t *__restrict__ cnt,
+                                  uint32_t *__restrict__ slot) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nq) slot[i] = atomicAdd(&cnt[keys[i]], 1u);
+}
+__global__ __launch_bounds__(1024) void home_scan_kernel(uint32_t *__restrict__ cnt, uint32_t bins) {
+    using BlockScan = rocprim::block_scan<uint32_t, 1024>;
+    __shared__ typename BlockScan::storage_type sh;
+    const uint32_t per = (bins + 1023) / 1024, b0 = threadIdx.x * per, b1 = min(b0 + per, bins);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b) sum += cnt[b];
+    uint32_t pre = 0, tot = 0;
+    BlockScan().exclusive_scan(sum, pre, 0u, tot, sh);
+    for (uint32_t b = b0; b < b1; ++b) {  // in place: counts -> first slots
+        const uint32_t c = cnt[b];
+        cnt[b] = pre;
+        pre += c;
+    }
+}
+__global__ void home_scatter_kernel(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ idx,
+                                    const uint32_t *__restrict__ slot, uint32_t nq, const uint32_t *__restrict__ start,
+                                    uint32_t *__restrict__ keys2, uint32_t *__restrict__ perm) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const uint32_t k = keys[i], p = start[k] + slot[i];
+    keys2[p] = k;
+    perm[p] = idx[i];
+}
 inline hipError_t sort_home_keys(char *cub, size_t cub_bytes, const uint32_t *keys, uint32_t *keys2,
-                                 const uint32_t *idx, uint32_t *perm, uint32_t nq, int key_bits, hipStream_t st) {
+                                 const uint32_t *idx, uint32_t *perm, uint32_t nq, int key_bits, hipStream_t st,
+                                 uint32_t *qcount = nullptr, uint32_t bins = 0) {
+    static const int counting = [] {  // A/B switch: OMPL_GPU_QSORT=0 -> the radix sort
+        const char *v = std::getenv("OMPL_GPU_QSORT");
+        return v ? std::atoi(v) : 1;
+    }();
+    if (counting && qcount && bins && key_bits < 32 && cub_bytes >= 4ull * nq) {
+        uint32_t *slot = (uint32_t *)cub;  // the radix sort's temporary storage holds the slots
+        hipError_t e = hipMemsetAsync(qcount, 0, 4ull * bins, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(home_count_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, keys, nq, qcount, slot);
+        hipLaunchKernelGGL(home_scan_kernel, dim3(1), dim3(1024), 0, st, qcount, bins);
+        hipLaunchKernelGGL(home_scatter_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, keys, idx, slot, nq, qcount,
+                           keys2, perm);
+        return hipGetLastError();
+    }
     size_t cb = cub_bytes;
     return hipcub::DeviceRadixSort::SortPairs(cub, cb, keys, keys2, idx, perm, (int)nq, 0, key_bits, st);
 }
@@ -1963,8 +2009,8 @@ FastLayout fast_layout(const DevSpace &sp, const FeatGeom &g, const FastPlan &p,
     size_t cb = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                              (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nq, 0, 32);
-    L.cub_bytes = cb;
-    L.cub = take(cb);
+    L.cub_bytes = std::max<size_t>(cb, 4ull * nq);  // also the counting sort's per-query slots
+    L.cub = take(L.cub_bytes);
     const int FS = sp.kind == OMPL_GPU_SPACE_SE3 ? 8 : g.F;
     L.q32u = take(4ull * nq * FS);
     L.q32 = take(4ull * nq * FS);
@@ -1994,7 +2040,8 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     // states); Morton keys use all 32
     const bool home_keys = p.cull && ss && ss->nodes && ss->kd_tiles > 1;
     const int key_bits = home_keys ? 32 - __builtin_clz(ss->kd_tiles - 1) : 32;
-    hipError_t e = sort_home_keys(ws + L.cub, L.cub_bytes, keys, keys2, idx, perm, nq, key_bits, st);
+    hipError_t e = sort_home_keys(ws + L.cub, L.cub_bytes, keys, keys2, idx, perm, nq, key_bits, st,
+                                  home_keys ? ss->qcount : nullptr, home_keys ? ss->kd_tiles : 0u);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
     e = hipMemsetAsync(fail, 0, 4, st);
@@ -2175,8 +2222,8 @@ RadiusLayout radius_layout(const DevSpace &sp, const FeatGeom &g, uint32_t nq) {
     size_t cb = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                              (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nq, 0, 32);
-    L.cub_bytes = cb;
-    L.cub = take(cb);
+    L.cub_bytes = std::max<size_t>(cb, 4ull * nq);  // also the counting sort's per-query slots
+    L.cub = take(L.cub_bytes);
     const int FS = sp.kind == OMPL_GPU_SPACE_SE3 ? 8 : g.F;
     L.q32u = take(4ull * nq * FS);
     L.q32 = take(4ull * nq * FS);
@@ -2213,7 +2260,8 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
                            idx, ss->nodes, ss->kd_tiles);
         const bool home_keys = ss->nodes && ss->kd_tiles > 1;
         const int key_bits = home_keys ? 32 - __builtin_clz(ss->kd_tiles - 1) : 32;  // home tiles
-        if ((e = sort_home_keys(ws + L.cub, L.cub_bytes, keys, keys2, idx, perm, nq, key_bits, st)) != hipSuccess)
+        if ((e = sort_home_keys(ws + L.cub, L.cub_bytes, keys, keys2, idx, perm, nq, key_bits, st,
+                                home_keys ? ss->qcount : nullptr, home_keys ? ss->kd_tiles : 0u)) != hipSuccess)
             return e;
         hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
         if ((e = hipMemsetAsync(counts + nq, 0, 8, st)) != hipSuccess) return e;
@@ -3195,6 +3243,8 @@ hipError_t sorted_alloc(SortedStore *s, uint32_t pad_tiles, uint32_t max_nodes, 
         if ((e = grow_array(&s->sbox, dummy, (size_t)nsup * BW)) != hipSuccess) return e;
         dummy = 0;
         if ((e = grow_array(&s->tkey0, dummy, (size_t)pad_tiles)) != hipSuccess) return e;
+        dummy = 0;
+        if ((e = grow_array(&s->qcount, dummy, (size_t)pad_tiles + 1)) != hipSuccess) return e;
         s->cap_pos = n_pad;
         hipLaunchKernelGGL(iota_kernel, dim3((pad_tiles + 255) / 256), dim3(256), 0, st, s->tkey0, pad_tiles);
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/r4a; mkdir -p "$out"
-timeout -k 10 300 python -u -m pytest tests/test_gpu_spaces.py tests/test_gpu_large_k.py -x -q --timeout 120 --timeout-method thread > "$out/spaces.log" 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_spaces.py tests/test_gpu_large_k.py tests/test_gpu_motion.py tests/test_gpu_prm.py tests/test_gpu_batch.py tests/test_gpu_fullsize.py tests/test_shard_gloo.py -x -q --timeout 120 --timeout-method thread > "$out/spaces.log" 2>&1; rc=$?
 tail -3 "$out/spaces.log"; case $rc in 124|134|137|139) exit 1;; esac
 s=$(date +%s)
 timeout -k 10 400 python -u bench.py --workload cfg5 --bitstar-knn --steps 10 --warmup 2 --cpu-seconds 8 \
