@@ -498,7 +498,8 @@ def index_maintenance(torch, run, local, batches=10, batch=100, nq=1000):
     return {"states": len(run.tree), "full_build_ms": build_ms, "append_ms_per_batch": t_app / batches,
             "batch_states": batch, "query_ms_per_batch": t_q / batches, "queries_per_batch": nq,
             "builds": builds, "appends": appends,
-            "note": "device k-d build (one radix sort per level); appends place new states in a Morton tail"}
+            "note": ("device k-d build: global levels as median partitions (histogram, median bin, stable scatter of "
+                     "whole rows), the deep levels in LDS; appends place new states in a Morton-ordered tail")}
 
 
 def rrt_device(torch, nn, mv, sp, dev, iters):

@@ -3055,18 +3055,25 @@ __global__ __launch_bounds__(1024) void kd_lds_finish_kernel(
             }
         }
         __syncthreads();
-        // 2. widest coordinate of every sub-node that splits at this sub-level
+        // 2. widest coordinate of every sub-node that splits at this sub-level: a wave per
+        //    sub-node, a lane per tile (<= LT <= 32 tiles), the box extents by wave min / max
+        //    reductions (exact, so the same split as a serial scan; round 3 had one thread loop
+        //    over the node's tiles x coordinates, ~10 us of serial LDS reads at the top sub-level)
         const uint32_t nsub = 1u << l;
-        for (uint32_t sp = tid; sp < nsub; sp += BS) {
+        for (uint32_t sp = (uint32_t)wave; sp < nsub; sp += BS / 64) {
             const KdNodeRef sn = kd_node_at(T, l, sp);
-            if (!sn.valid || sn.T <= 1) continue;
+            if (!sn.valid || sn.T <= 1) continue;  // wave-uniform
+            const bool in = (uint32_t)lane < sn.T;
             int bd = 0;
             float be = -1.f, blo = 0.f;
+#pragma unroll
             for (int d = 0; d < NB; ++d) {
-                float lo = __builtin_inff(), hi = -__builtin_inff();
-                for (uint32_t t = sn.t0; t < sn.t0 + sn.T; ++t) {
-                    lo = fminf(lo, tbs[t][d]);
-                    hi = fmaxf(hi, tbs[t][NB + d]);
+                float lo = in ? tbs[sn.t0 + lane][d] : __builtin_inff();
+                float hi = in ? tbs[sn.t0 + lane][NB + d] : -__builtin_inff();
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    lo = fminf(lo, __shfl_xor(lo, o));
+                    hi = fmaxf(hi, __shfl_xor(hi, o));
                 }
                 if (hi - lo > be) {  // first widest, as the global levels
                     be = hi - lo;
@@ -3074,7 +3081,8 @@ __global__ __launch_bounds__(1024) void kd_lds_finish_kernel(
                     blo = lo;
                 }
             }
-            nsp[sp] = make_float4(__uint_as_float((uint32_t)bd), blo, be > 0.f ? (float)kKdQ / be : 0.f, 0.f);
+            if (lane == 0)
+                nsp[sp] = make_float4(__uint_as_float((uint32_t)bd), blo, be > 0.f ? (float)kKdQ / be : 0.f, 0.f);
         }
         __syncthreads();
         // 3. packed keys of the current order (blocked: thread tid holds positions tid * IPT + i)

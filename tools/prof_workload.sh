@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 w=$1; tag=$2; shift 2; out=gpurun_out/prof_$tag
 mkdir -p "$out"
-args="--workload $w --steps 2 --warmup 1 --no-cpu-baseline --single-query-reps 0 --rrt-iters 0 --no-extras $*"
+args="--workload $w --steps 2 --warmup 1 --no-cpu-baseline --single-query-reps 0 --rrt-iters 0 --no-extras --workloads none $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out" -o trace --output-format csv -- python bench.py $args > "$out/trace.log" 2>&1 || exit $?
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d "$out" -o pmc_fetch --output-format csv -- python bench.py $args > "$out/fetch.log" 2>&1 || exit $?
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d "$out" -o pmc_write --output-format csv -- python bench.py $args > "$out/write.log" 2>&1 || exit $?

@@ -1,6 +1,7 @@
 #!/bin/bash
-# round-4 walk A/B: parity tests on each variant build (var 7 scan cascade, 8 dynamic tile masks,
-# 9 both), then alternating bench runs: cfg3 (headline walk) and cfg5 (radius walk 7/8 waves)
+# round-4 A/B step: parity tests on the walk variants (var 7 scan cascade, 8 per-query tile masks,
+# 9 both), then alternating bench runs: cfg3 (walk variants, radix vs counting query sort), cfg4
+# (shared chain thresholds, fixed-width chain motion kernel), cfg5 (radius walk at 7 / 8 waves)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -9,7 +10,8 @@ T="tests/test_gpu_nn.py tests/test_gpu_cull.py"
 for v in ${VARS:-7 8 9}; do
   OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var$v.so timeout -k 10 300 python -u -m pytest $T -m gpu -x -q --timeout 200 \
       --timeout-method thread > "$out/pytest_v$v.log" 2>&1
-  rc=$?; echo "var$v: $(tail -1 "$out/pytest_v$v.log")"; if [ $rc != 0 ]; then echo "var$v pytest rc=$rc"; exit 1; fi
+  rc=$?; echo "var$v: $(tail -1 "$out/pytest_v$v.log")"; case $rc in 0) ;; 124|134|137|139) exit 1;; *) echo "var$v failed";; esac
 done
-bash tools/ab_bench.sh "cfg3" "${VARS:-7 8 9}" 3 || exit 1
-[ "${RADIUS:-1}" = 1 ] && bash tools/ab_bench.sh "cfg5" "5 6" 2
+bash tools/ab_env.sh cfg3 "--workload cfg3" 3 - VAR=7 VAR=8 VAR=9 OMPL_GPU_QSORT=0 || exit 1
+bash tools/ab_env.sh cfg4 "--workload cfg4" 2 - OMPL_GPU_CHAIN_SHARE=0 VAR=10 || exit 1
+bash tools/ab_env.sh cfg5 "--workload cfg5" 2 - VAR=5 VAR=6
