@@ -114,6 +114,7 @@ struct ompl_gpu_nn {
     DevBuf rrt_save;               // motion-validator counters before a persistent run (restored on abort)
     uint64_t rrt_aborts = 0;       // persistent runs that aborted and re-ran in the two-launch form
     DevBuf prm_bf, prm_raw, prm_kj, prm_sd, prm_si, prm_len, prm_off, prm_eoff, prm_cnt64;  // PRM* batches
+    DevBuf prm_p32;                                                                         // chain positions
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
     double lo[kKeyDims] = {0}, hi[kKeyDims] = {0}, absmax = 0.0;
@@ -1444,19 +1445,26 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     }
     // 2. in-batch causal candidates: count, offsets, fill, segmented sort by distance (stable:
     //    stored entries first, candidates in id order, so ties resolve by id)
-    HIP_OR_FAIL(h->prm_len.ensure(sizeof(uint64_t) * (rows + 1)));
+    HIP_OR_FAIL(h->prm_len.ensure(sizeof(uint64_t) * (rows + 2)));
     HIP_OR_FAIL(h->prm_off.ensure(sizeof(uint64_t) * (rows + 1)));
     uint64_t *len = (uint64_t *)h->prm_len.p, *off = (uint64_t *)h->prm_off.p;
-    HIP_OR_FAIL(hipMemsetAsync(len + rows, 0, sizeof(uint64_t), h->stream));
+    HIP_OR_FAIL(hipMemsetAsync(len + rows, 0, 2 * sizeof(uint64_t), h->stream));  // [rows]: 0, [rows + 1]: longest
+    float *p32 = nullptr;
+    if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN) {  // the causal scan's fp32 screen
+        HIP_OR_FAIL(h->prm_p32.ensure(sizeof(float) * m * F));
+        p32 = (float *)h->prm_p32.p;
+    }
     HIP_OR_FAIL(launch_prm_causal(h->sp, h->g, false, bf, (uint32_t)j0, (uint32_t)rows, (uint32_t)n0, dkj, sd, si, kq,
-                                  len, nullptr, nullptr, nullptr, h->stream));
+                                  len, nullptr, nullptr, nullptr, p32, (uint32_t)m,
+                                  (unsigned long long *)(len + rows + 1), h->stream));
     size_t sb = 0;
     HIP_OR_FAIL(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, len, off, (int)rows + 1, h->stream));
     HIP_OR_FAIL(h->tmp.ensure(sb));
     sb = h->tmp.bytes;
     HIP_OR_FAIL(hipcub::DeviceScan::ExclusiveSum(h->tmp.p, sb, len, off, (int)rows + 1, h->stream));
-    uint64_t tot = 0;
+    uint64_t tot = 0, longest = 0;
     HIP_OR_FAIL(hipMemcpyAsync(&tot, off + rows, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(&longest, len + rows + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     if (tot > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "in-batch candidate set above 2^31 entries");
     HIP_OR_FAIL(h->dists.ensure(sizeof(double) * std::max<uint64_t>(tot, 1)));
@@ -1467,7 +1475,11 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     uint32_t *ci = (uint32_t *)h->ids.p, *sii = (uint32_t *)h->sorted_ids.p;
     if (tot) {
         HIP_OR_FAIL(launch_prm_causal(h->sp, h->g, true, bf, (uint32_t)j0, (uint32_t)rows, (uint32_t)n0, dkj, sd, si,
-                                      kq, nullptr, off, cd, ci, h->stream));
+                                      kq, nullptr, off, cd, ci, p32, (uint32_t)m, nullptr, h->stream));
+    }
+    if (tot && longest <= kRankSortMax) {  // every segment fits a wave's LDS: rank placement by (distance, id)
+        HIP_OR_FAIL(launch_segment_rank_sort(off, ci, cd, (uint32_t)rows, sii, sdd, h->stream));
+    } else if (tot) {
         size_t tb = 0;
         HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, (const double *)cd, sdd,
                                                                 (const uint32_t *)ci, sii, (int)tot, (int)rows, off,

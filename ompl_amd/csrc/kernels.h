@@ -232,10 +232,12 @@ hipError_t launch_aos_rows(const double *soa, uint64_t cap, int dim, int da, uin
 // fill = false: seg_len[j] = stored entries kept + in-batch candidates; fill = true: segments
 // written at seg_off (stored entries, then candidates j' < j with d <= the k_j-th stored distance)
 // rows j0 .. j0 + rows - 1 of the batch (this rank's slice; sd / si / seg_* indexed by row)
+// p32 (KinematicChain; NULL: no screen): workspace of m x F floats for the batch's fp32 joint
+// positions (written by the count call, read by both); seg_max (count call): += the longest segment
 hipError_t launch_prm_causal(const DevSpace &sp, const FeatGeom &g, bool fill, const double *bf, uint32_t j0,
                              uint32_t rows, uint32_t n0, const uint32_t *kj, const double *sd, const uint32_t *si,
                              uint32_t kq, uint64_t *seg_len, const uint64_t *seg_off, double *out_d, uint32_t *out_i,
-                             hipStream_t st);
+                             float *p32, uint32_t m, unsigned long long *seg_max, hipStream_t st);
 hipError_t launch_prm_take(const uint32_t *sorted_i, const double *sorted_d, const uint64_t *seg_off,
                            const uint32_t *kj, uint32_t m, uint32_t k_cap, uint32_t *nbr, uint32_t *cnt, double *dist,
                            hipStream_t st);

@@ -35,15 +35,39 @@ __device__ __forceinline__ uint32_t stored_take(const uint32_t *si, uint32_t kq,
     return c;
 }
 
+// KinematicChain joint positions of the batch rows in fp32 (knn_fast_impl.h chain_positions: fp64
+// prefix sums of the cumulative cos / sin features, then rounded), for the causal screen
+template <int F>
+__global__ void prm_positions_kernel(const double *__restrict__ bf, uint32_t m, float *__restrict__ p32) {
+    constexpr int NM = F / 2;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    double cx = 0.0, cy = 0.0;
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        cx += bf[(size_t)j * F + i];
+        cy += bf[(size_t)j * F + NM + i];
+        p32[(size_t)j * F + i] = (float)cx;
+        p32[(size_t)j * F + NM + i] = (float)cy;
+    }
+}
+
 // one wave per milestone j: FILL = false counts the in-batch candidates j' < j with
-// d(j', j) <= bound; FILL = true writes the segment [stored entries | candidates in j' order]
+// d(j', j) <= bound; FILL = true writes the segment [stored entries | candidates in j' order].
+// KinematicChain with p32: each pair is screened first by the fp32 joint-position distance
+// link * sum_i |P_i(j') - P_i(j)| against bound + e (e: the chain screen's rounding bound,
+// knn_fast_impl.h screen_error<KCHAIN>), and only the survivors — a few per milestone, against
+// every earlier milestone of the batch before — take the exact fp64 distance with its 12 fp64
+// square roots.  The decision is still the exact d <= bound, so the segments are unchanged.
 template <int SP, int F, int NMAX, bool FILL>
 __global__ __launch_bounds__(256) void prm_causal_kernel(const double *__restrict__ bf, uint32_t j0, uint32_t rows,
                                                          uint32_t n0, DevSpace sp, const uint32_t *__restrict__ kj_arr,
                                                          const double *__restrict__ sd, const uint32_t *__restrict__ si,
                                                          uint32_t kq, uint64_t *__restrict__ seg_len,
                                                          const uint64_t *__restrict__ seg_off,
-                                                         double *__restrict__ out_d, uint32_t *__restrict__ out_i) {
+                                                         double *__restrict__ out_d, uint32_t *__restrict__ out_i,
+                                                         const float *__restrict__ p32,
+                                                         unsigned long long *__restrict__ seg_max) {
     const uint32_t row = blockIdx.x * 4 + (threadIdx.x >> 6), j = j0 + row;  // row of this rank's slice
     const int lane = threadIdx.x & 63;
     if (row >= rows) return;
@@ -52,6 +76,19 @@ __global__ __launch_bounds__(256) void prm_causal_kernel(const double *__restric
     double qv[F];
 #pragma unroll
     for (int f = 0; f < F; ++f) qv[f] = bf[(size_t)j * F + f];
+    constexpr int NM = F / 2;
+    float qp[SP == OMPL_GPU_SPACE_KCHAIN ? F : 1];
+    float thr32 = __builtin_inff();
+    if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+        if (p32) {
+#pragma unroll
+            for (int f = 0; f < F; ++f) qp[f] = p32[(size_t)j * F + f];
+            constexpr double u = 5.9604644775390625e-08, fmin = 1.1754943508222875e-38;
+            const double n = (double)sp.dim;
+            const double e = 2.0 * (sp.link * 8.0 * u * n * (n + 1.0) + (n + 2.0) * u * bound + sp.link * n * sqrt(2.0 * fmin));
+            thr32 = bound < __builtin_inf() ? (float)((bound + e) * (1.0 + 16.0 * u)) : __builtin_inff();
+        }
+    }
     uint64_t pos = 0;
     if (FILL) {
         pos = seg_off[row];
@@ -68,7 +105,21 @@ __global__ __launch_bounds__(256) void prm_causal_kernel(const double *__restric
         const uint32_t jp = b + lane;
         bool hit = false;
         double d = 0.0;
-        if (jp < j && bound >= 0.0) {
+        bool cand = jp < j && bound >= 0.0;
+        if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+            if (p32 && cand) {  // fp32 screen (see above); NaN never passes
+                float acc = 0.f;
+#pragma unroll
+                for (int i = 0; i < NM; ++i) {
+                    if (i < sp.dim) {
+                        const float dx = p32[(size_t)jp * F + i] - qp[i], dy = p32[(size_t)jp * F + NM + i] - qp[NM + i];
+                        acc += __builtin_amdgcn_sqrtf(fmaf(dy, dy, dx * dx));
+                    }
+                }
+                cand = acc * (float)sp.link <= thr32;
+            }
+        }
+        if (cand) {
             double sv[F];
 #pragma unroll
             for (int f = 0; f < F; ++f) sv[f] = bf[(size_t)jp * F + f];
@@ -83,7 +134,11 @@ __global__ __launch_bounds__(256) void prm_causal_kernel(const double *__restric
         }
         cnt += (uint64_t)__popcll(bm);
     }
-    if (!FILL && lane == 0) seg_len[row] = stored_take(si, kq, kj, row) + cnt;
+    if (!FILL && lane == 0) {
+        const uint64_t len = stored_take(si, kq, kj, row) + cnt;
+        seg_len[row] = len;
+        if (seg_max) atomicMax(seg_max, (unsigned long long)len);
+    }
 }
 
 // thread per (milestone, rank): the first min(k_j, segment) sorted entries
@@ -133,14 +188,18 @@ __global__ void prm_scatter_valid_kernel(const uint8_t *__restrict__ vc, const u
 template <int SP, int F, int NMAX>
 hipError_t run_prm_causal(const DevSpace &sp, bool fill, const double *bf, uint32_t j0, uint32_t rows, uint32_t n0,
                           const uint32_t *kj, const double *sd, const uint32_t *si, uint32_t kq, uint64_t *seg_len,
-                          const uint64_t *seg_off, double *out_d, uint32_t *out_i, hipStream_t st) {
+                          const uint64_t *seg_off, double *out_d, uint32_t *out_i, float *p32, uint32_t m,
+                          unsigned long long *seg_max, hipStream_t st) {
     const dim3 grid((rows + 3) / 4), block(256);
+    if constexpr (SP != OMPL_GPU_SPACE_KCHAIN) p32 = nullptr;
+    if (p32 && !fill)  // the positions of every batch row (earlier milestones of other slices too)
+        hipLaunchKernelGGL((prm_positions_kernel<F>), dim3((m + 255) / 256), dim3(256), 0, st, bf, m, p32);
     if (fill)
         hipLaunchKernelGGL((prm_causal_kernel<SP, F, NMAX, true>), grid, block, 0, st, bf, j0, rows, n0, sp, kj, sd, si,
-                           kq, seg_len, seg_off, out_d, out_i);
+                           kq, seg_len, seg_off, out_d, out_i, p32, nullptr);
     else
         hipLaunchKernelGGL((prm_causal_kernel<SP, F, NMAX, false>), grid, block, 0, st, bf, j0, rows, n0, sp, kj, sd,
-                           si, kq, seg_len, seg_off, out_d, out_i);
+                           si, kq, seg_len, seg_off, out_d, out_i, p32, seg_max);
     return hipGetLastError();
 }
 
@@ -165,10 +224,10 @@ hipError_t run_prm_causal(const DevSpace &sp, bool fill, const double *bf, uint3
 hipError_t launch_prm_causal(const DevSpace &sp, const FeatGeom &g, bool fill, const double *bf, uint32_t j0,
                              uint32_t rows, uint32_t n0, const uint32_t *kj, const double *sd, const uint32_t *si,
                              uint32_t kq, uint64_t *seg_len, const uint64_t *seg_off, double *out_d, uint32_t *out_i,
-                             hipStream_t st) {
+                             float *p32, uint32_t m, unsigned long long *seg_max, hipStream_t st) {
     if (rows == 0) return hipSuccess;
     OMPL_AMD_SPACE_DISPATCH(run_prm_causal, sp, fill, bf, j0, rows, n0, kj, sd, si, kq, seg_len, seg_off, out_d, out_i,
-                            st)
+                            p32, m, seg_max, st)
 }
 
 hipError_t launch_prm_take(const uint32_t *sorted_i, const double *sorted_d, const uint64_t *seg_off,
