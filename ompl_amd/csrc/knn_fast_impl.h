@@ -1672,7 +1672,17 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
     // re-read the wave-uniform query rows from LDS at every use through an offset the compiler
     // cannot see through, instead of letting it hoist them into VGPRs for the whole walk
     uint32_t qoff = 0;
-    // super-tiles whose box comes within some query's bound, 64 box tests per round
+    // super-tiles whose box comes within some query's bound, 64 box tests per round.
+    // kDyn (A/B variant 11): each lane also records which queries its super-tile passes
+    // (sneed, LDS), and a popped super-tile's tile bounds are computed only for those queries,
+    // paired onto the two half-waves (as knn32_group_kernel's kDyn)
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 11
+    constexpr bool kDyn = true;
+#else
+    constexpr bool kDyn = false;
+#endif
+    __shared__ uint32_t sneed[64];
+    uint32_t pop_bits = (1u << G) - 1u;
     uint32_t sb = 0, base = 0;
     uint64_t sm = 0;
     auto next_super = [&]() -> int {
@@ -1681,6 +1691,7 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
             asm volatile("" : "+s"(qoff));
             const uint32_t s = sb + lane;
             bool need = false;
+            uint32_t nb = 0;
             if (s < nsuper) {
                 float bx[BW];
                 const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
@@ -1691,9 +1702,15 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
                 }
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    need |= box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1) <= thr[g];
+                    const bool pg = box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1) <= thr[g];
+                    need |= pg;
+                    if (kDyn && pg) nb |= 1u << g;
                     __builtin_amdgcn_sched_barrier(0);  // one bound at a time (temporaries)
                 }
+            }
+            if constexpr (kDyn) {
+                sneed[lane] = nb;
+                __builtin_amdgcn_wave_barrier();
             }
             sm = __ballot(need);
             base = sb;
@@ -1701,7 +1718,20 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
         }
         const int l = __builtin_ctzll(sm);
         sm &= sm - 1;
+        if constexpr (kDyn) pop_bits = (uint32_t)__builtin_amdgcn_readfirstlane((int)sneed[l]);
         return (int)(base + l);
+    };
+    auto pair_of = [&](uint32_t bits, int p, int &qa, int &qb) {  // the needed pair of pass p
+        for (int i = 0; i < 2 * p; ++i) bits &= bits - 1;
+        qa = bits ? __builtin_ctz(bits) : -1;
+        bits &= bits - 1;
+        qb = bits ? __builtin_ctz(bits) : -1;
+    };
+    auto thr_of = [&](int q) -> float {
+        float v = -__builtin_inff();
+#pragma unroll
+        for (int g = 0; g < G; ++g) v = q == g ? thr[g] : v;
+        return v;
     };
     // this lane's row of super-tile ss's tile boxes (tile ss * 32 + (lane & 31)); rows past the
     // last tile read as empty boxes (bound +inf)
@@ -1726,13 +1756,22 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
         for (int rr = 0; rr < R; ++rr) x[rr] = rows[(uint64_t)rr * n_pad + p];
         id = ids[p];
     };
-    auto scan_tile = [&](uint32_t ss, int t, const float (&x)[R], uint32_t id, const float (&lb)[GH]) {
+    auto scan_tile = [&](uint32_t ss, int t, const float (&x)[R], uint32_t id, const float (&lb)[GH], uint32_t bits) {
         asm volatile("" : "+s"(qoff));
         const uint64_t p = (uint64_t)(ss * kSuperTiles + t) * kCullTile + lane;
         ++visited;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            if (!(readlane_f(lb[g % GH], t + (g < GH ? 0 : 32)) <= thr[g])) continue;
+            if constexpr (kDyn) {
+                if (!((bits >> g) & 1u)) continue;
+                const int rank = __builtin_popcount(bits & ((1u << g) - 1u));
+                float v = lb[0];
+#pragma unroll
+                for (int pp = 1; pp < GH; ++pp) v = (rank >> 1) == pp ? lb[pp] : v;
+                if (!(readlane_f(v, t + ((rank & 1) ? 32 : 0)) <= thr[g])) continue;
+            } else {
+                if (!(readlane_f(lb[g % GH], t + (g < GH ? 0 : 32)) <= thr[g])) continue;
+            }
             ++qscans;
             bool hit;  // NaN never hits
             if constexpr (SP == OMPL_GPU_SPACE_SE3) {  // chord bound first, as in the kNN walk
@@ -1792,16 +1831,34 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
     // writes each CSR segment in tile order.
     float bx[BW];
     int ss = next_super();
+    uint32_t bits = pop_bits;
     if (ss >= 0) load_tbox((uint32_t)ss, bx);
     while (ss >= 0) {
         float lb[GH];
         bool tneed = false;
         asm volatile("" : "+s"(qoff));
+        if constexpr (kDyn) {
 #pragma unroll
-        for (int j = 0; j < GH; ++j) {
-            lb[j] = box_lb<SP, F>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
-            tneed |= lb[j] <= (half ? thr[GH + j] : thr[j]);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int pp = 0; pp < GH; ++pp) {
+                lb[pp] = __builtin_inff();
+                int qa, qb;
+                pair_of(bits, pp, qa, qb);
+                if (qa < 0) continue;  // wave-uniform
+                const int qg = half ? qb : qa;
+                const float th = half ? thr_of(qb) : thr_of(qa);
+                if (qg >= 0) {
+                    lb[pp] = box_lb<SP, F>(bx, &qrow[qoff + qg * FS], w0, w1);
+                    tneed |= lb[pp] <= th;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < GH; ++j) {
+                lb[j] = box_lb<SP, F>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
+                tneed |= lb[j] <= (half ? thr[GH + j] : thr[j]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
         uint32_t m = fold_tiles(__ballot(tneed));
         float x[R], xn[R];
@@ -1814,6 +1871,7 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
             load_tile((uint32_t)ss, t, x, id);
         }
         const int ssn = next_super();
+        const uint32_t bitsn = pop_bits;
         if (ssn >= 0) load_tbox((uint32_t)ssn, bx);
         while (have) {
             const bool more = m != 0;
@@ -1822,7 +1880,7 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
                 m &= m - 1;
                 load_tile((uint32_t)ss, tn, xn, idn);
             }
-            scan_tile((uint32_t)ss, t, x, id, lb);
+            scan_tile((uint32_t)ss, t, x, id, lb, bits);
             if (!more) break;
 #pragma unroll
             for (int rr = 0; rr < R; ++rr) x[rr] = xn[rr];
@@ -1830,6 +1888,7 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
             t = tn;
         }
         ss = ssn;
+        bits = bitsn;
     }
     if (lane == 0) {
         if (!FILL) {
