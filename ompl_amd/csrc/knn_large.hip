@@ -742,7 +742,7 @@ __global__ __launch_bounds__(kSelBlock) void sel_sort_kernel(const double *__res
     if (tid < chunks) coff[tid] = pre;
     if (tid == 0) coff[chunks] = tot;
     __syncthreads();
-    if (stats && tid == 0) atomicAdd(&stats[sh_bad ? 1 : 0], sh_bad || nov > 0 ? 1ull : 0ull);
+    if (stats && tid == 0 && (sh_bad || nov > 0)) atomicAdd(&stats[sh_bad ? 1 : 0], 1ull);
     if (sh_bad) {
         if (tid == 0) fb_list[atomicAdd(fb_count, 1u)] = q;
         return;
