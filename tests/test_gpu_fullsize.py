@@ -197,3 +197,80 @@ def test_cfg4_chain_culled_scan_1e6(gpu):
     np.testing.assert_array_equal(d2[pick2], od2)
     np.testing.assert_array_equal(ids2[pick2].astype(np.int64), live_ids[oi2.astype(np.int64)])
     nn.close()
+
+
+# ---- every query at full size: the culled paths against the exact fp64 scan -------------------
+# The oracle checks above sample queries (the CPU brute force over 10^6-10^7 states is slow); here
+# every query of the bench batch is compared with the library's exact fp64 brute-force scan
+# (set_exact: no fp32 screen, no culling — itself pinned against the oracle by test_gpu_nn.py on
+# every space), bit for bit: ids and distances.
+def _culled_vs_exact(sp, tree, q, k, gpu):
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(tree)
+    ids, d, cnt = nn.nearestKBatch(q, k)
+    nn.set_exact(True)
+    ei, ed, ecnt = nn.nearestKBatch(q, k)
+    nn.close()
+    np.testing.assert_array_equal(cnt, ecnt)
+    np.testing.assert_array_equal(d, ed)
+    np.testing.assert_array_equal(ids, ei)
+
+
+def test_cfg3_every_query_vs_exact_scan(gpu):
+    import bench
+
+    sp = SE3StateSpace(0.0, 1.0)
+    tree, q = bench.reference_inputs(sp, 1_000_000, 100_000, 0)
+    _culled_vs_exact(sp, tree, q, 10, gpu)
+
+
+def test_cfg2_every_query_vs_exact_scan(gpu):
+    import bench
+    from ompl_amd.spaces import RealVectorStateSpace
+
+    sp = RealVectorStateSpace(6)
+    tree, q = bench.reference_inputs(sp, 100_000, 100_000, 0)
+    _culled_vs_exact(sp, tree, q, 10, gpu)
+
+
+def test_cfg4_every_milestone_vs_exact_scan(gpu):
+    import bench
+    from ompl_amd.spaces import KinematicChainSpace
+
+    sp = KinematicChainSpace(12, 1.0 / 12)
+    tree, q = bench.reference_inputs(sp, 1_000_000, 8_192, 0)
+    _culled_vs_exact(sp, tree, q, 41, gpu)
+
+
+def test_cfg5k_every_vertex_vs_exact_scan(gpu):
+    """BIT*'s kNN mode at its k = 57 on the 10^7 valid-sample set, 10^4 vertices."""
+    import bench
+
+    sp = SE3StateSpace(0.0, 1.0)
+    c, rr = W.sphere_field(32, 0.1, 7)
+    mv = DiscreteMotionValidatorGPU(sp, SpheresChecker(c, rr), gpu)
+    tree, q = bench.reference_inputs(sp, 10_000_000, 10_000, 0, valid=mv.isValid)
+    mv.close()
+    _culled_vs_exact(sp, tree, q, 57, gpu)
+
+
+def test_cfg5_every_vertex_radius_vs_exact_scan(gpu):
+    """BIT*'s radius mode (r = 0.1528) on the 10^7 valid-sample set, 2 x 10^4 vertices: the slab
+    walk's CSR equals the exact fp64 scan's, offsets, ids and distances."""
+    import bench
+
+    sp = SE3StateSpace(0.0, 1.0)
+    c, rr = W.sphere_field(32, 0.1, 7)
+    mv = DiscreteMotionValidatorGPU(sp, SpheresChecker(c, rr), gpu)
+    tree, q = bench.reference_inputs(sp, 10_000_000, 20_000, 0, valid=mv.isValid)
+    mv.close()
+    r = W.bitstar_radius(len(tree), 6, math.pi ** 2)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(tree)
+    off, ids, d = nn.nearestRBatch(q, r)
+    nn.set_exact(True)
+    eoff, eids, ed = nn.nearestRBatch(q, r)
+    nn.close()
+    np.testing.assert_array_equal(off, eoff)
+    np.testing.assert_array_equal(ids, eids)
+    np.testing.assert_array_equal(d, ed)
