@@ -582,6 +582,31 @@ __device__ __forceinline__ void wave_merge_sorted_k(uint64_t &L, uint64_t c, int
 // 1.42 / 1.41 ms at 64 / 8 / 32; R^6 1.60 / 1.12 / 1.13 / 1.21 ms at 64 / 8 / 16 / 32
 constexpr int kBulkThreshold = 8;
 
+// Group-walk A/B features (variant builds, make variant VARIANT=n):
+//   WALK_CASCADE (7, 9, 12): square-root-free rejects before the chord and square roots;
+//   WALK_DYN (8, 9, 12): tile bounds only for the queries whose super-tile bound passes;
+//   WALK_TFIRST (12): a mask pass whose translation gaps alone exclude every (tile, query) pair
+//   skips its rotation gaps.
+#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 7 || OMPL_AMD_VARIANT == 9 || OMPL_AMD_VARIANT == 12)
+#define OMPL_WALK_CASCADE 1
+#endif
+#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 8 || OMPL_AMD_VARIANT == 9 || OMPL_AMD_VARIANT == 12)
+#define OMPL_WALK_DYN 1
+#endif
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 12
+#define OMPL_WALK_TFIRST 1
+#endif
+// translation part of box_lb<SE3>: the squared gap of query row q to box bx
+__device__ __forceinline__ float box_tgap2(const float *bx, const float *q, int NB) {
+    float tg = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float g = gap(bx[c] - q[c], q[c] - bx[NB + c]);
+        tg = fmaf(g, g, tg);
+    }
+    return tg;
+}
+
 // K2: lanes per query in the output (16 / 32 / 64); k2 <= K2: the list length the walk keeps
 // (the certificate's margin: k + 3 for the culled spaces, whose screen error is small)
 template <int SP, int F, int K2, int G, int MINW, bool QS>
@@ -594,10 +619,15 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
     constexpr int GH = G / 2;
     static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
-#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 8 || OMPL_AMD_VARIANT == 9)
+#if defined(OMPL_WALK_DYN)
     constexpr bool kDyn = true;
 #else
     constexpr bool kDyn = false;
+#endif
+#if defined(OMPL_WALK_TFIRST)
+    constexpr bool kTFirst = SP == OMPL_GPU_SPACE_SE3;
+#else
+    constexpr bool kTFirst = false;
 #endif
     __shared__ __attribute__((aligned(16))) float qrow[G * FS];
     const int lane = threadIdx.x;
@@ -692,6 +722,10 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
                 if (qa < 0) continue;  // wave-uniform
                 const int qg = half ? qb : qa;
                 const float thr = half ? td_of(qb) : td_of(qa);
+                if constexpr (kTFirst) {  // w0 |t gap| >= thr for every lane: no tile of this pass
+                    const float tg = qg >= 0 ? box_tgap2(bx, &qrow[qoff + qg * FS], Geo<SP, F>::NB) : __builtin_inff();
+                    if (!__ballot(w0 * w0 * tg < thr * thr * 1.0001f)) continue;
+                }
                 if (qg >= 0) {
                     lb[p] = box_lb<SP, F, true>(bx, &qrow[qoff + qg * FS], w0, w1);
                     need |= lb[p] < thr;
@@ -777,7 +811,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
                 float t = dx * dx;
                 t = fmaf(dy, dy, t);
                 t = fmaf(dz, dz, t);
-#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 7 || OMPL_AMD_VARIANT == 9)
+#if defined(OMPL_WALK_CASCADE)
                 // square-root-free rejects first: d >= w0 |t| + w1 c and (a + b)^2 >= a^2 + b^2, so
                 // a lane with w0^2 t (+ w1^2 c^2) >= td^2 (1 + 1e-4) has d > td after any fp32
                 // rounding (the slack is far above it): no lane below -> the wave skips the

@@ -7,11 +7,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/r4b; mkdir -p "$out"
 T="tests/test_gpu_nn.py tests/test_gpu_cull.py"
-for v in ${VARS:-7 8 9}; do
+for v in ${VARS:-7 8 9 12}; do
   OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var$v.so timeout -k 10 300 python -u -m pytest $T -m gpu -x -q --timeout 200 \
       --timeout-method thread > "$out/pytest_v$v.log" 2>&1
   rc=$?; echo "var$v: $(tail -1 "$out/pytest_v$v.log")"; case $rc in 0) ;; 124|134|137|139) exit 1;; *) echo "var$v failed";; esac
 done
-bash tools/ab_env.sh cfg3 "--workload cfg3" 3 - VAR=7 VAR=8 VAR=9 OMPL_GPU_QSORT=0 || exit 1
+bash tools/ab_env.sh cfg3 "--workload cfg3" 3 - VAR=7 VAR=8 VAR=9 VAR=12 OMPL_GPU_QSORT=0 || exit 1
 bash tools/ab_env.sh cfg4 "--workload cfg4" 2 - OMPL_GPU_CHAIN_SHARE=0 VAR=10 || exit 1
 bash tools/ab_env.sh cfg5 "--workload cfg5" 2 - VAR=5 VAR=6 VAR=11
