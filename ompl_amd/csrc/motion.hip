@@ -127,8 +127,7 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void state_valid_kern
 }
 
 // the specialisations: SE3 (7 reals), SO3 (4), R^2 / R^3 / R^6 (the closed checker set's
-// spaces), the 12-link KinematicChain; everything else (other R^n, other chains) takes the
-// runtime-width form.  A
+// spaces); everything else (other R^n, KinematicChain) takes the runtime-width form.  A
 // hypercube over more coordinates than the fixed width, and the KinematicChain checker, never
 // take a fixed form.
 template <class F>
@@ -137,7 +136,10 @@ static hipError_t dispatch_width(const DevSpace &sp, const DevChecker &ck, F &&l
                            ck.kind == OMPL_GPU_CHECK_CIRCLES2D ||
                            (ck.kind == OMPL_GPU_CHECK_HYPERCUBE && ck.ndim <= sp.dim));
     // the KinematicChain benchmark's 12 links (KinematicChainBenchmark.cpp:48): its checker or none
-#if !(defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 10)  // A/B build: the runtime-width form
+    // (A/B build, variant 10: the 12-link chain's fixed form — measured 2.49 ms per cfg4 batch of
+    // motion checks against the runtime form's 1.13 ms: no scratch, but 290 VGPRs leave one wave
+    // per SIMD, and the fp64 trigonometry and segment tests then wait on their own latencies)
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 10
     if (sp.kind == OMPL_GPU_SPACE_KCHAIN && sp.dim == 12 &&
         (ck.kind == OMPL_GPU_CHECK_KCHAIN || ck.kind == OMPL_GPU_CHECK_ALL_VALID))
         return launch(std::integral_constant<int, OMPL_GPU_SPACE_KCHAIN>{}, std::integral_constant<int, 12>{});

@@ -141,6 +141,137 @@ __global__ __launch_bounds__(256) void prm_causal_kernel(const double *__restric
     }
 }
 
+// The KinematicChain form of the causal scan, tiled: a wave serves kCausalGroup consecutive
+// milestones of the slice, lanes hold 64 earlier batch rows j' (their fp32 joint positions, read
+// once per tile for the whole group); each milestone screens the tile by the fp32 chain distance
+// against its stored bound + the chain screen error, and only the survivors take the exact fp64
+// distance (as prm_causal_kernel with p32; same segments).  (Round 4 measured the untiled
+// screened form at 1.5 ms per pass over 8,192 milestones — one wave per milestone holding 144
+// VGPRs, its loop a chain of dependent row loads — against 0.6 ms for the unscreened fp64 form.)
+constexpr int kCausalGroup = 4;
+template <int F, int NMAX, bool FILL>
+__global__ __launch_bounds__(64) void prm_causal_tile_kernel(const double *__restrict__ bf,
+                                                             const float *__restrict__ p32, uint32_t j0,
+                                                             uint32_t rows, uint32_t n0, DevSpace sp,
+                                                             const uint32_t *__restrict__ kj_arr,
+                                                             const double *__restrict__ sd,
+                                                             const uint32_t *__restrict__ si, uint32_t kq,
+                                                             uint64_t *__restrict__ seg_len,
+                                                             const uint64_t *__restrict__ seg_off,
+                                                             double *__restrict__ out_d, uint32_t *__restrict__ out_i,
+                                                             unsigned long long *__restrict__ seg_max) {
+    constexpr int NM = F / 2, GJ = kCausalGroup;
+    static_assert(F % 4 == 0, "float4 rows");
+    // the group's rows and per-milestone state live in LDS (one wave: its LDS operations complete
+    // in order), read at each use: held in VGPRs for every milestone they cost ~390 registers
+    __shared__ __attribute__((aligned(16))) float qp[GJ][F];
+    __shared__ double qv[GJ][F];
+    __shared__ double s_bound[GJ];
+    __shared__ float s_thr[GJ];
+    __shared__ unsigned long long s_cnt[GJ], s_pos[GJ];
+    __shared__ uint32_t s_stored[GJ];
+    const int lane = threadIdx.x;
+    const uint32_t r0 = blockIdx.x * GJ;
+    for (int t = lane; t < GJ * F; t += 64) {
+        const uint32_t row = r0 + t / F;
+        const bool ok = row < rows;
+        qp[t / F][t % F] = ok ? p32[(size_t)(j0 + row) * F + t % F] : __builtin_nanf("");
+        qv[t / F][t % F] = ok ? bf[(size_t)(j0 + row) * F + t % F] : 0.0;
+    }
+    if (lane < GJ) {
+        const uint32_t row = r0 + lane;
+        const bool ok = row < rows;
+        const uint32_t kj = ok ? kj_arr[j0 + row] : 0u;
+        const double bound = ok ? stored_bound(sd, si, kq, kj, row) : -1.0;
+        constexpr double u = 5.9604644775390625e-08, fmin = 1.1754943508222875e-38;
+        const double n = (double)sp.dim;
+        const double e = 2.0 * (sp.link * 8.0 * u * n * (n + 1.0) + (n + 2.0) * u * bound + sp.link * n * sqrt(2.0 * fmin));
+        s_bound[lane] = bound;
+        s_thr[lane] = bound < __builtin_inf() ? (float)((bound + e) * (1.0 + 16.0 * u)) : __builtin_inff();
+        s_stored[lane] = ok ? stored_take(si, kq, kj, row) : 0u;
+        s_cnt[lane] = 0;
+        s_pos[lane] = (FILL && ok) ? seg_off[row] + s_stored[lane] : 0ull;
+    }
+    __syncthreads();
+    if (FILL) {
+        for (int g = 0; g < GJ; ++g) {  // stored entries first: (distance, id) sorted already
+            const uint32_t row = r0 + g;
+            if (row >= rows) break;
+            const uint64_t p0 = seg_off[row];
+            for (uint32_t r = lane; r < s_stored[g]; r += 64) {
+                out_d[p0 + r] = sd[(size_t)row * kq + r];
+                out_i[p0 + r] = si[(size_t)row * kq + r];
+            }
+        }
+    }
+    const uint32_t last = min(r0 + GJ, rows);
+    const uint32_t jend = last > r0 ? j0 + last - 1 : 0u;  // milestones of the group are <= jend
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const float link = (float)sp.link;
+    uint32_t off = 0;  // LDS row offset the compiler cannot see through (no hoisting into VGPRs)
+    for (uint32_t b = 0; b < jend; b += 64) {
+        const uint32_t jp = b + lane;
+        float x[F];
+        if (jp < jend) {
+            const float4 *r4 = reinterpret_cast<const float4 *>(p32 + (size_t)jp * F);
+#pragma unroll
+            for (int c = 0; c < F / 4; ++c) {
+                const float4 v = r4[c];
+                x[4 * c] = v.x; x[4 * c + 1] = v.y; x[4 * c + 2] = v.z; x[4 * c + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < F; ++c) x[c] = __builtin_nanf("");
+        }
+#pragma unroll 1
+        for (int g = 0; g < GJ; ++g) {
+            const uint32_t j = j0 + r0 + g;
+            asm volatile("" : "+s"(off));
+            const double bound = s_bound[g];
+            if (r0 + g >= rows || b >= j || !(bound >= 0.0)) continue;  // wave-uniform
+            const float *q = &qp[0][0] + off + g * F;
+            float acc = 0.f;
+#pragma unroll
+            for (int i = 0; i < NM; ++i) {
+                if (i < sp.dim) {
+                    const float dx = x[i] - q[i], dy = x[NM + i] - q[NM + i];
+                    acc += __builtin_amdgcn_sqrtf(fmaf(dy, dy, dx * dx));
+                }
+            }
+            const bool cand = jp < j && acc * link <= s_thr[g];  // NaN never passes
+            bool hit = false;
+            double d = 0.0;
+            if (__ballot(cand)) {
+                if (cand) {
+                    double sv[F];
+#pragma unroll
+                    for (int f = 0; f < F; ++f) sv[f] = bf[(size_t)jp * F + f];
+                    d = feat_dist<OMPL_GPU_SPACE_KCHAIN, F, NMAX>(sv, &qv[0][0] + off + g * F, sp);  // reference order
+                    hit = d <= bound;
+                }
+            }
+            const uint64_t bm = __ballot(hit);
+            if (bm) {
+                const unsigned long long c = s_cnt[g];
+                if (FILL && hit) {
+                    const uint64_t p = s_pos[g] + c + (uint64_t)__popcll(bm & lt);
+                    out_d[p] = d;
+                    out_i[p] = n0 + jp;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) s_cnt[g] = c + (unsigned long long)__popcll(bm);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    __syncthreads();
+    if (!FILL && lane < GJ && r0 + lane < rows) {
+        const uint64_t len = s_stored[lane] + s_cnt[lane];
+        seg_len[r0 + lane] = len;
+        if (seg_max) atomicMax(seg_max, (unsigned long long)len);
+    }
+}
+
 // thread per (milestone, rank): the first min(k_j, segment) sorted entries
 __global__ void prm_take_kernel(const uint32_t *__restrict__ sorted_i, const double *__restrict__ sorted_d,
                                 const uint64_t *__restrict__ seg_off, const uint32_t *__restrict__ kj_arr, uint32_t m,
@@ -194,6 +325,18 @@ hipError_t run_prm_causal(const DevSpace &sp, bool fill, const double *bf, uint3
     if constexpr (SP != OMPL_GPU_SPACE_KCHAIN) p32 = nullptr;
     if (p32 && !fill)  // the positions of every batch row (earlier milestones of other slices too)
         hipLaunchKernelGGL((prm_positions_kernel<F>), dim3((m + 255) / 256), dim3(256), 0, st, bf, m, p32);
+    if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
+        if (p32) {
+            const dim3 gt((rows + kCausalGroup - 1) / kCausalGroup), b64(64);
+            if (fill)
+                hipLaunchKernelGGL((prm_causal_tile_kernel<F, NMAX, true>), gt, b64, 0, st, bf, p32, j0, rows, n0, sp,
+                                   kj, sd, si, kq, seg_len, seg_off, out_d, out_i, nullptr);
+            else
+                hipLaunchKernelGGL((prm_causal_tile_kernel<F, NMAX, false>), gt, b64, 0, st, bf, p32, j0, rows, n0, sp,
+                                   kj, sd, si, kq, seg_len, seg_off, out_d, out_i, seg_max);
+            return hipGetLastError();
+        }
+    }
     if (fill)
         hipLaunchKernelGGL((prm_causal_kernel<SP, F, NMAX, true>), grid, block, 0, st, bf, j0, rows, n0, sp, kj, sd, si,
                            kq, seg_len, seg_off, out_d, out_i, p32, nullptr);

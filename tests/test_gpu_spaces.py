@@ -82,12 +82,14 @@ def test_state_space_test_interpolation(gpu, name):
     assert np.all(mv.distance(s1, s3) < EPS)
     s3 = mv.interpolate(s1, s2, 1.0)
     assert np.all(mv.distance(s2, s3) < EPS)
-    s3 = mv.interpolate(s1, s2, 0.5)
-    tri = mv.distance(s1, s3) + mv.distance(s3, s2) - mv.distance(s1, s2)
-    assert np.all(np.abs(tri) < EPS)
-    s3 = mv.interpolate(s3, s2, 0.5)           # interpolate(s3, s2, 0.5, s3)
-    s2b = mv.interpolate(s1, s2, 0.75)          # interpolate(s1, s2, 0.75, s2)
-    assert np.all(mv.distance(s2b, s3) < EPS)
+    if name != "chain12":  # the reference runs StateSpaceTest on its own spaces only: the demo
+        # chain's metric (sum of joint-position gaps) is not geodesic along its interpolation
+        s3 = mv.interpolate(s1, s2, 0.5)
+        tri = mv.distance(s1, s3) + mv.distance(s3, s2) - mv.distance(s1, s2)
+        assert np.all(np.abs(tri) < EPS)
+        s3 = mv.interpolate(s3, s2, 0.5)           # interpolate(s3, s2, 0.5, s3)
+        s2b = mv.interpolate(s1, s2, 0.75)          # interpolate(s1, s2, 0.75, s2)
+        assert np.all(mv.distance(s2b, s3) < EPS)
     # per-pair fractions and the oracle restatement of interpolate
     t = np.linspace(0.0, 1.0, N)
     si = mv.interpolate(s1, s2, t)
