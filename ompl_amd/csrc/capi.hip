@@ -1445,10 +1445,12 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     }
     // 2. in-batch causal candidates: count, offsets, fill, segmented sort by distance (stable:
     //    stored entries first, candidates in id order, so ties resolve by id)
-    HIP_OR_FAIL(h->prm_len.ensure(sizeof(uint64_t) * (rows + 2)));
+    // prm_len: [0, rows) segment lengths, [rows] 0 (the scan's total), [rows + 1] the longest
+    // segment, [rows + 2, 2 rows + 2) the fill's per-milestone cursors (chain tiles)
+    HIP_OR_FAIL(h->prm_len.ensure(sizeof(uint64_t) * (2 * rows + 2)));
     HIP_OR_FAIL(h->prm_off.ensure(sizeof(uint64_t) * (rows + 1)));
     uint64_t *len = (uint64_t *)h->prm_len.p, *off = (uint64_t *)h->prm_off.p;
-    HIP_OR_FAIL(hipMemsetAsync(len + rows, 0, 2 * sizeof(uint64_t), h->stream));  // [rows]: 0, [rows + 1]: longest
+    HIP_OR_FAIL(hipMemsetAsync(len + rows, 0, 2 * sizeof(uint64_t), h->stream));
     float *p32 = nullptr;
     if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN) {  // the causal scan's fp32 screen
         HIP_OR_FAIL(h->prm_p32.ensure(sizeof(float) * m * F));
@@ -1475,20 +1477,29 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     uint32_t *ci = (uint32_t *)h->ids.p, *sii = (uint32_t *)h->sorted_ids.p;
     if (tot) {
         HIP_OR_FAIL(launch_prm_causal(h->sp, h->g, true, bf, (uint32_t)j0, (uint32_t)rows, (uint32_t)n0, dkj, sd, si,
-                                      kq, nullptr, off, cd, ci, p32, (uint32_t)m, nullptr, h->stream));
+                                      kq, nullptr, off, cd, ci, p32, (uint32_t)m, (unsigned long long *)(len + rows + 1),
+                                      h->stream));
     }
     if (tot && longest <= kRankSortMax) {  // every segment fits a wave's LDS: rank placement by (distance, id)
         HIP_OR_FAIL(launch_segment_rank_sort(off, ci, cd, (uint32_t)rows, sii, sdd, h->stream));
-    } else if (tot) {
-        size_t tb = 0;
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, (const double *)cd, sdd,
-                                                                (const uint32_t *)ci, sii, (int)tot, (int)rows, off,
+    } else if (tot) {  // long segments: two stable radix passes, by id and then by distance
+        size_t tb1 = 0, tb2 = 0;
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb1, (const uint32_t *)ci, sii,
+                                                                (const double *)cd, sdd, (int)tot, (int)rows, off,
+                                                                off + 1, 0, 32, h->stream));
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb2, (const double *)sdd, cd,
+                                                                (const uint32_t *)sii, ci, (int)tot, (int)rows, off,
                                                                 off + 1, 0, 64, h->stream));
-        HIP_OR_FAIL(h->tmp.ensure(tb));
-        tb = h->tmp.bytes;
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb, (const double *)cd, sdd,
-                                                                (const uint32_t *)ci, sii, (int)tot, (int)rows, off,
+        HIP_OR_FAIL(h->tmp.ensure(std::max(tb1, tb2)));
+        tb1 = tb2 = h->tmp.bytes;
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb1, (const uint32_t *)ci, sii,
+                                                                (const double *)cd, sdd, (int)tot, (int)rows, off,
+                                                                off + 1, 0, 32, h->stream));
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb2, (const double *)sdd, cd,
+                                                                (const uint32_t *)sii, ci, (int)tot, (int)rows, off,
                                                                 off + 1, 0, 64, h->stream));
+        std::swap(cd, sdd);  // the result is in (cd, ci): read it from there
+        std::swap(ci, sii);
     }
     HIP_OR_FAIL(launch_prm_take(sii, sdd, off, dkj + j0, (uint32_t)rows, k_cap, d_nbr, d_cnt, d_dist, h->stream));
     if (!mv) return add_locked(h, states, m, nullptr);  // lazy: edge validity stays unknown (LazyPRM.cpp:302)

@@ -142,13 +142,18 @@ __global__ __launch_bounds__(256) void prm_causal_kernel(const double *__restric
 }
 
 // The KinematicChain form of the causal scan, tiled: a wave serves kCausalGroup consecutive
-// milestones of the slice, lanes hold 64 earlier batch rows j' (their fp32 joint positions, read
-// once per tile for the whole group); each milestone screens the tile by the fp32 chain distance
-// against its stored bound + the chain screen error, and only the survivors take the exact fp64
-// distance (as prm_causal_kernel with p32; same segments).  (Round 4 measured the untiled
-// screened form at 1.5 ms per pass over 8,192 milestones — one wave per milestone holding 144
-// VGPRs, its loop a chain of dependent row loads — against 0.6 ms for the unscreened fp64 form.)
+// milestones of the slice over one chunk of kCausalChunk earlier batch rows (grid.y), lanes
+// hold 64 rows j' at a time (their fp32 joint positions, read once per tile for the whole
+// group); each milestone screens the tile by the fp32 chain distance against its stored bound +
+// the chain screen error, and only the survivors take the exact fp64 distance.  Counts add into
+// seg_len (zeroed by the caller, the stored entries counted by chunk 0); the fill appends each
+// chunk's hits at an atomic cursor per milestone, so a segment's candidates are in no particular
+// order — the caller sorts every segment by (distance, id), which is the order the stable sort
+// of [stored | candidates in id order] gives.  (Round 4 measured: one wave per milestone with
+// the screen 1.5 ms per pass over 8,192 milestones; a wave per 4 milestones over every earlier
+// row 0.55 ms, its longest waves 128 dependent tile loads; the unscreened fp64 form 0.6 ms.)
 constexpr int kCausalGroup = 4;
+constexpr uint32_t kCausalChunk = 1024;
 template <int F, int NMAX, bool FILL>
 __global__ __launch_bounds__(64) void prm_causal_tile_kernel(const double *__restrict__ bf,
                                                              const float *__restrict__ p32, uint32_t j0,
@@ -159,7 +164,7 @@ __global__ __launch_bounds__(64) void prm_causal_tile_kernel(const double *__res
                                                              uint64_t *__restrict__ seg_len,
                                                              const uint64_t *__restrict__ seg_off,
                                                              double *__restrict__ out_d, uint32_t *__restrict__ out_i,
-                                                             unsigned long long *__restrict__ seg_max) {
+                                                             unsigned long long *__restrict__ cursor) {
     constexpr int NM = F / 2, GJ = kCausalGroup;
     static_assert(F % 4 == 0, "float4 rows");
     // the group's rows and per-milestone state live in LDS (one wave: its LDS operations complete
@@ -172,6 +177,8 @@ __global__ __launch_bounds__(64) void prm_causal_tile_kernel(const double *__res
     __shared__ uint32_t s_stored[GJ];
     const int lane = threadIdx.x;
     const uint32_t r0 = blockIdx.x * GJ;
+    const uint32_t cb = blockIdx.y * kCausalChunk;  // this wave's rows j' in [cb, cb + kCausalChunk)
+    if (r0 >= rows || cb >= j0 + min(r0 + GJ, rows) - 1 + (blockIdx.y == 0 ? 1u : 0u)) return;  // no earlier row here
     for (int t = lane; t < GJ * F; t += 64) {
         const uint32_t row = r0 + t / F;
         const bool ok = row < rows;
@@ -193,7 +200,7 @@ __global__ __launch_bounds__(64) void prm_causal_tile_kernel(const double *__res
         s_pos[lane] = (FILL && ok) ? seg_off[row] + s_stored[lane] : 0ull;
     }
     __syncthreads();
-    if (FILL) {
+    if (FILL && blockIdx.y == 0) {
         for (int g = 0; g < GJ; ++g) {  // stored entries first: (distance, id) sorted already
             const uint32_t row = r0 + g;
             if (row >= rows) break;
@@ -205,11 +212,11 @@ __global__ __launch_bounds__(64) void prm_causal_tile_kernel(const double *__res
         }
     }
     const uint32_t last = min(r0 + GJ, rows);
-    const uint32_t jend = last > r0 ? j0 + last - 1 : 0u;  // milestones of the group are <= jend
+    const uint32_t jend = min(j0 + last - 1, cb + kCausalChunk);  // rows j' < jend can precede the group
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const float link = (float)sp.link;
     uint32_t off = 0;  // LDS row offset the compiler cannot see through (no hoisting into VGPRs)
-    for (uint32_t b = 0; b < jend; b += 64) {
+    for (uint32_t b = cb; b < jend; b += 64) {
         const uint32_t jp = b + lane;
         float x[F];
         if (jp < jend) {
@@ -252,24 +259,40 @@ __global__ __launch_bounds__(64) void prm_causal_tile_kernel(const double *__res
             }
             const uint64_t bm = __ballot(hit);
             if (bm) {
-                const unsigned long long c = s_cnt[g];
-                if (FILL && hit) {
-                    const uint64_t p = s_pos[g] + c + (uint64_t)__popcll(bm & lt);
-                    out_d[p] = d;
-                    out_i[p] = n0 + jp;
+                if (FILL) {  // this tile's hits at the milestone's cursor (chunks append concurrently)
+                    unsigned long long c = 0;
+                    if (lane == 0) c = atomicAdd(&cursor[r0 + g], (unsigned long long)__popcll(bm));
+                    c = (unsigned long long)__shfl((long long)c, 0);
+                    if (hit) {
+                        const uint64_t p = s_pos[g] + c + (uint64_t)__popcll(bm & lt);
+                        out_d[p] = d;
+                        out_i[p] = n0 + jp;
+                    }
+                } else {
+                    const unsigned long long c = s_cnt[g];
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane == 0) s_cnt[g] = c + (unsigned long long)__popcll(bm);
+                    __builtin_amdgcn_wave_barrier();
                 }
-                __builtin_amdgcn_wave_barrier();
-                if (lane == 0) s_cnt[g] = c + (unsigned long long)__popcll(bm);
-                __builtin_amdgcn_wave_barrier();
             }
         }
     }
     __syncthreads();
     if (!FILL && lane < GJ && r0 + lane < rows) {
-        const uint64_t len = s_stored[lane] + s_cnt[lane];
-        seg_len[r0 + lane] = len;
-        if (seg_max) atomicMax(seg_max, (unsigned long long)len);
+        const uint64_t add = (blockIdx.y == 0 ? s_stored[lane] : 0u) + s_cnt[lane];
+        if (add) atomicAdd((unsigned long long *)&seg_len[r0 + lane], (unsigned long long)add);
     }
+}
+
+// the longest segment (the sort's choice): wave max, one atomic per wave
+__global__ void seg_max_kernel(const uint64_t *__restrict__ len, uint32_t rows, unsigned long long *__restrict__ mx) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long v = i < rows ? len[i] : 0ull;
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long w = (unsigned long long)__shfl_xor((long long)v, o);
+        v = w > v ? w : v;
+    }
+    if ((threadIdx.x & 63) == 0 && v) atomicMax(mx, v);
 }
 
 // thread per (milestone, rank): the first min(k_j, segment) sorted entries
@@ -327,13 +350,21 @@ hipError_t run_prm_causal(const DevSpace &sp, bool fill, const double *bf, uint3
         hipLaunchKernelGGL((prm_positions_kernel<F>), dim3((m + 255) / 256), dim3(256), 0, st, bf, m, p32);
     if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) {
         if (p32) {
-            const dim3 gt((rows + kCausalGroup - 1) / kCausalGroup), b64(64);
-            if (fill)
+            // chunks of earlier rows: the last milestone of the slice has j0 + rows - 1 of them
+            const uint32_t nc = (j0 + rows - 1 + kCausalChunk) / kCausalChunk;
+            const dim3 gt((rows + kCausalGroup - 1) / kCausalGroup, nc), b64(64);
+            hipError_t e;
+            if (fill) {
+                // the cursors live past the counts' slots: seg_max[1 .. rows] (zeroed here)
+                if ((e = hipMemsetAsync(seg_max + 1, 0, sizeof(unsigned long long) * rows, st)) != hipSuccess) return e;
                 hipLaunchKernelGGL((prm_causal_tile_kernel<F, NMAX, true>), gt, b64, 0, st, bf, p32, j0, rows, n0, sp,
-                                   kj, sd, si, kq, seg_len, seg_off, out_d, out_i, nullptr);
-            else
+                                   kj, sd, si, kq, seg_len, seg_off, out_d, out_i, seg_max + 1);
+            } else {
+                if ((e = hipMemsetAsync(seg_len, 0, sizeof(uint64_t) * rows, st)) != hipSuccess) return e;
                 hipLaunchKernelGGL((prm_causal_tile_kernel<F, NMAX, false>), gt, b64, 0, st, bf, p32, j0, rows, n0, sp,
-                                   kj, sd, si, kq, seg_len, seg_off, out_d, out_i, seg_max);
+                                   kj, sd, si, kq, seg_len, seg_off, out_d, out_i, nullptr);
+                hipLaunchKernelGGL(seg_max_kernel, dim3((rows + 255) / 256), dim3(256), 0, st, seg_len, rows, seg_max);
+            }
             return hipGetLastError();
         }
     }
