@@ -1728,10 +1728,15 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
     // kDyn (A/B variant 11): each lane also records which queries its super-tile passes
     // (sneed, LDS), and a popped super-tile's tile bounds are computed only for those queries,
     // paired onto the two half-waves (as knn32_group_kernel's kDyn)
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 11
+#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 11 || OMPL_AMD_VARIANT == 13)
     constexpr bool kDyn = true;
 #else
     constexpr bool kDyn = false;
+#endif
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 13
+    constexpr bool kCascade = SP == OMPL_GPU_SPACE_SE3;  // A/B variant 13: + square-root-free rejects
+#else
+    constexpr bool kCascade = false;
 #endif
     __shared__ uint32_t sneed[64];
     uint32_t pop_bits = (1u << G) - 1u;
@@ -1832,6 +1837,10 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
                 float tt = dx * dx;
                 tt = fmaf(dy, dy, tt);
                 tt = fmaf(dz, dz, tt);
+                if constexpr (kCascade) {  // as the kNN walk's cascade: (a + b)^2 >= a^2 + b^2
+                    const float t2 = thr[g] * thr[g] * 1.0001f;
+                    if (!__ballot(w0 * w0 * tt <= t2)) continue;  // no lane can hit: nothing to count or write
+                }
                 const float c2 = chord2(x + 3, qq + 4);
                 const float c = __builtin_amdgcn_sqrtf(c2), wt = w0 * __builtin_amdgcn_sqrtf(tt);
                 hit = __ballot(fmaf(w1, c, wt) <= thr[g]) && fmaf(w1, chord_theta(c, c2), wt) <= thr[g];
