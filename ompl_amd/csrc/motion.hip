@@ -171,6 +171,10 @@ static hipError_t dispatch_width(const DevSpace &sp, const DevChecker &ck, F &&l
 // 12-link horn benchmark spread over the lanes (any intersection = invalid).  The motion
 // validator walks an edge's samples in the same FIFO-bisection order with the same early exit,
 // so the isValid count is the reference's.  Same arithmetic as chain_valid, bit for bit.
+// Measured on cfg4 (round 4): 1.88 ms per batch of motion checks against 1.17 ms for the
+// thread-per-edge runtime-width form — every check pays the serial prefix loops, 64 lanes of
+// sincos and all 364 tests, where a thread leaves at its first intersection — so it stays an
+// A/B form (OMPL_GPU_CHAIN_WAVE=1); the product keeps the thread-per-edge kernels.
 constexpr int kChainWaveMax = 62;  // links: positions n + 2 <= 64 lanes
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -361,9 +365,9 @@ __global__ __launch_bounds__(256) void state_valid_chain_wave_kernel(DevSpace sp
 }
 
 static bool chain_wave(const DevSpace &sp, const DevChecker &ck) {
-    static const int on = [] {  // A/B switch: OMPL_GPU_CHAIN_WAVE=0 -> the thread-per-edge kernels
+    static const int on = [] {  // A/B switch: OMPL_GPU_CHAIN_WAVE=1 -> the wave-per-check kernels
         const char *v = std::getenv("OMPL_GPU_CHAIN_WAVE");
-        return v ? std::atoi(v) : 1;
+        return v ? std::atoi(v) : 0;
     }();
     return on && sp.kind == OMPL_GPU_SPACE_KCHAIN && ck.kind == OMPL_GPU_CHECK_KCHAIN && sp.dim >= 1 &&
            sp.dim <= kChainWaveMax;

@@ -13,5 +13,5 @@ for v in ${VARS:-7 8 9 12}; do
   rc=$?; echo "var$v: $(tail -1 "$out/pytest_v$v.log")"; case $rc in 0) ;; 124|134|137|139) exit 1;; *) echo "var$v failed";; esac
 done
 bash tools/ab_env.sh cfg3 "--workload cfg3" 3 - VAR=7 VAR=8 VAR=9 VAR=12 OMPL_GPU_QSORT=0 || exit 1
-bash tools/ab_env.sh cfg4 "--workload cfg4" 2 - OMPL_GPU_CHAIN_SHARE=0 OMPL_GPU_CHAIN_WAVE=0 || exit 1
+bash tools/ab_env.sh cfg4 "--workload cfg4" 2 - OMPL_GPU_CHAIN_SHARE=0 OMPL_GPU_CHAIN_WAVE=1 || exit 1
 bash tools/ab_env.sh cfg5 "--workload cfg5" 2 - VAR=5 VAR=6 VAR=11 VAR=13
