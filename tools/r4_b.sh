@@ -7,11 +7,20 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/r4b; mkdir -p "$out"
 T="tests/test_gpu_nn.py tests/test_gpu_cull.py"
+if [ "${PART2:-0}" != 1 ]; then
 for v in ${VARS:-7 8 9 12}; do
   OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var$v.so timeout -k 10 300 python -u -m pytest $T -m gpu -x -q --timeout 200 \
       --timeout-method thread > "$out/pytest_v$v.log" 2>&1
   rc=$?; echo "var$v: $(tail -1 "$out/pytest_v$v.log")"; case $rc in 0) ;; 124|134|137|139) exit 1;; *) echo "var$v failed";; esac
 done
-bash tools/ab_env.sh cfg3 "--workload cfg3" 3 - VAR=7 VAR=8 VAR=9 VAR=12 OMPL_GPU_QSORT=0 || exit 1
+bash tools/ab_env.sh cfg3 "--workload cfg3" 2 - VAR=7 VAR=8 VAR=9 VAR=12 OMPL_GPU_QSORT=0 || exit 1
+exit 0
+fi
 bash tools/ab_env.sh cfg4 "--workload cfg4" 2 - OMPL_GPU_CHAIN_SHARE=0 OMPL_GPU_CHAIN_WAVE=1 || exit 1
+TESTS_R="tests/test_gpu_fullsize.py::test_cfg5_every_vertex_radius_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg5_radius_1e7_valid_samples"
+for v in 11 13; do
+  OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var$v.so timeout -k 10 300 python -u -m pytest $TESTS_R -m gpu -x -q --timeout 200 \
+      --timeout-method thread > "$out/pytest_r$v.log" 2>&1
+  rc=$?; echo "var$v radius: $(tail -1 "$out/pytest_r$v.log")"; case $rc in 0) ;; 124|134|137|139) exit 1;; *) echo "var$v failed";; esac
+done
 bash tools/ab_env.sh cfg5 "--workload cfg5" 2 - VAR=5 VAR=6 VAR=11 VAR=13
