@@ -45,7 +45,9 @@ HBM_PEAK_GBS = 8000.0                       # HBM3E spec
 # flops per distance evaluation (SURVEY.md §8d constants; sqrt and acos counted as 1 each)
 F_SE3, F_L2_6, F_CHAIN = 21, 18, 84
 B_SE3 = {"f32": 28, "f64": 56}              # bytes per stored SE(3) state streamed by a scan
-PMC_PROFILES = {"cfg3": "r3_cfg3", "cfg2": "r3_cfg2", "cfg4": "r3_cfg4", "cfg5": "r3_cfg5"}
+# committed PMC passes per workload, newest round first (cfg5k = configs[4] in kNN mode)
+PMC_PROFILES = {w: [f"r4_{w}", f"r3_{w}"] for w in ("cfg3", "cfg2", "cfg4", "cfg5")}
+PMC_PROFILES["cfg5k"] = ["r4_cfg5k"]
 DEFAULTS = {  # tree states, queries (samples / milestones / vertices) per GPU per step, k
     "cfg3": (1_000_000, 100_000, 10),
     "cfg2": (100_000, 100_000, 10),
@@ -57,16 +59,17 @@ DEFAULTS = {  # tree states, queries (samples / milestones / vertices) per GPU p
 def pmc_traffic(workload, kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
     (FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction, + WRITE_SIZE)."""
-    path = os.path.join(ROOT, "profiles", PMC_PROFILES[workload], "pmc_summary.json")
-    try:
-        with open(path) as f:
-            per = json.load(f)["per_kernel_mean"]
-    except (OSError, ValueError, KeyError):
-        return None
-    for name, c in per.items():
-        if name.split("<")[0].endswith(kernel) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            return {"bytes": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0,
-                    "source": os.path.relpath(path, ROOT) + f" [{name}]"}
+    for d in PMC_PROFILES.get(workload, ()):
+        path = os.path.join(ROOT, "profiles", d, "pmc_summary.json")
+        try:
+            with open(path) as f:
+                per = json.load(f)["per_kernel_mean"]
+        except (OSError, ValueError, KeyError):
+            continue
+        for name, c in per.items():
+            if name.split("<")[0].endswith(kernel) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                return {"bytes": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0,
+                        "source": os.path.relpath(path, ROOT) + f" [{name}]"}
     return None
 
 
@@ -451,10 +454,14 @@ def rrt_star_knn(torch, run, n_tree, nq=1000, reps=3):
     ids = torch.empty((nq, k), dtype=torch.int32, device=run.dev)
     dd = torch.empty((nq, k), dtype=torch.float64, device=run.dev)
     q = run.queries.data_ptr()
+    run.nn.profile(True)  # HIP events around sel_fill_kernel (the first query block's launch)
     ms0, n0, _ = run.nn.kernel_time()
     ms = _timed(torch, run.stream, lambda: run.nn.knn_device(q, nq, k, ids.data_ptr(), dd.data_ptr()), reps)
     ms1, n1, name = run.nn.kernel_time()
-    kern_ms = (ms1 - ms0) / max(n1 - n0, 1)
+    run.nn.profile(False)
+    if n1 == n0:
+        raise RuntimeError("large-k path recorded no kernel time")
+    kern_ms = (ms1 - ms0) / (n1 - n0)
     assert bool((dd[:, 1:] >= dd[:, :-1]).all().item()), "large-k lists must be sorted"
     return {"k": k, "queries": nq, "queries_per_s": nq / (ms * 1e-3), "ms_per_batch": ms, "kernel": name,
             "kernel_ms": kern_ms, "pairs_per_batch": float(nq) * n_tree}
@@ -797,7 +804,7 @@ class Runner:
     def roofline(self, kern_ms, kern_name, before, after, launches):
         wl, nq = self.args.workload, self.nq
         n = getattr(self, "n_mid", self.args.tree)
-        traffic = pmc_traffic(wl, kern_name)
+        traffic = pmc_traffic("cfg5k" if wl == "cfg5" and self.k else wl, kern_name)
         if kern_name == "radius32_group_kernel":
             pairs = (after["rq"] - before["rq"]) * 64 / launches
             flop, dt, frac_of = F_SE3, "f32", f"{pairs / (float(nq) * n):.4%}"

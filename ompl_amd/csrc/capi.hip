@@ -572,6 +572,8 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
         if (cull) {
             ompl_gpu_status s = ensure_sorted(h);
             if (s != OMPL_GPU_OK) return s;
+            if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN && chain_q16_enabled())
+                HIP_OR_FAIL(refresh_chain_rows16(h->g, &h->sorted, h->stream));
         }
         FastBounds b = current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);

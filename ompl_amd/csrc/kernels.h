@@ -114,6 +114,11 @@ struct SortedStore {
     uint64_t main_covered = 0, covered = 0, removed = 0;
     size_t cap_pos = 0, cap_nodes = 0, cap_inv = 0;  // allocated positions / nodes / inv entries
     uint32_t *qcount = nullptr;  // [pad_tiles + 1] per-tile query counts of the home-key counting sort
+    // KinematicChain: the joint positions as 16-bit fixed point, two per word, [F / 2][n_pad]
+    // (chain_q16_code), re-encoded from `rows` when the store changed (gen != gen16)
+    uint32_t *rows16 = nullptr;
+    size_t cap16 = 0;
+    uint64_t gen = 0, gen16 = ~0ull;
     void *scratch = nullptr;     // build / append workspace (grow-only)
     size_t scratch_bytes = 0;
     size_t bytes = 0;
@@ -135,6 +140,16 @@ hipError_t append_sorted_store(const DevSpace &sp, const FeatGeom &g, const floa
                                bool *fits);
 // removal of a placed id: its sorted fp32 row 0 becomes NaN
 hipError_t tombstone_sorted_store(SortedStore *s, uint64_t id, hipStream_t st);
+// The culled chain scan's 16-bit copy of the joint positions.  Coordinate f of link i = f mod nm
+// lies in [-(i + 1), i + 1] (a sum of i + 1 unit vectors); its code is rint((x + i + 1) * S_i),
+// S_i = kChainQ16 / (2 (i + 1)), clamped to [0, kChainQ16]; 0xFFFF in coordinate 0 marks a state
+// with a NaN row (padding, tombstones).  OMPL_GPU_CHAIN_Q16=0 keeps the fp32 rows (A/B).
+constexpr float kChainQ16 = 65534.f;
+bool chain_q16_enabled();
+hipError_t refresh_chain_rows16(const FeatGeom &g, SortedStore *s, hipStream_t st);
+// bound on |d16 - d32| of one screened chain distance: link * sum_i sqrt(2) * 0.6 quanta * 2 (i + 1) / kChainQ16
+// (0.5 for the rounding, the rest for the fp32 scaling of state and query)
+double chain_q16_error(const DevSpace &sp);
 void free_sorted_store(SortedStore *s);
 
 int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq, bool cull);  // screening list size, 0 = not eligible

@@ -44,7 +44,7 @@ bool radius_cull_supported(const DevSpace &sp) {
 
 void free_sorted_store(SortedStore *s) {
     for (void *x : {(void *)s->rows, (void *)s->ids, (void *)s->tbox, (void *)s->sbox, (void *)s->tkey0, (void *)s->nodes,
-                    (void *)s->rows64, (void *)s->inv, (void *)s->qcount, s->scratch})
+                    (void *)s->rows64, (void *)s->inv, (void *)s->qcount, (void *)s->rows16, s->scratch})
         if (x) (void)hipFree(x);
     *s = SortedStore{};
 }
@@ -54,18 +54,69 @@ __global__ void tombstone_kernel(const uint32_t *__restrict__ inv, uint64_t id, 
     const uint32_t p = inv[id];
     if (p != kNoId) rows[p] = __builtin_nanf("");  // row 0 of the fp32 copy: every distance is NaN
 }
+// thread = sorted position: the F = 2 nm fp32 coordinates (SoA, stride n_pad) to nm words
+__global__ void chain_rows16_kernel(const float *__restrict__ rows, uint32_t n_pad, uint32_t n, int nm,
+                                    uint32_t *__restrict__ r16) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    bool dead = false;
+    uint32_t w0 = 0;
+    for (int w = 0; w < nm; ++w) {
+        uint32_t c[2];
+        for (int h = 0; h < 2; ++h) {
+            const int f = 2 * w + h, li = f < nm ? f : f - nm;
+            const float v = rows[(size_t)f * n_pad + p];
+            dead |= !(v == v);
+            const float t = rintf((v + (float)(li + 1)) * (kChainQ16 / (float)(2 * (li + 1))));
+            c[h] = (uint32_t)fminf(fmaxf(t, 0.f), kChainQ16);
+        }
+        const uint32_t word = c[0] | (c[1] << 16);
+        if (w == 0) w0 = word;
+        else r16[(size_t)w * n_pad + p] = word;
+    }
+    r16[p] = dead ? (w0 | 0xFFFFu) : w0;
+}
 }  // namespace
+
+bool chain_q16_enabled() {
+    static const bool on = [] {
+        const char *v = std::getenv("OMPL_GPU_CHAIN_Q16");
+        return v ? std::atoi(v) != 0 : true;
+    }();
+    return on;
+}
+
+double chain_q16_error(const DevSpace &sp) {
+    const double n = (double)sp.dim;
+    return sp.link * 1.4142135623730951 * 0.6 * n * (n + 1.0) / (double)kChainQ16;
+}
+
+hipError_t refresh_chain_rows16(const FeatGeom &g, SortedStore *s, hipStream_t st) {
+    if (!s->built || !s->rows || s->ntiles == 0) return hipSuccess;
+    if (s->rows16 && s->gen16 == s->gen) return hipSuccess;
+    const int nm = g.F / 2;
+    hipError_t e = grow_array(&s->rows16, s->cap16, (size_t)nm * s->n_pad);
+    if (e != hipSuccess) return e;
+    const uint32_t n = s->ntiles * kCullTile;
+    hipLaunchKernelGGL(chain_rows16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, s->rows, s->n_pad, n, nm,
+                       s->rows16);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    s->gen16 = s->gen;
+    return hipSuccess;
+}
 
 hipError_t tombstone_sorted_store(SortedStore *s, uint64_t id, hipStream_t st) {
     if (!s->built || id >= s->covered || id >= s->cap_inv) return hipSuccess;
     hipLaunchKernelGGL(tombstone_kernel, dim3(1), dim3(1), 0, st, s->inv, id, s->rows);
     s->removed += 1;
+    s->gen += 1;
     return hipGetLastError();
 }
 
 hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, const double *feat64,
                               uint64_t cap, uint64_t n_total, uint32_t n_live, const uint8_t *live, SortedStore *s,
                               hipStream_t st) {
+    s->gen += 1;
     switch (sp.kind) {
     case OMPL_GPU_SPACE_SE3: return fast_se3_build(g, feat32, feat64, cap, n_total, n_live, live, s, st);
     case OMPL_GPU_SPACE_REALVECTOR: return fast_rv_build(g, feat32, feat64, cap, n_total, n_live, live, s, st);
@@ -77,6 +128,7 @@ hipError_t build_sorted_store(const DevSpace &sp, const FeatGeom &g, const float
 hipError_t append_sorted_store(const DevSpace &sp, const FeatGeom &g, const float *feat32, const double *feat64,
                                uint64_t cap, uint64_t n_total, const FastBounds &b, SortedStore *s, hipStream_t st,
                                bool *fits) {
+    s->gen += 1;
     switch (sp.kind) {
     case OMPL_GPU_SPACE_SE3: return fast_se3_append(g, feat32, feat64, cap, n_total, b, s, st, fits);
     case OMPL_GPU_SPACE_REALVECTOR: return fast_rv_append(g, feat32, feat64, cap, n_total, b, s, st, fits);

@@ -1256,21 +1256,34 @@ __global__ __launch_bounds__(256) void knn_chunk_merge_kernel(float *__restrict_
 //     from the one holding the home tile on (wrapping), so that chunk publishes early.
 // The merge stays exact: a store state among the K2 best has a key <= every published key, and
 // fewer than K2 states of its own chunk are below it, so it is in its chunk's list.
+//
+// Q16 (the default): the tiles are read from the 16-bit fixed-point copy (SortedStore::rows16,
+// half the bytes of the fp32 rows) and the screen works in quanta: term i = step_i *
+// |code_i(s) - (P_i(q) + i + 1) S_i|, step_i = 1 / S_i.  Every quantity that decides what a list
+// keeps is this d16; the tile bounds stay on the fp32 boxes and are lowered by qerr
+// (chain_q16_error, >= |d16 - d32|), and the certificate's screen error grows by the same qerr.
 constexpr int kChainTauTiles = 16;
-template <int F, int K2, int G, int MODE>
+template <int F, int K2, int G, int MODE, bool Q16>
 __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
-    const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
-    const float *__restrict__ tbox, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys, uint32_t nq,
-    uint32_t chunk_tiles, float link, int nlinks, float *__restrict__ pd, uint32_t *__restrict__ pi,
-    unsigned long long *__restrict__ counters, unsigned long long *__restrict__ shared_key) {
+    const float *__restrict__ rows, const uint32_t *__restrict__ rows16, uint32_t n_pad,
+    const uint32_t *__restrict__ ids, uint32_t ntiles, const float *__restrict__ tbox, const float *__restrict__ q32,
+    const uint32_t *__restrict__ qkeys, uint32_t nq, uint32_t chunk_tiles, float link, int nlinks, float qerr,
+    float *__restrict__ pd, uint32_t *__restrict__ pi, unsigned long long *__restrict__ counters,
+    unsigned long long *__restrict__ shared_key) {
     constexpr int NM = F / 2;
     static_assert(K2 <= 64 && NM % 2 == 0, "chain cull shape");
     __shared__ __attribute__((aligned(16))) float qrow[G * F];
+    __shared__ __attribute__((aligned(16))) float qcode[Q16 ? G * F : 1];  // the queries in quanta
     const int lane = threadIdx.x;
     const uint32_t g0 = blockIdx.x * G;
     for (int t = lane; t < G * F; t += 64) {
         const uint32_t qi = g0 + t / F;
-        qrow[t] = qi < nq ? q32[(size_t)qi * F + t % F] : __builtin_nanf("");
+        const float v = qi < nq ? q32[(size_t)qi * F + t % F] : __builtin_nanf("");
+        qrow[t] = v;
+        if constexpr (Q16) {
+            const int f = t % F, li = f < NM ? f : f - NM;
+            qcode[t] = (v + (float)(li + 1)) * (kChainQ16 / (float)(2 * (li + 1)));
+        }
     }
     __syncthreads();
     uint32_t qoff = 0;  // re-read the wave-uniform query rows from LDS (see knn32_group_kernel)
@@ -1306,14 +1319,26 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
     uint32_t visited = 0, qscans = 0;
     auto load_tile = [&](uint32_t t, float (&x)[F]) {
         const uint64_t p = (uint64_t)t * kCullTile + lane;
+        if constexpr (Q16) {
+            uint32_t w[NM];
 #pragma unroll
-        for (int f = 0; f < F; ++f) x[f] = rows[(uint64_t)f * n_pad + p];
+            for (int j = 0; j < NM; ++j) w[j] = rows16[(uint64_t)j * n_pad + p];
+#pragma unroll
+            for (int j = 0; j < NM; ++j) {
+                x[2 * j] = (float)(w[j] & 0xFFFFu);
+                x[2 * j + 1] = (float)(w[j] >> 16);
+            }
+            if ((w[0] & 0xFFFFu) == 0xFFFFu) x[0] = __builtin_nanf("");  // padding / removed
+        } else {
+#pragma unroll
+            for (int f = 0; f < F; ++f) x[f] = rows[(uint64_t)f * n_pad + p];
+        }
     };
     // query g against the lane's state x, outermost links first (|P_i(a) - P_i(b)| grows with
     // i), the wave leaving as soon as no lane's partial sum is below the threshold
     auto scan = [&](int g, const float (&x)[F], uint32_t id) {
         ++qscans;
-        const float *qq = &qrow[qoff + g * F];
+        const float *qq = Q16 ? &qcode[qoff + g * F] : &qrow[qoff + g * F];
         float acc = 0.f;
 #pragma unroll
         for (int s = 0; s < NM; s += 2) {
@@ -1322,8 +1347,13 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
                 const f2 dx = f2{x[i], x[i + 1]} - f2{qq[i], qq[i + 1]};
                 const f2 dy = f2{x[NM + i], x[NM + i + 1]} - f2{qq[NM + i], qq[NM + i + 1]};
                 const f2 s2 = pk_fma(dy, dy, dx * dx);
-                acc += __builtin_amdgcn_sqrtf(s2.x);
-                if (i + 1 < nlinks) acc += __builtin_amdgcn_sqrtf(s2.y);
+                if constexpr (Q16) {  // back from quanta: step_i = 2 (i + 1) / kChainQ16 (immediates)
+                    acc = fmaf(__builtin_amdgcn_sqrtf(s2.x), (float)(2 * (i + 1)) / kChainQ16, acc);
+                    if (i + 1 < nlinks) acc = fmaf(__builtin_amdgcn_sqrtf(s2.y), (float)(2 * (i + 2)) / kChainQ16, acc);
+                } else {
+                    acc += __builtin_amdgcn_sqrtf(s2.x);
+                    if (i + 1 < nlinks) acc += __builtin_amdgcn_sqrtf(s2.y);
+                }
             }
             if (s + 2 < NM && !__ballot(acc * link < td[g])) return;
         }
@@ -1427,7 +1457,7 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
             // the sum of the per-link bounds rounds like the distance's own sum (monotone in its
             // terms): shave (n + 2) u off so that the bound stays below every screened distance
 #pragma unroll
-            for (int g = 0; g < G; ++g) lb[g] = lb[g] * link * (1.f - 4e-6f);
+            for (int g = 0; g < G; ++g) lb[g] = lb[g] * link * (1.f - 4e-6f) - qerr;
         }
         uint64_t need = 0;
 #pragma unroll
@@ -1477,7 +1507,8 @@ __device__ __forceinline__ double screen_error(const DevSpace &sp, double B, dou
         // coordinate, each term <= 14.2 u i, so the terms together <= 7.1 u n (n + 1); the n
         // additions and the final link product cost <= (n + 1) u of the sum
         const double n = (double)sp.dim;
-        e = sp.link * 8.0 * kU * n * (n + 1.0) + (n + 2.0) * kU * L + sp.link * n * sqrt(2.0 * kFltMin);
+        // eta: the 16-bit screen's quantisation bound (chain_q16_error) when it ran, else 0
+        e = sp.link * 8.0 * kU * n * (n + 1.0) + (n + 2.0) * kU * L + sp.link * n * sqrt(2.0 * kFltMin) + eta;
     } else {
         e = 6.0 * sqrt((double)sp.dim) * kU * B + 6.0 * kU * L;
     }
@@ -2171,6 +2202,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     e = hipMemsetAsync(fail, 0, 4, st);
     if (e != hipSuccess) return e;
     bool walked = false;
+    float chain_qerr = 0.f;  // the culled chain scan's 16-bit screen error (certificate)
     if constexpr (SP == OMPL_GPU_SPACE_SE3 || SP == OMPL_GPU_SPACE_REALVECTOR) {  // cull_supported
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
@@ -2200,20 +2232,28 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             }();
             unsigned long long *skey = (unsigned long long *)(ws + L.tau);
             const uint32_t ng = (nq + kChainCullG - 1) / kChainCullG;
-            if (share)
-                hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, 1>), dim3(ng, 1), dim3(64), 0, st,
-                                   ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,
-                                   (float)sp.link, sp.dim, pd, pi, nullptr, skey);
-            timer_begin(st, "knn32_chain_cull_kernel");
-            if (share)
-                hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, 2>), dim3(ng, p.chunks), dim3(64), 0,
-                                   st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,
-                                   (float)sp.link, sp.dim, pd, pi, ss->counters, skey);
-            else
-                hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, 0>), dim3(ng, p.chunks), dim3(64), 0,
-                                   st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,
-                                   (float)sp.link, sp.dim, pd, pi, ss->counters, nullptr);
+            // the 16-bit rows when the store's copy is current (refresh_chain_rows16; share only)
+            const bool q16 = share && ss->rows16 && ss->gen16 == ss->gen;
+            const float qerr = q16 ? (float)(chain_q16_error(sp) * (1.0 + 1e-5)) : 0.f;
+#define OMPL_AMD_CHAIN_CULL(MODE, Q, GY, CNT, KEY)                                                              \
+    hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, MODE, Q>), dim3(ng, GY), dim3(64), 0, st,  \
+                       ss->rows, ss->rows16, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,      \
+                       (float)sp.link, sp.dim, qerr, pd, pi, CNT, KEY)
+            if (q16) {
+                OMPL_AMD_CHAIN_CULL(1, true, 1, nullptr, skey);
+                timer_begin(st, "knn32_chain_cull_kernel");
+                OMPL_AMD_CHAIN_CULL(2, true, p.chunks, ss->counters, skey);
+            } else if (share) {
+                OMPL_AMD_CHAIN_CULL(1, false, 1, nullptr, skey);
+                timer_begin(st, "knn32_chain_cull_kernel");
+                OMPL_AMD_CHAIN_CULL(2, false, p.chunks, ss->counters, skey);
+            } else {
+                timer_begin(st, "knn32_chain_cull_kernel");
+                OMPL_AMD_CHAIN_CULL(0, false, p.chunks, ss->counters, nullptr);
+            }
+#undef OMPL_AMD_CHAIN_CULL
             timer_end(st);
+            chain_qerr = qerr;
             walked = true;
         }
     }
@@ -2258,8 +2298,8 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             hipLaunchKernelGGL((knn_chunk_merge_kernel<K2>), dim3((nq + 3) / 4), b256, 0, st, pd, pi, p.chunks, nq);
         constexpr uint32_t QPB = 256 / K2;
         hipLaunchKernelGGL((knn_certify_wave_kernel<SP, F, K2>), dim3((nq + QPB - 1) / QPB), b256, 0, st, pd, pi, nq,
-                           perm, f64, cap, nullptr, nullptr, qf64, sp, b.absmax, b.qeta, b.n_live, (uint32_t)K2, od,
-                           oi, k, fail, fail + 1);
+                           perm, f64, cap, nullptr, nullptr, qf64, sp, b.absmax, b.qeta + chain_qerr, b.n_live,
+                           (uint32_t)K2, od, oi, k, fail, fail + 1);
     } else if (p.chunks == 1) {
         constexpr uint32_t QPB = 256 / K2;
         // the group walk's lists hold positions in the sorted store (rows64 / ids map them)

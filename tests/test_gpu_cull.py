@@ -7,7 +7,7 @@ import pytest
 import pyoracle as O
 from ompl_amd import NearestNeighborsGPU
 from ompl_amd import workloads as W
-from ompl_amd.spaces import RealVectorStateSpace, SE3StateSpace
+from ompl_amd.spaces import KinematicChainSpace, RealVectorStateSpace, SE3StateSpace
 from parity import assert_knn_parity
 
 pytestmark = pytest.mark.gpu
@@ -94,3 +94,28 @@ def test_group_tail_and_small_batches(gpu):
     for nq in (64, 67, 131, 1001):
         q = W.uniform_rv(rng, nq, 5)
         _check(nn, sp, data, np.arange(len(data)), q, 7)
+
+
+@pytest.mark.parametrize("links", [4, 8, 12, 16])
+def test_chain_culled_scan_16bit_rows(gpu, links):
+    """The culled chain scan reads the joint positions as 16-bit fixed point (SortedStore::rows16,
+    re-encoded whenever the store changes): exact against the oracle for every link bucket, for
+    queries equal to stored states (distance 0, ties with the duplicates), after appends and after
+    tombstones (a removed state's code carries the NaN marker and never enters a list)."""
+    rng = np.random.default_rng(70 + links)
+    sp = KinematicChainSpace(links, 1.0 / links)
+    data = W.uniform_chain(rng, 30000, links)
+    data[29000:] = data[:1000]                       # duplicates: tie classes resolved by id
+    q = np.concatenate([W.uniform_chain(rng, 400, links), data[:100]])
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data[:20000])
+    _check(nn, sp, data[:20000], np.arange(20000), q, 10)
+    nn.add(data[20000:])
+    _check(nn, sp, data, np.arange(30000), q, 41)
+    gone = rng.choice(30000, 3000, replace=False)
+    for i in gone:
+        nn.remove(int(i))
+    keep = np.setdiff1d(np.arange(30000), gone)
+    _check(nn, sp, data[keep], keep, q, 41)
+    screened, fallbacks = nn.stats()
+    assert screened == 3 * len(q) and fallbacks <= len(q) // 20

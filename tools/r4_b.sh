@@ -16,7 +16,10 @@ done
 bash tools/ab_env.sh cfg3 "--workload cfg3" 2 - VAR=7 VAR=8 VAR=9 VAR=12 OMPL_GPU_QSORT=0 || exit 1
 exit 0
 fi
-bash tools/ab_env.sh cfg4 "--workload cfg4" 2 - OMPL_GPU_CHAIN_SHARE=0 OMPL_GPU_CHAIN_WAVE=1 || exit 1
+TESTS_C="tests/test_gpu_cull.py tests/test_gpu_prm.py tests/test_gpu_fullsize.py::test_cfg4_chain_culled_scan_1e6 tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan"
+timeout -k 10 400 python -u -m pytest $TESTS_C -m gpu -x -q --timeout 300 --timeout-method thread > "$out/pytest_q16.log" 2>&1
+rc=$?; echo "chain q16: $(tail -1 "$out/pytest_q16.log")"; [ $rc = 0 ] || exit 1
+bash tools/ab_env.sh cfg4 "--workload cfg4" 2 - OMPL_GPU_CHAIN_Q16=0 OMPL_GPU_CHAIN_SHARE=0 OMPL_GPU_CHAIN_WAVE=1 || exit 1
 TESTS_R="tests/test_gpu_fullsize.py::test_cfg5_every_vertex_radius_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg5_radius_1e7_valid_samples"
 for v in 11 13; do
   OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var$v.so timeout -k 10 300 python -u -m pytest $TESTS_R -m gpu -x -q --timeout 200 \

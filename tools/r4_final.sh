@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 closing GPU run: every -m gpu test, smoke, the default bench line (all five configs with
-# their CPU baselines), then the tree-sharded lines at N = 1 (cfg3, cfg5 radius) through RCCL.
+# their CPU baselines), then the tree-sharded lines at N = 1 (cfg3, cfg5 radius: the merge kernels on a single shard).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
