@@ -695,6 +695,8 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
         // culled walk over the Morton-sorted copy (knn_fast_impl.h)
         ompl_gpu_status s = ensure_sorted(h);
         if (s != OMPL_GPU_OK) return s;
+        if (h->sp.kind == OMPL_GPU_SPACE_SE3 && se3_q16_enabled())
+            HIP_OR_FAIL(refresh_se3_rows16(h->lo, h->hi, &h->sorted, h->stream));
         FastBounds b = current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
         HIP_OR_FAIL(h->ws.ensure(radius_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq)));

@@ -91,6 +91,14 @@ constexpr int kSuperTiles = 32;
 // the walk is long (SE3, 10^6 states), wider ones where the store is small and L2-resident.
 template <int SP>
 constexpr int group_queries() { return SP == OMPL_GPU_SPACE_SE3 ? 4 : 8; }  // measured (k-d tiles): SE3 G = 2 / 4 / 8 -> 2.04 / 1.41 / 1.73 ms; R^6 G = 4 / 8 -> 1.01 / 0.70 ms
+// 16-bit fixed-point coding of an SE3 store's fp32 rows: code = rint((v - lo) * inv) clamped to
+// [0, kQ16Max], decoded as lo + code * step (step = 1 / inv); translation over the stored
+// states' box, quaternion components over [-1.001, 1.001].  0xFFFF in coordinate 0: NaN row.
+constexpr float kQ16Max = 65534.f;
+struct Q16Geo {
+    float lo[8], step[8], inv[8];
+};
+
 struct SortedStore {
     float *rows = nullptr;       // [rows32][n_pad] (SE3 quaternions sign-canonical: w >= 0)
     uint32_t *ids = nullptr;     // [n_pad] original id of each sorted slot (kNoId = padding)
@@ -116,9 +124,11 @@ struct SortedStore {
     uint32_t *qcount = nullptr;  // [pad_tiles + 1] per-tile query counts of the home-key counting sort
     // KinematicChain: the joint positions as 16-bit fixed point, two per word, [F / 2][n_pad]
     // (chain_q16_code), re-encoded from `rows` when the store changed (gen != gen16)
+    // SE3 (the radius walk): the 7 coordinates as 16-bit codes over q16 (4 words per state)
     uint32_t *rows16 = nullptr;
     size_t cap16 = 0;
     uint64_t gen = 0, gen16 = ~0ull;
+    Q16Geo q16{};
     void *scratch = nullptr;     // build / append workspace (grow-only)
     size_t scratch_bytes = 0;
     size_t bytes = 0;
@@ -150,6 +160,11 @@ hipError_t refresh_chain_rows16(const FeatGeom &g, SortedStore *s, hipStream_t s
 // bound on |d16 - d32| of one screened chain distance: link * sum_i sqrt(2) * 0.6 quanta * 2 (i + 1) / kChainQ16
 // (0.5 for the rounding, the rest for the fp32 scaling of state and query)
 double chain_q16_error(const DevSpace &sp);
+// SE3 radius walk (OMPL_GPU_RADIUS_Q16=1): the 16-bit copy over the stored box [lo, hi] of the
+// translation, and the bound on |d16 - d32| it adds to the walk's threshold
+bool se3_q16_enabled();
+hipError_t refresh_se3_rows16(const double *lo, const double *hi, SortedStore *s, hipStream_t st);
+double se3_q16_error(const DevSpace &sp, const Q16Geo &q);
 void free_sorted_store(SortedStore *s);
 
 int fast_k2(const DevSpace &sp, uint32_t k, uint32_t nq, bool cull);  // screening list size, 0 = not eligible

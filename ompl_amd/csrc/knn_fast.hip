@@ -76,7 +76,64 @@ __global__ void chain_rows16_kernel(const float *__restrict__ rows, uint32_t n_p
     }
     r16[p] = dead ? (w0 | 0xFFFFu) : w0;
 }
+// thread = sorted position: the 7 SE3 coordinates to 4 words (the last half unused)
+__global__ void se3_rows16_kernel(const float *__restrict__ rows, uint32_t n_pad, uint32_t n, Q16Geo q,
+                                  uint32_t *__restrict__ r16) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    bool dead = false;
+    uint32_t c[8];
+#pragma unroll
+    for (int f = 0; f < 7; ++f) {
+        const float v = rows[(size_t)f * n_pad + p];
+        dead |= !(v == v);
+        const float t = rintf((v - q.lo[f]) * q.inv[f]);
+        c[f] = (uint32_t)fminf(fmaxf(t, 0.f), kQ16Max);
+    }
+    c[7] = 0u;
+    if (dead) c[0] = 0xFFFFu;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) r16[(size_t)w * n_pad + p] = c[2 * w] | (c[2 * w + 1] << 16);
+}
 }  // namespace
+
+bool se3_q16_enabled() {
+    static const bool on = [] {
+        const char *v = std::getenv("OMPL_GPU_RADIUS_Q16");
+        return v ? std::atoi(v) != 0 : false;
+    }();
+    return on;
+}
+
+hipError_t refresh_se3_rows16(const double *lo, const double *hi, SortedStore *s, hipStream_t st) {
+    if (!s->built || !s->rows || s->ntiles == 0) return hipSuccess;
+    if (s->rows16 && s->gen16 == s->gen) return hipSuccess;
+    Q16Geo q{};
+    for (int f = 0; f < 8; ++f) {
+        // quaternion components: |q_i| <= sqrt(1 + eta) < 1.001 (screen_safe: eta <= 1e-4)
+        const double l = f < 3 ? lo[f] : -1.001, ext = f < 3 ? hi[f] - lo[f] : 2.002;
+        q.lo[f] = (float)l;
+        q.step[f] = ext > 0.0 ? (float)(ext / (double)kQ16Max) : 0.f;
+        q.inv[f] = ext > 0.0 ? (float)((double)kQ16Max / ext) : 0.f;
+    }
+    hipError_t e = grow_array(&s->rows16, s->cap16, (size_t)4 * s->n_pad);
+    if (e != hipSuccess) return e;
+    const uint32_t n = s->ntiles * kCullTile;
+    hipLaunchKernelGGL(se3_rows16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, s->rows, s->n_pad, n, q, s->rows16);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    s->q16 = q;
+    s->gen16 = s->gen;
+    return hipSuccess;
+}
+
+// per coordinate the decoded value is within 0.52 step of the fp32 row (no clamping: the
+// ranges hold every stored value) (0.5 rounding, the rest
+// the fp32 scaling); the translation gap moves by <= sqrt(3) of that, the chord by <= |dq| <= 2 of
+// the quaternion's, and theta(c) = 2 asin(c / 2) by <= 1.415 |dc| on c <= sqrt(2) (+ 5 %)
+double se3_q16_error(const DevSpace &sp, const Q16Geo &q) {
+    const double st = std::max({(double)q.step[0], (double)q.step[1], (double)q.step[2]});
+    return sp.w0 * 1.7320508075688772 * 0.52 * st * 1.01 + sp.w1 * 1.415 * 2.0 * 0.52 * (double)q.step[3] * 1.05 + 1e-7;
+}
 
 bool chain_q16_enabled() {
     static const bool on = [] {

@@ -46,6 +46,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "feat_dist.h"
 #include "kernels.h"
@@ -1699,14 +1700,20 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
 #else
 #define OMPL_RADIUS_LB __launch_bounds__(64)
 #endif
-template <int SP, int F, int G, int MODE>
+// Q16 (SE3, MODE 2; OMPL_GPU_RADIUS_Q16=1): the tiles come from the 16-bit copy
+// (SortedStore::rows16, 16 B per state against 28), decoded to fp32 once per tile; every
+// threshold grows by qerr >= |d16 - d32| (se3_q16_error), so no state with d32 <= r + e is lost
+// and the box bounds (over the fp32 rows) stay valid.
+template <int SP, int F, int G, int MODE, bool Q16 = false>
 __global__ OMPL_RADIUS_LB void radius32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ q32,
     const uint32_t *__restrict__ perm, uint32_t nq, const double *__restrict__ rows64,
     const double *__restrict__ qf64, DevSpace sp, float absmax, float qeta, double r, uint64_t *__restrict__ counts,
     const uint64_t *__restrict__ offsets, uint32_t *__restrict__ out_i, double *__restrict__ out_d,
-    unsigned long long *__restrict__ counters, uint32_t slab) {
+    unsigned long long *__restrict__ counters, uint32_t slab, const uint32_t *__restrict__ rows16 = nullptr,
+    Q16Geo qg = Q16Geo{}, double qerr = 0.0) {
+    static_assert(!Q16 || SP == OMPL_GPU_SPACE_SE3, "16-bit rows: SE3");
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
     constexpr int GH = G / 2;
     constexpr bool FILL = MODE == 1, SLAB = MODE == 2;
@@ -1742,7 +1749,8 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
         const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : F;
         for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qd[c]));
         // every element with d <= r has d32 <= r + e; rounding to fp32 is covered by the 16 u
-        const double t = (r + screen_error<SP>(sp, B, r, (double)qeta + query_eta<SP>(qd))) * (1.0 + 16.0 * kU);
+        const double t = (r + screen_error<SP>(sp, B, r, (double)qeta + query_eta<SP>(qd)) + (Q16 ? qerr : 0.0)) *
+                         (1.0 + 16.0 * kU);
         thr[g] = live ? (float)t : -__builtin_inff();
         cur[g] = (FILL && live) ? offsets[qo[g]] : 0ull;
     }
@@ -1843,6 +1851,22 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
 #pragma unroll
         for (int rr = 0; rr < R; ++rr) x[rr] = rows[(uint64_t)rr * n_pad + p];
         id = ids[p];
+    };
+    // Q16: a tile in flight stays raw (4 words per lane) and is decoded when it is scanned, so
+    // the next tile's loads overlap the current scan
+    auto load_raw = [&](uint32_t ss, int t, uint32_t (&w)[4], uint32_t &id) {
+        const uint64_t p = (uint64_t)(ss * kSuperTiles + t) * kCullTile + lane;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = rows16[(uint64_t)j * n_pad + p];
+        id = ids[p];
+    };
+    auto decode = [&](const uint32_t (&w)[4], float (&v)[R]) {
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) {
+            const uint32_t c = (rr & 1) ? (w[rr >> 1] >> 16) : (w[rr >> 1] & 0xFFFFu);
+            v[rr] = fmaf((float)c, qg.step[rr], qg.lo[rr]);
+            if (rr == 0 && c == 0xFFFFu) v[0] = __builtin_nanf("");  // padding / removed
+        }
     };
     auto scan_tile = [&](uint32_t ss, int t, const float (&x)[R], uint32_t id, const float (&lb)[GH], uint32_t bits) {
         asm volatile("" : "+s"(qoff));
@@ -1953,10 +1977,40 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
             }
         }
         uint32_t m = fold_tiles(__ballot(tneed));
-        float x[R], xn[R];
         uint32_t id = 0, idn = 0;
         int t = 0, tn = 0;
         const bool have = m != 0;
+        if constexpr (Q16) {
+            uint32_t x[4], xn[4];
+            if (have) {
+                t = __builtin_ctz(m);
+                m &= m - 1;
+                load_raw((uint32_t)ss, t, x, id);
+            }
+            const int ssn = next_super();
+            const uint32_t bitsn = pop_bits;
+            if (ssn >= 0) load_tbox((uint32_t)ssn, bx);
+            while (have) {
+                const bool more = m != 0;
+                if (more) {
+                    tn = __builtin_ctz(m);
+                    m &= m - 1;
+                    load_raw((uint32_t)ss, tn, xn, idn);
+                }
+                float xd[R];
+                decode(x, xd);
+                scan_tile((uint32_t)ss, t, xd, id, lb, bits);
+                if (!more) break;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) x[j] = xn[j];
+                id = idn;
+                t = tn;
+            }
+            ss = ssn;
+            bits = bitsn;
+            continue;
+        }
+        float x[R], xn[R];
         if (have) {
             t = __builtin_ctz(m);
             m &= m - 1;
@@ -2431,10 +2485,22 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
         if ((e = hipMemsetAsync(counts + nq, 0, 8, st)) != hipSuccess) return e;
         if (phase == 2) {
             timer_begin(st, "radius32_group_kernel");
-            hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusSlabGroup, 2>),
-                               dim3((nq + kRadiusSlabGroup - 1) / kRadiusSlabGroup), b64, 0, st, ss->rows, ss->n_pad,
-                               ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64,
-                               sp, b.absmax, b.qeta, r, counts, nullptr, out_i, out_d, ss->counters, b.slab);
+            const dim3 gs((nq + kRadiusSlabGroup - 1) / kRadiusSlabGroup);
+            bool q16 = false;
+            if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+                if (ss->rows16 && ss->gen16 == ss->gen && se3_q16_enabled()) {
+                    q16 = true;
+                    hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusSlabGroup, 2, true>), gs, b64, 0, st,
+                                       ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32,
+                                       perm, nq, ss->rows64, qf64, sp, b.absmax, b.qeta, r, counts, nullptr, out_i,
+                                       out_d, ss->counters, b.slab, ss->rows16, ss->q16, se3_q16_error(sp, ss->q16));
+                }
+            }
+            if (!q16)
+                hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusSlabGroup, 2>), gs, b64, 0, st, ss->rows,
+                                   ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq,
+                                   ss->rows64, qf64, sp, b.absmax, b.qeta, r, counts, nullptr, out_i, out_d,
+                                   ss->counters, b.slab);
             timer_end(st);
             hipLaunchKernelGGL((radius_slab_exact_kernel<SP, F>), dim3(nq), b64, 0, st, ss->rows64, ss->ids, qf64, sp,
                                r, b.slab, counts, out_i, out_d);

@@ -26,4 +26,8 @@ for v in 11 13; do
       --timeout-method thread > "$out/pytest_r$v.log" 2>&1
   rc=$?; echo "var$v radius: $(tail -1 "$out/pytest_r$v.log")"; case $rc in 0) ;; 124|134|137|139) exit 1;; *) echo "var$v failed";; esac
 done
-bash tools/ab_env.sh cfg5 "--workload cfg5" 2 - VAR=5 VAR=6 VAR=11 VAR=13
+TESTS_Q="tests/test_gpu_nn.py tests/test_gpu_batch.py tests/test_gpu_bitstar.py tests/test_gpu_index.py $TESTS_R"
+OMPL_GPU_RADIUS_Q16=1 timeout -k 10 500 python -u -m pytest $TESTS_Q -m gpu -x -q --timeout 300 --timeout-method thread \
+    > "$out/pytest_rq16.log" 2>&1
+rc=$?; echo "radius q16: $(tail -1 "$out/pytest_rq16.log")"; case $rc in 0) ;; 124|134|137|139) exit 1;; *) echo "radius q16 failed";; esac
+bash tools/ab_env.sh cfg5 "--workload cfg5" 2 - OMPL_GPU_RADIUS_Q16=1 VAR=5 VAR=6 VAR=11 VAR=13
