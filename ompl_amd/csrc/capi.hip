@@ -574,6 +574,8 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
             if (s != OMPL_GPU_OK) return s;
             if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN && chain_q16_enabled())
                 HIP_OR_FAIL(refresh_chain_rows16(h->g, &h->sorted, h->stream));
+            if (h->sp.kind == OMPL_GPU_SPACE_SE3 && se3_knn_q16_enabled())
+                HIP_OR_FAIL(refresh_se3_rows16(h->lo, h->hi, &h->sorted, h->stream));
         }
         FastBounds b = current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);

@@ -163,6 +163,7 @@ double chain_q16_error(const DevSpace &sp);
 // SE3 radius walk (OMPL_GPU_RADIUS_Q16=1): the 16-bit copy over the stored box [lo, hi] of the
 // translation, and the bound on |d16 - d32| it adds to the walk's threshold
 bool se3_q16_enabled();
+bool se3_knn_q16_enabled();  // the SE3 kNN group walk on the same copy (OMPL_GPU_KNN_Q16=1)
 hipError_t refresh_se3_rows16(const double *lo, const double *hi, SortedStore *s, hipStream_t st);
 double se3_q16_error(const DevSpace &sp, const Q16Geo &q);
 void free_sorted_store(SortedStore *s);

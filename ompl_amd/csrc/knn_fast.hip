@@ -105,6 +105,14 @@ bool se3_q16_enabled() {
     return on;
 }
 
+bool se3_knn_q16_enabled() {
+    static const bool on = [] {
+        const char *v = std::getenv("OMPL_GPU_KNN_Q16");
+        return v ? std::atoi(v) != 0 : false;
+    }();
+    return on;
+}
+
 hipError_t refresh_se3_rows16(const double *lo, const double *hi, SortedStore *s, hipStream_t st) {
     if (!s->built || !s->rows || s->ntiles == 0) return hipSuccess;
     if (s->rows16 && s->gen16 == s->gen) return hipSuccess;

@@ -628,14 +628,22 @@ __device__ __forceinline__ float box_tgap2(const float *bx, const float *q, int 
 
 // K2: lanes per query in the output (16 / 32 / 64); k2 <= K2: the list length the walk keeps
 // (the certificate's margin: k + 3 for the culled spaces, whose screen error is small)
-template <int SP, int F, int K2, int G, int MINW, bool QS>
+// Q16 (SE3, OMPL_GPU_KNN_Q16=1): tiles from the 16-bit copy (SortedStore::rows16), decoded
+// when scanned; the lists hold d16, every box bound is lowered by qerr >= |d16 - d32|
+// (se3_q16_error) and the certificate's error grows by the same qerr.
+template <int SP, int F, int K2, int G, int MINW, bool QS, bool Q16 = false>
 __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
     const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
     uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi,
-    unsigned long long *__restrict__ counters, int bulk, int k2, int recheck) {
+    unsigned long long *__restrict__ counters, int bulk, int k2, int recheck,
+    const uint32_t *__restrict__ rows16 = nullptr, Q16Geo qg = Q16Geo{}, float qerr = 0.f) {
+    static_assert(!Q16 || SP == OMPL_GPU_SPACE_SE3, "16-bit rows: SE3");
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
+    // a tile in flight: the R fp32 rows, or (Q16) 4 raw words decoded when it is scanned
+    constexpr int RW = Q16 ? 4 : R;
+    using TileE = std::conditional_t<Q16, uint32_t, float>;
     constexpr int GH = G / 2;
     static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
 #if defined(OMPL_WALK_DYN)
@@ -747,6 +755,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
                 }
                 if (qg >= 0) {
                     lb[p] = box_lb<SP, F, true>(bx, &qrow[qoff + qg * FS], w0, w1);
+                    if constexpr (Q16) lb[p] -= qerr;
                     need |= lb[p] < thr;
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -755,18 +764,30 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 #pragma unroll
             for (int j = 0; j < GH; ++j) {
                 lb[j] = box_lb<SP, F, true>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
+                if constexpr (Q16) lb[j] -= qerr;
                 need |= lb[j] < (half ? td[GH + j] : td[j]);
                 __builtin_amdgcn_sched_barrier(0);  // one bound at a time (temporaries)
             }
         }
         return fold_tiles(__ballot(need));
     };
-    auto load_state = [&](uint32_t t, float (&x)[R], uint32_t &id) {
+    auto load_state = [&](uint32_t t, TileE (&x)[RW], uint32_t &id) {
         const uint64_t p = (uint64_t)t * kCullTile + lane;
 #pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = rows[(uint64_t)r * n_pad + p];
+        for (int r = 0; r < RW; ++r) {
+            if constexpr (Q16) x[r] = rows16[(uint64_t)r * n_pad + p];
+            else x[r] = rows[(uint64_t)r * n_pad + p];
+        }
         id = (uint32_t)p;  // lists hold sorted positions; the certificate maps them to ids
         (void)ids;
+    };
+    auto decode = [&](const uint32_t (&w)[4], float (&v)[R]) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t c = (r & 1) ? (w[r >> 1] >> 16) : (w[r >> 1] & 0xFFFFu);
+            v[r] = fmaf((float)c, qg.step[r], qg.lo[r]);
+            if (r == 0 && c == 0xFFFFu) v[0] = __builtin_nanf("");  // padding / removed
+        }
     };
     // scan tile tin (index inside its super-tile) against every query whose own box bound
     // lb (held by lane tin + 32 * (g / GH)) is still below its threshold: the tile was
@@ -866,13 +887,19 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     // exclude more tiles; the home tile is then dropped from its super-tile's mask
     const uint32_t th = min(key, ntiles - 1);
     {
-        float x[R];
+        TileE x[RW];
         uint32_t id;
         load_state(th, x, id);
         float lbh[GH];
 #pragma unroll
         for (int j = 0; j < GH; ++j) lbh[j] = -__builtin_inff();
-        scan_state(x, id, 0, lbh, (1u << G) - 1u);
+        if constexpr (Q16) {
+            float xd[R];
+            decode(x, xd);
+            scan_state(xd, id, 0, lbh, (1u << G) - 1u);
+        } else {
+            scan_state(x, id, 0, lbh, (1u << G) - 1u);
+        }
         ++visited;
     }
     // visit order: s0 - 1, s0, s0 + 1 (the group's neighbourhood, which sets the thresholds),
@@ -925,6 +952,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     lbs[g] = box_lb<SP, F, true>(bx, &qrow[qoff + g * FS], w0, w1);
+                    if constexpr (Q16) lbs[g] -= qerr;
                     need |= lbs[g] < td[g];
                     // one query's bound at a time: interleaving the G bounds needs ~40 temporaries
                     __builtin_amdgcn_sched_barrier(0);
@@ -967,7 +995,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         return mm;
     };
     float lb[GH];
-    float x[R], xn[R];
+    TileE x[RW], xn[RW];
     uint32_t idn = kNoId, m = 0;  // (the scan recomputes the position ids)
     uint32_t bits = (1u << G) - 1u;  // queries that need the current super-tile s (kDyn)
     int t = 0, tn = 0, s = -1;
@@ -995,7 +1023,14 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             got = true;
         }
         if (have) {  // the list ids are sorted positions: recomputed, not carried in a VGPR
-            scan_state(x, ((uint32_t)s * kSuperTiles + (uint32_t)t) * kCullTile + (uint32_t)lane, t, lb, bits);
+            const uint32_t pid = ((uint32_t)s * kSuperTiles + (uint32_t)t) * kCullTile + (uint32_t)lane;
+            if constexpr (Q16) {
+                float xd[R];
+                decode(x, xd);
+                scan_state(xd, pid, t, lb, bits);
+            } else {
+                scan_state(x, pid, t, lb, bits);
+            }
             ++visited;
         }
         if (cross) {
@@ -1025,7 +1060,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         have = got;
         if (got) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) x[r] = xn[r];
+            for (int r = 0; r < RW; ++r) x[r] = xn[r];
             t = tn;
         } else if (sn < 0 && !m) {
             break;
@@ -1611,7 +1646,8 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
                                                                uint32_t k2, double *__restrict__ out_d,
                                                                uint32_t *__restrict__ out_i, uint32_t out_k,
                                                                uint32_t *__restrict__ fail_count,
-                                                               uint32_t *__restrict__ fail_list) {
+                                                               uint32_t *__restrict__ fail_list,
+                                                               float xerr = 0.f) {
     static_assert(K2 == 16 || K2 == 32 || K2 == 64, "lanes per query");
     constexpr int QPB = 256 / K2;
     const uint32_t qs = blockIdx.x * QPB + threadIdx.x / K2;
@@ -1669,7 +1705,9 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
         const int nc = SP == OMPL_GPU_SPACE_SE3 ? 3 : (SP == OMPL_GPU_SPACE_REALVECTOR ? F : 0);
         for (int c = 0; c < nc; ++c) B = fmax(B, fabs(qv[c]));
         const double L = (double)L32;
-        ok = dk + screen_error<SP>(sp, B, L, (double)qeta + query_eta<SP>(qv)) < L * (1.0 - 8.0 * kU);
+        // xerr: a 16-bit screen's coding bound, on both sides like the screen error (x 2)
+        ok = dk + screen_error<SP>(sp, B, L, (double)qeta + query_eta<SP>(qv)) + 2.0 * (double)xerr <
+             L * (1.0 - 8.0 * kU);
     }
     if (!live) return;
     if (rank < out_k) {
@@ -2257,6 +2295,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     if (e != hipSuccess) return e;
     bool walked = false;
     float chain_qerr = 0.f;  // the culled chain scan's 16-bit screen error (certificate)
+    float knn_qerr = 0.f;    // the SE3 group walk's (certificate xerr)
     if constexpr (SP == OMPL_GPU_SPACE_SE3 || SP == OMPL_GPU_SPACE_REALVECTOR) {  // cull_supported
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
@@ -2265,10 +2304,22 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
                 const char *v = std::getenv("OMPL_GPU_SUPER_RECHECK");
                 return v ? std::atoi(v) : 1;
             }();
-            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
-                               ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0,
-                               q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, kBulkThreshold,
-                               p.k2, recheck);
+            bool q16 = false;
+            if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+                if (ss->rows16 && ss->gen16 == ss->gen && se3_knn_q16_enabled()) {
+                    q16 = true;
+                    knn_qerr = (float)(se3_q16_error(sp, ss->q16) * (1.0 + 1e-5));
+                    hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true, true>), dim3((nq + G - 1) / G),
+                                       dim3(64), 0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox,
+                                       ss->nsuper, ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi,
+                                       ss->counters, kBulkThreshold, p.k2, recheck, ss->rows16, ss->q16, knn_qerr);
+                }
+            }
+            if (!q16)
+                hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true>), dim3((nq + G - 1) / G), dim3(64), 0,
+                                   st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
+                                   ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters,
+                                   kBulkThreshold, p.k2, recheck);
             timer_end(st);
             walked = true;
         }
@@ -2361,7 +2412,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (pos && !ss->rows64) return hipErrorInvalidValue;
         hipLaunchKernelGGL((knn_certify_wave_kernel<SP, F, K2>), dim3((nq + QPB - 1) / QPB), b256, 0, st, pd, pi, nq,
                            perm, f64, cap, pos ? ss->ids : nullptr, pos ? ss->rows64 : nullptr, qf64, sp, b.absmax,
-                           b.qeta, b.n_live, (uint32_t)p.k2, od, oi, k, fail, fail + 1);
+                           b.qeta, b.n_live, (uint32_t)p.k2, od, oi, k, fail, fail + 1, knn_qerr);
     } else {
         if (p.cull) return hipErrorInvalidValue;  // position lists need the wave certificate
         if constexpr (K == 64 && SP != OMPL_GPU_SPACE_KCHAIN) {
