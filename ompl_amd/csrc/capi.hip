@@ -17,6 +17,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ompl_gpu.h"
@@ -332,7 +333,30 @@ static ompl_gpu_status grow(ompl_gpu_nn *h, uint64_t need) {
     return OMPL_GPU_OK;
 }
 
-static ompl_gpu_status add_locked(ompl_gpu_nn *h, const double *states, size_t n, uint64_t *first_id);
+static ompl_gpu_status add_locked(ompl_gpu_nn *h, const double *states, size_t n, uint64_t *first_id,
+                                  const double *d_feat = nullptr, const double *d_raw = nullptr);
+
+// feature rows of n AoS states (host_features: glibc libm, bit-identical to the reference),
+// split over host threads for large batches: 8,192 chain states cost ~3 ms on one core, all of
+// it GPU idle time at the head of a PRM* batch
+static void host_features_batch(const DevSpace &sp, const FeatGeom &g, const double *states, size_t n, double *out) {
+    const size_t per_thread = 1024;
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t T = std::min<size_t>(hw, (n + per_thread - 1) / per_thread);
+    auto work = [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) host_features(sp, g, states + i * sp.dim, out + i * g.F);
+    };
+    if (T <= 1) {
+        work(0, n);
+        return;
+    }
+    std::vector<std::thread> pool;
+    pool.reserve(T - 1);
+    const size_t chunk = (n + T - 1) / T;
+    for (size_t t = 1; t < T; ++t) pool.emplace_back(work, std::min(n, t * chunk), std::min(n, (t + 1) * chunk));
+    work(0, std::min(n, chunk));
+    for (std::thread &th : pool) th.join();
+}
 
 ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, uint64_t *first_id) {
     if (!h || (n && !states)) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
@@ -340,8 +364,10 @@ ompl_gpu_status ompl_gpu_nn_add(ompl_gpu_nn *h, const double *states, size_t n, 
     return add_locked(h, states, n, first_id);
 }
 
-// append n AoS states (caller holds the lock)
-static ompl_gpu_status add_locked(ompl_gpu_nn *h, const double *states, size_t n, uint64_t *first_id) {
+// append n AoS states (caller holds the lock); d_feat / d_raw: the states' feature rows and raw
+// rows already on the device (AoS, a PRM* batch's), else computed and uploaded here
+static ompl_gpu_status add_locked(ompl_gpu_nn *h, const double *states, size_t n, uint64_t *first_id,
+                                  const double *d_feat, const double *d_raw) {
     HIP_OR_FAIL(hipSetDevice(h->device));
     if (first_id) *first_id = h->n_total;
     if (n == 0) return OMPL_GPU_OK;
@@ -349,19 +375,23 @@ static ompl_gpu_status add_locked(ompl_gpu_nn *h, const double *states, size_t n
     ompl_gpu_status s = grow(h, h->n_total + n);
     if (s != OMPL_GPU_OK) return s;
     const int F = h->g.F, dim = h->sp.dim;
-    h->hfeat.resize((size_t)n * F);
-    for (size_t i = 0; i < n; ++i) host_features(h->sp, h->g, states + i * dim, h->hfeat.data() + i * F);
     const bool sep_raw = h->raw != h->feat;
-    const size_t stage_bytes = sizeof(double) * n * (F + (sep_raw ? dim : 0));
-    HIP_OR_FAIL(h->stage.ensure(stage_bytes));
-    double *sf = (double *)h->stage.p;
-    HIP_OR_FAIL(hipMemcpyAsync(sf, h->hfeat.data(), sizeof(double) * n * F, hipMemcpyHostToDevice, h->stream));
-    HIP_OR_FAIL(launch_store_soa(sf, (uint32_t)n, F, h->feat, h->cap, h->n_total, h->stream));
-    if (sep_raw) {
-        double *sr = sf + n * F;
-        HIP_OR_FAIL(hipMemcpyAsync(sr, states, sizeof(double) * n * dim, hipMemcpyHostToDevice, h->stream));
-        HIP_OR_FAIL(launch_store_soa(sr, (uint32_t)n, dim, h->raw, h->cap, h->n_total, h->stream));
+    if (!d_feat || (sep_raw && !d_raw)) {
+        h->hfeat.resize((size_t)n * F);
+        host_features_batch(h->sp, h->g, states, n, h->hfeat.data());
+        const size_t stage_bytes = sizeof(double) * n * (F + (sep_raw ? dim : 0));
+        HIP_OR_FAIL(h->stage.ensure(stage_bytes));
+        double *sf = (double *)h->stage.p;
+        HIP_OR_FAIL(hipMemcpyAsync(sf, h->hfeat.data(), sizeof(double) * n * F, hipMemcpyHostToDevice, h->stream));
+        d_feat = sf;
+        if (sep_raw) {
+            double *sr = sf + n * F;
+            HIP_OR_FAIL(hipMemcpyAsync(sr, states, sizeof(double) * n * dim, hipMemcpyHostToDevice, h->stream));
+            d_raw = sr;
+        }
     }
+    HIP_OR_FAIL(launch_store_soa(d_feat, (uint32_t)n, F, h->feat, h->cap, h->n_total, h->stream));
+    if (sep_raw) HIP_OR_FAIL(launch_store_soa(d_raw, (uint32_t)n, dim, h->raw, h->cap, h->n_total, h->stream));
     if (h->rows32) HIP_OR_FAIL(launch_rows32(h->sp, h->g, h->feat, h->cap, h->n_total, n, h->feat32, h->stream));
     HIP_OR_FAIL(hipMemsetAsync(h->live + h->n_total, 1, n, h->stream));
     // screening bounds (knn_fast.hip): key box of the first <= 6 coordinates, max |coordinate|;
@@ -1429,7 +1459,7 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     if (kmax > k_cap) return fail(OMPL_GPU_ERR_INVALID_ARG, "k_cap below the largest k of the batch");
     // batch features (host, as add() computes them) and raw rows
     h->hfeat.resize(m * F);
-    for (size_t j = 0; j < m; ++j) host_features(h->sp, h->g, states + j * dim, h->hfeat.data() + j * F);
+    host_features_batch(h->sp, h->g, states, m, h->hfeat.data());
     HIP_OR_FAIL(h->prm_bf.ensure(sizeof(double) * m * F));
     HIP_OR_FAIL(h->prm_raw.ensure(sizeof(double) * m * dim));
     HIP_OR_FAIL(h->prm_kj.ensure(sizeof(uint32_t) * m));
@@ -1438,7 +1468,7 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     HIP_OR_FAIL(hipMemcpyAsync(bf, h->hfeat.data(), sizeof(double) * m * F, hipMemcpyHostToDevice, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(braw, states, sizeof(double) * m * dim, hipMemcpyHostToDevice, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(dkj, kj.data(), sizeof(uint32_t) * m, hipMemcpyHostToDevice, h->stream));
-    if (rows == 0) return add_locked(h, states, m, nullptr);
+    if (rows == 0) return add_locked(h, states, m, nullptr, bf, braw);
     // 1. the stored part: batched kNN of the slice's milestones (not yet inserted), k = min(kmax, live)
     const uint32_t kq = (uint32_t)std::min<uint64_t>(kmax, h->n_live);
     HIP_OR_FAIL(h->prm_sd.ensure(sizeof(double) * rows * std::max<uint32_t>(kq, 1)));
@@ -1508,7 +1538,7 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
         std::swap(ci, sii);
     }
     HIP_OR_FAIL(launch_prm_take(sii, sdd, off, dkj + j0, (uint32_t)rows, k_cap, d_nbr, d_cnt, d_dist, h->stream));
-    if (!mv) return add_locked(h, states, m, nullptr);  // lazy: edge validity stays unknown (LazyPRM.cpp:302)
+    if (!mv) return add_locked(h, states, m, nullptr, bf, braw);  // lazy: edge validity unknown (LazyPRM.cpp:302)
     // 3. edges checkMotion(state[n], state[m]) (PRM.cpp:582): compact, check, scatter to [m][k_cap]
     HIP_OR_FAIL(h->prm_eoff.ensure(sizeof(uint64_t) * (rows + 1)));
     HIP_OR_FAIL(h->prm_cnt64.ensure(sizeof(uint64_t) * (rows + 1)));
@@ -1541,8 +1571,8 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     HIP_OR_FAIL(launch_prm_scatter_valid((const uint8_t *)mv->valid.p, d_cnt, eoff, (uint32_t)rows, k_cap, d_valid,
                                          h->stream));
     if (edges) *edges = E;
-    // 4. the milestones join the structure (PRM.cpp:593)
-    return add_locked(h, states, m, nullptr);
+    // 4. the milestones join the structure (PRM.cpp:593): the batch's rows are on the device already
+    return add_locked(h, states, m, nullptr, bf, braw);
 }
 
 ompl_gpu_status prm_check_args(ompl_gpu_nn *h, const double *states, size_t m, size_t j0, size_t j1, uint32_t k_cap) {
