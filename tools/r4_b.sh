@@ -34,7 +34,8 @@ TESTS_Q="tests/test_gpu_nn.py tests/test_gpu_batch.py tests/test_gpu_bitstar.py 
 OMPL_GPU_RADIUS_Q16=1 timeout -k 10 500 python -u -m pytest $TESTS_Q -m gpu -x -q --timeout 300 --timeout-method thread \
     > "$out/pytest_rq16.log" 2>&1
 rc=$?; echo "radius q16: $(tail -1 "$out/pytest_rq16.log")"; rc_ok $rc "radius q16"
-bash tools/ab_env.sh cfg5 "--workload cfg5" 2 - OMPL_GPU_RADIUS_Q16=1 VAR=5 VAR=6 VAR=11 VAR=13 || exit 1
+bash tools/ab_env.sh cfg5 "--workload cfg5" 2 - OMPL_GPU_RADIUS_Q16=1 || exit 1
+bash tools/ab_env.sh cfg5v "--workload cfg5" 1 - VAR=5 VAR=6 VAR=11 VAR=13 || exit 1
 fi
 if [ "$P" = 4 ]; then
 TESTS_K="tests/test_gpu_nn.py tests/test_gpu_cull.py tests/test_gpu_fullsize.py::test_cfg3_every_query_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg5k_every_vertex_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg3_reference_tree_k10"
