@@ -17,31 +17,29 @@ for v in ${VARS:-7 8 9 12}; do
 done
 bash tools/ab_env.sh cfg3 "--workload cfg3" 2 - VAR=7 VAR=8 VAR=9 VAR=12 OMPL_GPU_QSORT=0 || exit 1
 fi
-if [ "$P" = 2 ]; then
+if [ "$P" = 2 ]; then  # the 16-bit rows: chain cull (default on), SE3 kNN and radius walks (A/B)
 TESTS_C="tests/test_gpu_cull.py tests/test_gpu_prm.py tests/test_gpu_fullsize.py::test_cfg4_chain_culled_scan_1e6 tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan"
 timeout -k 10 400 python -u -m pytest $TESTS_C -m gpu -x -q --timeout 300 --timeout-method thread > "$out/pytest_q16.log" 2>&1
 rc=$?; echo "chain q16: $(tail -1 "$out/pytest_q16.log")"; [ $rc = 0 ] || exit 1
-bash tools/ab_env.sh cfg4 "--workload cfg4" 2 - OMPL_GPU_CHAIN_Q16=0 OMPL_GPU_CHAIN_SHARE=0 OMPL_GPU_CHAIN_WAVE=1 || exit 1
+bash tools/ab_env.sh cfg4 "--workload cfg4" 2 - OMPL_GPU_CHAIN_Q16=0 || exit 1
+TESTS_K="tests/test_gpu_nn.py tests/test_gpu_fullsize.py::test_cfg3_every_query_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg5k_every_vertex_vs_exact_scan"
+OMPL_GPU_KNN_Q16=1 timeout -k 10 400 python -u -m pytest $TESTS_K -m gpu -x -q --timeout 300 --timeout-method thread \
+    > "$out/pytest_kq16.log" 2>&1
+rc=$?; echo "knn q16: $(tail -1 "$out/pytest_kq16.log")"; rc_ok $rc "knn q16"
+bash tools/ab_env.sh cfg5k "--workload cfg5 --bitstar-knn" 2 - OMPL_GPU_KNN_Q16=1 || exit 1
+bash tools/ab_env.sh cfg3q "--workload cfg3" 1 - OMPL_GPU_KNN_Q16=1 || exit 1
+TESTS_Q="tests/test_gpu_batch.py tests/test_gpu_bitstar.py tests/test_gpu_fullsize.py::test_cfg5_every_vertex_radius_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg5_radius_1e7_valid_samples"
+OMPL_GPU_RADIUS_Q16=1 timeout -k 10 400 python -u -m pytest $TESTS_Q -m gpu -x -q --timeout 300 --timeout-method thread \
+    > "$out/pytest_rq16.log" 2>&1
+rc=$?; echo "radius q16: $(tail -1 "$out/pytest_rq16.log")"; rc_ok $rc "radius q16"
+bash tools/ab_env.sh cfg5 "--workload cfg5" 2 - OMPL_GPU_RADIUS_Q16=1 || exit 1
 fi
-if [ "$P" = 3 ]; then
+if [ "$P" = 3 ]; then  # the radius walk's occupancy / per-query-mask variants
 TESTS_R="tests/test_gpu_fullsize.py::test_cfg5_every_vertex_radius_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg5_radius_1e7_valid_samples"
 for v in 11 13; do
   OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var$v.so timeout -k 10 300 python -u -m pytest $TESTS_R -m gpu -x -q --timeout 200 \
       --timeout-method thread > "$out/pytest_r$v.log" 2>&1
   rc=$?; echo "var$v radius: $(tail -1 "$out/pytest_r$v.log")"; rc_ok $rc var$v
 done
-TESTS_Q="tests/test_gpu_nn.py tests/test_gpu_batch.py tests/test_gpu_bitstar.py tests/test_gpu_index.py $TESTS_R"
-OMPL_GPU_RADIUS_Q16=1 timeout -k 10 500 python -u -m pytest $TESTS_Q -m gpu -x -q --timeout 300 --timeout-method thread \
-    > "$out/pytest_rq16.log" 2>&1
-rc=$?; echo "radius q16: $(tail -1 "$out/pytest_rq16.log")"; rc_ok $rc "radius q16"
-bash tools/ab_env.sh cfg5 "--workload cfg5" 2 - OMPL_GPU_RADIUS_Q16=1 || exit 1
 bash tools/ab_env.sh cfg5v "--workload cfg5" 1 - VAR=5 VAR=6 VAR=11 VAR=13 || exit 1
-fi
-if [ "$P" = 4 ]; then
-TESTS_K="tests/test_gpu_nn.py tests/test_gpu_cull.py tests/test_gpu_fullsize.py::test_cfg3_every_query_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg5k_every_vertex_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg3_reference_tree_k10"
-OMPL_GPU_KNN_Q16=1 timeout -k 10 500 python -u -m pytest $TESTS_K -m gpu -x -q --timeout 300 --timeout-method thread \
-    > "$out/pytest_kq16.log" 2>&1
-rc=$?; echo "knn q16: $(tail -1 "$out/pytest_kq16.log")"; [ $rc = 0 ] || exit 1
-bash tools/ab_env.sh cfg3q "--workload cfg3" 2 - OMPL_GPU_KNN_Q16=1 || exit 1
-bash tools/ab_env.sh cfg5k "--workload cfg5 --bitstar-knn" 2 - OMPL_GPU_KNN_Q16=1 || exit 1
 fi
