@@ -50,9 +50,12 @@ void free_sorted_store(SortedStore *s) {
 }
 
 namespace {
-__global__ void tombstone_kernel(const uint32_t *__restrict__ inv, uint64_t id, float *__restrict__ rows) {
+__global__ void tombstone_kernel(const uint32_t *__restrict__ inv, uint64_t id, float *__restrict__ rows,
+                                 uint32_t *__restrict__ rows16) {
     const uint32_t p = inv[id];
-    if (p != kNoId) rows[p] = __builtin_nanf("");  // row 0 of the fp32 copy: every distance is NaN
+    if (p == kNoId) return;
+    rows[p] = __builtin_nanf("");  // row 0 of the fp32 copy: every distance is NaN
+    if (rows16) rows16[p] |= 0xFFFFu;  // the 16-bit copy's NaN marker (coordinate 0)
 }
 // thread = sorted position: the F = 2 nm fp32 coordinates (SoA, stride n_pad) to nm words
 __global__ void chain_rows16_kernel(const float *__restrict__ rows, uint32_t n_pad, uint32_t n, int nm,
@@ -172,9 +175,12 @@ hipError_t refresh_chain_rows16(const FeatGeom &g, SortedStore *s, hipStream_t s
 
 hipError_t tombstone_sorted_store(SortedStore *s, uint64_t id, hipStream_t st) {
     if (!s->built || id >= s->covered || id >= s->cap_inv) return hipSuccess;
-    hipLaunchKernelGGL(tombstone_kernel, dim3(1), dim3(1), 0, st, s->inv, id, s->rows);
+    // a current 16-bit copy is patched in place and stays current
+    const bool q16 = s->rows16 && s->gen16 == s->gen;
+    hipLaunchKernelGGL(tombstone_kernel, dim3(1), dim3(1), 0, st, s->inv, id, s->rows, q16 ? s->rows16 : nullptr);
     s->removed += 1;
     s->gen += 1;
+    if (q16) s->gen16 = s->gen;
     return hipGetLastError();
 }
 
