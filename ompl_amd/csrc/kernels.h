@@ -160,10 +160,14 @@ hipError_t refresh_chain_rows16(const FeatGeom &g, SortedStore *s, hipStream_t s
 // bound on |d16 - d32| of one screened chain distance: link * sum_i sqrt(2) * 0.6 quanta * 2 (i + 1) / kChainQ16
 // (0.5 for the rounding, the rest for the fp32 scaling of state and query)
 double chain_q16_error(const DevSpace &sp);
-// SE3 radius walk (OMPL_GPU_RADIUS_Q16=1): the 16-bit copy over the stored box [lo, hi] of the
-// translation, and the bound on |d16 - d32| it adds to the walk's threshold
+// SE3 radius walk (default; OMPL_GPU_RADIUS_Q16=0: the fp32 rows): the 16-bit copy over the
+// stored box [lo, hi] of the translation, and the bound on |d16 - d32| it adds to the threshold.
+// Measured on cfg5: 1.694 ms per walk against 1.741-1.783 on the fp32 rows.
 bool se3_q16_enabled();
-bool se3_knn_q16_enabled();  // the SE3 kNN group walk on the same copy (OMPL_GPU_KNN_Q16=1)
+// the SE3 kNN group walk on the same copy (A/B only, OMPL_GPU_KNN_Q16=1): measured slower —
+// cfg3 1.383 against 1.263 ms, cfg5k 4.58-4.62 against 4.22-4.28 ms — the decode costs more
+// VALU than the halved tile bytes save in a walk bound by issue and latency
+bool se3_knn_q16_enabled();
 hipError_t refresh_se3_rows16(const double *lo, const double *hi, SortedStore *s, hipStream_t st);
 double se3_q16_error(const DevSpace &sp, const Q16Geo &q);
 void free_sorted_store(SortedStore *s);

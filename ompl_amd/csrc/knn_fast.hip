@@ -103,7 +103,7 @@ __global__ void se3_rows16_kernel(const float *__restrict__ rows, uint32_t n_pad
 bool se3_q16_enabled() {
     static const bool on = [] {
         const char *v = std::getenv("OMPL_GPU_RADIUS_Q16");
-        return v ? std::atoi(v) != 0 : false;
+        return v ? std::atoi(v) != 0 : true;
     }();
     return on;
 }

@@ -1299,7 +1299,9 @@ __global__ __launch_bounds__(256) void knn_chunk_merge_kernel(float *__restrict_
 // keeps is this d16; the tile bounds stay on the fp32 boxes and are lowered by qerr
 // (chain_q16_error, >= |d16 - d32|), and the certificate's screen error grows by the same qerr.
 constexpr int kChainTauTiles = 16;
-template <int F, int K2, int G, int MODE, bool Q16>
+// PF (A/B, OMPL_GPU_CHAIN_PREFETCH=1; Q16 only): the next passing tile's 16-bit words are in
+// flight while the current tile is scanned.
+template <int F, int K2, int G, int MODE, bool Q16, bool PF = false>
 __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
     const float *__restrict__ rows, const uint32_t *__restrict__ rows16, uint32_t n_pad,
     const uint32_t *__restrict__ ids, uint32_t ntiles, const float *__restrict__ tbox, const float *__restrict__ q32,
@@ -1353,18 +1355,25 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
         }
     };
     uint32_t visited = 0, qscans = 0;
+    auto load_raw = [&](uint32_t t, uint32_t (&w)[NM]) {
+        const uint64_t p = (uint64_t)t * kCullTile + lane;
+#pragma unroll
+        for (int j = 0; j < NM; ++j) w[j] = rows16[(uint64_t)j * n_pad + p];
+    };
+    auto decode = [&](const uint32_t (&w)[NM], float (&x)[F]) {
+#pragma unroll
+        for (int j = 0; j < NM; ++j) {
+            x[2 * j] = (float)(w[j] & 0xFFFFu);
+            x[2 * j + 1] = (float)(w[j] >> 16);
+        }
+        if ((w[0] & 0xFFFFu) == 0xFFFFu) x[0] = __builtin_nanf("");  // padding / removed
+    };
     auto load_tile = [&](uint32_t t, float (&x)[F]) {
         const uint64_t p = (uint64_t)t * kCullTile + lane;
         if constexpr (Q16) {
             uint32_t w[NM];
-#pragma unroll
-            for (int j = 0; j < NM; ++j) w[j] = rows16[(uint64_t)j * n_pad + p];
-#pragma unroll
-            for (int j = 0; j < NM; ++j) {
-                x[2 * j] = (float)(w[j] & 0xFFFFu);
-                x[2 * j + 1] = (float)(w[j] >> 16);
-            }
-            if ((w[0] & 0xFFFFu) == 0xFFFFu) x[0] = __builtin_nanf("");  // padding / removed
+            load_raw(t, w);
+            decode(w, x);
         } else {
 #pragma unroll
             for (int f = 0; f < F; ++f) x[f] = rows[(uint64_t)f * n_pad + p];
@@ -1498,6 +1507,42 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
         uint64_t need = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) need |= __ballot(lb[g] < td[g]);
+        if constexpr (Q16 && PF) {
+            uint32_t w[NM], wn[NM];
+            uint32_t id = 0, idn = 0;
+            int l = -1;
+            if (need) {
+                l = __builtin_ctzll(need);
+                need &= need - 1;
+                load_raw(tb + (uint32_t)l, w);
+                id = ids[(uint64_t)(tb + l) * kCullTile + lane];
+            }
+            while (l >= 0) {
+                int ln = -1;
+                if (need) {  // the next passing tile, in flight during this scan
+                    ln = __builtin_ctzll(need);
+                    need &= need - 1;
+                    load_raw(tb + (uint32_t)ln, wn);
+                    idn = ids[(uint64_t)(tb + ln) * kCullTile + lane];
+                }
+                float x[F];
+                decode(w, x);
+                ++visited;
+                asm volatile("" : "+s"(qoff));
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    if (readlane_f(lb[g], l) < td[g]) scan(g, x, id);
+                uint64_t still = 0;  // the fetched next tile is re-checked per query in its scan
+#pragma unroll
+                for (int g = 0; g < G; ++g) still |= __ballot(lb[g] < td[g]);
+                need &= still;
+                l = ln;
+#pragma unroll
+                for (int j = 0; j < NM; ++j) w[j] = wn[j];
+                id = idn;
+            }
+            continue;
+        }
         while (need) {
             const int l = __builtin_ctzll(need);
             need &= need - 1;
@@ -1738,7 +1783,7 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
 #else
 #define OMPL_RADIUS_LB __launch_bounds__(64)
 #endif
-// Q16 (SE3, MODE 2; OMPL_GPU_RADIUS_Q16=1): the tiles come from the 16-bit copy
+// Q16 (SE3, MODE 2; the default; OMPL_GPU_RADIUS_Q16=0 reads the fp32 rows): the tiles come from the 16-bit copy
 // (SortedStore::rows16, 16 B per state against 28), decoded to fp32 once per tile; every
 // threshold grows by qerr >= |d16 - d32| (se3_q16_error), so no state with d32 <= r + e is lost
 // and the box bounds (over the fp32 rows) stay valid.
@@ -2340,14 +2385,22 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             // the 16-bit rows when the store's copy is current (refresh_chain_rows16; share only)
             const bool q16 = share && ss->rows16 && ss->gen16 == ss->gen;
             const float qerr = q16 ? (float)(chain_q16_error(sp) * (1.0 + 1e-5)) : 0.f;
-#define OMPL_AMD_CHAIN_CULL(MODE, Q, GY, CNT, KEY)                                                              \
-    hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, MODE, Q>), dim3(ng, GY), dim3(64), 0, st,  \
+            static const bool pf = [] {  // A/B: the next tile in flight (Q16 only)
+                const char *v = std::getenv("OMPL_GPU_CHAIN_PREFETCH");
+                return v ? std::atoi(v) != 0 : false;
+            }();
+#define OMPL_AMD_CHAIN_CULL(MODE, Q, GY, CNT, KEY) OMPL_AMD_CHAIN_CULL_PF(MODE, Q, false, GY, CNT, KEY)
+#define OMPL_AMD_CHAIN_CULL_PF(MODE, Q, P, GY, CNT, KEY)                                                         \
+    hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, MODE, Q, P>), dim3(ng, GY), dim3(64), 0, st, \
                        ss->rows, ss->rows16, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,      \
                        (float)sp.link, sp.dim, qerr, pd, pi, CNT, KEY)
             if (q16) {
                 OMPL_AMD_CHAIN_CULL(1, true, 1, nullptr, skey);
                 timer_begin(st, "knn32_chain_cull_kernel");
-                OMPL_AMD_CHAIN_CULL(2, true, p.chunks, ss->counters, skey);
+                if (pf)
+                    OMPL_AMD_CHAIN_CULL_PF(2, true, true, p.chunks, ss->counters, skey);
+                else
+                    OMPL_AMD_CHAIN_CULL(2, true, p.chunks, ss->counters, skey);
             } else if (share) {
                 OMPL_AMD_CHAIN_CULL(1, false, 1, nullptr, skey);
                 timer_begin(st, "knn32_chain_cull_kernel");
@@ -2357,6 +2410,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
                 OMPL_AMD_CHAIN_CULL(0, false, p.chunks, ss->counters, nullptr);
             }
 #undef OMPL_AMD_CHAIN_CULL
+#undef OMPL_AMD_CHAIN_CULL_PF
             timer_end(st);
             chain_qerr = qerr;
             walked = true;

@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/r4b; mkdir -p "$out"
-P=${PART:-1}  # 1: walk variants (cfg3); 2: chain (cfg4); 3: radius (cfg5); 4: SE3 kNN on 16-bit rows
+P=${PART:-1}  # 1: walk variants (cfg3); 2: 16-bit rows (cfg4, cfg5k, cfg3, cfg5); 3: radius variants; 5: chain prefetch
 rc_ok() { case $1 in 0) ;; 124|134|137|139) exit 1;; *) echo "$2 failed";; esac; }
 if [ "$P" = 1 ]; then
 T="tests/test_gpu_nn.py tests/test_gpu_cull.py"
@@ -42,4 +42,11 @@ for v in 11 13; do
   rc=$?; echo "var$v radius: $(tail -1 "$out/pytest_r$v.log")"; rc_ok $rc var$v
 done
 bash tools/ab_env.sh cfg5v "--workload cfg5" 1 - VAR=5 VAR=6 VAR=11 VAR=13 || exit 1
+fi
+if [ "$P" = 5 ]; then  # the chain cull with the next tile in flight; radius 16-bit default
+T5="tests/test_gpu_prm.py tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan"
+OMPL_GPU_CHAIN_PREFETCH=1 timeout -k 10 400 python -u -m pytest $T5 -m gpu -x -q --timeout 300 --timeout-method thread \
+    > "$out/pytest_pf.log" 2>&1
+rc=$?; echo "chain prefetch: $(tail -1 "$out/pytest_pf.log")"; [ $rc = 0 ] || exit 1
+bash tools/ab_env.sh cfg4pf "--workload cfg4" 2 - OMPL_GPU_CHAIN_PREFETCH=1 || exit 1
 fi
