@@ -50,3 +50,6 @@ OMPL_GPU_CHAIN_PREFETCH=1 timeout -k 10 400 python -u -m pytest $T5 -m gpu -x -q
 rc=$?; echo "chain prefetch: $(tail -1 "$out/pytest_pf.log")"; [ $rc = 0 ] || exit 1
 bash tools/ab_env.sh cfg4pf "--workload cfg4" 2 - OMPL_GPU_CHAIN_PREFETCH=1 || exit 1
 fi
+if [ "$P" = 6 ]; then  # chunks of the chain cull's MODE 2 pass (waves per CU) now that thresholds are shared
+bash tools/ab_env.sh cfg4wpc "--workload cfg4" 1 - OMPL_GPU_CHAIN_WPC=24 OMPL_GPU_CHAIN_WPC=48 OMPL_GPU_CHAIN_WPC=192 OMPL_GPU_CHAIN_WPC=384 || exit 1
+fi
