@@ -2235,11 +2235,19 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
         p.k2 = p.K2;
         const uint64_t ntile = std::max<uint64_t>(1, (n_end + kCullTile - 1) / kCullTile);
         const uint64_t groups = (nq + kChainCullG - 1) / kChainCullG;
-        static const uint64_t wpc = [] {  // waves per CU the chunks aim at (OMPL_GPU_CHAIN_WPC: A/B)
+        // waves per CU the chunks aim at and the chunk cap (OMPL_GPU_CHAIN_WPC / _SMAX: A/B).  With
+        // the thresholds shared across chunks (MODE 2) more chunks only add parallelism: measured
+        // on cfg4 (8,192 milestones, 1,024 groups) 24 / 48 / 96 / 192 / 384 waves per CU ->
+        // 8.14 / 6.79 / 5.59 / 4.88 / 4.67 ms (384 reaches the 64-chunk cap)
+        static const uint64_t wpc = [] {
             const char *v = std::getenv("OMPL_GPU_CHAIN_WPC");
-            return v ? (uint64_t)std::max(1, std::atoi(v)) : (uint64_t)96;
+            return v ? (uint64_t)std::max(1, std::atoi(v)) : (uint64_t)384;
         }();
-        const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)num_cus * wpc + groups - 1) / groups, 64));
+        static const uint64_t smax = [] {
+            const char *v = std::getenv("OMPL_GPU_CHAIN_SMAX");
+            return v ? (uint64_t)std::max(1, std::atoi(v)) : (uint64_t)64;
+        }();
+        const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)num_cus * wpc + groups - 1) / groups, smax));
         const uint64_t per = (ntile + S - 1) / S;
         p.chunk_len = (uint32_t)per;  // tiles per chunk
         p.chunks = (uint32_t)((ntile + per - 1) / per);

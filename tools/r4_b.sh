@@ -53,3 +53,8 @@ fi
 if [ "$P" = 6 ]; then  # chunks of the chain cull's MODE 2 pass (waves per CU) now that thresholds are shared
 bash tools/ab_env.sh cfg4wpc "--workload cfg4" 1 - OMPL_GPU_CHAIN_WPC=24 OMPL_GPU_CHAIN_WPC=48 OMPL_GPU_CHAIN_WPC=192 OMPL_GPU_CHAIN_WPC=384 || exit 1
 fi
+if [ "$P" = 7 ]; then  # the chunk cap of the chain cull's MODE 2 pass
+bash tools/ab_env.sh cfg4s "--workload cfg4" 1 - "OMPL_GPU_CHAIN_WPC=1024 OMPL_GPU_CHAIN_SMAX=128" "OMPL_GPU_CHAIN_WPC=1024 OMPL_GPU_CHAIN_SMAX=256" - || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_prm.py tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_wpc.log" 2>&1
+rc=$?; echo "wpc 384: $(tail -1 "$out/pytest_wpc.log")"; [ $rc = 0 ] || exit 1
+fi
