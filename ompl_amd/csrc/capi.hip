@@ -340,7 +340,7 @@ static ompl_gpu_status add_locked(ompl_gpu_nn *h, const double *states, size_t n
 // split over host threads for large batches: 8,192 chain states cost ~3 ms on one core, all of
 // it GPU idle time at the head of a PRM* batch
 static void host_features_batch(const DevSpace &sp, const FeatGeom &g, const double *states, size_t n, double *out) {
-    const size_t per_thread = 1024;
+    const size_t per_thread = 512;
     const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const size_t T = std::min<size_t>(hw, (n + per_thread - 1) / per_thread);
     auto work = [&](size_t a, size_t b) {
@@ -1457,6 +1457,14 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
         kmax = std::max(kmax, kj[j]);
     }
     if (kmax > k_cap) return fail(OMPL_GPU_ERR_INVALID_ARG, "k_cap below the largest k of the batch");
+    // the sorted store takes up the previous batch (tail append, 16-bit copy) on the device while
+    // the host computes this batch's feature rows (the kNN below finds it current)
+    if (n0 && rows && h->fast && h->cull && cull_supported(h->sp) && screen_safe(h)) {
+        ompl_gpu_status s = ensure_sorted(h);
+        if (s != OMPL_GPU_OK) return s;
+        if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN && chain_q16_enabled())
+            HIP_OR_FAIL(refresh_chain_rows16(h->g, &h->sorted, h->stream));
+    }
     // batch features (host, as add() computes them) and raw rows
     h->hfeat.resize(m * F);
     host_features_batch(h->sp, h->g, states, m, h->hfeat.data());
