@@ -1251,7 +1251,13 @@ __global__ __launch_bounds__(256) void knn_chunk_merge_kernel(float *__restrict_
         return id == kNoId ? kMaxKey : kpack(pd[o], id);
     };
     uint64_t L = entry(0);
-    for (uint32_t c = 1; c < S; ++c) wave_merge_sorted_k(L, entry(c), lane);
+    for (uint32_t c = 1; c < S; ++c) {
+        const uint64_t e = entry(c);
+        // a chunk list whose smallest key is not below the merged K2-th cannot change the merge
+        // (with shared thresholds most chunks hold only keys above it)
+        if (readlane_k(e, 0) >= readlane_k(L, K2 - 1)) continue;
+        wave_merge_sorted_k(L, e, lane);
+    }
     if (lane < K2) {
         const size_t o = (size_t)qs * K2 + lane;
         pd[o] = L == kMaxKey ? __builtin_inff() : kdist(L);
