@@ -66,10 +66,16 @@ def pmc_traffic(workload, kernel):
                 per = json.load(f)["per_kernel_mean"]
         except (OSError, ValueError, KeyError):
             continue
+        # the timed launch is the kernel's dominant instance (the chain cull: its MODE 2 pass, not
+        # the pre-pass): the largest per-dispatch traffic among the instances of that name
+        best = None
         for name, c in per.items():
             if name.split("<")[0].endswith(kernel) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-                return {"bytes": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0,
-                        "source": os.path.relpath(path, ROOT) + f" [{name}]"}
+                b = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+                if best is None or b > best["bytes"]:
+                    best = {"bytes": b, "source": os.path.relpath(path, ROOT) + f" [{name}]"}
+        if best:
+            return best
     return None
 
 
