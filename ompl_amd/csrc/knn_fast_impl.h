@@ -1313,7 +1313,7 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
     const uint32_t *__restrict__ ids, uint32_t ntiles, const float *__restrict__ tbox, const float *__restrict__ q32,
     const uint32_t *__restrict__ qkeys, uint32_t nq, uint32_t chunk_tiles, float link, int nlinks, float qerr,
     float *__restrict__ pd, uint32_t *__restrict__ pi, unsigned long long *__restrict__ counters,
-    unsigned long long *__restrict__ shared_key) {
+    unsigned long long *__restrict__ shared_key, int kd_order = 0) {
     constexpr int NM = F / 2;
     static_assert(K2 <= 64 && NM % 2 == 0, "chain cull shape");
     __shared__ __attribute__((aligned(16))) float qrow[G * F];
@@ -1457,8 +1457,12 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
     const uint32_t c0 = blockIdx.y * chunk_tiles, c1 = min(c0 + chunk_tiles, ntiles);
     const uint32_t nblk = c1 > c0 ? (c1 - c0 + 63) / 64 : 0u;
     const uint32_t sblk = (MODE == 2 && home >= c0 && home < c1) ? (home - c0) / 64 : 0u;
+    // blocks nearest the home tile in k-d order first (kd_order > 0, MODE 2): a chunk below the
+    // home tile walks its blocks backwards, one above it forwards, the home chunk from the home
+    // block on (wrapping) — each chunk's own list then tightens on its nearest tiles first
+    const bool backwards = MODE == 2 && kd_order && c1 <= home;
     for (uint32_t bi = 0; bi < nblk; ++bi) {
-        const uint32_t tb = c0 + ((sblk + bi) % nblk) * 64;
+        const uint32_t tb = c0 + (backwards ? nblk - 1 - bi : (sblk + bi) % nblk) * 64;
         if constexpr (MODE == 2) {  // share the thresholds: publish this chunk's K2-th keys, take the smallest
             if (bi) {
                 uint64_t mine = kMaxKey;
@@ -2399,6 +2403,10 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             // the 16-bit rows when the store's copy is current (refresh_chain_rows16; share only)
             const bool q16 = share && ss->rows16 && ss->gen16 == ss->gen;
             const float qerr = q16 ? (float)(chain_q16_error(sp) * (1.0 + 1e-5)) : 0.f;
+            static const int kd_ord = [] {  // A/B: chunk blocks nearest the home tile first
+                const char *v = std::getenv("OMPL_GPU_CHAIN_KDORDER");
+                return v ? std::atoi(v) : 0;
+            }();
             static const bool pf = [] {  // A/B: the next tile in flight (Q16 only)
                 const char *v = std::getenv("OMPL_GPU_CHAIN_PREFETCH");
                 return v ? std::atoi(v) != 0 : false;
@@ -2407,7 +2415,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
 #define OMPL_AMD_CHAIN_CULL_PF(MODE, Q, P, GY, CNT, KEY)                                                         \
     hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, MODE, Q, P>), dim3(ng, GY), dim3(64), 0, st, \
                        ss->rows, ss->rows16, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,      \
-                       (float)sp.link, sp.dim, qerr, pd, pi, CNT, KEY)
+                       (float)sp.link, sp.dim, qerr, pd, pi, CNT, KEY, kd_ord)
             if (q16) {
                 OMPL_AMD_CHAIN_CULL(1, true, 1, nullptr, skey);
                 timer_begin(st, "knn32_chain_cull_kernel");

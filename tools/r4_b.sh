@@ -58,3 +58,8 @@ bash tools/ab_env.sh cfg4s "--workload cfg4" 1 - "OMPL_GPU_CHAIN_WPC=1024 OMPL_G
 timeout -k 10 300 python -u -m pytest tests/test_gpu_prm.py tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_wpc.log" 2>&1
 rc=$?; echo "wpc 384: $(tail -1 "$out/pytest_wpc.log")"; [ $rc = 0 ] || exit 1
 fi
+if [ "$P" = 8 ]; then  # chain chunks: blocks nearest the home tile first
+OMPL_GPU_CHAIN_KDORDER=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_prm.py tests/test_gpu_cull.py tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_kdo.log" 2>&1
+rc=$?; echo "kd order: $(tail -1 "$out/pytest_kdo.log")"; [ $rc = 0 ] || exit 1
+bash tools/ab_env.sh cfg4kdo "--workload cfg4" 2 - OMPL_GPU_CHAIN_KDORDER=1 || exit 1
+fi
