@@ -1457,7 +1457,7 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
     const uint32_t c0 = blockIdx.y * chunk_tiles, c1 = min(c0 + chunk_tiles, ntiles);
     const uint32_t nblk = c1 > c0 ? (c1 - c0 + 63) / 64 : 0u;
     const uint32_t sblk = (MODE == 2 && home >= c0 && home < c1) ? (home - c0) / 64 : 0u;
-    // blocks nearest the home tile in k-d order first (kd_order > 0, MODE 2): a chunk below the
+    // blocks nearest the home tile in k-d order first (kd_order > 0, MODE 2; the default): a chunk below the
     // home tile walks its blocks backwards, one above it forwards, the home chunk from the home
     // block on (wrapping) — each chunk's own list then tightens on its nearest tiles first
     const bool backwards = MODE == 2 && kd_order && c1 <= home;
@@ -2405,7 +2405,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             const float qerr = q16 ? (float)(chain_q16_error(sp) * (1.0 + 1e-5)) : 0.f;
             static const int kd_ord = [] {  // A/B: chunk blocks nearest the home tile first
                 const char *v = std::getenv("OMPL_GPU_CHAIN_KDORDER");
-                return v ? std::atoi(v) : 0;
+                return v ? std::atoi(v) : 1;  // measured: 4.75-4.82 against 4.84-4.85 ms on cfg4
             }();
             static const bool pf = [] {  // A/B: the next tile in flight (Q16 only)
                 const char *v = std::getenv("OMPL_GPU_CHAIN_PREFETCH");
