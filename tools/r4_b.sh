@@ -63,3 +63,11 @@ OMPL_GPU_CHAIN_KDORDER=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_pr
 rc=$?; echo "kd order: $(tail -1 "$out/pytest_kdo.log")"; [ $rc = 0 ] || exit 1
 bash tools/ab_env.sh cfg4kdo "--workload cfg4" 2 - OMPL_GPU_CHAIN_KDORDER=1 || exit 1
 fi
+if [ "$P" = 9 ]; then  # queries per wave of the 64-lane (k = 57) group walk
+for v in 14 15; do
+  OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_fullsize.py::test_cfg5k_every_vertex_vs_exact_scan tests/test_gpu_nn.py -m gpu -x -q --timeout 200 \
+      --timeout-method thread > "$out/pytest_g$v.log" 2>&1
+  rc=$?; echo "var$v: $(tail -1 "$out/pytest_g$v.log")"; rc_ok $rc var$v
+done
+bash tools/ab_env.sh cfg5kg "--workload cfg5 --bitstar-knn" 2 - VAR=14 VAR=15 || exit 1
+fi
