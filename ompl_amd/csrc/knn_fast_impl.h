@@ -1427,8 +1427,16 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
     } else {
         const uint32_t h = home;
         const uint32_t span = MODE == 1 ? (uint32_t)kChainTauTiles : 4u;
-        const uint32_t t0 = h >= span / 2 - (MODE == 1 ? 0u : 1u) ? h - (span / 2 - (MODE == 1 ? 0u : 1u)) : 0u;
-        const uint32_t t1 = min(t0 + span, ntiles);
+        uint32_t t0, t1;
+        if constexpr (MODE == 1) {  // part blockIdx.y of a window of gridDim.y spans around home
+            const uint32_t W = span * gridDim.y;
+            const uint32_t w0 = h >= W / 2 ? h - W / 2 : 0u;
+            t0 = min(w0 + blockIdx.y * span, ntiles);
+            t1 = min(t0 + span, ntiles);
+        } else {
+            t0 = h >= span / 2 - 1u ? h - (span / 2 - 1u) : 0u;
+            t1 = min(t0 + span, ntiles);
+        }
         for (uint32_t t = t0; t < t1; ++t) {
             float x[F];
             load_tile(t, x);
@@ -1446,10 +1454,12 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
             tk[g] = tauk[g];
             td[g] = g0 + g < nq ? up_of(tau) : -__builtin_inff();
         }
-        if constexpr (MODE == 1) {
+        if constexpr (MODE == 1) {  // each part's K2-th key bounds the store's: keep the smallest
 #pragma unroll
             for (int g = 0; g < G; ++g)
-                if (lane == g && g0 + g < nq) shared_key[g0 + g] = tauk[g];
+                if (lane == g && g0 + g < nq)
+                    (void)__hip_atomic_fetch_min(&shared_key[g0 + g], tauk[g], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
     }
@@ -2423,15 +2433,23 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, MODE, Q, P>), dim3(ng, GY), dim3(64), 0, st, \
                        ss->rows, ss->rows16, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,      \
                        (float)sp.link, sp.dim, qerr, pd, pi, CNT, KEY, kd_ord)
+            static const uint32_t tau_parts = [] {  // pre-pass parts (A/B): 16 tiles each
+                const char *v = std::getenv("OMPL_GPU_CHAIN_TAU_PARTS");
+                return (uint32_t)std::max(1, v ? std::atoi(v) : 1);
+            }();
+            if (share) {  // the parts publish with atomicMin: start from all-ones (above every key)
+                hipError_t me = hipMemsetAsync(skey, 0xFF, 8ull * nq, st);
+                if (me != hipSuccess) return me;
+            }
             if (q16) {
-                OMPL_AMD_CHAIN_CULL(1, true, 1, nullptr, skey);
+                OMPL_AMD_CHAIN_CULL(1, true, tau_parts, nullptr, skey);
                 timer_begin(st, "knn32_chain_cull_kernel");
                 if (pf)
                     OMPL_AMD_CHAIN_CULL_PF(2, true, true, p.chunks, ss->counters, skey);
                 else
                     OMPL_AMD_CHAIN_CULL(2, true, p.chunks, ss->counters, skey);
             } else if (share) {
-                OMPL_AMD_CHAIN_CULL(1, false, 1, nullptr, skey);
+                OMPL_AMD_CHAIN_CULL(1, false, tau_parts, nullptr, skey);
                 timer_begin(st, "knn32_chain_cull_kernel");
                 OMPL_AMD_CHAIN_CULL(2, false, p.chunks, ss->counters, skey);
             } else {

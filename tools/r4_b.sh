@@ -71,3 +71,8 @@ for v in 14 15; do
 done
 bash tools/ab_env.sh cfg5kg "--workload cfg5 --bitstar-knn" 2 - VAR=14 VAR=15 || exit 1
 fi
+if [ "$P" = 10 ]; then  # the chain pre-pass in parts (atomicMin of the parts' K2-th keys)
+OMPL_GPU_CHAIN_TAU_PARTS=4 timeout -k 10 300 python -u -m pytest tests/test_gpu_prm.py tests/test_gpu_cull.py tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_tp.log" 2>&1
+rc=$?; echo "tau parts: $(tail -1 "$out/pytest_tp.log")"; [ $rc = 0 ] || exit 1
+bash tools/ab_env.sh cfg4tp "--workload cfg4" 2 - OMPL_GPU_CHAIN_TAU_PARTS=2 OMPL_GPU_CHAIN_TAU_PARTS=4 || exit 1
+fi
