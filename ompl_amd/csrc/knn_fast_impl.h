@@ -2372,13 +2372,12 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     if constexpr (SP == OMPL_GPU_SPACE_SE3 || SP == OMPL_GPU_SPACE_REALVECTOR) {  // cull_supported
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
-            // (A/B variants 14 / 15: G = 8 / 2 for the 64-lane lists of BIT*'s k = 57)
+            // SE3 with 64-lane lists (BIT*'s k = 57): 2 queries per wave — measured on cfg5k 4.08-4.14
+            // ms against 4.24-4.35 at G = 4 and 5.07-5.09 at G = 8 (A/B variant 14 keeps G = 8)
 #if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 14
             constexpr int G = (SP == OMPL_GPU_SPACE_SE3 && K2 == 64) ? 8 : group_queries<SP>();
-#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 15
-            constexpr int G = (SP == OMPL_GPU_SPACE_SE3 && K2 == 64) ? 2 : group_queries<SP>();
 #else
-            constexpr int G = group_queries<SP>();
+            constexpr int G = (SP == OMPL_GPU_SPACE_SE3 && K2 == 64) ? 2 : group_queries<SP>();
 #endif
             static const int recheck = [] {  // A/B switch of the popped super-tile re-check
                 const char *v = std::getenv("OMPL_GPU_SUPER_RECHECK");
