@@ -2376,6 +2376,10 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             // ms against 4.24-4.35 at G = 4 and 5.07-5.09 at G = 8 (A/B variant 14 keeps G = 8)
 #if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 14
             constexpr int G = (SP == OMPL_GPU_SPACE_SE3 && K2 == 64) ? 8 : group_queries<SP>();
+#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 15  // A/B: G = 2 for every SE3 list (cfg3)
+            constexpr int G = SP == OMPL_GPU_SPACE_SE3 ? 2 : group_queries<SP>();
+#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 16  // A/B: G = 4 for R^n (cfg2)
+            constexpr int G = (SP == OMPL_GPU_SPACE_SE3 && K2 == 64) ? 2 : 4;
 #else
             constexpr int G = (SP == OMPL_GPU_SPACE_SE3 && K2 == 64) ? 2 : group_queries<SP>();
 #endif
