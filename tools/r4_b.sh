@@ -76,3 +76,12 @@ OMPL_GPU_CHAIN_TAU_PARTS=4 timeout -k 10 300 python -u -m pytest tests/test_gpu_
 rc=$?; echo "tau parts: $(tail -1 "$out/pytest_tp.log")"; [ $rc = 0 ] || exit 1
 bash tools/ab_env.sh cfg4tp "--workload cfg4" 2 - OMPL_GPU_CHAIN_TAU_PARTS=2 OMPL_GPU_CHAIN_TAU_PARTS=4 || exit 1
 fi
+if [ "$P" = 11 ]; then  # queries per wave: SE3 G = 2 on cfg3 (variant 15), R^n G = 4 on cfg2 (variant 16)
+for v in 15 16; do
+  OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_nn.py tests/test_gpu_cull.py -m gpu -x -q --timeout 200 \
+      --timeout-method thread > "$out/pytest_g$v.log" 2>&1
+  rc=$?; echo "var$v: $(tail -1 "$out/pytest_g$v.log")"; rc_ok $rc var$v
+done
+bash tools/ab_env.sh cfg3g "--workload cfg3" 2 - VAR=15 || exit 1
+bash tools/ab_env.sh cfg2g "--workload cfg2" 2 - VAR=16 || exit 1
+fi
