@@ -1283,7 +1283,11 @@ __global__ __launch_bounds__(256) void knn_chunk_merge_kernel(float *__restrict_
 //      per query; the passing tiles are fetched (lane = state) and scanned for every query whose
 //      own bound is still below its threshold, with the wave scan's outer-links-first partial
 //      sums and wave-wide early exit.
-// Lists hold original ids (the chunked certificate reads the fp64 features by id).
+// Lists hold sorted positions (round 4; were original ids): the certificate reads each
+// candidate's fp64 features as one contiguous AoS row (SortedStore::rows64, 192 B for 12 links)
+// instead of 24 gathers by id, and maps positions to ids (SortedStore::ids).  Keys (distance,
+// position) are a total order as (distance, id) was, which is all the thresholds' argument needs;
+// the certificate ranks by (exact distance, id).
 //
 // MODE 0: as above.  MODE 1 / 2 (the default, two launches): the thresholds are shared across the
 // chunks.  Each chunk only sees 1/S of the store, so its own list converges to its chunk's K2-th
@@ -1440,7 +1444,7 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
         for (uint32_t t = t0; t < t1; ++t) {
             float x[F];
             load_tile(t, x);
-            const uint32_t id = ids[(uint64_t)t * kCullTile + lane];
+            const uint32_t id = t * kCullTile + (uint32_t)lane;  // sorted position
             asm volatile("" : "+s"(qoff));
 #pragma unroll
             for (int g = 0; g < G; ++g) scan(g, x, id);
@@ -1535,7 +1539,7 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
                 l = __builtin_ctzll(need);
                 need &= need - 1;
                 load_raw(tb + (uint32_t)l, w);
-                id = ids[(uint64_t)(tb + l) * kCullTile + lane];
+                id = (tb + (uint32_t)l) * kCullTile + (uint32_t)lane;
             }
             while (l >= 0) {
                 int ln = -1;
@@ -1543,7 +1547,7 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
                     ln = __builtin_ctzll(need);
                     need &= need - 1;
                     load_raw(tb + (uint32_t)ln, wn);
-                    idn = ids[(uint64_t)(tb + ln) * kCullTile + lane];
+                    idn = (tb + (uint32_t)ln) * kCullTile + (uint32_t)lane;
                 }
                 float x[F];
                 decode(w, x);
@@ -1568,7 +1572,7 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
             need &= need - 1;
             float x[F];
             load_tile(tb + (uint32_t)l, x);
-            const uint32_t id = ids[(uint64_t)(tb + l) * kCullTile + lane];
+            const uint32_t id = (tb + (uint32_t)l) * kCullTile + (uint32_t)lane;
             ++visited;
             asm volatile("" : "+s"(qoff));
 #pragma unroll
@@ -2506,8 +2510,9 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (p.chunks > 1)
             hipLaunchKernelGGL((knn_chunk_merge_kernel<K2>), dim3((nq + 3) / 4), b256, 0, st, pd, pi, p.chunks, nq);
         constexpr uint32_t QPB = 256 / K2;
+        if (!ss->rows64) return hipErrorInvalidValue;
         hipLaunchKernelGGL((knn_certify_wave_kernel<SP, F, K2>), dim3((nq + QPB - 1) / QPB), b256, 0, st, pd, pi, nq,
-                           perm, f64, cap, nullptr, nullptr, qf64, sp, b.absmax, b.qeta + chain_qerr, b.n_live,
+                           perm, f64, cap, ss->ids, ss->rows64, qf64, sp, b.absmax, b.qeta + chain_qerr, b.n_live,
                            (uint32_t)K2, od, oi, k, fail, fail + 1);
     } else if (p.chunks == 1) {
         constexpr uint32_t QPB = 256 / K2;

@@ -85,3 +85,9 @@ done
 bash tools/ab_env.sh cfg3g "--workload cfg3" 2 - VAR=15 || exit 1
 bash tools/ab_env.sh cfg2g "--workload cfg2" 2 - VAR=16 || exit 1
 fi
+if [ "$P" = 12 ]; then  # chain lists of sorted positions (AoS certificate rows)
+timeout -k 10 400 python -u -m pytest tests/test_gpu_prm.py tests/test_gpu_cull.py tests/test_gpu_nn.py tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg4_chain_culled_scan_1e6 -m gpu -x -q --timeout 300 --timeout-method thread > "$out/pytest_pos.log" 2>&1
+rc=$?; echo "chain positions: $(tail -1 "$out/pytest_pos.log")"; [ $rc = 0 ] || exit 1
+bash tools/ab_env.sh cfg4pos "--workload cfg4" 2 - || exit 1
+bash tools/prof_workload.sh cfg4 r4_cfg4 || exit 1
+fi
