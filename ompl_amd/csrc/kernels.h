@@ -90,7 +90,11 @@ constexpr int kSuperTiles = 32;
 // The walk is a chain of dependent memory round trips per wave, so narrower waves win where
 // the walk is long (SE3, 10^6 states), wider ones where the store is small and L2-resident.
 template <int SP>
-constexpr int group_queries() { return SP == OMPL_GPU_SPACE_SE3 ? 4 : 8; }  // measured (k-d tiles): SE3 G = 2 / 4 / 8 -> 2.04 / 1.41 / 1.73 ms; R^6 G = 4 / 8 -> 1.01 / 0.70 ms
+// queries per wave of the culled kNN walk.  Round 1 measured SE3 G = 2 / 4 / 8 -> 2.04 / 1.41 / 1.73
+// ms and R^6 G = 4 / 8 -> 1.01 / 0.70 ms; on round 4's walk (pipelined, packed keys, k-d
+// neighbourhood first) fewer queries per wave win: cfg3 G = 2 1.208-1.211 against 1.271 ms at
+// G = 4, cfg2 G = 4 0.552-0.557 against 0.655-0.658 ms at G = 8 (profiles/r4_ab)
+constexpr int group_queries() { return SP == OMPL_GPU_SPACE_SE3 ? 2 : 4; }
 // 16-bit fixed-point coding of an SE3 store's fp32 rows: code = rint((v - lo) * inv) clamped to
 // [0, kQ16Max], decoded as lo + code * step (step = 1 / inv); translation over the stored
 // states' box, quaternion components over [-1.001, 1.001].  0xFFFF in coordinate 0: NaN row.

@@ -2376,16 +2376,11 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     if constexpr (SP == OMPL_GPU_SPACE_SE3 || SP == OMPL_GPU_SPACE_REALVECTOR) {  // cull_supported
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
-            // SE3 with 64-lane lists (BIT*'s k = 57): 2 queries per wave — measured on cfg5k 4.08-4.14
-            // ms against 4.24-4.35 at G = 4 and 5.07-5.09 at G = 8 (A/B variant 14 keeps G = 8)
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 14
-            constexpr int G = (SP == OMPL_GPU_SPACE_SE3 && K2 == 64) ? 8 : group_queries<SP>();
-#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 15  // A/B: G = 2 for every SE3 list (cfg3)
-            constexpr int G = SP == OMPL_GPU_SPACE_SE3 ? 2 : group_queries<SP>();
-#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 16  // A/B: G = 4 for R^n (cfg2)
-            constexpr int G = (SP == OMPL_GPU_SPACE_SE3 && K2 == 64) ? 2 : 4;
+            // (BIT*'s 64-lane lists too: cfg5k G = 2 4.08-4.14 ms, 4 4.24-4.35, 8 5.07-5.09)
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 17  // A/B: G = 2 for R^n (cfg2)
+            constexpr int G = 2;
 #else
-            constexpr int G = (SP == OMPL_GPU_SPACE_SE3 && K2 == 64) ? 2 : group_queries<SP>();
+            constexpr int G = group_queries<SP>();
 #endif
             static const int recheck = [] {  // A/B switch of the popped super-tile re-check
                 const char *v = std::getenv("OMPL_GPU_SUPER_RECHECK");
@@ -2576,6 +2571,8 @@ constexpr int kRadiusGroup = 4;  // 10^7-state radius pass: G=2 2.37 ms, G=4 2.2
 // more queries (A/B build: OMPL_AMD_VARIANT 2 -> 8)
 #if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 2
 constexpr int kRadiusSlabGroup = 8;
+#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 18  // A/B: 2 queries per wave
+constexpr int kRadiusSlabGroup = 2;
 #else
 constexpr int kRadiusSlabGroup = 4;
 #endif

@@ -91,3 +91,12 @@ rc=$?; echo "chain positions: $(tail -1 "$out/pytest_pos.log")"; [ $rc = 0 ] || 
 bash tools/ab_env.sh cfg4pos "--workload cfg4" 2 - || exit 1
 bash tools/prof_workload.sh cfg4 r4_cfg4 || exit 1
 fi
+if [ "$P" = 13 ]; then  # R^n G = 2 (variant 17, cfg2); radius slab walk G = 2 (variant 18, cfg5)
+OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var17.so timeout -k 10 300 python -u -m pytest tests/test_gpu_nn.py tests/test_gpu_cull.py -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_g17.log" 2>&1
+rc=$?; echo "var17: $(tail -1 "$out/pytest_g17.log")"; rc_ok $rc var17
+OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var18.so timeout -k 10 300 python -u -m pytest tests/test_gpu_fullsize.py::test_cfg5_every_vertex_radius_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg5_radius_1e7_valid_samples tests/test_gpu_batch.py -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_g18.log" 2>&1
+rc=$?; echo "var18: $(tail -1 "$out/pytest_g18.log")"; rc_ok $rc var18
+bash tools/ab_env.sh cfg2g2 "--workload cfg2" 2 - VAR=17 || exit 1
+bash tools/ab_env.sh cfg5g2 "--workload cfg5" 2 - VAR=18 || exit 1
+bash tools/ab_env.sh cfg3g2 "--workload cfg3" 1 - || exit 1
+fi
