@@ -2377,6 +2377,12 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             // (BIT*'s 64-lane lists too: cfg5k G = 2 4.08-4.14 ms, 4 4.24-4.35, 8 5.07-5.09)
+            // (A/B variant 19: at least 8 waves per SIMD, i.e. <= 64 VGPRs, against the natural 67)
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 19
+            constexpr int kWalkMinWaves = 8;
+#else
+            constexpr int kWalkMinWaves = 1;
+#endif
 #if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 17  // A/B: G = 2 for R^n (cfg2)
             constexpr int G = 2;
 #else
@@ -2398,7 +2404,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
                 }
             }
             if (!q16)
-                hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true>), dim3((nq + G - 1) / G), dim3(64), 0,
+                hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, kWalkMinWaves, true>), dim3((nq + G - 1) / G), dim3(64), 0,
                                    st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
                                    ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters,
                                    kBulkThreshold, p.k2, recheck);
