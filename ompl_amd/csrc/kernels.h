@@ -93,8 +93,8 @@ template <int SP>
 // queries per wave of the culled kNN walk.  Round 1 measured SE3 G = 2 / 4 / 8 -> 2.04 / 1.41 / 1.73
 // ms and R^6 G = 4 / 8 -> 1.01 / 0.70 ms; on round 4's walk (pipelined, packed keys, k-d
 // neighbourhood first) fewer queries per wave win: cfg3 G = 2 1.208-1.211 against 1.271 ms at
-// G = 4, cfg2 G = 4 0.552-0.557 against 0.655-0.658 ms at G = 8 (profiles/r4_ab)
-constexpr int group_queries() { return SP == OMPL_GPU_SPACE_SE3 ? 2 : 4; }
+// G = 4, cfg2 G = 2 / 4 / 8 0.538-0.541 / 0.552-0.562 / 0.655-0.658 ms (profiles/r4_ab)
+constexpr int group_queries() { return 2; }
 // 16-bit fixed-point coding of an SE3 store's fp32 rows: code = rint((v - lo) * inv) clamped to
 // [0, kQ16Max], decoded as lo + code * step (step = 1 / inv); translation over the stored
 // states' box, quaternion components over [-1.001, 1.001].  0xFFFF in coordinate 0: NaN row.

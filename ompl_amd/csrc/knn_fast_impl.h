@@ -2383,11 +2383,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
 #else
             constexpr int kWalkMinWaves = 1;
 #endif
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 17  // A/B: G = 2 for R^n (cfg2)
-            constexpr int G = 2;
-#else
             constexpr int G = group_queries<SP>();
-#endif
             static const int recheck = [] {  // A/B switch of the popped super-tile re-check
                 const char *v = std::getenv("OMPL_GPU_SUPER_RECHECK");
                 return v ? std::atoi(v) : 1;

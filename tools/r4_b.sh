@@ -100,3 +100,12 @@ bash tools/ab_env.sh cfg2g2 "--workload cfg2" 2 - VAR=17 || exit 1
 bash tools/ab_env.sh cfg5g2 "--workload cfg5" 2 - VAR=18 || exit 1
 bash tools/ab_env.sh cfg3g2 "--workload cfg3" 1 - || exit 1
 fi
+if [ "$P" = 14 ]; then  # the SE3 walk held to 64 VGPRs (8 waves per SIMD, variant 19) on cfg3 and cfg5k; R^n G = 2 product on cfg2
+OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var19.so timeout -k 10 300 python -u -m pytest tests/test_gpu_nn.py tests/test_gpu_cull.py -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_g19.log" 2>&1
+rc=$?; echo "var19: $(tail -1 "$out/pytest_g19.log")"; rc_ok $rc var19
+timeout -k 10 300 python -u -m pytest tests/test_gpu_nn.py tests/test_gpu_cull.py tests/test_gpu_fullsize.py::test_cfg2_every_query_vs_exact_scan tests/test_gpu_fullsize.py::test_cfg2_reference_store_k10 -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_rv2.log" 2>&1
+rc=$?; echo "rv G=2: $(tail -1 "$out/pytest_rv2.log")"; [ $rc = 0 ] || exit 1
+bash tools/ab_env.sh cfg3w8 "--workload cfg3" 2 - VAR=19 || exit 1
+bash tools/ab_env.sh cfg5kw8 "--workload cfg5 --bitstar-knn" 1 - VAR=19 || exit 1
+bash tools/ab_env.sh cfg2p "--workload cfg2" 1 - || exit 1
+fi
