@@ -2384,6 +2384,10 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             constexpr int kWalkMinWaves = 1;
 #endif
             constexpr int G = group_queries<SP>();
+            static const int bulk = [] {  // A/B: candidates per ballot above which the bulk merge runs
+                const char *v = std::getenv("OMPL_GPU_BULK");
+                return v ? std::atoi(v) : kBulkThreshold;
+            }();
             static const int recheck = [] {  // A/B switch of the popped super-tile re-check
                 const char *v = std::getenv("OMPL_GPU_SUPER_RECHECK");
                 return v ? std::atoi(v) : 1;
@@ -2396,14 +2400,14 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
                     hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true, true>), dim3((nq + G - 1) / G),
                                        dim3(64), 0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox,
                                        ss->nsuper, ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi,
-                                       ss->counters, kBulkThreshold, p.k2, recheck, ss->rows16, ss->q16, knn_qerr);
+                                       ss->counters, bulk, p.k2, recheck, ss->rows16, ss->q16, knn_qerr);
                 }
             }
             if (!q16)
                 hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, kWalkMinWaves, true>), dim3((nq + G - 1) / G), dim3(64), 0,
                                    st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
                                    ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters,
-                                   kBulkThreshold, p.k2, recheck);
+                                   bulk, p.k2, recheck);
             timer_end(st);
             walked = true;
         }

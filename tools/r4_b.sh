@@ -109,3 +109,8 @@ bash tools/ab_env.sh cfg3w8 "--workload cfg3" 2 - VAR=19 || exit 1
 bash tools/ab_env.sh cfg5kw8 "--workload cfg5 --bitstar-knn" 1 - VAR=19 || exit 1
 bash tools/ab_env.sh cfg2p "--workload cfg2" 1 - || exit 1
 fi
+if [ "$P" = 15 ]; then  # the bulk-merge threshold of the group walk at G = 2
+bash tools/ab_env.sh cfg3bulk "--workload cfg3" 2 - OMPL_GPU_BULK=4 OMPL_GPU_BULK=16 || exit 1
+bash tools/ab_env.sh cfg5kbulk "--workload cfg5 --bitstar-knn" 1 - OMPL_GPU_BULK=4 OMPL_GPU_BULK=16 || exit 1
+bash tools/ab_env.sh cfg2bulk "--workload cfg2" 1 - OMPL_GPU_BULK=4 OMPL_GPU_BULK=16 || exit 1
+fi
