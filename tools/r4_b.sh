@@ -114,3 +114,7 @@ bash tools/ab_env.sh cfg3bulk "--workload cfg3" 2 - OMPL_GPU_BULK=4 OMPL_GPU_BUL
 bash tools/ab_env.sh cfg5kbulk "--workload cfg5 --bitstar-knn" 1 - OMPL_GPU_BULK=4 OMPL_GPU_BULK=16 || exit 1
 bash tools/ab_env.sh cfg2bulk "--workload cfg2" 1 - OMPL_GPU_BULK=4 OMPL_GPU_BULK=16 || exit 1
 fi
+if [ "$P" = 16 ]; then  # the bulk-merge threshold, wider
+bash tools/ab_env.sh cfg3bulk2 "--workload cfg3" 2 OMPL_GPU_BULK=16 OMPL_GPU_BULK=32 OMPL_GPU_BULK=64 || exit 1
+bash tools/ab_env.sh cfg5kbulk2 "--workload cfg5 --bitstar-knn" 1 OMPL_GPU_BULK=16 OMPL_GPU_BULK=32 OMPL_GPU_BULK=64 || exit 1
+fi
