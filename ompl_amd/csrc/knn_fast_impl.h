@@ -599,7 +599,9 @@ __device__ __forceinline__ void wave_merge_sorted_k(uint64_t &L, uint64_t c, int
 }
 // candidates in one ballot above which the bulk merge is used.  Measured (G = 4): SE3 1.58 /
 // 1.42 / 1.41 ms at 64 / 8 / 32; R^6 1.60 / 1.12 / 1.13 / 1.21 ms at 64 / 8 / 16 / 32
-constexpr int kBulkThreshold = 8;
+// At G = 2 (round 4): 4 / 8 / 16 / 32 / 64 -> cfg3 1.17-1.24 / 1.22-1.23 / 1.18-1.23 / 1.20-1.21 /
+// 1.29-1.30 ms, cfg5k 4.06 / 4.10 / 3.93-3.97 / 4.03 / 4.29 ms, cfg2 flat (profiles/r4_ab)
+constexpr int kBulkThreshold = 16;
 
 // Group-walk A/B features (variant builds, make variant VARIANT=n):
 //   WALK_CASCADE (7, 9, 12): square-root-free rejects before the chord and square roots;
