@@ -1100,7 +1100,11 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 // positions, chain_positions), and query g's K2-list lives across the wave (lane j = entry j).
 // The store is split in chunks along grid.y; the certificate merges the chunk lists.
 constexpr int kWaveGroup = 8;
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 20  // A/B: 4 queries per wave
+constexpr int kChainCullG = 4;
+#else
 constexpr int kChainCullG = 8;  // queries per wave of the culled chain scan
+#endif
 
 // ORD 0: links in the reference's order, the wave-wide exit tested after links 4 and 8; ORD 1:
 // outermost links first (|P_i(a) - P_i(b)| grows with i, so the partial sum nears the distance

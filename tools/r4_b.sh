@@ -118,3 +118,9 @@ if [ "$P" = 16 ]; then  # the bulk-merge threshold, wider
 bash tools/ab_env.sh cfg3bulk2 "--workload cfg3" 2 OMPL_GPU_BULK=16 OMPL_GPU_BULK=32 OMPL_GPU_BULK=64 || exit 1
 bash tools/ab_env.sh cfg5kbulk2 "--workload cfg5 --bitstar-knn" 1 OMPL_GPU_BULK=16 OMPL_GPU_BULK=32 OMPL_GPU_BULK=64 || exit 1
 fi
+if [ "$P" = 17 ]; then  # chain cull at 4 queries per wave (variant 20); the super-tile re-check at G = 2
+OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var20.so timeout -k 10 300 python -u -m pytest tests/test_gpu_prm.py tests/test_gpu_cull.py tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_g20.log" 2>&1
+rc=$?; echo "var20: $(tail -1 "$out/pytest_g20.log")"; rc_ok $rc var20
+bash tools/ab_env.sh cfg4g4 "--workload cfg4" 2 - VAR=20 || exit 1
+bash tools/ab_env.sh cfg3rc "--workload cfg3" 2 - OMPL_GPU_SUPER_RECHECK=0 || exit 1
+fi
