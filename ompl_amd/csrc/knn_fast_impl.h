@@ -1100,10 +1100,12 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 // positions, chain_positions), and query g's K2-list lives across the wave (lane j = entry j).
 // The store is split in chunks along grid.y; the certificate merges the chunk lists.
 constexpr int kWaveGroup = 8;
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 20  // A/B: 4 queries per wave
-constexpr int kChainCullG = 4;
+// queries per wave of the culled chain scan: 4 (57 VGPRs, 8 waves per SIMD) — measured on cfg4 step
+// 7.58-7.65 against 7.90-7.92 ms at 8 (73 VGPRs); A/B variant 20 keeps 8
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 20
+constexpr int kChainCullG = 8;
 #else
-constexpr int kChainCullG = 8;  // queries per wave of the culled chain scan
+constexpr int kChainCullG = 4;
 #endif
 
 // ORD 0: links in the reference's order, the wave-wide exit tested after links 4 and 8; ORD 1:
