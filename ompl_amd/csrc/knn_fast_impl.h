@@ -1104,6 +1104,8 @@ constexpr int kWaveGroup = 8;
 // 7.58-7.65 against 7.90-7.92 ms at 8 (73 VGPRs); A/B variant 20 keeps 8
 #if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 20
 constexpr int kChainCullG = 8;
+#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 21  // A/B: 2 queries per wave
+constexpr int kChainCullG = 2;
 #else
 constexpr int kChainCullG = 4;
 #endif

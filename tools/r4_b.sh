@@ -124,3 +124,8 @@ rc=$?; echo "var20: $(tail -1 "$out/pytest_g20.log")"; rc_ok $rc var20
 bash tools/ab_env.sh cfg4g4 "--workload cfg4" 2 - VAR=20 || exit 1
 bash tools/ab_env.sh cfg3rc "--workload cfg3" 2 - OMPL_GPU_SUPER_RECHECK=0 || exit 1
 fi
+if [ "$P" = 18 ]; then  # chain cull at 2 queries per wave (variant 21)
+OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var21.so timeout -k 10 300 python -u -m pytest tests/test_gpu_prm.py tests/test_gpu_cull.py tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_g21.log" 2>&1
+rc=$?; echo "var21: $(tail -1 "$out/pytest_g21.log")"; rc_ok $rc var21
+bash tools/ab_env.sh cfg4g2 "--workload cfg4" 2 - VAR=21 || exit 1
+fi
