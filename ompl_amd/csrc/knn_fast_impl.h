@@ -1101,7 +1101,8 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 // The store is split in chunks along grid.y; the certificate merges the chunk lists.
 constexpr int kWaveGroup = 8;
 // queries per wave of the culled chain scan: 4 (57 VGPRs, 8 waves per SIMD) — measured on cfg4 step
-// 7.58-7.65 against 7.90-7.92 ms at 8 (73 VGPRs); A/B variant 20 keeps 8
+// 7.58-7.65 against 7.90-7.92 ms at 8 (73 VGPRs) and a 5.55-5.60 ms kernel at 2 (against 4.50-4.53);
+// A/B variants 20 / 21 keep 8 / 2
 #if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 20
 constexpr int kChainCullG = 8;
 #elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 21  // A/B: 2 queries per wave
