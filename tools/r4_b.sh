@@ -129,3 +129,7 @@ OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var21.so timeout -k 10 300 python -u -m
 rc=$?; echo "var21: $(tail -1 "$out/pytest_g21.log")"; rc_ok $rc var21
 bash tools/ab_env.sh cfg4g2 "--workload cfg4" 2 - VAR=21 || exit 1
 fi
+if [ "$P" = 19 ]; then  # the popped super-tile re-check at G = 2, more reps
+bash tools/ab_env.sh cfg3rc2 "--workload cfg3" 3 - OMPL_GPU_SUPER_RECHECK=0 || exit 1
+bash tools/ab_env.sh cfg5krc "--workload cfg5 --bitstar-knn" 2 - OMPL_GPU_SUPER_RECHECK=0 || exit 1
+fi
