@@ -1319,7 +1319,13 @@ __global__ __launch_bounds__(256) void knn_chunk_merge_kernel(float *__restrict_
 // |code_i(s) - (P_i(q) + i + 1) S_i|, step_i = 1 / S_i.  Every quantity that decides what a list
 // keeps is this d16; the tile bounds stay on the fp32 boxes and are lowered by qerr
 // (chain_q16_error, >= |d16 - d32|), and the certificate's screen error grows by the same qerr.
+#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 22  // A/B: a wider pre-pass window
+constexpr int kChainTauTiles = 32;
+#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 23  // A/B: a narrower one
+constexpr int kChainTauTiles = 8;
+#else
 constexpr int kChainTauTiles = 16;
+#endif
 // PF (A/B, OMPL_GPU_CHAIN_PREFETCH=1; Q16 only): the next passing tile's 16-bit words are in
 // flight while the current tile is scanned.
 template <int F, int K2, int G, int MODE, bool Q16, bool PF = false>

@@ -133,3 +133,10 @@ if [ "$P" = 19 ]; then  # the popped super-tile re-check at G = 2, more reps
 bash tools/ab_env.sh cfg3rc2 "--workload cfg3" 3 - OMPL_GPU_SUPER_RECHECK=0 || exit 1
 bash tools/ab_env.sh cfg5krc "--workload cfg5 --bitstar-knn" 2 - OMPL_GPU_SUPER_RECHECK=0 || exit 1
 fi
+if [ "$P" = 20 ]; then  # the chain pre-pass window: 32 / 8 tiles (variants 22 / 23)
+for v in 22 23; do
+  OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_var$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_prm.py tests/test_gpu_fullsize.py::test_cfg4_every_milestone_vs_exact_scan -m gpu -x -q --timeout 200 --timeout-method thread > "$out/pytest_t$v.log" 2>&1
+  rc=$?; echo "var$v: $(tail -1 "$out/pytest_t$v.log")"; rc_ok $rc var$v
+done
+bash tools/ab_env.sh cfg4tw "--workload cfg4" 2 - VAR=22 VAR=23 || exit 1
+fi
