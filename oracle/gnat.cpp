@@ -234,15 +234,19 @@ struct oracle_gnat {
         *cnt = (uint32_t)heap.size();
     }
 
-    // Node::nearestR — :622-662 ; nearestRInternal — :358-376 (count only: the baseline leg)
-    uint64_t radiusCount(const double *q, double r, size_t &offset) const {
-        if (!root) return 0;
-        uint64_t hits = 0;
+    // Node::nearestR — :622-662 ; nearestRInternal — :358-376.  hit(d, id) is called for every
+    // element with d <= r (inclusive), in traversal order.
+    template <class Hit>
+    void radiusVisit(const double *q, double r, size_t &offset, Hit &&hit) const {
+        if (!root) return;
         std::priority_queue<NodeEntry, std::vector<NodeEntry>, NodeOrder> nq;
-        if (dist(q, root->pivot) <= r) ++hits;
+        const double d0 = dist(q, root->pivot);
+        if (d0 <= r) hit(d0, root->pivot);
         auto visit = [&](const Node *nd) {
-            for (uint32_t id : nd->data)
-                if (dist(q, id) <= r) ++hits;
+            for (uint32_t id : nd->data) {
+                const double d = dist(q, id);
+                if (d <= r) hit(d, id);
+            }
             if (nd->kids.empty()) return;
             const size_t sz = nd->kids.size(), off = offset++;
             double dp[64];
@@ -252,7 +256,7 @@ struct oracle_gnat {
                 if (perm[i] < 0) continue;
                 const Node *c = nd->kids[perm[i]];
                 dp[perm[i]] = dist(q, c->pivot);
-                if (dp[perm[i]] <= r) ++hits;
+                if (dp[perm[i]] <= r) hit(dp[perm[i]], c->pivot);
                 for (size_t j = 0; j < sz; ++j)
                     if (perm[j] >= 0 && i != j &&
                         (dp[perm[i]] - r > c->maxRange[perm[j]] || dp[perm[i]] + r < c->minRange[perm[j]]))
@@ -272,8 +276,22 @@ struct oracle_gnat {
             if (e.dist > e.node->maxRadius + r || e.dist < e.node->minRadius - r) continue;
             visit(e.node);
         }
+    }
+
+    uint64_t radiusCount(const double *q, double r, size_t &offset) const {
+        uint64_t hits = 0;
+        radiusVisit(q, r, offset, [&](double, uint32_t) { ++hits; });
         return hits;
     }
+
+    // nearestR's result list: sorted ascending (postprocessNearest, :379-384), ties by id
+    void radius(const double *q, double r, size_t &offset, std::vector<Cand> &out) const {
+        out.clear();
+        radiusVisit(q, r, offset, [&](double d, uint32_t id) { out.emplace_back(d, id); });
+        std::sort(out.begin(), out.end());
+    }
+
+    std::vector<std::vector<Cand>> radiusResults;  // oracle_gnat_radius -> oracle_gnat_radius_fetch
 };
 
 extern "C" {
@@ -371,6 +389,42 @@ uint64_t oracle_gnat_radius_count(const oracle_gnat *g, const double *q, size_t 
     uint64_t tot = 0;
     for (uint64_t v : part) tot += v;
     return tot;
+}
+
+// nearestR with the results: offsets[nq + 1] (CSR), returns the total; the ids / distances are
+// kept in the handle until oracle_gnat_radius_fetch copies them out (sorted by (distance, id))
+uint64_t oracle_gnat_radius(oracle_gnat *g, const double *q, size_t nq, double r, uint64_t *offsets, int nthreads) {
+    g->radiusResults.assign(nq, {});
+    auto work = [=](size_t b, size_t e) {
+        size_t offset = 0;
+        for (size_t i = b; i < e; ++i) g->radius(q + i * g->sp.dim, r, offset, g->radiusResults[i]);
+    };
+    if (nthreads <= 1) {
+        work(0, nq);
+    } else {
+        std::vector<std::thread> th;
+        const size_t per = (nq + nthreads - 1) / nthreads;
+        for (int t = 0; t < nthreads; ++t) {
+            size_t b = t * per, e = std::min(nq, b + per);
+            if (b < e) th.emplace_back(work, b, e);
+        }
+        for (auto &t : th) t.join();
+    }
+    offsets[0] = 0;
+    for (size_t i = 0; i < nq; ++i) offsets[i + 1] = offsets[i] + g->radiusResults[i].size();
+    return offsets[nq];
+}
+
+void oracle_gnat_radius_fetch(oracle_gnat *g, uint32_t *ids, double *dists) {
+    size_t at = 0;
+    for (auto &v : g->radiusResults) {
+        for (const Cand &c : v) {
+            ids[at] = c.second;
+            dists[at] = c.first;
+            ++at;
+        }
+    }
+    std::vector<std::vector<Cand>>().swap(g->radiusResults);
 }
 
 }  // extern "C"

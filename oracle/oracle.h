@@ -78,6 +78,11 @@ void oracle_gnat_knn(const oracle_gnat *g, const double *q, size_t nq, uint32_t 
                      double *dists, uint32_t *counts, int nthreads);
 uint64_t oracle_gnat_radius_count(const oracle_gnat *g, const double *q, size_t nq, double r,
                                   uint64_t *counts, int nthreads);
+/* nearestR with the results: CSR offsets[nq + 1], returns the total; the (distance, id)-sorted
+ * ids / distances stay in the handle until oracle_gnat_radius_fetch copies them out */
+uint64_t oracle_gnat_radius(oracle_gnat *g, const double *q, size_t nq, double r, uint64_t *offsets,
+                            int nthreads);
+void oracle_gnat_radius_fetch(oracle_gnat *g, uint32_t *ids, double *dists);
 /* multi-threaded motion checks (for the all-cores CPU baseline) */
 uint64_t oracle_check_motions_mt(const ompl_gpu_space *sp, const ompl_gpu_checker *ck, const double *s1,
                                  const double *s2, size_t m, uint8_t *valid, int nthreads);

@@ -41,6 +41,8 @@ _ORACLE_SIGS = {
     "oracle_gnat_size": (C.c_size_t, [C.c_void_p]),
     "oracle_gnat_knn": (None, [C.c_void_p, _D, C.c_size_t, C.c_uint32, _U32, _D, _U32, C.c_int]),
     "oracle_gnat_radius_count": (C.c_uint64, [C.c_void_p, _D, C.c_size_t, C.c_double, _U64, C.c_int]),
+    "oracle_gnat_radius": (C.c_uint64, [C.c_void_p, _D, C.c_size_t, C.c_double, _U64, C.c_int]),
+    "oracle_gnat_radius_fetch": (None, [C.c_void_p, _U32, _D]),
     "oracle_prm_causal": (None, [_SP, _CK, _D, C.c_size_t, C.c_double, C.c_uint32, _U32, _U32, _U8]),
     "oracle_mt19937_10000th": (C.c_uint32, []),
     "oracle_ranlux24_base_10000th": (C.c_uint32, []),
@@ -199,7 +201,7 @@ class Gnat:
         self._h = lib.oracle_gnat_create(C.byref(self._s), degree, min_degree, max_degree, leaf, seed)
 
     def __del__(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and lib is not None:  # lib is None at interpreter shutdown
             lib.oracle_gnat_destroy(self._h)
             self._h = None
 
@@ -226,6 +228,17 @@ class Gnat:
         tot = lib.oracle_gnat_radius_count(self._h, abi.dptr(q), q.shape[0], float(r), cnt.ctypes.data_as(_U64),
                                            int(nthreads))
         return cnt, int(tot)
+
+    def radius(self, queries, r, nthreads=1):
+        """nearestR: CSR (offsets [nq + 1], ids, distances), each segment sorted by (distance, id)."""
+        q = _arr(queries).reshape(-1, self.sp.dim)
+        off = np.zeros(q.shape[0] + 1, np.uint64)
+        tot = lib.oracle_gnat_radius(self._h, abi.dptr(q), q.shape[0], float(r), off.ctypes.data_as(_U64),
+                                     int(nthreads))
+        ids = np.zeros(max(int(tot), 1), np.uint32)
+        dist = np.zeros(max(int(tot), 1))
+        lib.oracle_gnat_radius_fetch(self._h, ids.ctypes.data_as(_U32), abi.dptr(dist))
+        return off, ids[:tot], dist[:tot]
 
 
 # ---- the reference's own NearestNeighborsLinear (built from /root/reference) ----

@@ -54,6 +54,21 @@ def assert_knn_parity(gi, gd, oi_ext, od_ext, k):
     return exact
 
 
+def assert_knn_parity_rows(gi, gd, oi_ext, od_ext, k):
+    """assert_knn_parity for large batches: distances vectorised, the per-row tie-class walk only
+    on the rows whose ids differ from the oracle's first k."""
+    gi, gd = np.asarray(gi, dtype=np.int64), np.asarray(gd)
+    oi_ext, od_ext = np.asarray(oi_ext, dtype=np.int64), np.asarray(od_ext)
+    exact = assert_dist_close(gd, od_ext[:, :k])
+    bad = np.flatnonzero(np.any(gi[:, :k] != oi_ext[:, :k], axis=1))
+    if len(bad):
+        assert_knn_parity(gi[bad], gd[bad], oi_ext[bad], od_ext[bad], k)
+    return exact, len(bad)
+
+
+CPU_THREADS = 16  # the GPU box's CPU share per GPU (the oracle's const queries run on this many threads)
+
+
 def oracle_knn_mt(O, sp, data, queries, k, threads=8):
     """The oracle's brute force over query slices on `threads` threads (ctypes drops the GIL),
     for parity checks at the configs' full store sizes."""

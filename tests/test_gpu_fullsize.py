@@ -1,108 +1,295 @@
-"""GPU parity at the benchmark configurations' full sizes, on the bench's own inputs (the
-reference RNG streams: RNG::setSeed(42), a tree sampler, then a query sampler), plus a device
-port of the reference's randomAccessPatternTest (tests/datastructures/nearestneighbors.cpp:208-287).
+"""GPU parity at the benchmark configurations' full sizes, on one bench step of each workload
+(bench.Runner: the reference RNG streams, RNG::setSeed(42), a tree sampler, then a query sampler),
+checked against the CPU oracle for EVERY query and EVERY edge of the step — the GNAT restatement
+(oracle/gnat.cpp, itself checked exact against brute force in test_oracle.py, as the reference's
+tests/datastructures/nearestneighbors.cpp:147-184 checks GNAT against Linear) and the oracle
+DiscreteMotionValidator (oracle/oracle.cpp, DiscreteMotionValidator.cpp:93-145).  No test here
+compares the library with itself.
 
-* cfg3: the 10^6-state SE(3) tree, 10^5 queries through the culled group walk
-  at k = 10, 128 of them checked against the oracle's brute force.
-* cfg2 (M1): the 10^5-state R^6 store, 10^5 queries through the culled group walk at k = 10,
-  128 of them checked against the oracle's brute force (bit-exact distances).
-* cfg5 (M4): the 10^7 valid-sample SE(3) set, 10^5 vertices through the radius walk at BIT*'s
-  r = 0.1528, 32 CSR segments checked against the oracle's brute force.
+* cfg3: 10^6-state SE(3) tree, 10^5 samples: every nearestK(k = 10) list, every
+  steered state (RRT.cpp:137-146) and every checkMotion bit / segment count.
+* cfg2 (M1): 10^5-state R^6 store, 10^5 queries, k = 10, bit-exact distances.
+* cfg4 (M3): PRM* on the 10^6-vertex KinematicChain roadmap, two causal 8,192-milestone batches
+  (the bench's step: 8 causal 1,024-row chunks, concurrent per-milestone cursors; the second batch
+  sees the first in the store's tail): every milestone's stored neighbours against GNAT, 96
+  milestones per batch in full against the sequential loop's list over roadmap + earlier
+  milestones (PRM.cpp:562-596, ConnectionStrategy.h:145-149), every edge's validity bit.
+* cfg5 (M4): 10^7 valid SE(3) samples, 10^5 vertices: every nearestR(r = 0.1528) segment and
+  every edge bit; BIT*'s kNN mode (k = 57) for every vertex and every edge bit.
+Also the device port of the reference's randomAccessPatternTest
+(tests/datastructures/nearestneighbors.cpp:208-287).
 """
+import argparse
 import math
 
 import numpy as np
 import pytest
 
 import pyoracle as O
-from ompl_amd import DiscreteMotionValidatorGPU, NearestNeighborsGPU
-from ompl_amd import workloads as W
-from ompl_amd.checkers import SpheresChecker
+from ompl_amd import NearestNeighborsGPU
 from ompl_amd.spaces import SE3StateSpace
-from parity import assert_dist_close, assert_knn_parity, oracle_knn_mt
+from parity import CPU_THREADS, assert_dist_close, assert_knn_parity_rows, dist_tol
 
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_radius_mt(sp, data, queries, r, threads=8):
-    from concurrent.futures import ThreadPoolExecutor
+def _run_steps(workload, steps=1, bitstar_knn=False, queries=None):
+    """one bench.Runner of `workload` at its bench defaults; `steps` steps, each step's device
+    outputs copied to the host"""
+    import torch
 
-    parts = np.array_split(np.arange(len(queries)), min(threads, len(queries)))
-    with ThreadPoolExecutor(len(parts)) as ex:
-        res = list(ex.map(lambda ix: O.radius(sp, data, queries[ix], r), parts))
-    segs = []
-    for off, ids, d in res:
-        for q in range(len(off) - 1):
-            segs.append((ids[int(off[q]):int(off[q + 1])], d[int(off[q]):int(off[q + 1])]))
-    return segs
-
-
-def test_cfg3_reference_tree_k10(gpu):
     import bench
 
-    sp = SE3StateSpace(0.0, 1.0)
-    tree, q = bench.reference_inputs(sp, 1_000_000, 100_000, 0)
+    t, q, k = bench.DEFAULTS[workload]
+    a = argparse.Namespace(workload=workload, tree=t, queries=queries or q, k=k, exact=False,
+                           partition="replicated", warmup=0, steps=steps, bitstar_knn=bitstar_knn)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    run = bench.Runner(a, torch, dev, 0, 0, stream)
+    run.stream = stream
+    outs = []
+    for _ in range(steps):
+        run.step()
+        torch.cuda.synchronize(dev)
+        o = {"m": run.m}
+        for name in ("ids", "dd", "s_from", "s_to", "valid", "off", "cnt", "evalid"):
+            if hasattr(run, name):
+                o[name] = getattr(run, name).cpu().numpy()
+        outs.append(o)
+    return run, outs
+
+
+def _gnat(sp, data):
+    g = O.Gnat(sp)
+    g.add(data, bulk=True)
+    return g
+
+
+def _check_edges(sp, ck, s1, s2, valid):
+    """every edge's checkMotion bit against the oracle validator on the same endpoints"""
+    ov = O.check_motions_mt(sp, ck, s1, s2, CPU_THREADS)
+    bad = np.flatnonzero(ov != valid.astype(bool))
+    assert len(bad) == 0, f"{len(bad)} of {len(s1)} edges differ from the oracle (first {bad[:8]})"
+    return float(ov.mean())
+
+
+# ---- cfg3 --------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def cfg3(gpu):
+    run, (o,) = _run_steps("cfg3")
+    out = dict(sp=run.sp, ck=run.ck, tree=run.tree, q=run.q_host, maxd=run.maxd, **o)
+    run.close()
+    return out
+
+
+def test_cfg3_every_query_vs_gnat(cfg3):
+    """all 10^5 nearestK(k = 10) lists of the headline step against GNAT (k + 4 exposes the k-th
+    rank's tie class)"""
+    c = cfg3
+    g = _gnat(c["sp"], c["tree"])
+    oi, od, oc = g.knn(c["q"], 14, CPU_THREADS)
+    assert (oc == 14).all()
+    assert_knn_parity_rows(c["ids"], c["dd"], oi, od, 10)
+
+
+def test_cfg3_every_edge_vs_oracle(cfg3):
+    """the step's 10^5 motions: from = the nearest stored state; to = the sample, or
+    interpolate(nearest, sample, maxDistance / d) when d > maxDistance (RRT.cpp:141-146), within
+    4 ulps of the oracle's interpolation (bit-exact translation); every validity bit and
+    validSegmentCount equal to the oracle validator's on the same endpoints"""
+    c = cfg3
+    sp, nq = c["sp"], len(c["q"])
+    near = c["ids"][:, 0].astype(np.int64)
+    np.testing.assert_array_equal(c["s_from"][:nq], c["tree"][near])
+    d = c["dd"][:, 0]
+    far = np.flatnonzero(d > c["maxd"])
+    want = c["q"].copy()
+    for i in far:
+        want[i] = O.interpolate(sp, c["tree"][near[i]], c["q"][i], c["maxd"] / d[i])
+    got = c["s_to"][:nq]
+    np.testing.assert_array_equal(got[:, :3], want[:, :3])
+    assert np.all(np.abs(got - want) <= dist_tol(want)), "steered rotations beyond 4 ulps"
+    ov, ond, _, _ = O.check_motions(sp, c["ck"], c["s_from"][:nq], got)
+    np.testing.assert_array_equal(c["valid"][:nq].astype(bool), ov)
+    _check_edges(sp, c["ck"], c["s_from"][:nq], got, c["valid"][:nq])
+
+
+# ---- cfg2 --------------------------------------------------------------------------------------
+def test_cfg2_every_query_vs_gnat(gpu):
+    """all 10^5 nearestK(k = 10) lists of the R^6 step against GNAT, bit-exact distances (the R^n
+    metric is exact in the reference's operation order)"""
+    run, (o,) = _run_steps("cfg2")
+    g = _gnat(run.sp, run.tree)
+    oi, od, _ = g.knn(run.q_host, 14, CPU_THREADS)
+    np.testing.assert_array_equal(o["dd"], od[:, :10])
+    assert_knn_parity_rows(o["ids"], o["dd"], oi, od, 10)
+    assert bool(np.all(np.diff(o["dd"], axis=1) >= 0))
+    run.close()
+
+
+# ---- cfg4: PRM* causal batches at the bench's size ---------------------------------------------
+@pytest.fixture(scope="module")
+def cfg4(gpu):
+    run, outs = _run_steps("cfg4", steps=2)
+    assert len(run.milestones) == 2 and all(len(b) == 8192 for b in run.milestones)
+    out = dict(sp=run.sp, ck=run.ck, kc=run.kc, roadmap=run.tree, batches=run.milestones, outs=outs,
+               k_cap=run.k)
+    run.close()
+    out["gnat"] = _gnat(out["sp"], out["roadmap"])
+    return out
+
+
+def _cfg4_batch(c, b):
+    """batch b (0 or 1) of the cfg4 run against the sequential PRM* loop"""
+    sp, n0 = c["sp"], len(c["roadmap"])
+    x = c["batches"][b]
+    m = len(x)
+    earlier = np.concatenate([c["batches"][i] for i in range(b)] + [np.empty((0, sp.dim))])
+    base = n0 + len(earlier)  # id of the batch's first milestone
+    o = c["outs"][b]
+    nbr, cnt, val = o["ids"].view(np.uint32).astype(np.int64), o["cnt"].astype(np.int64), o["evalid"].astype(bool)
+    kj = np.array([int(math.ceil(c["kc"] * math.log(base + j + 1))) for j in range(m)])
+    np.testing.assert_array_equal(cnt, np.minimum(kj, base + np.arange(m)))
+    # every milestone: the stored roadmap entries of its list are GNAT's first entries, in order
+    kg = int(kj.max())
+    gi, gd, _ = c["gnat"].knn(x, kg, CPU_THREADS)
+    allst = np.concatenate([c["roadmap"], earlier, x])
+    for j in range(m):
+        row = nbr[j, :cnt[j]]
+        st = row[row < n0]
+        np.testing.assert_array_equal(st, gi[j, :len(st)].astype(np.int64), err_msg=f"milestone {base + j}")
+    # sampled milestones in full: roadmap (GNAT) + every earlier milestone (brute force), merged by
+    # (distance, id), first k_j — includes the causal chunk boundaries (1,024-row chunks)
+    pick = sorted(set([0, 1, 2, 63, 64, 1023, 1024, 1025, 2047, 2048, 4095, 4096, 6143, 8190, 8191])
+                  | set(np.random.default_rng(50 + b).choice(m, 81, replace=False).tolist()))
+    for j in pick:
+        prev = np.concatenate([earlier, x[:j]])
+        ci, cd = gi[j].astype(np.int64), gd[j]
+        if len(prev):
+            pi, pd, pc = O.knn(sp, prev, x[j][None], int(kj[j]))
+            ci = np.concatenate([ci, pi[0, :pc[0]].astype(np.int64) + n0])
+            cd = np.concatenate([cd, pd[0, :pc[0]]])
+        order = np.lexsort((ci, cd))[: kj[j]]
+        want = ci[order]
+        np.testing.assert_array_equal(nbr[j, :cnt[j]], want, err_msg=f"milestone {base + j}")
+        # the distances behind that order, from the oracle metric
+        dd = np.array([O.distance(sp, allst[i], x[j]) for i in want])
+        np.testing.assert_array_equal(dd, cd[order])
+    # every edge: checkMotion(state[neighbour], state[milestone]) (PRM.cpp:582)
+    live = np.arange(nbr.shape[1])[None, :] < cnt[:, None]
+    s1 = allst[nbr[live]]
+    s2 = np.repeat(x, cnt, axis=0)
+    frac = _check_edges(sp, c["ck"], s1, s2, val[live])
+    assert 0.0 < frac < 1.0
+    return int(live.sum())
+
+
+def test_cfg4_prm_batch_1_vs_sequential_loop(cfg4):
+    """the first 8,192-milestone batch over the 10^6-vertex roadmap (8 causal chunks)"""
+    assert _cfg4_batch(cfg4, 0) > 8192 * 30
+
+
+def test_cfg4_prm_batch_2_tail_vs_sequential_loop(cfg4):
+    """the second batch: the first batch's milestones are stored in the culled store's tail"""
+    assert _cfg4_batch(cfg4, 1) > 8192 * 30
+
+
+def test_cfg4_chain_store_after_removals(cfg4, gpu):
+    """the culled chain scan after a tail append and 500 removals, 64 milestones against the
+    oracle's brute force over the live states (bit-exact chain distances)"""
+    from parity import oracle_knn_mt
+
+    c = cfg4
+    sp = c["sp"]
     nn = NearestNeighborsGPU(sp, gpu)
-    nn.add(tree)
+    nn.add(c["roadmap"])
+    nn.add(c["batches"][0])
+    gone = np.random.default_rng(6).choice(len(c["roadmap"]), 500, replace=False)
+    for i in gone:
+        nn.remove(int(i))
+    q2 = c["batches"][1]
     before = nn.cull_stats()[2]
-    ids, d, cnt = nn.nearestKBatch(q, 10)
-    assert nn.cull_stats()[2] > before, "the batch did not take the culled group walk"
-    assert (cnt == 10).all()
-    pick = np.concatenate([np.arange(64), np.random.default_rng(3).choice(np.arange(64, len(q)), 64, replace=False)])
-    oi, od = oracle_knn_mt(O, sp, tree, q[pick], 16)
-    assert_knn_parity(ids[pick], d[pick], oi, od, 10)
+    ids2, d2, _ = nn.nearestKBatch(q2, 41)
+    assert nn.cull_stats()[2] > before, "the batch did not take the culled chain scan"
+    keep = np.ones(len(c["roadmap"]) + len(c["batches"][0]), dtype=bool)
+    keep[gone] = False
+    store = np.concatenate([c["roadmap"], c["batches"][0]])
+    live_ids = np.flatnonzero(keep)
+    pick2 = np.random.default_rng(7).choice(len(q2), 64, replace=False)
+    oi2, od2 = oracle_knn_mt(O, sp, store[live_ids], q2[pick2], 41, CPU_THREADS)
+    np.testing.assert_array_equal(d2[pick2], od2)
+    np.testing.assert_array_equal(ids2[pick2].astype(np.int64), live_ids[oi2.astype(np.int64)])
     nn.close()
 
 
-def test_cfg2_reference_store_k10(gpu):
-    """cfg2: RealVectorStateSpace(6) over [0,1]^6, the bench's reference-stream
-    10^5-state store and 10^5 queries, nearestK(k = 10) through the culled group walk; 128 queries
-    (the first 64 and 64 random) against the oracle's brute force: identical ids (ties aside) and
-    bit-identical fp64 distances (the R^n metric is exact in the reference's operation order)."""
+# ---- cfg5: BIT* batches over 10^7 valid samples -------------------------------------------------
+def _assert_csr_ties(off, ids, oids, od):
+    """equal CSR ids, except that inside a segment two ids may trade places when their oracle
+    distances are within 4 ulps of each other (a tie class: the device acos may differ from
+    glibc's by an ulp)"""
+    bad = np.flatnonzero(ids != oids)
+    if not len(bad):
+        return
+    seg = np.searchsorted(off.astype(np.int64), bad, side="right") - 1
+    for q in np.unique(seg):
+        a, b = int(off[q]), int(off[q + 1])
+        assert sorted(ids[a:b].tolist()) == sorted(oids[a:b].tolist()), f"segment {q}: different neighbour sets"
+        pos = {int(i): a + j for j, i in enumerate(oids[a:b])}
+        for p in bad[seg == q]:
+            o = pos[int(ids[p])]  # where the oracle has the device's id of position p
+            assert abs(od[o] - od[p]) <= 2 * dist_tol(od[p]), f"segment {q}: ids out of order beyond a tie"
+
+
+@pytest.fixture(scope="module")
+def cfg5_gnat(gpu):
     import bench
-    from ompl_amd.spaces import RealVectorStateSpace
-
-    sp = RealVectorStateSpace(6)
-    tree, q = bench.reference_inputs(sp, 100_000, 100_000, 0)
-    nn = NearestNeighborsGPU(sp, gpu)
-    nn.add(tree)
-    before = nn.cull_stats()[2]
-    ids, d, cnt = nn.nearestKBatch(q, 10)
-    assert nn.cull_stats()[2] > before, "the batch did not take the culled group walk"
-    assert (cnt == 10).all()
-    pick = np.concatenate([np.arange(64), np.random.default_rng(8).choice(np.arange(64, len(q)), 64, replace=False)])
-    oi, od = oracle_knn_mt(O, sp, tree, q[pick], 16)
-    np.testing.assert_array_equal(d[pick], od[:, :10])
-    assert_knn_parity(ids[pick], d[pick], oi, od, 10)
-    assert bool(np.all(np.diff(d, axis=1) >= 0)), "every list sorted ascending"
-    nn.close()
-
-
-def test_cfg5_radius_1e7_valid_samples(gpu):
-    import bench
+    from ompl_amd import DiscreteMotionValidatorGPU
+    from ompl_amd import workloads as W
+    from ompl_amd.checkers import SpheresChecker
 
     sp = SE3StateSpace(0.0, 1.0)
     c, rr = W.sphere_field(32, 0.1, 7)
     mv = DiscreteMotionValidatorGPU(sp, SpheresChecker(c, rr), gpu)
-    tree, q = bench.reference_inputs(sp, 10_000_000, 100_000, 0, valid=mv.isValid)
-    r = W.bitstar_radius(len(tree), 6, math.pi ** 2)
-    assert abs(r - 0.1528) < 5e-4
-    nn = NearestNeighborsGPU(sp, gpu)
-    nn.add(tree)
-    off, ids, d = nn.nearestRBatch(q, r)
-    assert int(off[-1]) > 10 * len(q)  # ~10.8 neighbours per vertex at this radius
-    pick = np.concatenate([np.arange(16), np.random.default_rng(4).choice(np.arange(16, len(q)), 16, replace=False)])
-    segs = _oracle_radius_mt(sp, tree, q[pick], r)
-    for j, qi in enumerate(pick):
-        gi, gd = ids[int(off[qi]):int(off[qi + 1])], d[int(off[qi]):int(off[qi + 1])]
-        oi, od = segs[j]
-        assert len(gi) == len(oi), f"query {qi}: {len(gi)} vs {len(oi)} neighbours"
-        assert np.array_equal(gi.astype(np.int64), oi.astype(np.int64)), f"query {qi}: ids differ"
-        assert_dist_close(gd, od)
-    nn.close()
+    key = ("cfg5", 10_000_000, 100_000)
+    tree, _ = bench.shared_inputs("cfg5", sp, key[1], key[2], mv.isValid, None, None)
     mv.close()
+    return _gnat(sp, tree)
 
 
+def test_cfg5_radius_every_vertex_vs_gnat(cfg5_gnat):
+    """all 10^5 nearestR(r = 0.1528) segments of the BIT* step (offsets, ids, distances) and
+    every edge's checkMotion(vertex, sample) bit"""
+    run, (o,) = _run_steps("cfg5")
+    assert abs(run.radius - 0.1528) < 5e-4
+    q = run.q_host
+    off, ids, d = o["off"].astype(np.uint64), o["ids"][: o["m"]].astype(np.int64), o["dd"][: o["m"]]
+    goff, gids, gd = cfg5_gnat.radius(q, run.radius, CPU_THREADS)
+    np.testing.assert_array_equal(off, goff)
+    assert int(off[-1]) > 10 * len(q)  # ~10.8 neighbours per vertex at this radius
+    assert_dist_close(d, gd)
+    _assert_csr_ties(off, ids, gids.astype(np.int64), gd)
+    s1 = np.repeat(q, np.diff(off).astype(np.int64), axis=0)
+    np.testing.assert_array_equal(o["s_from"][: o["m"]], s1)
+    np.testing.assert_array_equal(o["s_to"][: o["m"]], run.tree[ids])
+    _check_edges(run.sp, run.ck, s1, run.tree[ids], o["valid"][: o["m"]])
+    run.close()
+
+
+def test_cfg5_knn_every_vertex_vs_gnat(cfg5_gnat):
+    """BIT*'s kNN mode (k = 57): all 10^5 lists and every edge's checkMotion(vertex, sample) bit"""
+    run, (o,) = _run_steps("cfg5", bitstar_knn=True)
+    k = run.k
+    assert k == 57
+    oi, od, _ = cfg5_gnat.knn(run.q_host, k + 4, CPU_THREADS)
+    assert_knn_parity_rows(o["ids"], o["dd"], oi, od, k)
+    ids = o["ids"].astype(np.int64).reshape(-1)
+    s1 = np.repeat(run.q_host, k, axis=0)
+    np.testing.assert_array_equal(o["s_to"][: o["m"]], run.tree[ids])
+    _check_edges(run.sp, run.ck, s1, run.tree[ids], o["valid"][: o["m"]])
+    run.close()
+
+
+# ---- the reference's randomAccessPatternTest on the device ------------------------------------
 def test_random_access_pattern(gpu):
     """randomAccessPatternTest (nearestneighbors.cpp:208-287) on SE(3) [0,1]^3: m = 200 rounds of
     n = 10 adds, n queries each with nearestK(k uniform in [1, maxk = 30]) and nearestR(r uniform in
@@ -112,6 +299,7 @@ def test_random_access_pattern(gpu):
     (size and list checked).  Each round also answers its queries as one batch of 64, so the
     culled walk sees the same interleaving of adds, removals and index rebuilds."""
     from ompl_amd import sampling as S
+    from parity import assert_knn_parity
 
     sp = SE3StateSpace(0.0, 1.0)
     S.set_seed(42)
@@ -158,119 +346,3 @@ def test_random_access_pattern(gpu):
     builds, appends = nn.index_stats()
     assert builds >= 2 and appends >= 1  # removals forced rebuilds; adds went to the tail
     nn.close()
-
-
-def test_cfg4_chain_culled_scan_1e6(gpu):
-    """cfg4: PRM*'s stored-part kNN on the KinematicChain space at the bench's
-    size — 10^6 reference-stream states, k = 41 (ConnectionStrategy.h:145-149) — through the
-    culled chain scan over the k-d sorted joint-position store; 64 of 8,192 milestones checked
-    against the oracle's brute force, then again after a tail append (a PRM* batch's 8,192 new
-    milestones) and 500 removals."""
-    import bench
-    from ompl_amd.spaces import KinematicChainSpace
-
-    sp = KinematicChainSpace(12, 1.0 / 12)
-    tree, q = bench.reference_inputs(sp, 1_000_000, 8_192, 0)
-    nn = NearestNeighborsGPU(sp, gpu)
-    nn.add(tree)
-    before = nn.cull_stats()[2]
-    ids, d, cnt = nn.nearestKBatch(q, 41)
-    assert nn.cull_stats()[2] > before, "the batch did not take the culled chain scan"
-    assert (cnt == 41).all()
-    pick = np.random.default_rng(5).choice(len(q), 64, replace=False)
-    oi, od = oracle_knn_mt(O, sp, tree, q[pick], 41)
-    np.testing.assert_array_equal(d[pick], od)  # the chain metric is bit-exact (fp64, reference order)
-    np.testing.assert_array_equal(ids[pick].astype(np.int64), oi.astype(np.int64))
-    # a PRM* batch later: the milestones join the store (tail tiles), some states go away
-    nn.add(q)
-    gone = np.random.default_rng(6).choice(len(tree), 500, replace=False)
-    for i in gone:
-        nn.remove(int(i))
-    q2 = bench.reference_inputs(sp, 0, 2 * 8_192, 0)[1][8_192:]
-    ids2, d2, _ = nn.nearestKBatch(q2, 41)
-    keep = np.ones(len(tree) + len(q), dtype=bool)
-    keep[gone] = False
-    store = np.concatenate([tree, q])
-    live_ids = np.flatnonzero(keep)
-    pick2 = np.random.default_rng(7).choice(len(q2), 64, replace=False)
-    oi2, od2 = oracle_knn_mt(O, sp, store[live_ids], q2[pick2], 41)
-    np.testing.assert_array_equal(d2[pick2], od2)
-    np.testing.assert_array_equal(ids2[pick2].astype(np.int64), live_ids[oi2.astype(np.int64)])
-    nn.close()
-
-
-# ---- every query at full size: the culled paths against the exact fp64 scan -------------------
-# The oracle checks above sample queries (the CPU brute force over 10^6-10^7 states is slow); here
-# every query of the bench batch is compared with the library's exact fp64 brute-force scan
-# (set_exact: no fp32 screen, no culling — itself pinned against the oracle by test_gpu_nn.py on
-# every space), bit for bit: ids and distances.
-def _culled_vs_exact(sp, tree, q, k, gpu):
-    nn = NearestNeighborsGPU(sp, gpu)
-    nn.add(tree)
-    ids, d, cnt = nn.nearestKBatch(q, k)
-    nn.set_exact(True)
-    ei, ed, ecnt = nn.nearestKBatch(q, k)
-    nn.close()
-    np.testing.assert_array_equal(cnt, ecnt)
-    np.testing.assert_array_equal(d, ed)
-    np.testing.assert_array_equal(ids, ei)
-
-
-def test_cfg3_every_query_vs_exact_scan(gpu):
-    import bench
-
-    sp = SE3StateSpace(0.0, 1.0)
-    tree, q = bench.reference_inputs(sp, 1_000_000, 100_000, 0)
-    _culled_vs_exact(sp, tree, q, 10, gpu)
-
-
-def test_cfg2_every_query_vs_exact_scan(gpu):
-    import bench
-    from ompl_amd.spaces import RealVectorStateSpace
-
-    sp = RealVectorStateSpace(6)
-    tree, q = bench.reference_inputs(sp, 100_000, 100_000, 0)
-    _culled_vs_exact(sp, tree, q, 10, gpu)
-
-
-def test_cfg4_every_milestone_vs_exact_scan(gpu):
-    import bench
-    from ompl_amd.spaces import KinematicChainSpace
-
-    sp = KinematicChainSpace(12, 1.0 / 12)
-    tree, q = bench.reference_inputs(sp, 1_000_000, 8_192, 0)
-    _culled_vs_exact(sp, tree, q, 41, gpu)
-
-
-def test_cfg5k_every_vertex_vs_exact_scan(gpu):
-    """BIT*'s kNN mode at its k = 57 on the 10^7 valid-sample set, 10^4 vertices."""
-    import bench
-
-    sp = SE3StateSpace(0.0, 1.0)
-    c, rr = W.sphere_field(32, 0.1, 7)
-    mv = DiscreteMotionValidatorGPU(sp, SpheresChecker(c, rr), gpu)
-    tree, q = bench.reference_inputs(sp, 10_000_000, 10_000, 0, valid=mv.isValid)
-    mv.close()
-    _culled_vs_exact(sp, tree, q, 57, gpu)
-
-
-def test_cfg5_every_vertex_radius_vs_exact_scan(gpu):
-    """BIT*'s radius mode (r = 0.1528) on the 10^7 valid-sample set, 2 x 10^4 vertices: the slab
-    walk's CSR equals the exact fp64 scan's, offsets, ids and distances."""
-    import bench
-
-    sp = SE3StateSpace(0.0, 1.0)
-    c, rr = W.sphere_field(32, 0.1, 7)
-    mv = DiscreteMotionValidatorGPU(sp, SpheresChecker(c, rr), gpu)
-    tree, q = bench.reference_inputs(sp, 10_000_000, 20_000, 0, valid=mv.isValid)
-    mv.close()
-    r = W.bitstar_radius(len(tree), 6, math.pi ** 2)
-    nn = NearestNeighborsGPU(sp, gpu)
-    nn.add(tree)
-    off, ids, d = nn.nearestRBatch(q, r)
-    nn.set_exact(True)
-    eoff, eids, ed = nn.nearestRBatch(q, r)
-    nn.close()
-    np.testing.assert_array_equal(off, eoff)
-    np.testing.assert_array_equal(ids, eids)
-    np.testing.assert_array_equal(d, ed)

@@ -53,6 +53,19 @@ def test_prm_star_se3_spheres(gpu):
     assert cnt[0] == 0 and cnt[-1] == math.ceil((math.e + math.e / 6) * math.log(3000))
 
 
+def test_prm_star_long_segments(gpu):
+    """A first batch of 1,500 milestones on an empty roadmap: milestone j's stored list is empty,
+    so every earlier milestone is an in-batch candidate and the longest segment (1,499 entries)
+    exceeds the LDS rank sort's 1,024 (kernels.h kRankSortMax) — the two stable radix passes sort
+    the segments instead; then a second batch over the stored 1,500."""
+    sp = SE3StateSpace()
+    c, r = W.sphere_field(32, 0.1, 7)
+    ck = SpheresChecker(c, r)
+    states, _ = W.reference_valid_states(sp, 2000, lambda x: O.is_valid(sp, ck, x), seed=9, chunk=6000)
+    cnt = _run(sp, ck, states, (1500, 500), gpu)
+    assert cnt[1499] == math.ceil((math.e + math.e / 6) * math.log(1500))
+
+
 def test_prm_star_kinematic_chain(gpu):
     sp = KinematicChainSpace(12, 1.0 / 12)  # KinematicChainBenchmark.cpp:48-49
     ck = KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))

@@ -5,8 +5,8 @@ getMotionStates kernels use), not only on the oracle (test_oracle.py):
   StateSpaceTest::testDistance / testInterpolation   tests/base/StateSpaceTest.h:72-116
       (n = 1000 random pairs, eps = 1e-12 as SO3_Simple / RealVector_Simple pass it,
        tests/base/state_spaces.cpp:203, :278)
-  SO3_Simple: extent pi/2, getMotionStates(s1, s2, 100, endpoints) -> 102 states of unit norm
-      within 1e-15                                   tests/base/state_spaces.cpp:197-240
+  SO3_Simple: extent pi/2, getMotionStates(s1, s2, 100, endpoints) -> 102 states whose
+      SO3StateSpace::norm is within 1e-15 of 1                                  tests/base/state_spaces.cpp:197-240
   RealVector_Simple: d(s0, s0) = 0, interpolate(s0, s0, 0.6) = s0, interpolate(s0, (0,0,1), 0.5)[2] = 0.5
                                                      tests/base/state_spaces.cpp:266-300
 
@@ -112,8 +112,13 @@ def test_so3_simple_known_answers(gpu):
     assert ms.shape == (32, 102, 4)
     np.testing.assert_array_equal(ms[:, 0], s[:32])
     np.testing.assert_array_equal(ms[:, -1], s[32:])
-    nrm = np.sqrt(np.sum(ms * ms, axis=2))
-    assert np.all(np.abs(nrm - 1.0) <= 1e-15 * 4)   # norm() of the state, reference eps 1e-15 (+ our sqrt rounding)
+    # SO3StateSpace::norm (SO3StateSpace.cpp:177-181): quaternionNormSquared x*x + y*y + z*z + w*w
+    # (:80-83, left to right, no fused multiply-add), its square root only when it differs from 1
+    # by more than DBL_EPSILON; BOOST_OMPL_EXPECT_NEAR(nrm, 1.0, 1e-15) = |nrm - 1| < 1e-15
+    x, y, z, w = ms[..., 0], ms[..., 1], ms[..., 2], ms[..., 3]
+    sq = ((x * x + y * y) + z * z) + w * w
+    nrm = np.where(np.abs(sq - 1.0) > np.finfo(np.float64).eps, np.sqrt(sq), 1.0)
+    assert np.all(np.abs(nrm - 1.0) < 1e-15)
 
 
 def test_realvector_simple_known_answers(gpu):
