@@ -2,8 +2,10 @@
 // IEEE fp64 with the reference's operation order.  Every function is __host__ __device__:
 // the library's host side runs the same code (StateValidityCheckerGPU's single-state isValid,
 // the distance the NN plugin's verify mode compares against), so host and device agree bit for
-// bit wherever no libm call is involved (the device math library may differ from glibc by an
-// ulp in cos / sin / acos).  This translation unit is
+// bit.  The KinematicChain's cos / sin are glibc's own algorithm (glibc_sincos.h: the device math
+// library differs from glibc by an ulp on 3 % of the arguments, enough to flip validity bits and
+// segment counts at the chain's knife edges); SO3's acos is the device library's (<= 1 ulp from
+// glibc: SO3 / SE3 distances are compared within 4 ulps).  This translation unit is
 // compiled with -ffp-contract=off: no multiply-add is fused, matching the
 // reference x86-64 build (CMakeModules/CompilerSettings.cmake:8, no -march).
 //
@@ -19,6 +21,7 @@
 #include <stdint.h>
 
 #include "../../include/ompl_gpu.h"
+#include "glibc_sincos.h"
 
 namespace ompl_amd {
 
@@ -85,8 +88,11 @@ __host__ __device__ __forceinline__ double chain_dist_raw(const double *a, const
     for (int i = 0; i < n; ++i) {
         th1 += a[i];
         th2 += b[i];
-        dx += cos(th1) - cos(th2);
-        dy += sin(th1) - sin(th2);
+        double s1, c1, s2, c2;
+        glibc_sincos(th1, s1, c1);
+        glibc_sincos(th2, s2, c2);
+        dx += c1 - c2;
+        dy += s1 - s2;
         dist += sqrt(dx * dx + dy * dy);
     }
     return dist * link;
@@ -136,9 +142,9 @@ __host__ __device__ __forceinline__ void lerp(const double *f, const double *t_,
 __host__ __device__ inline void slerp(const double *f, const double *to, double t, double *o) {
     double theta = so3_arc(f, to);
     if (theta > kDblEps) {
-        double d = 1.0 / sin(theta);
-        double s0 = sin((1.0 - t) * theta);
-        double s1 = sin(t * theta);
+        double d = 1.0 / glibc_sin(theta);
+        double s0 = glibc_sin((1.0 - t) * theta);
+        double s1 = glibc_sin(t * theta);
         double dq = f[0] * to[0] + f[1] * to[1] + f[2] * to[2] + f[3] * to[3];
         if (dq < 0) s1 = -s1;
         o[0] = (f[0] * s0 + to[0] * s1) * d;
@@ -253,17 +259,20 @@ __host__ __device__ inline bool chain_valid(const double *s, int n, double link,
     double theta = 0., x = 0., y = 0.;
     px[0] = 0.;
     py[0] = 0.;
+    double st = 0.0, ct = 1.0;
     for (int i = 0; i < n; ++i) {
         theta += s[i];
-        double xN = x + cos(theta) * link;
-        double yN = y + sin(theta) * link;
+        glibc_sincos(theta, st, ct);
+        double xN = x + ct * link;
+        double yN = y + st * link;
         px[i + 1] = xN;
         py[i + 1] = yN;
         x = xN;
         y = yN;
     }
-    px[n + 1] = x + cos(theta) * 0.001;
-    py[n + 1] = y + sin(theta) * 0.001;
+    if (n == 0) glibc_sincos(theta, st, ct);
+    px[n + 1] = x + ct * 0.001;
+    py[n + 1] = y + st * 0.001;
     const int ns = n + 1;
     for (int i = 0; i < ns; ++i)
         for (int j = i + 1; j < ns; ++j)
@@ -296,18 +305,20 @@ __device__ __forceinline__ bool chain_valid_fixed(const double *s, double link, 
     double theta = 0., x = 0., y = 0.;
     px[0] = 0.;
     py[0] = 0.;
+    double st = 0.0, ct = 1.0;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
         theta += s[i];
-        const double xN = x + cos(theta) * link;
-        const double yN = y + sin(theta) * link;
+        glibc_sincos(theta, st, ct);
+        const double xN = x + ct * link;
+        const double yN = y + st * link;
         px[i + 1] = xN;
         py[i + 1] = yN;
         x = xN;
         y = yN;
     }
-    px[NL + 1] = x + cos(theta) * 0.001;
-    py[NL + 1] = y + sin(theta) * 0.001;
+    px[NL + 1] = x + ct * 0.001;
+    py[NL + 1] = y + st * 0.001;
     constexpr int ns = NL + 1;
 #pragma unroll
     for (int i = 0; i < ns; ++i)

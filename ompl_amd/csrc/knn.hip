@@ -448,8 +448,7 @@ __global__ void features_kernel(DevSpace sp, FeatGeom g, const double *__restric
         for (int j = 0; j < g.nmax; ++j) {
             if (j < sp.dim) {
                 th += s[j];
-                o[j] = cos(th);
-                o[g.nmax + j] = sin(th);
+                glibc_sincos(th, o[g.nmax + j], o[j]);  // glibc's cos / sin, as the host's features
             } else {
                 o[j] = 0.;
                 o[g.nmax + j] = 0.;

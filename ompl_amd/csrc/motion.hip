@@ -192,7 +192,8 @@ __device__ bool chain_valid_wave(double x, int n, double link, const double *__r
         const double xj = readlane_d(x, j);
         if (j <= lane) theta += xj;
     }
-    const double c = lane < n ? cos(theta) : 0.0, sn = lane < n ? sin(theta) : 0.0;
+    double c = 0.0, sn = 0.0;
+    if (lane < n) glibc_sincos(theta, sn, c);
     const double cl = c * link, sl = sn * link;
     double xn = 0.0, yn = 0.0;  // position i + 1 = sum_{j <= i} (cos(theta_j) link), in order
     for (int j = 0; j < n; ++j) {
@@ -242,7 +243,14 @@ __device__ double chain_dist_wave(double a, double b, int n, double link) {
             t2 += bj;
         }
     }
-    const double ddx = lane < n ? cos(t1) - cos(t2) : 0.0, ddy = lane < n ? sin(t1) - sin(t2) : 0.0;
+    double ddx = 0.0, ddy = 0.0;
+    if (lane < n) {
+        double s1, c1, s2, c2;
+        glibc_sincos(t1, s1, c1);
+        glibc_sincos(t2, s2, c2);
+        ddx = c1 - c2;
+        ddy = s1 - s2;
+    }
     double dx = 0.0, dy = 0.0;
     for (int j = 0; j < n; ++j) {
         const double u = readlane_d(ddx, j), v = readlane_d(ddy, j);

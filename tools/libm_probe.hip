@@ -1,11 +1,14 @@
 // libm_probe.hip — measurement tool (not product): the device math library's sin / cos / acos
 // against the host's, on the argument ranges the hot path uses (cumulative KinematicChain angles
 // |theta| <= 12 pi; SO3 |q1 . q2| in [0, 1]).  Reads n doubles from argv[1], writes
-// sin, cos, acos of each to argv[2] (3 n doubles); tools/libm_probe.py compares with glibc.
+// sin, cos, acos of each and the glibc restatement's sin, cos, sincos (ompl_amd/csrc/glibc_sincos.h) to
+// argv[2] (7 n doubles, the last two = sincos); tools/libm_probe.py compares with glibc.
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
 #include <vector>
+
+#include "../ompl_amd/csrc/glibc_sincos.h"
 
 __global__ void probe(const double *x, size_t n, double *o) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -14,6 +17,9 @@ __global__ void probe(const double *x, size_t n, double *o) {
     o[i] = sin(v);
     o[n + i] = cos(v);
     o[2 * n + i] = acos(fabs(v) <= 1.0 ? v : 0.5);
+    o[3 * n + i] = ompl_amd::glibc_sin(v);
+    o[4 * n + i] = ompl_amd::glibc_cos(v);
+    ompl_amd::glibc_sincos(v, o[7 * n + i], o[6 * n + i]);
 }
 
 int main(int argc, char **argv) {
@@ -27,12 +33,12 @@ int main(int argc, char **argv) {
     fclose(f);
     const size_t n = x.size();
     double *dx, *dout;
-    if (hipMalloc(&dx, n * sizeof(double)) != hipSuccess || hipMalloc(&dout, 3 * n * sizeof(double)) != hipSuccess)
+    if (hipMalloc(&dx, n * sizeof(double)) != hipSuccess || hipMalloc(&dout, 7 * n * sizeof(double)) != hipSuccess)
         return 3;
     hipMemcpy(dx, x.data(), n * sizeof(double), hipMemcpyHostToDevice);
     hipLaunchKernelGGL(probe, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dx, n, dout);
-    std::vector<double> out(3 * n);
-    if (hipMemcpy(out.data(), dout, 3 * n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return 4;
+    std::vector<double> out(7 * n);
+    if (hipMemcpy(out.data(), dout, 7 * n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return 4;
     hipFree(dx);
     hipFree(dout);
     FILE *g = fopen(argv[2], "wb");

@@ -1,7 +1,9 @@
 """Measurement tool (not product): device sin / cos / acos (tools/libm_probe.hip, the device
-math library the kernels use) against the host's glibc on the hot path's argument ranges.
+math library) and the device form of the glibc restatement (ompl_amd/csrc/glibc_sincos.h)
+against the host's glibc on the hot path's argument ranges.
 
     python tools/libm_probe.py [n]   (runs tools/libm_probe, writes gpurun_out/libm_probe.json)"""
+import ctypes
 import json
 import math
 import os
@@ -12,6 +14,17 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
+
+
+_libm = ctypes.CDLL("libm.so.6")
+_libm.sincos.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+_libm.sincos.restype = None
+
+
+def _sincos(v):
+    s, c = ctypes.c_double(), ctypes.c_double()
+    _libm.sincos(v, ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
 
 
 def main():
@@ -25,13 +38,17 @@ def main():
         fi, fo = f"/tmp/libm_in_{name}.bin", f"/tmp/libm_out_{name}.bin"
         x.astype(np.float64).tofile(fi)
         subprocess.run([os.path.join(HERE, "libm_probe"), fi, fo], check=True)
-        y = np.fromfile(fo, dtype=np.float64).reshape(3, n)
+        y = np.fromfile(fo, dtype=np.float64).reshape(7, n)
         res = {}
-        for k, fn in enumerate(("sin", "cos", "acos")):
+        sc = np.array([_sincos(v) for v in x])  # glibc's sincos
+        for k, fn in enumerate(("sin", "cos", "acos", "glibc_sin", "glibc_cos", "glibc_sincos_s", "glibc_sincos_c")):
             if fn == "acos" and name != "unit_interval":
                 continue
-            f = getattr(math, fn)
-            ref = np.array([f(v) for v in x])  # glibc
+            if fn.startswith("glibc_sincos"):
+                ref = sc[:, 0 if fn.endswith("_s") else 1]
+            else:
+                f = getattr(math, fn.replace("glibc_", ""))
+                ref = np.array([f(v) for v in x])  # glibc
             diff = y[k] != ref
             ulps = np.abs(y[k] - ref) / np.spacing(np.abs(ref))
             res[fn] = {"n": n, "mismatch": int(diff.sum()), "rate": float(diff.mean()), "max_ulps": float(ulps.max())}
