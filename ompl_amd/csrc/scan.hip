@@ -1,0 +1,100 @@
+// scan.hip — exclusive prefix sums of 64-bit counts on the device (CSR offsets of the radius,
+// PRM* and RRT* paths): out[i] = in[0] + ... + in[i - 1] for i in [0, n], so out[n] is the total.
+// Three launches, no host round trip: per-1,024-element block totals, one block scanning the
+// totals, then every block's local scan plus its offset.  Wave scans by DPP-free shuffles.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace ompl_amd {
+
+namespace {
+
+constexpr uint32_t kScanBlock = 1024;  // elements per block (256 threads x 4)
+
+__device__ __forceinline__ uint64_t wave_inclusive(uint64_t v) {
+    const int lane = threadIdx.x & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t u = (uint64_t)__shfl_up((long long)v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+// block exclusive scan of one value per thread (256 threads); *total = the block's sum
+__device__ __forceinline__ uint64_t block_exclusive(uint64_t v, uint64_t *total) {
+    __shared__ uint64_t ws[4];
+    const uint64_t inc = wave_inclusive(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) ws[w] = inc;
+    __syncthreads();
+    uint64_t off = 0, tot = 0;
+    for (int i = 0; i < 4; ++i) {
+        if (i < w) off += ws[i];
+        tot += ws[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
+__global__ __launch_bounds__(256) void scan_totals_kernel(const uint64_t *__restrict__ in, uint64_t n,
+                                                          uint64_t *__restrict__ part) {
+    const uint64_t b = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
+    uint64_t s = 0;
+    for (int k = 0; k < 4; ++k) s += b + k < n ? in[b + k] : 0;
+    uint64_t tot;
+    block_exclusive(s, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// one block: exclusive scan of nb block totals in place, chunk by chunk
+__global__ __launch_bounds__(256) void scan_parts_kernel(uint64_t *__restrict__ part, uint32_t nb) {
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t c = 0; c < nb; c += 256) {
+        const uint32_t i = c + threadIdx.x;
+        const uint64_t v = i < nb ? part[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive(v, &tot);
+        const uint64_t base = carry;
+        if (i < nb) part[i] = base + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) carry = base + tot;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void scan_apply_kernel(const uint64_t *__restrict__ in, uint64_t n,
+                                                         const uint64_t *__restrict__ part, uint64_t *__restrict__ out) {
+    const uint64_t b = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
+    uint64_t v[4], s = 0;
+    for (int k = 0; k < 4; ++k) {
+        v[k] = b + k < n ? in[b + k] : 0;
+        s += v[k];
+    }
+    uint64_t tot;
+    uint64_t run = part[blockIdx.x] + block_exclusive(s, &tot);
+    for (int k = 0; k < 4; ++k) {
+        if (b + k < n) out[b + k] = run;
+        run += v[k];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 255) out[n] = part[blockIdx.x] + tot;
+}
+
+}  // namespace
+
+size_t exclusive_scan_u64_workspace(uint64_t n) { return sizeof(uint64_t) * ((n + kScanBlock - 1) / kScanBlock + 1); }
+
+hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t n, uint64_t *out, void *ws, hipStream_t st) {
+    if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+    const uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
+    uint64_t *part = (uint64_t *)ws;
+    hipLaunchKernelGGL(scan_totals_kernel, dim3(nb), dim3(256), 0, st, in, n, part);
+    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(256), 0, st, part, nb);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(256), 0, st, in, n, part, out);
+    return hipGetLastError();
+}
+
+}  // namespace ompl_amd

@@ -19,7 +19,7 @@ __global__ void probe(const double *x, size_t n, double *o) {
     o[2 * n + i] = acos(fabs(v) <= 1.0 ? v : 0.5);
     o[3 * n + i] = ompl_amd::glibc_sin(v);
     o[4 * n + i] = ompl_amd::glibc_cos(v);
-    ompl_amd::glibc_sincos(v, o[7 * n + i], o[6 * n + i]);
+    ompl_amd::glibc_sincos(v, o[5 * n + i], o[6 * n + i]);
 }
 
 int main(int argc, char **argv) {
