@@ -37,6 +37,7 @@
  *   ompl_gpu_steer_device  the RRT extend step (nearest -> interpolate to range)
  *                          src/ompl/geometric/planners/rrt/src/RRT.cpp:137-146
  *   ompl_gpu_rrt_grow_device  the RRT loop itself                 RRT.cpp:128-192
+ *   ompl_gpu_rrtstar_batch_device  RRT*'s iterations (geometric part) RRTstar.cpp:247-542, :603-618
  *   ompl_gpu_prm_add_milestones  PRM* causal roadmap batches      prm/src/PRM.cpp:562-596
  *   ompl_gpu_knn_merge_device  per-shard nearestK lists -> global top k (tree-sharded mode)
  *   ompl_gpu_csr_merge_device  per-shard nearestR CSR results -> one CSR (tree-sharded mode)
@@ -358,6 +359,42 @@ ompl_gpu_status ompl_gpu_rrt_solve_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, cons
                                           double max_distance, const double *goal, double goal_threshold,
                                           uint32_t *d_nearest, uint32_t *d_added, uint64_t *solved_at,
                                           uint32_t *approx_id, double *approx_dist);
+
+/* ---- RRT* iteration batches ----------------------------------------------------
+ * RRTstar::solve (geometric/planners/rrt/src/RRTstar.cpp:247-542) with its defaults (k-nearest
+ * neighbourhoods, useKNearest_ RRTstar.h:445; delayed collision checking, delayCC_ :458; no
+ * new-state rejection or pruning) for ns samples in order: nmotion = nearest(s_i) (:266); x_i =
+ * s_i, or interpolate(nmotion, s_i, max_distance / d) when d > max_distance (:271-279); when
+ * mv's checkMotion(nmotion, x_i) holds (:282), x_i joins the tree (:410) after its neighbourhood
+ * nearestK(x_i, k_i), k_i = ceil(k_rrt * ln(size + 1)) over the tree as it stands (getNeighbors
+ * :603-618), is taken.  Sample i sees every state samples < i added, as in the sequential loop.
+ * This is the geometric part of every iteration: which states join, the neighbourhoods, and both
+ * motion bits of every (neighbour, x_i) pair — checkMotion(nbh, x_i) for the parent choice in
+ * cost order (:319-357) and checkMotion(x_i, nbh) for the rewiring (:414-440) — so the planner's
+ * cost logic needs only lookups (ompl_amd/rrtstar.py).  None of it depends on costs.
+ * Inputs: d_samples ns AoS rows (device).  Outputs (device, caller-owned, ns entries each, may be
+ * NULL): d_nearest[i] = id of nmotion; d_added[i] = the id x_i got, or 0xFFFFFFFF; d_inc[i] =
+ * distance(nmotion, x_i) (the motion's incCost, :288); d_states[i] = x_i (dim reals).  The
+ * neighbourhoods are library-owned device arrays, valid until the next call on nn: a CSR over the
+ * samples (out->offsets, ns + 1 entries; empty for samples not added) of neighbour ids, their
+ * distances distance(nbh, x_i) and bits (bit 0 = checkMotion(nbh, x_i), bit 1 = checkMotion(x_i,
+ * nbh)), each segment sorted by (distance, id) and k_i long (fewer if the tree was smaller).
+ * mv's counters are not updated (the planner performs only the checks its cost logic asks for).
+ * Both handles describe the same space (R^n, SO3 or SE3) on the same device.  Synchronous. */
+typedef struct ompl_gpu_rrtstar_result {
+    const uint64_t *offsets; /* device, ns + 1 */
+    const uint32_t *ids;     /* device, total */
+    const double *dist;      /* device, total */
+    const uint8_t *bits;     /* device, total */
+    uint64_t total;          /* neighbourhood entries */
+    uint64_t added;          /* samples whose state joined the tree */
+    uint32_t rounds;         /* fixed-point rounds over the batch's in-batch nearest states */
+    uint32_t reserved;
+} ompl_gpu_rrtstar_result;
+ompl_gpu_status ompl_gpu_rrtstar_batch_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
+                                              double max_distance, double k_rrt, uint32_t *d_nearest,
+                                              uint32_t *d_added, double *d_inc, double *d_states,
+                                              ompl_gpu_rrtstar_result *out);
 
 /* ---- BIT* batch sampling -----------------------------------------------------
  * BITstar::ImplicitGraph::updateSamples before a solution exists (ImplicitGraph.cpp:924-1000: the

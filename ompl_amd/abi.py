@@ -47,6 +47,20 @@ class CheckerStruct(C.Structure):
     ]
 
 
+class RrtStarResult(C.Structure):
+    """ompl_gpu_rrtstar_result: library-owned device arrays of one RRT* batch"""
+    _fields_ = [
+        ("offsets", C.c_void_p),
+        ("ids", C.c_void_p),
+        ("dist", C.c_void_p),
+        ("bits", C.c_void_p),
+        ("total", C.c_uint64),
+        ("added", C.c_uint64),
+        ("rounds", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
 class GpuError(RuntimeError):
     def __init__(self, status: int, msg: str):
         super().__init__(f"[ompl_gpu status {status}] {msg}")
@@ -99,6 +113,8 @@ SIGNATURES = {
     "ompl_gpu_nn_edges_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P, C.c_uint32, C.c_size_t, C.c_int, _P, _P]),
     "ompl_gpu_rrt_grow_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, _P, _P]),
     "ompl_gpu_rrt_aborts": (C.c_int, [_P, _U64]),
+    "ompl_gpu_rrtstar_batch_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, C.c_double, _P, _P, _P, _P,
+                                                C.POINTER(RrtStarResult)]),
     "ompl_gpu_csr_merge_device": (C.c_int, [_P, C.c_uint32, C.c_size_t, _P, _P, C.c_size_t, _P, _P, _P, _P]),
     "ompl_gpu_knn_merge_device": (C.c_int, [_P, _P, C.c_uint32, C.c_size_t, C.c_uint32, _P, _P, _P]),
     "ompl_gpu_rrt_solve_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, _D, C.c_double, _P, _P, _U64,

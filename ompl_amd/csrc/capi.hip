@@ -116,6 +116,10 @@ struct ompl_gpu_nn {
     uint64_t rrt_aborts = 0;       // persistent runs that aborted and re-ran in the two-launch form
     DevBuf prm_bf, prm_raw, prm_kj, prm_sd, prm_si, prm_len, prm_off, prm_eoff, prm_cnt64;  // PRM* batches
     DevBuf prm_p32;                                                                         // chain positions
+    struct {  // RRT* iteration batches (ompl_gpu_rrtstar_batch_device)
+        DevBuf near_i, near_d, src, xa, xb, from, inc, va, vb, rank, list, chg, xc, bf, kj, sd, si, len, off, cd, ci,
+            scnt, ocnt, ooff, oi, od, oseg, fwd, bwd, bits, soff, scan, p32, sorti, sortd, ovf;
+    } rs;
     std::vector<double> hfeat;
     // screening bounds: box of the first three coordinates and max |coordinate|
     double lo[kKeyDims] = {0}, hi[kKeyDims] = {0}, absmax = 0.0;
@@ -1615,6 +1619,228 @@ ompl_gpu_status ompl_gpu_lazyprm_add_milestones(ompl_gpu_nn *h, const double *st
     if (s != OMPL_GPU_OK) return s;
     std::lock_guard<std::mutex> lk(h->mu);
     return prm_batch_locked(h, nullptr, states, m, j0, j1, k_const, k_cap, d_nbr, d_cnt, nullptr, d_dist, nullptr);
+}
+
+// ------------------------------------------------------------------------------ RRT*
+
+namespace {
+ompl_gpu_status rrtstar_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples, size_t ns, double maxd,
+                               double k_rrt, uint32_t *d_nearest, uint32_t *d_added, double *d_inc, double *d_states,
+                               ompl_gpu_rrtstar_result *out) {
+    auto &R = h->rs;
+    const int dim = h->sp.dim, F = h->g.F;
+    const uint64_t n0 = h->n_total, nlive0 = h->n_live;
+    const uint32_t n = (uint32_t)ns;
+    hipStream_t st = h->stream;
+    HIP_OR_FAIL(R.near_i.ensure(sizeof(uint32_t) * ns));
+    HIP_OR_FAIL(R.near_d.ensure(sizeof(double) * ns));
+    HIP_OR_FAIL(R.src.ensure(sizeof(uint32_t) * ns));
+    HIP_OR_FAIL(R.xa.ensure(sizeof(double) * ns * dim));
+    HIP_OR_FAIL(R.xb.ensure(sizeof(double) * ns * dim));
+    HIP_OR_FAIL(R.from.ensure(sizeof(double) * ns * dim));
+    HIP_OR_FAIL(R.inc.ensure(sizeof(double) * ns));
+    HIP_OR_FAIL(R.va.ensure(ns));
+    HIP_OR_FAIL(R.vb.ensure(ns));
+    HIP_OR_FAIL(R.rank.ensure(sizeof(uint32_t) * (ns + 1)));
+    HIP_OR_FAIL(R.list.ensure(sizeof(uint32_t) * ns));
+    HIP_OR_FAIL(R.chg.ensure(sizeof(uint32_t)));
+    uint32_t *near_i = (uint32_t *)R.near_i.p, *src = (uint32_t *)R.src.p, *rank = (uint32_t *)R.rank.p,
+             *list = (uint32_t *)R.list.p, *chg = (uint32_t *)R.chg.p;
+    double *near_d = (double *)R.near_d.p, *xa = (double *)R.xa.p, *xb = (double *)R.xb.p, *from = (double *)R.from.p,
+           *inc = (double *)R.inc.p;
+    uint8_t *va = (uint8_t *)R.va.p, *vb = (uint8_t *)R.vb.p;
+    // 1. every sample against the stored tree: nearest, steer, checkMotion (RRTstar.cpp:266-282)
+    const double *qf = nullptr;
+    ompl_gpu_status s = device_query_features(h, d_samples, ns, &qf);
+    if (s != OMPL_GPU_OK) return s;
+    s = knn_features_locked(h, qf, ns, 1, near_i, near_d);
+    if (s != OMPL_GPU_OK) return s;
+    HIP_OR_FAIL(hipMemcpyAsync(src, near_i, sizeof(uint32_t) * ns, hipMemcpyDeviceToDevice, st));
+    HIP_OR_FAIL(launch_rrtstar_steer(h->sp, h->raw, h->cap, d_samples, n, src, xb, maxd, from, xa, inc, st));
+    HIP_OR_FAIL(launch_motion(mv->sp, mv->ck, from, xa, n, va, nullptr, nullptr, nullptr, st));
+    // 2. fixed point: the nearest earlier added state of the batch against the stored nearest
+    uint32_t rounds = 0;
+    for (;;) {
+        HIP_OR_FAIL(launch_rrtstar_rank(va, n, rank, list, st));
+        HIP_OR_FAIL(launch_rrtstar_causal(h->sp, d_samples, n, xa, rank, list, near_i, near_d, src, st));
+        HIP_OR_FAIL(launch_rrtstar_steer(h->sp, h->raw, h->cap, d_samples, n, src, xa, maxd, from, xb, inc, st));
+        HIP_OR_FAIL(launch_motion(mv->sp, mv->ck, from, xb, n, vb, nullptr, nullptr, nullptr, st));
+        HIP_OR_FAIL(hipMemsetAsync(chg, 0, sizeof(uint32_t), st));
+        HIP_OR_FAIL(launch_rrtstar_diff(xa, xb, va, vb, n, dim, chg, st));
+        uint32_t changed = 0;
+        HIP_OR_FAIL(hipMemcpyAsync(&changed, chg, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIP_OR_FAIL(hipStreamSynchronize(st));
+        std::swap(xa, xb);
+        std::swap(va, vb);
+        ++rounds;
+        if (changed == 0) break;
+        if (rounds > n + 1) return fail(OMPL_GPU_ERR_DEVICE, "RRT* batch: the in-batch nearest states did not settle");
+    }
+    // the settled state: ranks, ids, the added states in rank order
+    HIP_OR_FAIL(launch_rrtstar_rank(va, n, rank, list, st));
+    HIP_OR_FAIL(R.xc.ensure(sizeof(double) * ns * dim));
+    double *xc = (double *)R.xc.p;
+    HIP_OR_FAIL(R.ooff.ensure(sizeof(uint32_t) * 2 * ns));  // nearest / added when the caller passes none
+    uint32_t *tmp_near = d_nearest ? d_nearest : (uint32_t *)R.ooff.p, *tmp_added = d_added ? d_added : tmp_near + ns;
+    HIP_OR_FAIL(launch_rrtstar_finish(src, va, rank, xa, n, dim, (uint32_t)n0, tmp_near, tmp_added, xc, st));
+    if (d_inc) HIP_OR_FAIL(hipMemcpyAsync(d_inc, inc, sizeof(double) * ns, hipMemcpyDeviceToDevice, st));
+    if (d_states) HIP_OR_FAIL(hipMemcpyAsync(d_states, xa, sizeof(double) * ns * dim, hipMemcpyDeviceToDevice, st));
+    uint32_t m = 0;
+    HIP_OR_FAIL(hipMemcpyAsync(&m, rank + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+    HIP_OR_FAIL(R.soff.ensure(sizeof(uint64_t) * (ns + 1)));
+    uint64_t *soff = (uint64_t *)R.soff.p;
+    *out = ompl_gpu_rrtstar_result{};
+    out->rounds = rounds;
+    out->added = m;
+    out->offsets = soff;
+    if (m == 0) {
+        HIP_OR_FAIL(hipMemsetAsync(soff, 0, sizeof(uint64_t) * (ns + 1), st));
+        HIP_OR_FAIL(hipStreamSynchronize(st));
+        return OMPL_GPU_OK;
+    }
+    // 3. neighbourhoods of the added states: k_j = ceil(k_rrt ln(size + 1)), size = the tree when
+    //    added state j is about to join (getNeighbors, RRTstar.cpp:605-611) — host libm, as the reference
+    std::vector<uint32_t> kj(m);
+    uint32_t kmax = 0;
+    for (uint32_t j = 0; j < m; ++j) {
+        const double kk = std::ceil(k_rrt * std::log((double)(nlive0 + j + 1)));
+        kj[j] = kk > 0 ? (uint32_t)kk : 0u;
+        kmax = std::max(kmax, kj[j]);
+    }
+    HIP_OR_FAIL(R.kj.ensure(sizeof(uint32_t) * m));
+    uint32_t *dkj = (uint32_t *)R.kj.p;
+    HIP_OR_FAIL(hipMemcpyAsync(dkj, kj.data(), sizeof(uint32_t) * m, hipMemcpyHostToDevice, st));
+    const double *bf = xc;  // the added states' feature rows
+    if (!(h->sp.kind == OMPL_GPU_SPACE_SE3 || h->sp.kind == OMPL_GPU_SPACE_SO3 ||
+          (h->sp.kind == OMPL_GPU_SPACE_REALVECTOR && F == dim))) {
+        HIP_OR_FAIL(R.bf.ensure(sizeof(double) * m * F));
+        HIP_OR_FAIL(launch_features(h->sp, h->g, xc, m, (double *)R.bf.p, st));
+        bf = (const double *)R.bf.p;
+    }
+    const uint32_t kq = (uint32_t)std::min<uint64_t>(kmax, nlive0);  // the stored part
+    HIP_OR_FAIL(R.sd.ensure(sizeof(double) * (size_t)m * std::max<uint32_t>(kq, 1)));
+    HIP_OR_FAIL(R.si.ensure(sizeof(uint32_t) * (size_t)m * std::max<uint32_t>(kq, 1)));
+    double *sd = (double *)R.sd.p;
+    uint32_t *si = (uint32_t *)R.si.p;
+    if (kq > 0) {
+        s = knn_features_locked(h, bf, m, kq, si, sd);
+        if (s != OMPL_GPU_OK) return s;
+    }
+    // in-batch candidates (earlier added states within the stored list's k_j-th distance)
+    HIP_OR_FAIL(R.len.ensure(sizeof(uint64_t) * (m + 2)));
+    HIP_OR_FAIL(R.off.ensure(sizeof(uint64_t) * (m + 1)));
+    HIP_OR_FAIL(R.scan.ensure(exclusive_scan_u64_workspace(m + 1)));
+    uint64_t *len = (uint64_t *)R.len.p, *off = (uint64_t *)R.off.p;
+    HIP_OR_FAIL(hipMemsetAsync(len + m, 0, 2 * sizeof(uint64_t), st));
+    float *p32 = nullptr;
+    if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN) {
+        HIP_OR_FAIL(R.p32.ensure(sizeof(float) * m * F));
+        p32 = (float *)R.p32.p;
+    }
+    HIP_OR_FAIL(launch_prm_causal(h->sp, h->g, false, bf, 0, m, (uint32_t)n0, dkj, sd, si, kq, len, nullptr, nullptr,
+                                  nullptr, p32, m, (unsigned long long *)(len + m + 1), st));
+    HIP_OR_FAIL(launch_exclusive_scan_u64(len, m, off, R.scan.p, st));
+    uint64_t hdr[2] = {0, 0};  // total, longest
+    HIP_OR_FAIL(hipMemcpyAsync(&hdr[0], off + m, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+    const uint64_t tot = hdr[0];
+    HIP_OR_FAIL(R.cd.ensure(sizeof(double) * std::max<uint64_t>(tot, 1)));
+    HIP_OR_FAIL(R.ci.ensure(sizeof(uint32_t) * std::max<uint64_t>(tot, 1)));
+    double *cd = (double *)R.cd.p;
+    uint32_t *ci = (uint32_t *)R.ci.p;
+    if (tot)
+        HIP_OR_FAIL(launch_prm_causal(h->sp, h->g, true, bf, 0, m, (uint32_t)n0, dkj, sd, si, kq, nullptr, off, cd, ci,
+                                      p32, m, (unsigned long long *)(len + m + 1), st));
+    // merged lists cut at k_j: counts, offsets
+    HIP_OR_FAIL(R.scnt.ensure(sizeof(uint32_t) * m));
+    HIP_OR_FAIL(R.ocnt.ensure(sizeof(uint64_t) * (m + 1)));
+    HIP_OR_FAIL(R.ovf.ensure(sizeof(uint32_t)));
+    uint32_t *scnt = (uint32_t *)R.scnt.p, *ovf = (uint32_t *)R.ovf.p;
+    uint64_t *ocnt = (uint64_t *)R.ocnt.p;
+    HIP_OR_FAIL(launch_rrtstar_counts(si, kq, dkj, off, m, scnt, ocnt, st));
+    HIP_OR_FAIL(R.od.ensure(sizeof(uint64_t) * (m + 1)));
+    uint64_t *ooff = (uint64_t *)R.od.p;
+    HIP_OR_FAIL(launch_exclusive_scan_u64(ocnt, m, ooff, R.scan.p, st));
+    uint64_t E = 0;
+    HIP_OR_FAIL(hipMemcpyAsync(&E, ooff + m, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipMemsetAsync(ovf, 0, sizeof(uint32_t), st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+    if (E > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "RRT* batch: more than 2^32 neighbourhood entries");
+    HIP_OR_FAIL(R.oi.ensure(sizeof(uint32_t) * std::max<uint64_t>(E, 1)));
+    HIP_OR_FAIL(R.sortd.ensure(sizeof(double) * std::max<uint64_t>(E, 1)));
+    HIP_OR_FAIL(R.oseg.ensure(sizeof(uint32_t) * std::max<uint64_t>(E, 1)));
+    uint32_t *oi = (uint32_t *)R.oi.p, *oseg = (uint32_t *)R.oseg.p;
+    double *odist = (double *)R.sortd.p;
+    HIP_OR_FAIL(launch_rrtstar_merge(off, scnt, dkj, ci, cd, ooff, oi, odist, oseg, m, ovf, st));
+    uint32_t overflow = 0;
+    HIP_OR_FAIL(hipMemcpyAsync(&overflow, ovf, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+    if (overflow) {  // a segment with more than kRrtStarMergeCands candidates (a small tree, a large
+                     // batch): every segment sorted by two stable radix passes (id, then distance)
+        HIP_OR_FAIL(R.sorti.ensure(sizeof(uint32_t) * std::max<uint64_t>(tot, 1)));
+        HIP_OR_FAIL(R.bits.ensure(sizeof(double) * std::max<uint64_t>(tot, 1)));
+        uint32_t *sii = (uint32_t *)R.sorti.p;
+        double *sdd = (double *)R.bits.p;
+        size_t tb1 = 0, tb2 = 0;
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb1, (const uint32_t *)ci, sii, (const double *)cd,
+                                                                sdd, (int)tot, (int)m, off, off + 1, 0, 32, st));
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb2, (const double *)sdd, cd, (const uint32_t *)sii,
+                                                                ci, (int)tot, (int)m, off, off + 1, 0, 64, st));
+        HIP_OR_FAIL(h->tmp.ensure(std::max(tb1, tb2)));
+        tb1 = tb2 = h->tmp.bytes;
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb1, (const uint32_t *)ci, sii, (const double *)cd,
+                                                                sdd, (int)tot, (int)m, off, off + 1, 0, 32, st));
+        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb2, (const double *)sdd, cd, (const uint32_t *)sii,
+                                                                ci, (int)tot, (int)m, off, off + 1, 0, 64, st));
+        HIP_OR_FAIL(launch_rrtstar_take(off, ci, cd, ooff, m, oi, odist, oseg, st));
+    }
+    // 4. both motion bits of every neighbourhood entry: checkMotion(nbh, x_j), checkMotion(x_j, nbh)
+    s = ensure_aos(h);
+    if (s != OMPL_GPU_OK) return s;
+    HIP_OR_FAIL(mv->s1.ensure(sizeof(double) * std::max<uint64_t>(E, 1) * dim));
+    HIP_OR_FAIL(mv->s2.ensure(sizeof(double) * std::max<uint64_t>(E, 1) * dim));
+    HIP_OR_FAIL(R.fwd.ensure(std::max<uint64_t>(E, 1)));
+    HIP_OR_FAIL(R.bwd.ensure(std::max<uint64_t>(E, 1)));
+    HIP_OR_FAIL(R.bits.ensure(std::max<uint64_t>(E, 1)));
+    double *e1 = (double *)mv->s1.p, *e2 = (double *)mv->s2.p;
+    HIP_OR_FAIL(launch_rrtstar_edges(oi, oseg, E, (uint32_t)n0, dim, (const double *)h->raw_aos.p, aos_width(h), xc, e1,
+                                     e2, st));
+    HIP_OR_FAIL(launch_motion(mv->sp, mv->ck, e1, e2, (uint32_t)E, (uint8_t *)R.fwd.p, nullptr, nullptr, nullptr, st));
+    HIP_OR_FAIL(launch_motion(mv->sp, mv->ck, e2, e1, (uint32_t)E, (uint8_t *)R.bwd.p, nullptr, nullptr, nullptr, st));
+    HIP_OR_FAIL(launch_rrtstar_bits((const uint8_t *)R.fwd.p, (const uint8_t *)R.bwd.p, E, (uint8_t *)R.bits.p, st));
+    HIP_OR_FAIL(launch_rrtstar_sample_offsets(va, rank, ooff, n, soff, st));
+    // 5. the added states join the tree (RRTstar.cpp:410), ids n0 + rank
+    std::vector<double> hx((size_t)m * dim);
+    HIP_OR_FAIL(hipMemcpyAsync(hx.data(), xc, sizeof(double) * m * dim, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+    uint64_t first = 0;
+    s = add_locked(h, hx.data(), m, &first, bf, xc);
+    if (s != OMPL_GPU_OK) return s;
+    out->ids = oi;
+    out->dist = odist;
+    out->bits = (const uint8_t *)R.bits.p;
+    out->total = E;
+    return OMPL_GPU_OK;
+}
+}  // namespace
+
+ompl_gpu_status ompl_gpu_rrtstar_batch_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples, size_t ns,
+                                              double max_distance, double k_rrt, uint32_t *d_nearest,
+                                              uint32_t *d_added, double *d_inc, double *d_states,
+                                              ompl_gpu_rrtstar_result *out) {
+    if (!h || !mv || !out || (ns && !d_samples)) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (h->device != mv->device) return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles are on different devices");
+    if (h->sp.kind != mv->sp.kind || h->sp.dim != mv->sp.dim)
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "nn and mv handles describe different state spaces");
+    if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN) return fail(OMPL_GPU_ERR_UNSUPPORTED, "RRT* batches: R^n, SO3 or SE3");
+    if (ns > 0x7FFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many samples in one batch");
+    std::scoped_lock lk(h->mu, mv->mu);
+    *out = ompl_gpu_rrtstar_result{};
+    if (ns == 0) return OMPL_GPU_OK;
+    if (h->n_live == 0) return fail(OMPL_GPU_ERR_EMPTY, "No elements found in nearest neighbors data structure");
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    return rrtstar_locked(h, mv, d_samples, ns, max_distance, k_rrt, d_nearest, d_added, d_inc, d_states, out);
 }
 
 // ------------------------------------------------------------------------------ RRT

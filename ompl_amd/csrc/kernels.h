@@ -303,6 +303,43 @@ hipError_t launch_rrt_grow(const DevSpace &sp, const DevSpace &msp, const DevChe
 // goal record of a run (64-bit words, zero-initialised by the host as {~0, +inf bits, ~0})
 size_t rrt_goal_words();
 
+// ---- RRT* iteration batches (rrtstar.hip) --------------------------------------------------
+// nearest sources: a stored id, or kRrtStarInBatch | j (sample j of the batch)
+constexpr uint32_t kRrtStarInBatch = 0x80000000u;
+hipError_t launch_rrtstar_steer(const DevSpace &sp, const double *raw, uint64_t cap, const double *samples, uint32_t ns,
+                                const uint32_t *src, const double *x_prev, double maxd, double *from, double *to,
+                                double *inc, hipStream_t st);
+hipError_t launch_rrtstar_rank(const uint8_t *valid, uint32_t ns, uint32_t *rank, uint32_t *list, hipStream_t st);
+hipError_t launch_rrtstar_causal(const DevSpace &sp, const double *samples, uint32_t ns, const double *x,
+                                 const uint32_t *rank, const uint32_t *list, const uint32_t *near_id,
+                                 const double *near_d, uint32_t *src, hipStream_t st);
+hipError_t launch_rrtstar_diff(const double *xa, const double *xb, const uint8_t *va, const uint8_t *vb, uint32_t ns,
+                               int dim, uint32_t *changed, hipStream_t st);
+hipError_t launch_rrtstar_finish(const uint32_t *src, const uint8_t *valid, const uint32_t *rank, const double *x,
+                                 uint32_t ns, int dim, uint32_t n0, uint32_t *nearest, uint32_t *added, double *xa,
+                                 hipStream_t st);
+hipError_t launch_rrtstar_counts(const uint32_t *si, uint32_t kq, const uint32_t *kj, const uint64_t *seg_off,
+                                 uint32_t rows, uint32_t *stored_cnt, uint64_t *out_cnt, hipStream_t st);
+// merge of each segment's sorted stored entries with its (at most kRrtStarMergeCands) in-batch
+// candidates, cut at out_off's counts; *overflow += segments with more candidates (not written)
+constexpr uint32_t kRrtStarMergeCands = 1024;
+hipError_t launch_rrtstar_merge(const uint64_t *seg_off, const uint32_t *stored_cnt, const uint32_t *kj,
+                                const uint32_t *in_i, const double *in_d, const uint64_t *out_off, uint32_t *out_i,
+                                double *out_d, uint32_t *out_seg, uint32_t rows, uint32_t *overflow, hipStream_t st);
+// the same from fully sorted segments (the radix fallback): the first out counts of each segment
+hipError_t launch_rrtstar_take(const uint64_t *seg_off, const uint32_t *in_i, const double *in_d, const uint64_t *out_off,
+                               uint32_t rows, uint32_t *out_i, double *out_d, uint32_t *out_seg, hipStream_t st);
+hipError_t launch_rrtstar_edges(const uint32_t *ids, const uint32_t *seg, uint64_t E, uint32_t n0, int dim,
+                                const double *aos, int da, const double *xa, double *s1, double *s2, hipStream_t st);
+hipError_t launch_rrtstar_bits(const uint8_t *fwd, const uint8_t *bwd, uint64_t E, uint8_t *bits, hipStream_t st);
+hipError_t launch_rrtstar_sample_offsets(const uint8_t *valid, const uint32_t *rank, const uint64_t *out_off,
+                                         uint32_t ns, uint64_t *off, hipStream_t st);
+
+// ---- exclusive prefix sums (scan.hip): out[0..n], out[n] = the total; ws of
+// exclusive_scan_u64_workspace(n) bytes; asynchronous
+size_t exclusive_scan_u64_workspace(uint64_t n);
+hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t n, uint64_t *out, void *ws, hipStream_t st);
+
 // radius search, pass 1 (count per (query, chunk)) and pass 2 (fill CSR in id order).
 struct RadiusPlan {
     uint32_t chunks;      // chunks per query

@@ -92,6 +92,18 @@ uint64_t oracle_check_motions_mt(const ompl_gpu_space *sp, const ompl_gpu_checke
 void oracle_prm_causal(const ompl_gpu_space *sp, const ompl_gpu_checker *ck, const double *states, size_t n,
                        double k_const, uint32_t k_cap, uint32_t *nbr, uint32_t *cnt, uint8_t *valid);
 
+/* RRT*'s iteration, sequential (oracle/rrtstar.cpp; RRTstar.cpp:247-542 with its defaults) from
+ * the tree (states0, parent0 (-1 = root), inc0, cost0) over the given samples; use_gnat: the GNAT
+ * restatement as the neighbour structure (else brute force); time_budget_s > 0 stops early.
+ * Per sample: nearest_out, added_out (0xFFFFFFFF: not added), parent_choice (-1); the final tree
+ * (n0 + added entries) in parent_out / inc_out / cost_out (may be NULL); stats[4] = samples
+ * processed, added, rewires, checkMotion calls.  Returns the samples processed. */
+uint64_t oracle_rrtstar(const ompl_gpu_space *sp, const ompl_gpu_checker *ck, const double *states0, size_t n0,
+                        const int64_t *parent0, const double *inc0, const double *cost0, const double *samples,
+                        size_t ns, double maxd, double k_rrt, int use_gnat, double time_budget_s, uint32_t *nearest_out,
+                        uint32_t *added_out, int64_t *parent_choice, int64_t *parent_out, double *inc_out,
+                        double *cost_out, uint64_t *stats);
+
 /* ---- the reference's input streams (oracle/rng.cpp) ------------------- */
 uint32_t oracle_mt19937_10000th(void);
 uint32_t oracle_ranlux24_base_10000th(void);

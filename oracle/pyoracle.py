@@ -23,6 +23,7 @@ REF_PATH = os.path.join(HERE, "_ref", "libref_linear.so")
 _SP = C.POINTER(abi.SpaceStruct)
 _CK = C.POINTER(abi.CheckerStruct)
 _D, _U8, _U32, _I32, _U64 = abi._D, abi._U8, abi._U32, abi._I32, abi._U64
+_I64 = C.POINTER(C.c_int64)
 
 _ORACLE_SIGS = {
     "oracle_distance": (C.c_double, [_SP, _D, _D]),
@@ -44,6 +45,8 @@ _ORACLE_SIGS = {
     "oracle_gnat_radius": (C.c_uint64, [C.c_void_p, _D, C.c_size_t, C.c_double, _U64, C.c_int]),
     "oracle_gnat_radius_fetch": (None, [C.c_void_p, _U32, _D]),
     "oracle_prm_causal": (None, [_SP, _CK, _D, C.c_size_t, C.c_double, C.c_uint32, _U32, _U32, _U8]),
+    "oracle_rrtstar": (C.c_uint64, [_SP, _CK, _D, C.c_size_t, _I64, _D, _D, _D, C.c_size_t, C.c_double, C.c_double,
+                                    C.c_int, C.c_double, _U32, _U32, _I64, _I64, _D, _D, _U64]),
     "oracle_mt19937_10000th": (C.c_uint32, []),
     "oracle_ranlux24_base_10000th": (C.c_uint32, []),
     "oracle_seed_stream": (None, [C.c_uint32, C.c_size_t, _U32]),
@@ -171,6 +174,33 @@ def prm_causal(sp, ck, states, k_const, k_cap):
     lib.oracle_prm_causal(C.byref(s), C.byref(c), abi.dptr(x), n, float(k_const), int(k_cap),
                           nbr.ctypes.data_as(_U32), cnt.ctypes.data_as(_U32), val.ctypes.data_as(_U8))
     return nbr, cnt, val
+
+
+def rrtstar(sp, ck, states0, parent0, inc0, cost0, samples, maxd, k_rrt, use_gnat=False, time_budget_s=0.0):
+    """RRT*'s sequential iteration (oracle/rrtstar.cpp) from the given tree over the samples:
+    dict with nearest / added / parent_choice per sample, the final tree's parent / inc / cost,
+    and stats (processed, added, rewires, checkMotion calls)."""
+    s, c = sp.to_abi(), ck.to_abi()
+    x0 = _arr(states0).reshape(-1, sp.dim)
+    smp = _arr(samples).reshape(-1, sp.dim)
+    n0, ns = x0.shape[0], smp.shape[0]
+    p0 = np.ascontiguousarray(parent0, dtype=np.int64)
+    i0, c0 = _arr(inc0), _arr(cost0)
+    near = np.zeros(ns, np.uint32)
+    added = np.zeros(ns, np.uint32)
+    choice = np.zeros(ns, np.int64)
+    par = np.zeros(n0 + ns, np.int64)
+    inc = np.zeros(n0 + ns)
+    cost = np.zeros(n0 + ns)
+    st = np.zeros(4, np.uint64)
+    lib.oracle_rrtstar(C.byref(s), C.byref(c), abi.dptr(x0), n0, p0.ctypes.data_as(_I64), abi.dptr(i0), abi.dptr(c0),
+                       abi.dptr(smp), ns, float(maxd), float(k_rrt), int(use_gnat), float(time_budget_s),
+                       near.ctypes.data_as(_U32), added.ctypes.data_as(_U32), choice.ctypes.data_as(_I64),
+                       par.ctypes.data_as(_I64), abi.dptr(inc), abi.dptr(cost), st.ctypes.data_as(_U64))
+    m = n0 + int(st[1])
+    return {"nearest": near, "added": added, "parent_choice": choice, "parent": par[:m], "inc": inc[:m],
+            "cost": cost[:m], "processed": int(st[0]), "n_added": int(st[1]), "rewires": int(st[2]),
+            "checks": int(st[3])}
 
 
 def seed_stream(seed, n):
