@@ -118,7 +118,7 @@ class RRTstarGPU:
         typestr = {torch.int64: "<i8", torch.int32: "<i4", torch.float64: "<f8", torch.uint8: "|u1"}[dtype]
 
         class _View:
-            __cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (int(ptr), True), "version": 3}
+            __cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (int(ptr), False), "version": 3}
 
         return torch.as_tensor(_View(), device="cuda").cpu().numpy()
 

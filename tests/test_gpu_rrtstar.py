@@ -52,9 +52,12 @@ def _run(sp, ck, start, samples, batches, gpu, exact):
     if exact:
         np.testing.assert_array_equal(planner.cost[:n], ref["cost"])
         np.testing.assert_array_equal(planner.inc[:n], ref["inc"])
-    else:  # SO3 distances: the device's acos may differ from glibc's by an ulp
-        np.testing.assert_allclose(planner.cost[:n], ref["cost"], rtol=1e-13, atol=0)
-        assert_dist_close(planner.inc[:n], ref["inc"])
+    else:
+        # SO3: the device's acos may differ from glibc's by an ulp, so a steered rotation (slerp
+        # to maxDistance / d) can differ from the oracle's in its last bits, and a distance from it
+        # with a small rotation angle moves by up to ulp / angle (acos' slope near 1)
+        np.testing.assert_allclose(planner.cost[:n], ref["cost"], rtol=1e-12, atol=0)
+        np.testing.assert_allclose(planner.inc[:n], ref["inc"], rtol=1e-12, atol=1e-14)
     assert ref["rewires"] > 0 and planner.stats["rewires"] == ref["rewires"]
     return planner, ref
 
@@ -141,8 +144,9 @@ def test_rrtstar_se3_hypercube_existing_tree(gpu):
     ck = HypercubeChecker(3, 0.1)
     S.set_seed(7)
     smp = S.StateSampler(sp)
-    x = smp.sample_uniform(80000)
-    v = O.is_valid(sp, ck, x)
+    x = smp.sample_uniform(150000)
+    v = O.check_motions_mt(sp, ck, x, x, 16)  # isValid of each (a motion of length 0)
+    assert v.sum() >= 2600
     tree = x[v][:2000]
     parent = np.full(len(tree), -1, np.int64)
     inc = np.zeros(len(tree))
@@ -167,6 +171,6 @@ def test_rrtstar_se3_hypercube_existing_tree(gpu):
     np.testing.assert_array_equal(chosen, ref["parent_choice"])
     n = planner.n
     np.testing.assert_array_equal(planner.parent[:n], ref["parent"])
-    np.testing.assert_allclose(planner.cost[:n], ref["cost"], rtol=1e-13, atol=0)
+    np.testing.assert_allclose(planner.cost[:n], ref["cost"], rtol=1e-12, atol=0)
     assert ref["n_added"] > 50
     planner.close()
