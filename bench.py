@@ -104,6 +104,9 @@ def parse():
                          "k = ceil(1.1 (e + e/6) ln n) = 57 at 10^7, instead of the radius mode")
     ap.add_argument("--rrt-star-queries", type=int, default=1000,
                     help="cfg3: batch of RRT* neighbourhood queries at k = 6,169 (0 = skip)")
+    ap.add_argument("--rrt-star-samples", type=int, default=10_000,
+                    help="RRT* workload (configs[2], the `workloads` record's rrt_star entry): samples per step "
+                         "(0 = skip)")
     ap.add_argument("--workloads", default="auto",
                     help="configs measured after the headline into the line's `workloads` record: 'auto' = "
                          f"{','.join(SUB_WORKLOADS)} when the headline is cfg3 replicated, 'none', or a comma list")
@@ -471,6 +474,147 @@ def rrt_star_knn(torch, run, n_tree, nq=1000, reps=3):
     assert bool((dd[:, 1:] >= dd[:, :-1]).all().item()), "large-k lists must be sorted"
     return {"k": k, "queries": nq, "queries_per_s": nq / (ms * 1e-3), "ms_per_batch": ms, "kernel": name,
             "kernel_ms": kern_ms, "pairs_per_batch": float(nq) * n_tree}
+
+
+def _rrtstar_tree(torch, sp, mv, n_tree, local, batch=10_000):
+    """configs[2]'s starting tree: the first n_tree valid states of the reference stream
+    (RNG::setSeed(42), a tree sampler; UniformValidStateSampler order) joined in batches of `batch`,
+    each state's parent its nearest state among the earlier batches (the first batch hangs off
+    state 0), incCost = that distance, cost = the path length from state 0 — an RRT-like tree built
+    on the device (batched nearest), so that the RRT* steps rewire a realistic tree."""
+    from ompl_amd import NearestNeighborsGPU
+    from ompl_amd import sampling as S
+    from ompl_amd import workloads as W
+
+    S.set_seed(42)
+    ts, qs = S.StateSampler(sp), S.StateSampler(sp)
+    tree, _ = W.reference_valid_states(sp, n_tree, mv.isValid, sampler=ts, chunk=4_000_000)
+    parent = np.zeros(n_tree, np.int64)
+    inc = np.zeros(n_tree)
+    cost = np.zeros(n_tree)
+    parent[0] = -1
+    first = tree[1:batch]
+    inc[1:batch] = mv.distance(np.repeat(tree[:1], len(first), axis=0), first)
+    cost[1:batch] = inc[1:batch]
+    nn = NearestNeighborsGPU(sp, local)
+    nn.add(tree[:batch])
+    for b in range(batch, n_tree, batch):
+        x = tree[b:b + batch]
+        ids, d, _ = nn.nearestKBatch(x, 1)
+        p = ids[:, 0].astype(np.int64)
+        parent[b:b + len(x)] = p
+        inc[b:b + len(x)] = d[:, 0]
+        cost[b:b + len(x)] = cost[p] + d[:, 0]
+        nn.add(x)
+    nn.close()
+    return tree, parent, inc, cost, qs
+
+
+def rrt_star_workload(torch, dev, local, stream, steps, warmup, ns=10_000, n_tree=1_000_000, cpu_seconds=8.0,
+                      cpu=True):
+    """configs[2], RRT* (SURVEY §8f row 1): SE(3) [0,1]^3, the HypercubeBenchmark passage on the
+    translation (edgeWidth 0.1, resolution 0.01), a 10^6-state tree (_rrtstar_tree), then per step a
+    batch of ns samples through RRTstar::solve's iteration (RRTstar.cpp:247-542, defaults:
+    k-nearest, delayCC): the device batch (nearest, steer, checkMotion, neighbourhoods
+    k = ceil(446.5 ln(size + 1)) ~ 6,169, both motion bits of every neighbour — exact for the
+    sequential loop) and the host cost logic (parent in cost order, rewiring, child costs,
+    ompl_amd/rrtstar.py).  value = RRT* iterations (samples processed) per second, device + host.
+    cpu_baseline: the oracle's sequential RRT* loop (oracle/rrtstar.cpp) over the GNAT restatement
+    on the same tree and samples, one thread (the reference's RRT* is single-threaded)."""
+    from ompl_amd import DiscreteMotionValidatorGPU
+    from ompl_amd.checkers import HypercubeChecker
+    from ompl_amd.rrtstar import RRTstarGPU
+    from ompl_amd.spaces import SE3StateSpace
+
+    t_setup = time.perf_counter()
+    sp, ck = SE3StateSpace(0.0, 1.0), HypercubeChecker(3, 0.1)
+    maxd = 0.2 * sp.getMaximumExtent()
+    mv0 = DiscreteMotionValidatorGPU(sp, ck, local)
+    tree, parent, inc, cost, qs = _rrtstar_tree(torch, sp, mv0, n_tree, local)
+    mv0.close()
+    samples_h = qs.sample_uniform(ns * (warmup + steps))
+    samples = torch.from_numpy(samples_h).to(dev)
+    planner = RRTstarGPU(sp, ck, maxd, local, stream.cuda_stream)
+    planner.add_tree(tree, parent, inc, cost)
+    near = torch.empty(ns, dtype=torch.int32, device=dev)
+    added = torch.empty(ns, dtype=torch.int32, device=dev)
+    incs = torch.empty(ns, dtype=torch.float64, device=dev)
+    setup_s = time.perf_counter() - t_setup
+
+    def step(i, ev=None):
+        if ev:
+            ev[0].record(stream)
+        res = planner.batch_device(samples[i * ns].data_ptr(), ns, near.data_ptr(), added.data_ptr(), incs.data_ptr())
+        if ev:
+            ev[1].record(stream)
+        t0 = time.perf_counter()
+        planner.commit(near, added, incs, res)
+        return res, time.perf_counter() - t0
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    planner.nn.profile(True)
+    planner.nn.kernel_time()
+    k0 = planner.nn.kernel_time()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+    a0, e0 = planner.stats["added"], planner.stats["neighbours"]
+    host_s = 0.0
+    rounds = []
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for j in range(steps):
+        res, hs = step(warmup + j, ev[j])
+        host_s += hs
+        rounds.append(int(res.rounds))
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    k1 = planner.nn.kernel_time()
+    planner.nn.profile(False)
+    dev_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    n_added = planner.stats["added"] - a0
+    E = planner.stats["neighbours"] - e0
+    units = steps * 2 * ns + n_added + 2 * E  # nearest + steer checkMotion per sample, kNN per added, 2 bits per entry
+    kern_ms = (k1[0] - k0[0]) / max(k1[1] - k0[1], 1)
+    n_mid = n_tree + planner.stats["added"] - n_added / 2
+    pairs = (n_added / steps) * n_mid  # the neighbourhood kNN's fill pass: every (added state, stored state) pair
+    achieved = pairs * F_SE3 / (kern_ms * 1e-3) / 1e12
+    line = {
+        "metric": "RRT* iterations/sec (nearest + steer + checkMotion + neighbourhood + motion bits + cost logic), "
+                  "SE(3) 10^6-state tree",
+        "value": steps * ns / elapsed, "unit": "RRT* iterations/s", "steps": steps, "warmup": warmup,
+        "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True, "dtype": "f32 screen + f64 exact",
+        "config": {"workload": "configs[2]: SE(3) RRT* (k-nearest, delayCC), HypercubeBenchmark passage on the "
+                               "translation (edgeWidth 0.1), resolution 0.01", "tree_states": n_tree,
+                   "samples_per_step": ns, "k_rrt": planner.k_rrt, "max_distance": maxd,
+                   "tree": "the first 10^6 valid states of the reference stream, parents = nearest among earlier "
+                           "batches of 10^4 (an RRT-like tree), costs = path lengths"},
+        "nn_queries_plus_motion_checks_per_s": units / elapsed,
+        "phase_ms": {"device_batch": dev_ms, "host_cost_logic": host_s * 1e3 / steps},
+        "added_per_step": n_added / steps, "neighbourhood_entries_per_step": E / steps,
+        "fixed_point_rounds": rounds, "rewires": planner.stats["rewires"],
+        "setup_s": setup_s,
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_TFLOPS["f32"], "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_TFLOPS["f32"], "traffic": None, "kernel": k1[2], "kernel_ms": kern_ms,
+                     "algorithmic": f"the neighbourhood kNN's fp32 fill pass ({k1[2]}): every (added state, stored "
+                                    f"state) pair, {pairs:.4g} per step x {F_SE3} flop"},
+    }
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as O
+
+        t1 = time.perf_counter()
+        ref = O.rrtstar(sp, ck, tree, parent, inc, cost, samples_h[warmup * ns:(warmup + 1) * ns], maxd,
+                        planner.k_rrt, use_gnat=True, time_budget_s=cpu_seconds)
+        line["cpu_baseline"] = {
+            "value": ref["processed"] / ref["loop_s"], "unit": "RRT* iterations/s", "cores": 1, "kind": "port",
+            "sample": (f"the oracle's sequential RRT* loop (oracle/rrtstar.cpp) over the GNAT restatement, same tree "
+                       f"and the first timed step's samples: {ref['processed']} iterations ({ref['n_added']} added, "
+                       f"{ref['rewires']} rewires, {ref['checks']} checkMotion calls) in {ref['loop_s']:.2f} s on one "
+                       f"thread (the reference's RRT* is single-threaded); GNAT build excluded"),
+            "wall_s": time.perf_counter() - t1}
+    planner.close()
+    return line
 
 
 def index_maintenance(torch, run, local, batches=10, batch=100, nq=1000):
@@ -1059,6 +1203,8 @@ def main():
     subs = {}
     names = [] if args.workloads == "none" else (
         list(SUB_WORKLOADS) if args.workloads == "auto" else [w for w in args.workloads.split(",") if w])
+    want_rrt_star = "rrt_star" in names or args.workloads == "auto"
+    names = [w for w in names if w != "rrt_star"]
     if args.workload != "cfg3" or args.partition != "replicated":
         names = [] if args.workloads == "auto" else names
     for name in names:
@@ -1071,6 +1217,15 @@ def main():
             subs[name] = sline
         srun.close()
         del srun
+        torch.cuda.synchronize(dev)
+
+    if (rank == 0 and world == 1 and args.workload == "cfg3" and args.partition == "replicated"
+            and want_rrt_star and args.rrt_star_samples > 0):
+        t0 = time.perf_counter()
+        sub = rrt_star_workload(torch, dev, local, stream, args.steps, args.warmup, ns=args.rrt_star_samples,
+                                cpu_seconds=args.sub_cpu_seconds, cpu=not args.no_cpu_baseline)
+        sub["wall_s"] = time.perf_counter() - t0
+        subs["rrt_star"] = sub
         torch.cuda.synchronize(dev)
 
     if rank == 0:

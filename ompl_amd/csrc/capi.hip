@@ -1653,7 +1653,10 @@ ompl_gpu_status rrtstar_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_
     const double *qf = nullptr;
     ompl_gpu_status s = device_query_features(h, d_samples, ns, &qf);
     if (s != OMPL_GPU_OK) return s;
+    const bool prof = h->profile;  // the profile bracket (ompl_gpu_nn_profile) goes to the neighbourhoods' kNN
+    h->profile = false;
     s = knn_features_locked(h, qf, ns, 1, near_i, near_d);
+    h->profile = prof;
     if (s != OMPL_GPU_OK) return s;
     HIP_OR_FAIL(hipMemcpyAsync(src, near_i, sizeof(uint32_t) * ns, hipMemcpyDeviceToDevice, st));
     HIP_OR_FAIL(launch_rrtstar_steer(h->sp, h->raw, h->cap, d_samples, n, src, xb, maxd, from, xa, inc, st));

@@ -96,8 +96,9 @@ void oracle_prm_causal(const ompl_gpu_space *sp, const ompl_gpu_checker *ck, con
  * the tree (states0, parent0 (-1 = root), inc0, cost0) over the given samples; use_gnat: the GNAT
  * restatement as the neighbour structure (else brute force); time_budget_s > 0 stops early.
  * Per sample: nearest_out, added_out (0xFFFFFFFF: not added), parent_choice (-1); the final tree
- * (n0 + added entries) in parent_out / inc_out / cost_out (may be NULL); stats[4] = samples
- * processed, added, rewires, checkMotion calls.  Returns the samples processed. */
+ * (n0 + added entries) in parent_out / inc_out / cost_out (may be NULL); stats[5] = samples
+ * processed, added, rewires, checkMotion calls, nanoseconds in the loop (the neighbour structure's
+ * build excluded).  Returns the samples processed. */
 uint64_t oracle_rrtstar(const ompl_gpu_space *sp, const ompl_gpu_checker *ck, const double *states0, size_t n0,
                         const int64_t *parent0, const double *inc0, const double *cost0, const double *samples,
                         size_t ns, double maxd, double k_rrt, int use_gnat, double time_budget_s, uint32_t *nearest_out,

@@ -192,7 +192,7 @@ def rrtstar(sp, ck, states0, parent0, inc0, cost0, samples, maxd, k_rrt, use_gna
     par = np.zeros(n0 + ns, np.int64)
     inc = np.zeros(n0 + ns)
     cost = np.zeros(n0 + ns)
-    st = np.zeros(4, np.uint64)
+    st = np.zeros(5, np.uint64)
     lib.oracle_rrtstar(C.byref(s), C.byref(c), abi.dptr(x0), n0, p0.ctypes.data_as(_I64), abi.dptr(i0), abi.dptr(c0),
                        abi.dptr(smp), ns, float(maxd), float(k_rrt), int(use_gnat), float(time_budget_s),
                        near.ctypes.data_as(_U32), added.ctypes.data_as(_U32), choice.ctypes.data_as(_I64),
@@ -200,7 +200,7 @@ def rrtstar(sp, ck, states0, parent0, inc0, cost0, samples, maxd, k_rrt, use_gna
     m = n0 + int(st[1])
     return {"nearest": near, "added": added, "parent_choice": choice, "parent": par[:m], "inc": inc[:m],
             "cost": cost[:m], "processed": int(st[0]), "n_added": int(st[1]), "rewires": int(st[2]),
-            "checks": int(st[3])}
+            "checks": int(st[3]), "loop_s": float(st[4]) * 1e-9}
 
 
 def seed_stream(seed, n):

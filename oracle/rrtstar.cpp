@@ -210,6 +210,7 @@ extern "C" uint64_t oracle_rrtstar(const ompl_gpu_space *sp, const ompl_gpu_chec
         stats[1] = added;
         stats[2] = rewires;
         stats[3] = calls;
+        stats[4] = (uint64_t)(1e9 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     }
     if (t.gnat) oracle_gnat_destroy(t.gnat);
     return processed;
