@@ -95,6 +95,9 @@ def parse():
     ap.add_argument("--rrt-iters", type=int, default=2000, help="device RRT iterations after the bench (0 = skip)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra measurements (index maintenance, sphere checker, RRT* k) after the timed steps")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="replicated tree: --queries per GPU (weak, the default) or --queries in total split over "
+                         "the GPUs (strong)")
     ap.add_argument("--partition", default="replicated", choices=["replicated", "tree"],
                     help="cfg3: replicated tree + sharded samples (default, weak scaling), or the tree sharded over "
                          "the ranks with every sample answered by every shard and the per-shard top-k lists merged "
@@ -693,6 +696,14 @@ class Runner:
         self.radius = None
         self.tree_mode = args.partition == "tree"
         world = int(os.environ.get("WORLD_SIZE", "1"))
+        # strong scaling (replicated tree): a fixed global batch of args.queries samples, rank r
+        # answering its contiguous share; weak: args.queries per rank
+        self.strong = getattr(args, "scaling", "weak") == "strong" and not self.tree_mode
+        if self.strong:
+            if wl not in ("cfg3", "cfg2"):
+                raise SystemExit("bench.py: --scaling strong is implemented for cfg3 / cfg2")
+            self.global_q = nq
+            nq = (nq + world - 1) // world
         if wl == "cfg3":
             self.sp, self.ck = SE3StateSpace(0.0, 1.0), HypercubeChecker(3, 0.1)
         elif wl == "cfg2":
@@ -718,7 +729,9 @@ class Runner:
             # tree mode: one global batch of samples for every rank (the rank-0 slice of the stream)
             tree, qa = shared_inputs(wl, self.sp, args.tree, nq * world, None, dist, dev)
             r0 = 0 if self.tree_mode else rank
-            self.tree, q = tree, np.ascontiguousarray(qa[r0 * nq:(r0 + 1) * nq])
+            hi = min((r0 + 1) * nq, self.global_q) if self.strong else (r0 + 1) * nq
+            self.tree, q = tree, np.ascontiguousarray(qa[r0 * nq:hi])
+            nq = len(q)
         elif wl == "cfg5":  # sample sets hold valid states (ImplicitGraph.cpp:981)
             self.tree, qa = shared_inputs("cfg5", self.sp, args.tree, nq * world, self.mv.isValid, dist, dev)
             r0 = 0 if self.tree_mode else rank  # tree mode: every shard answers the same vertices
@@ -910,6 +923,11 @@ class Runner:
         a = self.args
         base = {"tree_states": a.tree, "queries_per_gpu": self.nq,
                 "parallelism": f"queries sharded over {world} GPU(s), tree replicated"}
+        if self.strong:
+            base.update(queries_per_gpu=None, queries_per_step=self.global_q, queries_this_rank=self.nq,
+                        parallelism=(f"a fixed global batch of {self.global_q} samples split over {world} GPU(s) "
+                                     f"(about {self.global_q // world} each), tree replicated, no collective in the "
+                                     f"data path"))
         if self.tree_mode and a.workload == "cfg5":
             base.update(queries_per_gpu=None, queries_per_step=self.nq, partition="tree",
                         parallelism=(f"sample set sharded over {world} GPU(s) ({a.tree // world} samples each), every "
@@ -1031,6 +1049,10 @@ def spawn_ranks(n):
 
 
 SUB_WORKLOADS = {  # the default line's `workloads` record: every other config, same steps / warmup
+    # the headline's strong-scaling forms: 10^5 samples in total over the N GPUs on the replicated
+    # tree, and the tree sharded over the ranks (every sample answered by every shard, merged)
+    "cfg3_strong": {"workload": "cfg3", "scaling": "strong"},
+    "cfg3_tree": {"workload": "cfg3", "partition": "tree"},
     "cfg2": {"workload": "cfg2"},
     "cfg4": {"workload": "cfg4"},
     "cfg5": {"workload": "cfg5"},
@@ -1043,7 +1065,8 @@ def sub_args(args, spec):
     a = argparse.Namespace(**vars(args))
     a.workload = spec["workload"]
     a.bitstar_knn = spec.get("bitstar_knn", False)
-    a.partition = "replicated"
+    a.partition = spec.get("partition", "replicated")
+    a.scaling = spec.get("scaling", "weak")
     a.tree, a.queries, a.k = DEFAULTS[a.workload]
     a.exact = False
     return a
@@ -1117,7 +1140,7 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "strong" if run.tree_mode else "weak",
+        "scaling": "strong" if (run.tree_mode or run.strong) else "weak",
         "vs_baseline": None,
         "dtype": "f32 screen + f64 certify" if screen else "f64",
         "config": run.config(world),
@@ -1211,7 +1234,9 @@ def main():
         t0 = time.perf_counter()
         sa = sub_args(args, SUB_WORKLOADS[name])
         sline, srun = measure(sa, torch, dev, local, rank, world, dist, stream, args.sub_cpu_seconds)
-        if rank == 0:
+        if rank == 0 and sa.workload == args.workload:  # the headline's workload in another partition
+            sline["cpu_baseline"] = {"same_as": "the headline line's cpu_baseline (the same samples and tree)"}
+        elif rank == 0:
             attach_cpu_baseline(sline, srun, sa, rank, world, args.sub_cpu_seconds)
             sline["wall_s"] = time.perf_counter() - t0
             subs[name] = sline

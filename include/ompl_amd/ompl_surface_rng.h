@@ -59,7 +59,7 @@ public:
             std::fprintf(stderr, "Warning: Random generator seed cannot be 0. Using 1 instead.\n");
             seed = 1;
         }
-        sGen_.seed(seed);  // reseeds even after seeds were drawn (the reference only logs)
+        sGen_.seed(seed);  // as the reference: reseeds after the error too (RandomNumbers.cpp:71-97)
     }
     std::uint_fast32_t nextSeed() {
         std::lock_guard<std::mutex> lk(mu_);

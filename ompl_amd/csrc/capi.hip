@@ -17,6 +17,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -108,6 +109,7 @@ struct ompl_gpu_nn {
     DevBuf rrt_n, rrt_pd, rrt_pi;  // device RRT growth: live size + barrier words, per-block partial minima
     int rrt_coop = -1;             // persistent RRT grid size (0: two-launch form), found on first use
     int rrt_abort_streak = 0;      // consecutive aborted persistent grids (a device kept busy by others)
+    int rrt_latched = 0;           // two-launch batches since the streak latched (retry after kRrtRetryAfter)
     bool rrt_spin_read = false;    // OMPL_GPU_RRT_SPIN_LIMIT read (tests)
     uint64_t rrt_spin_override = 0;
     void *rrt_sync = nullptr;      // its uncached synchronisation record
@@ -249,8 +251,7 @@ ompl_gpu_status ompl_gpu_nn_create(ompl_gpu_nn **out, const ompl_gpu_space *spac
     h->sp = sp;
     h->g = g;
     h->rows32 = fp32_rows(sp, g);
-    const char *exact = std::getenv("OMPL_GPU_EXACT_ONLY");
-    h->fast = !(exact && exact[0] == '1');
+    h->fast = true;  // ompl_gpu_nn_set_exact_only(h, 1): the fp64 kernels only
     hipError_t e = hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
@@ -357,8 +358,16 @@ static void host_features_batch(const DevSpace &sp, const FeatGeom &g, const dou
     std::vector<std::thread> pool;
     pool.reserve(T - 1);
     const size_t chunk = (n + T - 1) / T;
-    for (size_t t = 1; t < T; ++t) pool.emplace_back(work, std::min(n, t * chunk), std::min(n, (t + 1) * chunk));
+    size_t done = chunk;  // rows [0, done) are covered by this thread and the started ones
+    try {
+        for (size_t t = 1; t < T; ++t) {
+            pool.emplace_back(work, std::min(n, t * chunk), std::min(n, (t + 1) * chunk));
+            done = std::min(n, (t + 1) * chunk);
+        }
+    } catch (const std::system_error &) {  // no thread to be had: this one does the rest
+    }
     work(0, std::min(n, chunk));
+    work(done, n);
     for (std::thread &th : pool) th.join();
 }
 
@@ -460,6 +469,7 @@ ompl_gpu_status ompl_gpu_nn_clear(ompl_gpu_nn *h) {
     h->sorted.built = false;  // keeps its allocations
     h->aos_n = 0;
     h->removed.clear();
+    h->rrt_abort_streak = h->rrt_latched = 0;
     return OMPL_GPU_OK;
 }
 
@@ -587,13 +597,16 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
             HIP_OR_FAIL(h->large_counter.ensure(2 * sizeof(unsigned long long)));
             HIP_OR_FAIL(hipMemsetAsync(h->large_counter.p, 0, 2 * sizeof(unsigned long long), h->stream));
         }
-        const bool raw_rows = h->sp.kind != OMPL_GPU_SPACE_KCHAIN;  // features = raw coordinates
-        if (raw_rows) {
-            ompl_gpu_status s = ensure_aos(h);
-            if (s != OMPL_GPU_OK) return s;
+        // the select's exact pass reads one contiguous fp64 row per candidate from the AoS copy of
+        // the raw states (features = raw coordinates outside the chain); only the select path
+        // reads it, and without room for it the select reads the SoA features instead
+        bool aos = wsb && h->sp.kind != OMPL_GPU_SPACE_KCHAIN;
+        if (aos && ensure_aos(h) != OMPL_GPU_OK) {
+            (void)hipGetLastError();
+            aos = false;
         }
         HIP_OR_FAIL(launch_knn_large(h->sp, h->g, h->feat, h->feat32, h->cap, n_end,
-                                     raw_rows ? (const double *)h->raw_aos.p : nullptr, aos_width(h), d_qf,
+                                     aos ? (const double *)h->raw_aos.p : nullptr, aos_width(h), d_qf,
                                      (uint32_t)nq, k, (float)h->absmax * (1.0f + 1e-6f), (float)h->qeta * 1.01f,
                                      (float)dmax, d_dist, d_ids, size_t(4) << 30, h->num_cus, h->stream,
                                      wsb ? h->ws.p : nullptr, wsb ? h->ws.bytes : 0,
@@ -606,10 +619,8 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
         if (cull) {
             ompl_gpu_status s = ensure_sorted(h);
             if (s != OMPL_GPU_OK) return s;
-            if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN && chain_q16_enabled())
+            if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN)
                 HIP_OR_FAIL(refresh_chain_rows16(h->g, &h->sorted, h->stream));
-            if (h->sp.kind == OMPL_GPU_SPACE_SE3 && se3_knn_q16_enabled())
-                HIP_OR_FAIL(refresh_se3_rows16(h->lo, h->hi, &h->sorted, h->stream));
         }
         FastBounds b = current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
@@ -731,7 +742,7 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
         // culled walk over the Morton-sorted copy (knn_fast_impl.h)
         ompl_gpu_status s = ensure_sorted(h);
         if (s != OMPL_GPU_OK) return s;
-        if (h->sp.kind == OMPL_GPU_SPACE_SE3 && se3_q16_enabled())
+        if (h->sp.kind == OMPL_GPU_SPACE_SE3)
             HIP_OR_FAIL(refresh_se3_rows16(h->lo, h->hi, &h->sorted, h->stream));
         FastBounds b = current_bounds(h);
         b.absmax = (float)h->absmax * (1.0f + 1e-6f);
@@ -1466,7 +1477,7 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     if (n0 && rows && h->fast && h->cull && cull_supported(h->sp) && screen_safe(h)) {
         ompl_gpu_status s = ensure_sorted(h);
         if (s != OMPL_GPU_OK) return s;
-        if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN && chain_q16_enabled())
+        if (h->sp.kind == OMPL_GPU_SPACE_KCHAIN)
             HIP_OR_FAIL(refresh_chain_rows16(h->g, &h->sorted, h->stream));
     }
     // batch features (host, as add() computes them) and raw rows
@@ -1507,11 +1518,8 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     HIP_OR_FAIL(launch_prm_causal(h->sp, h->g, false, bf, (uint32_t)j0, (uint32_t)rows, (uint32_t)n0, dkj, sd, si, kq,
                                   len, nullptr, nullptr, nullptr, p32, (uint32_t)m,
                                   (unsigned long long *)(len + rows + 1), h->stream));
-    size_t sb = 0;
-    HIP_OR_FAIL(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, len, off, (int)rows + 1, h->stream));
-    HIP_OR_FAIL(h->tmp.ensure(sb));
-    sb = h->tmp.bytes;
-    HIP_OR_FAIL(hipcub::DeviceScan::ExclusiveSum(h->tmp.p, sb, len, off, (int)rows + 1, h->stream));
+    HIP_OR_FAIL(h->tmp.ensure(exclusive_scan_u64_workspace(rows)));
+    HIP_OR_FAIL(launch_exclusive_scan_u64(len, rows, off, h->tmp.p, h->stream));  // off[rows] = the total
     uint64_t tot = 0, longest = 0;
     HIP_OR_FAIL(hipMemcpyAsync(&tot, off + rows, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(&longest, len + rows + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
@@ -1556,12 +1564,8 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     HIP_OR_FAIL(h->prm_cnt64.ensure(sizeof(uint64_t) * (rows + 1)));
     uint64_t *eoff = (uint64_t *)h->prm_eoff.p, *c64 = (uint64_t *)h->prm_cnt64.p;
     HIP_OR_FAIL(launch_widen_u32(d_cnt, (uint32_t)rows, c64, h->stream));
-    HIP_OR_FAIL(hipMemsetAsync(c64 + rows, 0, sizeof(uint64_t), h->stream));
-    size_t need = 0;
-    HIP_OR_FAIL(hipcub::DeviceScan::ExclusiveSum(nullptr, need, c64, eoff, (int)rows + 1, h->stream));
-    HIP_OR_FAIL(h->tmp.ensure(need));
-    sb = h->tmp.bytes;
-    HIP_OR_FAIL(hipcub::DeviceScan::ExclusiveSum(h->tmp.p, sb, c64, eoff, (int)rows + 1, h->stream));
+    HIP_OR_FAIL(h->tmp.ensure(exclusive_scan_u64_workspace(rows)));
+    HIP_OR_FAIL(launch_exclusive_scan_u64(c64, rows, eoff, h->tmp.p, h->stream));
     uint64_t E = 0;
     HIP_OR_FAIL(hipMemcpyAsync(&E, eoff + rows, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
     if (n0) {
@@ -1915,8 +1919,14 @@ ompl_gpu_status rrt_run(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_samples
     if (h->sp.kind == OMPL_GPU_SPACE_SE3) h->qeta = std::max(h->qeta, 1e-12);
     // the persistent form screens in fp32 (rrt.hip): it needs the fp32 rows and screenable
     // coordinates, and starts from the store's bounds (words 7 = B, 28 = eta of its record)
-    // after two aborts in a row the handle keeps the two-launch form: its device is shared with
-    // long kernels, and every further persistent try would spin up to kSpinLimit first
+    // after two aborts in a row the handle takes the two-launch form for the next kRrtRetryAfter
+    // batches (its device is shared with long kernels, and every persistent try would spin up to
+    // kSpinLimit first), then tries the persistent form again; clear() resets the latch
+    constexpr int kRrtRetryAfter = 64;
+    if (h->rrt_abort_streak >= 2 && ++h->rrt_latched > kRrtRetryAfter) {
+        h->rrt_abort_streak = 0;
+        h->rrt_latched = 0;
+    }
     const bool coop = h->rrt_sync && h->rows32 && screen_safe(h) && h->rrt_abort_streak < 2;
     if (coop) {
         // OMPL_GPU_RRT_SPIN_LIMIT (tests): a small spin limit forces the abort-and-re-run path;

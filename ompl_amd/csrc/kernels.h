@@ -157,21 +157,16 @@ hipError_t tombstone_sorted_store(SortedStore *s, uint64_t id, hipStream_t st);
 // The culled chain scan's 16-bit copy of the joint positions.  Coordinate f of link i = f mod nm
 // lies in [-(i + 1), i + 1] (a sum of i + 1 unit vectors); its code is rint((x + i + 1) * S_i),
 // S_i = kChainQ16 / (2 (i + 1)), clamped to [0, kChainQ16]; 0xFFFF in coordinate 0 marks a state
-// with a NaN row (padding, tombstones).  OMPL_GPU_CHAIN_Q16=0 keeps the fp32 rows (A/B).
+// with a NaN row (padding, tombstones).
 constexpr float kChainQ16 = 65534.f;
-bool chain_q16_enabled();
 hipError_t refresh_chain_rows16(const FeatGeom &g, SortedStore *s, hipStream_t st);
 // bound on |d16 - d32| of one screened chain distance: link * sum_i sqrt(2) * 0.6 quanta * 2 (i + 1) / kChainQ16
 // (0.5 for the rounding, the rest for the fp32 scaling of state and query)
 double chain_q16_error(const DevSpace &sp);
-// SE3 radius walk (default; OMPL_GPU_RADIUS_Q16=0: the fp32 rows): the 16-bit copy over the
-// stored box [lo, hi] of the translation, and the bound on |d16 - d32| it adds to the threshold.
-// Measured on cfg5: 1.694 ms per walk against 1.741-1.783 on the fp32 rows.
-bool se3_q16_enabled();
-// the SE3 kNN group walk on the same copy (A/B only, OMPL_GPU_KNN_Q16=1): measured slower —
-// cfg3 1.383 against 1.263 ms, cfg5k 4.58-4.62 against 4.22-4.28 ms — the decode costs more
-// VALU than the halved tile bytes save in a walk bound by issue and latency
-bool se3_knn_q16_enabled();
+// SE3 radius walk: the 16-bit copy over the stored box [lo, hi] of the translation, and the
+// bound on |d16 - d32| it adds to the threshold.  Measured on cfg5: 1.694 ms per walk against
+// 1.741-1.783 on the fp32 rows.  (The kNN group walk on the same copy measured slower — cfg3 1.383
+// against 1.263 ms: its decode costs more VALU than the halved tile bytes save.)
 hipError_t refresh_se3_rows16(const double *lo, const double *hi, SortedStore *s, hipStream_t st);
 double se3_q16_error(const DevSpace &sp, const Q16Geo &q);
 void free_sorted_store(SortedStore *s);
@@ -338,7 +333,9 @@ hipError_t launch_rrtstar_sample_offsets(const uint8_t *valid, const uint32_t *r
 // ---- exclusive prefix sums (scan.hip): out[0..n], out[n] = the total; ws of
 // exclusive_scan_u64_workspace(n) bytes; asynchronous
 size_t exclusive_scan_u64_workspace(uint64_t n);
-hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t n, uint64_t *out, void *ws, hipStream_t st);
+// max_out (optional, device): the largest of in[0, n)
+hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t n, uint64_t *out, void *ws, hipStream_t st,
+                                     uint64_t *max_out = nullptr);
 
 // radius search, pass 1 (count per (query, chunk)) and pass 2 (fill CSR in id order).
 struct RadiusPlan {

@@ -967,7 +967,7 @@ __global__ __launch_bounds__(64) void csr_merge_kernel(const uint64_t *__restric
 
 hipError_t launch_csr_merge(const uint64_t *offs, uint32_t lists, uint32_t nq, const uint32_t *ids, const double *d,
                             uint64_t stride, uint64_t *out_off, uint32_t *out_i, double *out_d, hipStream_t st) {
-    if (nq == 0) return hipSuccess;
+    if (nq == 0) return hipMemsetAsync(out_off, 0, sizeof(uint64_t), st);  // out_off[0]: no entries
     hipLaunchKernelGGL(csr_merge_kernel, dim3(nq), dim3(64), 0, st, offs, lists, nq, ids, d, stride, out_off, out_i,
                        out_d);
     return hipGetLastError();

@@ -100,22 +100,6 @@ __global__ void se3_rows16_kernel(const float *__restrict__ rows, uint32_t n_pad
 }
 }  // namespace
 
-bool se3_q16_enabled() {
-    static const bool on = [] {
-        const char *v = std::getenv("OMPL_GPU_RADIUS_Q16");
-        return v ? std::atoi(v) != 0 : true;
-    }();
-    return on;
-}
-
-bool se3_knn_q16_enabled() {
-    static const bool on = [] {
-        const char *v = std::getenv("OMPL_GPU_KNN_Q16");
-        return v ? std::atoi(v) != 0 : false;
-    }();
-    return on;
-}
-
 hipError_t refresh_se3_rows16(const double *lo, const double *hi, SortedStore *s, hipStream_t st) {
     if (!s->built || !s->rows || s->ntiles == 0) return hipSuccess;
     if (s->rows16 && s->gen16 == s->gen) return hipSuccess;
@@ -137,21 +121,27 @@ hipError_t refresh_se3_rows16(const double *lo, const double *hi, SortedStore *s
     return hipSuccess;
 }
 
-// per coordinate the decoded value is within 0.52 step of the fp32 row (no clamping: the
-// ranges hold every stored value) (0.5 rounding, the rest
-// the fp32 scaling); the translation gap moves by <= sqrt(3) of that, the chord by <= |dq| <= 2 of
-// the quaternion's, and theta(c) = 2 asin(c / 2) by <= 1.415 |dc| on c <= sqrt(2) (+ 5 %)
+// per coordinate the decoded value lo + code * step is within 0.52 step of the fp32 row (no
+// clamping: the ranges hold every stored value; 0.5 for the rounding of the code, the rest the
+// fp32 scaling) plus the rounding of that fp32 fmaf itself, half an ulp of the largest decoded
+// magnitude (max(|lo|, |lo + ext|)): a box far from the origin with a narrow extent has steps near
+// that ulp.  The translation gap moves by <= sqrt(3) of the per-coordinate error, the
+// chord by <= |dq| <= 2 of the quaternion's, and theta(c) = 2 asin(c / 2) by <= 1.415 |dc| on
+// c <= sqrt(2) (+ 5 %)
 double se3_q16_error(const DevSpace &sp, const Q16Geo &q) {
-    const double st = std::max({(double)q.step[0], (double)q.step[1], (double)q.step[2]});
-    return sp.w0 * 1.7320508075688772 * 0.52 * st * 1.01 + sp.w1 * 1.415 * 2.0 * 0.52 * (double)q.step[3] * 1.05 + 1e-7;
-}
-
-bool chain_q16_enabled() {
-    static const bool on = [] {
-        const char *v = std::getenv("OMPL_GPU_CHAIN_Q16");
-        return v ? std::atoi(v) != 0 : true;
-    }();
-    return on;
+    auto half_ulp = [](double m) {
+        const float f = (float)m;
+        return 0.5 * ((double)std::nextafter(f, __builtin_inff()) - (double)f);
+    };
+    double st = 0.0, ut = 0.0;
+    for (int c = 0; c < 3; ++c) {
+        st = std::max(st, (double)q.step[c]);
+        const double top = (double)q.lo[c] + (double)q.step[c] * (double)kQ16Max;
+        ut = std::max(ut, half_ulp(std::max(std::fabs((double)q.lo[c]), std::fabs(top))));
+    }
+    const double uq = half_ulp(1.001);
+    return sp.w0 * 1.7320508075688772 * (0.52 * st + ut) * 1.01 +
+           sp.w1 * 1.415 * 2.0 * (0.52 * (double)q.step[3] + uq) * 1.05 + 1e-7;
 }
 
 double chain_q16_error(const DevSpace &sp) {

@@ -238,11 +238,9 @@ __global__ void home_scatter_kernel(const uint32_t *__restrict__ keys, const uin
 inline hipError_t sort_home_keys(char *cub, size_t cub_bytes, const uint32_t *keys, uint32_t *keys2,
                                  const uint32_t *idx, uint32_t *perm, uint32_t nq, int key_bits, hipStream_t st,
                                  uint32_t *qcount = nullptr, uint32_t bins = 0) {
-    static const int counting = [] {  // A/B switch: OMPL_GPU_QSORT=0 -> the radix sort
-        const char *v = std::getenv("OMPL_GPU_QSORT");
-        return v ? std::atoi(v) : 1;
-    }();
-    if (counting && qcount && bins && key_bits < 32 && cub_bytes >= 4ull * nq) {
+    // the counting sort (measured 0.081-0.083 ms against 0.113-0.115 ms for the radix sort of the
+    // nn phase outside the walk on cfg3); the radix sort stays for Morton keys (32 bits)
+    if (qcount && bins && key_bits < 32 && cub_bytes >= 4ull * nq) {
         uint32_t *slot = (uint32_t *)cub;  // the radix sort's temporary storage holds the slots
         hipError_t e = hipMemsetAsync(qcount, 0, 4ull * bins, st);
         if (e != hipSuccess) return e;
@@ -603,20 +601,6 @@ __device__ __forceinline__ void wave_merge_sorted_k(uint64_t &L, uint64_t c, int
 // 1.29-1.30 ms, cfg5k 4.06 / 4.10 / 3.93-3.97 / 4.03 / 4.29 ms, cfg2 flat (profiles/r4_ab)
 constexpr int kBulkThreshold = 16;
 
-// Group-walk A/B features (variant builds, make variant VARIANT=n):
-//   WALK_CASCADE (7, 9, 12): square-root-free rejects before the chord and square roots;
-//   WALK_DYN (8, 9, 12): tile bounds only for the queries whose super-tile bound passes;
-//   WALK_TFIRST (12): a mask pass whose translation gaps alone exclude every (tile, query) pair
-//   skips its rotation gaps.
-#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 7 || OMPL_AMD_VARIANT == 9 || OMPL_AMD_VARIANT == 12)
-#define OMPL_WALK_CASCADE 1
-#endif
-#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 8 || OMPL_AMD_VARIANT == 9 || OMPL_AMD_VARIANT == 12)
-#define OMPL_WALK_DYN 1
-#endif
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 12
-#define OMPL_WALK_TFIRST 1
-#endif
 // translation part of box_lb<SE3>: the squared gap of query row q to box bx
 __device__ __forceinline__ float box_tgap2(const float *bx, const float *q, int NB) {
     float tg = 0.f;
@@ -629,35 +613,20 @@ __device__ __forceinline__ float box_tgap2(const float *bx, const float *q, int 
 }
 
 // K2: lanes per query in the output (16 / 32 / 64); k2 <= K2: the list length the walk keeps
-// (the certificate's margin: k + 3 for the culled spaces, whose screen error is small)
-// Q16 (SE3, OMPL_GPU_KNN_Q16=1): tiles from the 16-bit copy (SortedStore::rows16), decoded
-// when scanned; the lists hold d16, every box bound is lowered by qerr >= |d16 - d32|
-// (se3_q16_error) and the certificate's error grows by the same qerr.
-template <int SP, int F, int K2, int G, int MINW, bool QS, bool Q16 = false>
-__global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
+// (the certificate's margin: k + 3 for the culled spaces, whose screen error is small).
+// (Measured and rejected, DESIGN §8: tile bounds only for the queries whose super-tile bound
+// passes; square-root-free rejects before the chord; a translation-only first mask pass; tiles
+// from a 16-bit copy.)
+template <int SP, int F, int K2, int G, bool QS>
+__global__ __launch_bounds__(64) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
     const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
     uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi,
-    unsigned long long *__restrict__ counters, int bulk, int k2, int recheck,
-    const uint32_t *__restrict__ rows16 = nullptr, Q16Geo qg = Q16Geo{}, float qerr = 0.f) {
-    static_assert(!Q16 || SP == OMPL_GPU_SPACE_SE3, "16-bit rows: SE3");
+    unsigned long long *__restrict__ counters, int k2) {
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
-    // a tile in flight: the R fp32 rows, or (Q16) 4 raw words decoded when it is scanned
-    constexpr int RW = Q16 ? 4 : R;
-    using TileE = std::conditional_t<Q16, uint32_t, float>;
     constexpr int GH = G / 2;
     static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
-#if defined(OMPL_WALK_DYN)
-    constexpr bool kDyn = true;
-#else
-    constexpr bool kDyn = false;
-#endif
-#if defined(OMPL_WALK_TFIRST)
-    constexpr bool kTFirst = SP == OMPL_GPU_SPACE_SE3;
-#else
-    constexpr bool kTFirst = false;
-#endif
     __shared__ __attribute__((aligned(16))) float qrow[G * FS];
     const int lane = threadIdx.x;
     const int half = lane >> 5;
@@ -718,78 +687,26 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     };
     // tiles of the super-tile whose boxes are in bx that some query may still need;
     // lb[j]: this lane's bound for its tile and query half * GH + j
-    // kDyn: the bounds are computed only for the queries whose own super-tile bound passes
-    // (`bits`, from the round's bounds in LDS): the needed queries are paired, pass p puts the
-    // (2p)-th on lanes 0-31 and the (2p+1)-th on lanes 32-63, and passes past the last needed
-    // pair are skipped wave-wide — otherwise every query costs its bound on every popped tile
-    // row.  A query's slot is (pass, half) = (rank / 2, rank % 2), rank = its index among the
-    // set bits.  Without kDyn lane half h always holds queries h*GH + j.
-    auto pair_of = [&](uint32_t bits, int p, int &qa, int &qb) {  // the needed pair of pass p
-        for (int i = 0; i < 2 * p; ++i) bits &= bits - 1;
-        qa = bits ? __builtin_ctz(bits) : -1;
-        bits &= bits - 1;
-        qb = bits ? __builtin_ctz(bits) : -1;
-    };
-    auto td_of = [&](int q) -> float {  // td[q] for a wave-uniform q (selects, no indexing)
-        float v = -__builtin_inff();
-#pragma unroll
-        for (int g = 0; g < G; ++g) v = q == g ? td[g] : v;
-        return v;
-    };
-    auto tile_mask = [&](const float (&bx)[BW], float (&lb)[GH], uint32_t bits) -> uint32_t {
+    auto tile_mask = [&](const float (&bx)[BW], float (&lb)[GH]) -> uint32_t {
         relaunder();
 #ifdef OMPL_AMD_PROBE
         ++pr_supers;
 #endif
         bool need = false;
-        if constexpr (kDyn) {
 #pragma unroll
-            for (int p = 0; p < GH; ++p) {
-                lb[p] = __builtin_inff();
-                int qa, qb;
-                pair_of(bits, p, qa, qb);
-                if (qa < 0) continue;  // wave-uniform
-                const int qg = half ? qb : qa;
-                const float thr = half ? td_of(qb) : td_of(qa);
-                if constexpr (kTFirst) {  // w0 |t gap| >= thr for every lane: no tile of this pass
-                    const float tg = qg >= 0 ? box_tgap2(bx, &qrow[qoff + qg * FS], Geo<SP, F>::NB) : __builtin_inff();
-                    if (!__ballot(w0 * w0 * tg < thr * thr * 1.0001f)) continue;
-                }
-                if (qg >= 0) {
-                    lb[p] = box_lb<SP, F, true>(bx, &qrow[qoff + qg * FS], w0, w1);
-                    if constexpr (Q16) lb[p] -= qerr;
-                    need |= lb[p] < thr;
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < GH; ++j) {
-                lb[j] = box_lb<SP, F, true>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
-                if constexpr (Q16) lb[j] -= qerr;
-                need |= lb[j] < (half ? td[GH + j] : td[j]);
-                __builtin_amdgcn_sched_barrier(0);  // one bound at a time (temporaries)
-            }
+        for (int j = 0; j < GH; ++j) {
+            lb[j] = box_lb<SP, F, true>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
+            need |= lb[j] < (half ? td[GH + j] : td[j]);
+            __builtin_amdgcn_sched_barrier(0);  // one bound at a time (temporaries)
         }
         return fold_tiles(__ballot(need));
     };
-    auto load_state = [&](uint32_t t, TileE (&x)[RW], uint32_t &id) {
+    auto load_state = [&](uint32_t t, float (&x)[R], uint32_t &id) {
         const uint64_t p = (uint64_t)t * kCullTile + lane;
 #pragma unroll
-        for (int r = 0; r < RW; ++r) {
-            if constexpr (Q16) x[r] = rows16[(uint64_t)r * n_pad + p];
-            else x[r] = rows[(uint64_t)r * n_pad + p];
-        }
+        for (int r = 0; r < R; ++r) x[r] = rows[(uint64_t)r * n_pad + p];
         id = (uint32_t)p;  // lists hold sorted positions; the certificate maps them to ids
         (void)ids;
-    };
-    auto decode = [&](const uint32_t (&w)[4], float (&v)[R]) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t c = (r & 1) ? (w[r >> 1] >> 16) : (w[r >> 1] & 0xFFFFu);
-            v[r] = fmaf((float)c, qg.step[r], qg.lo[r]);
-            if (r == 0 && c == 0xFFFFu) v[0] = __builtin_nanf("");  // padding / removed
-        }
     };
     // scan tile tin (index inside its super-tile) against every query whose own box bound
     // lb (held by lane tin + 32 * (g / GH)) is still below its threshold: the tile was
@@ -803,7 +720,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 #ifdef OMPL_AMD_PROBE
             ++pr_offers;
 #endif
-            if (__popcll(bm) > bulk) {  // many at once: sort-merge (same top K2)
+            if (__popcll(bm) > kBulkThreshold) {  // many at once: sort-merge (same top K2)
 #ifdef OMPL_AMD_PROBE
                 ++pr_bulk;
 #endif
@@ -829,20 +746,11 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
                 }
             }
     };
-    auto scan_state = [&](const float (&x)[R], uint32_t id, int tin, const float (&lb)[GH], uint32_t bits) {
+    auto scan_state = [&](const float (&x)[R], uint32_t id, int tin, const float (&lb)[GH]) {
         relaunder();
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            if constexpr (kDyn) {
-                if (!((bits >> g) & 1u)) continue;
-                const int rank = __builtin_popcount(bits & ((1u << g) - 1u));
-                float v = lb[0];
-#pragma unroll
-                for (int p = 1; p < GH; ++p) v = (rank >> 1) == p ? lb[p] : v;
-                if (!(readlane_f(v, tin + ((rank & 1) ? 32 : 0)) < td[g])) continue;
-            } else {
-                if (!(readlane_f(lb[g % GH], tin + (g < GH ? 0 : 32)) < td[g])) continue;
-            }
+            if (!(readlane_f(lb[g % GH], tin + (g < GH ? 0 : 32)) < td[g])) continue;
             ++qscans;
             if constexpr (SP == OMPL_GPU_SPACE_SE3) {
                 // screened d = fma(w1, theta, w0 |t|) with theta >= c: when no lane's chord
@@ -853,18 +761,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
                 float t = dx * dx;
                 t = fmaf(dy, dy, t);
                 t = fmaf(dz, dz, t);
-#if defined(OMPL_WALK_CASCADE)
-                // square-root-free rejects first: d >= w0 |t| + w1 c and (a + b)^2 >= a^2 + b^2, so
-                // a lane with w0^2 t (+ w1^2 c^2) >= td^2 (1 + 1e-4) has d > td after any fp32
-                // rounding (the slack is far above it): no lane below -> the wave skips the
-                // chord and both square roots (8-cycle issues each)
-                const float td2 = td[g] * td[g] * 1.0001f;
-                if (!__ballot(w0 * w0 * t < td2)) continue;
                 const float c2 = chord2(x + 3, qq + 4);
-                if (!__ballot(fmaf(w1 * w1, c2, w0 * w0 * t) < td2)) continue;
-#else
-                const float c2 = chord2(x + 3, qq + 4);
-#endif
                 const float c = __builtin_amdgcn_sqrtf(c2), wt = w0 * __builtin_amdgcn_sqrtf(t);
                 if (!__ballot(fmaf(w1, c, wt) < td[g])) continue;
                 offer(g, fmaf(w1, chord_theta(c, c2), wt), id);
@@ -889,19 +786,13 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     // exclude more tiles; the home tile is then dropped from its super-tile's mask
     const uint32_t th = min(key, ntiles - 1);
     {
-        TileE x[RW];
+        float x[R];
         uint32_t id;
         load_state(th, x, id);
         float lbh[GH];
 #pragma unroll
         for (int j = 0; j < GH; ++j) lbh[j] = -__builtin_inff();
-        if constexpr (Q16) {
-            float xd[R];
-            decode(x, xd);
-            scan_state(xd, id, 0, lbh, (1u << G) - 1u);
-        } else {
-            scan_state(x, id, 0, lbh, (1u << G) - 1u);
-        }
+        scan_state(x, id, 0, lbh);
         ++visited;
     }
     // visit order: s0 - 1, s0, s0 + 1 (the group's neighbourhood, which sets the thresholds),
@@ -918,7 +809,7 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     int pop_l = -1;           // round slot of the last popped super-tile (-1: the neighbourhood's)
     auto next_super = [&]() -> int {  // next super-tile to visit, -1 when done
         for (;;) {
-            if (sm && recheck && !first_round) {  // drop what the tightened thresholds exclude
+            if (sm && !first_round) {  // drop what the tightened thresholds exclude
                 bool keep = false;
 #pragma unroll
                 for (int g = 0; g < G; ++g) keep |= slb[g][lane] < td[g];
@@ -954,7 +845,6 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     lbs[g] = box_lb<SP, F, true>(bx, &qrow[qoff + g * FS], w0, w1);
-                    if constexpr (Q16) lbs[g] -= qerr;
                     need |= lbs[g] < td[g];
                     // one query's bound at a time: interleaving the G bounds needs ~40 temporaries
                     __builtin_amdgcn_sched_barrier(0);
@@ -978,18 +868,8 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
     // current thresholds before it is scanned.  (Measured: 1.27-1.29 -> 1.25-1.26 ms on cfg3.)
     float bx[BW];
     const uint32_t home_s = th / kSuperTiles;
-    auto mask_of = [&](int sv, float (&l)[GH], uint32_t &bits) -> uint32_t {
-        bits = (1u << G) - 1u;
-        if constexpr (kDyn) {
-            if (pop_l >= 0) {
-                bits = 0;
-#pragma unroll
-                for (int g = 0; g < G; ++g)
-                    if (__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(slb[g][pop_l]))) < td[g])
-                        bits |= 1u << g;
-            }
-        }
-        uint32_t mm = bits ? tile_mask(bx, l, bits) : 0u;
+    auto mask_of = [&](int sv, float (&l)[GH]) -> uint32_t {
+        uint32_t mm = tile_mask(bx, l);
         if ((uint32_t)sv == home_s) mm &= ~(1u << (th % kSuperTiles));  // scanned first
 #ifdef OMPL_AMD_PROBE
         if (!mm) ++pr_empty;
@@ -997,9 +877,8 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         return mm;
     };
     float lb[GH];
-    TileE x[RW], xn[RW];
+    float x[R], xn[R];
     uint32_t idn = kNoId, m = 0;  // (the scan recomputes the position ids)
-    uint32_t bits = (1u << G) - 1u;  // queries that need the current super-tile s (kDyn)
     int t = 0, tn = 0, s = -1;
     bool have = false;  // x holds a fetched tile of s
     int sn = next_super();
@@ -1010,10 +889,10 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         // fetch the next tile (xn) while x is scanned: the next of s, or else the first tile of
         // sn (bx holds its boxes) when its mask is not empty
         bool got = false, cross = false, consumed = false;
-        uint32_t mn = 0, bitsn = 0;
+        uint32_t mn = 0;
         float lbn[GH];
         if (!m && sn >= 0) {
-            mn = mask_of(sn, lbn, bitsn);
+            mn = mask_of(sn, lbn);
             consumed = true;
             cross = mn != 0;
         }
@@ -1026,19 +905,12 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
         }
         if (have) {  // the list ids are sorted positions: recomputed, not carried in a VGPR
             const uint32_t pid = ((uint32_t)s * kSuperTiles + (uint32_t)t) * kCullTile + (uint32_t)lane;
-            if constexpr (Q16) {
-                float xd[R];
-                decode(x, xd);
-                scan_state(xd, pid, t, lb, bits);
-            } else {
-                scan_state(x, pid, t, lb, bits);
-            }
+            scan_state(x, pid, t, lb);
             ++visited;
         }
         if (cross) {
             s = sn;
             m = mn;
-            bits = bitsn;
 #pragma unroll
             for (int j = 0; j < GH; ++j) lb[j] = lbn[j];
         }
@@ -1047,22 +919,13 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
             if (sn >= 0) load_tbox((uint32_t)sn, bx);
         }
         bool still = false;  // drop the tiles of s that the tightened thresholds exclude
-        if constexpr (kDyn) {
 #pragma unroll
-            for (int p = 0; p < GH; ++p) {
-                int qa, qb;
-                pair_of(bits, p, qa, qb);
-                still |= lb[p] < (half ? td_of(qb) : td_of(qa));
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
-        }
+        for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
         m &= fold_tiles(__ballot(still));
         have = got;
         if (got) {
 #pragma unroll
-            for (int r = 0; r < RW; ++r) x[r] = xn[r];
+            for (int r = 0; r < R; ++r) x[r] = xn[r];
             t = tn;
         } else if (sn < 0 && !m) {
             break;
@@ -1101,15 +964,8 @@ __global__ __launch_bounds__(64, MINW) void knn32_group_kernel(
 // The store is split in chunks along grid.y; the certificate merges the chunk lists.
 constexpr int kWaveGroup = 8;
 // queries per wave of the culled chain scan: 4 (57 VGPRs, 8 waves per SIMD) — measured on cfg4 step
-// 7.58-7.65 against 7.90-7.92 ms at 8 (73 VGPRs) and a 5.55-5.60 ms kernel at 2 (against 4.50-4.53);
-// A/B variants 20 / 21 keep 8 / 2
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 20
-constexpr int kChainCullG = 8;
-#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 21  // A/B: 2 queries per wave
-constexpr int kChainCullG = 2;
-#else
+// 7.58-7.65 against 7.90-7.92 ms at 8 (73 VGPRs) and a 5.55-5.60 ms kernel at 2 (against 4.50-4.53)
 constexpr int kChainCullG = 4;
-#endif
 
 // ORD 0: links in the reference's order, the wave-wide exit tested after links 4 and 8; ORD 1:
 // outermost links first (|P_i(a) - P_i(b)| grows with i, so the partial sum nears the distance
@@ -1319,24 +1175,19 @@ __global__ __launch_bounds__(256) void knn_chunk_merge_kernel(float *__restrict_
 // |code_i(s) - (P_i(q) + i + 1) S_i|, step_i = 1 / S_i.  Every quantity that decides what a list
 // keeps is this d16; the tile bounds stay on the fp32 boxes and are lowered by qerr
 // (chain_q16_error, >= |d16 - d32|), and the certificate's screen error grows by the same qerr.
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 22  // A/B: a wider pre-pass window
-constexpr int kChainTauTiles = 32;
-#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 23  // A/B: a narrower one
-constexpr int kChainTauTiles = 8;
-#else
 constexpr int kChainTauTiles = 16;
-#endif
-// PF (A/B, OMPL_GPU_CHAIN_PREFETCH=1; Q16 only): the next passing tile's 16-bit words are in
-// flight while the current tile is scanned.
-template <int F, int K2, int G, int MODE, bool Q16, bool PF = false>
+// MODE 1 is the pre-pass (the home window's thresholds, published by atomicMin), MODE 2 the chunk
+// pass.  (Measured and rejected, DESIGN §8: each chunk on its own thresholds; the next tile in
+// flight; pre-pass windows of 8 / 32 tiles and pre-passes split in parts.)
+template <int F, int K2, int G, int MODE, bool Q16>
 __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
     const float *__restrict__ rows, const uint32_t *__restrict__ rows16, uint32_t n_pad,
     const uint32_t *__restrict__ ids, uint32_t ntiles, const float *__restrict__ tbox, const float *__restrict__ q32,
     const uint32_t *__restrict__ qkeys, uint32_t nq, uint32_t chunk_tiles, float link, int nlinks, float qerr,
     float *__restrict__ pd, uint32_t *__restrict__ pi, unsigned long long *__restrict__ counters,
-    unsigned long long *__restrict__ shared_key, int kd_order = 0) {
+    unsigned long long *__restrict__ shared_key) {
     constexpr int NM = F / 2;
-    static_assert(K2 <= 64 && NM % 2 == 0, "chain cull shape");
+    static_assert(K2 <= 64 && NM % 2 == 0 && (MODE == 1 || MODE == 2), "chain cull shape");
     __shared__ __attribute__((aligned(16))) float qrow[G * F];
     __shared__ __attribute__((aligned(16))) float qcode[Q16 ? G * F : 1];  // the queries in quanta
     const int lane = threadIdx.x;
@@ -1445,19 +1296,9 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
             tk[g] = g0 + g < nq ? readlane_k(v, g) : 0ull;
             td[g] = g0 + g < nq ? up_of(kdist(tk[g])) : -__builtin_inff();
         }
-    } else {
-        const uint32_t h = home;
-        const uint32_t span = MODE == 1 ? (uint32_t)kChainTauTiles : 4u;
-        uint32_t t0, t1;
-        if constexpr (MODE == 1) {  // part blockIdx.y of a window of gridDim.y spans around home
-            const uint32_t W = span * gridDim.y;
-            const uint32_t w0 = h >= W / 2 ? h - W / 2 : 0u;
-            t0 = min(w0 + blockIdx.y * span, ntiles);
-            t1 = min(t0 + span, ntiles);
-        } else {
-            t0 = h >= span / 2 - 1u ? h - (span / 2 - 1u) : 0u;
-            t1 = min(t0 + span, ntiles);
-        }
+    } else {  // the pre-pass: the kChainTauTiles tiles around the home tile
+        const uint32_t h = home, span = (uint32_t)kChainTauTiles;
+        const uint32_t t0 = min(h >= span / 2 ? h - span / 2 : 0u, ntiles), t1 = min(t0 + span, ntiles);
         for (uint32_t t = t0; t < t1; ++t) {
             float x[F];
             load_tile(t, x);
@@ -1475,26 +1316,25 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
             tk[g] = tauk[g];
             td[g] = g0 + g < nq ? up_of(tau) : -__builtin_inff();
         }
-        if constexpr (MODE == 1) {  // each part's K2-th key bounds the store's: keep the smallest
+        // the window's K2-th key bounds the store's: publish it (keep the smallest)
 #pragma unroll
-            for (int g = 0; g < G; ++g)
-                if (lane == g && g0 + g < nq)
-                    (void)__hip_atomic_fetch_min(&shared_key[g0 + g], tauk[g], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
+        for (int g = 0; g < G; ++g)
+            if (lane == g && g0 + g < nq)
+                (void)__hip_atomic_fetch_min(&shared_key[g0 + g], tauk[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
     }
     // 2. the chunk's tiles (MODE 2: from the home tile's block on, wrapping)
     const uint32_t c0 = blockIdx.y * chunk_tiles, c1 = min(c0 + chunk_tiles, ntiles);
     const uint32_t nblk = c1 > c0 ? (c1 - c0 + 63) / 64 : 0u;
-    const uint32_t sblk = (MODE == 2 && home >= c0 && home < c1) ? (home - c0) / 64 : 0u;
-    // blocks nearest the home tile in k-d order first (kd_order > 0, MODE 2; the default): a chunk below the
-    // home tile walks its blocks backwards, one above it forwards, the home chunk from the home
-    // block on (wrapping) — each chunk's own list then tightens on its nearest tiles first
-    const bool backwards = MODE == 2 && kd_order && c1 <= home;
+    const uint32_t sblk = (home >= c0 && home < c1) ? (home - c0) / 64 : 0u;
+    // blocks nearest the home tile in k-d order first: a chunk below the home tile walks its
+    // blocks backwards, one above it forwards, the home chunk from the home block on (wrapping) —
+    // each chunk's own list then tightens on its nearest tiles first (measured: 4.75-4.82 against
+    // 4.84-4.85 ms on cfg4)
+    const bool backwards = c1 <= home;
     for (uint32_t bi = 0; bi < nblk; ++bi) {
         const uint32_t tb = c0 + (backwards ? nblk - 1 - bi : (sblk + bi) % nblk) * 64;
-        if constexpr (MODE == 2) {  // share the thresholds: publish this chunk's K2-th keys, take the smallest
+        {  // share the thresholds: publish this chunk's K2-th keys, take the smallest
             if (bi) {
                 uint64_t mine = kMaxKey;
 #pragma unroll
@@ -1548,42 +1388,6 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
         uint64_t need = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) need |= __ballot(lb[g] < td[g]);
-        if constexpr (Q16 && PF) {
-            uint32_t w[NM], wn[NM];
-            uint32_t id = 0, idn = 0;
-            int l = -1;
-            if (need) {
-                l = __builtin_ctzll(need);
-                need &= need - 1;
-                load_raw(tb + (uint32_t)l, w);
-                id = (tb + (uint32_t)l) * kCullTile + (uint32_t)lane;
-            }
-            while (l >= 0) {
-                int ln = -1;
-                if (need) {  // the next passing tile, in flight during this scan
-                    ln = __builtin_ctzll(need);
-                    need &= need - 1;
-                    load_raw(tb + (uint32_t)ln, wn);
-                    idn = (tb + (uint32_t)ln) * kCullTile + (uint32_t)lane;
-                }
-                float x[F];
-                decode(w, x);
-                ++visited;
-                asm volatile("" : "+s"(qoff));
-#pragma unroll
-                for (int g = 0; g < G; ++g)
-                    if (readlane_f(lb[g], l) < td[g]) scan(g, x, id);
-                uint64_t still = 0;  // the fetched next tile is re-checked per query in its scan
-#pragma unroll
-                for (int g = 0; g < G; ++g) still |= __ballot(lb[g] < td[g]);
-                need &= still;
-                l = ln;
-#pragma unroll
-                for (int j = 0; j < NM; ++j) w[j] = wn[j];
-                id = idn;
-            }
-            continue;
-        }
         while (need) {
             const int l = __builtin_ctzll(need);
             need &= need - 1;
@@ -1815,16 +1619,10 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
 // query's CSR segment in tile order; the caller sorts each segment by (distance, id).
 // MODE 2 (SLAB) counts like MODE 0 and also writes the first `slab` hits of each query to its
 // fixed-size slab, so that one walk suffices when no query has more hits than that.
-// (A/B builds: variants 5 / 6 ask the compiler for 7 / 8 waves per SIMD — 72 / 64 VGPRs with
-// 24 / 68 B of scratch spills — against the default's 80 VGPRs, 6 waves)
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 5
-#define OMPL_RADIUS_LB __launch_bounds__(64, 7)
-#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 6
-#define OMPL_RADIUS_LB __launch_bounds__(64, 8)
-#else
+// (Measured and rejected: 7 / 8 waves per SIMD from the compiler — 72 / 64 VGPRs with 24 / 68 B
+// of scratch spills — against the default's 80 VGPRs, 6 waves.)
 #define OMPL_RADIUS_LB __launch_bounds__(64)
-#endif
-// Q16 (SE3, MODE 2; the default; OMPL_GPU_RADIUS_Q16=0 reads the fp32 rows): the tiles come from the 16-bit copy
+// Q16 (SE3, MODE 2; Q16 = false reads the fp32 rows): the tiles come from the 16-bit copy
 // (SortedStore::rows16, 16 B per state against 28), decoded to fp32 once per tile; every
 // threshold grows by qerr >= |d16 - d32| (se3_q16_error), so no state with d32 <= r + e is lost
 // and the box bounds (over the fp32 rows) stay valid.
@@ -1887,22 +1685,9 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
     // re-read the wave-uniform query rows from LDS at every use through an offset the compiler
     // cannot see through, instead of letting it hoist them into VGPRs for the whole walk
     uint32_t qoff = 0;
-    // super-tiles whose box comes within some query's bound, 64 box tests per round.
-    // kDyn (A/B variant 11): each lane also records which queries its super-tile passes
-    // (sneed, LDS), and a popped super-tile's tile bounds are computed only for those queries,
-    // paired onto the two half-waves (as knn32_group_kernel's kDyn)
-#if defined(OMPL_AMD_VARIANT) && (OMPL_AMD_VARIANT == 11 || OMPL_AMD_VARIANT == 13)
-    constexpr bool kDyn = true;
-#else
-    constexpr bool kDyn = false;
-#endif
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 13
-    constexpr bool kCascade = SP == OMPL_GPU_SPACE_SE3;  // A/B variant 13: + square-root-free rejects
-#else
-    constexpr bool kCascade = false;
-#endif
-    __shared__ uint32_t sneed[64];
-    uint32_t pop_bits = (1u << G) - 1u;
+    // super-tiles whose box comes within some query's bound, 64 box tests per round.  (Measured
+    // and rejected, DESIGN §8: tile bounds only for the queries a super-tile passes, paired onto
+    // the half-waves; a translation-only pre-test before the chord bound.)
     uint32_t sb = 0, base = 0;
     uint64_t sm = 0;
     auto next_super = [&]() -> int {
@@ -1911,7 +1696,6 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
             asm volatile("" : "+s"(qoff));
             const uint32_t s = sb + lane;
             bool need = false;
-            uint32_t nb = 0;
             if (s < nsuper) {
                 float bx[BW];
                 const float4 *b4 = reinterpret_cast<const float4 *>(sbox + (size_t)s * BW);
@@ -1922,15 +1706,9 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
                 }
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    const bool pg = box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1) <= thr[g];
-                    need |= pg;
-                    if (kDyn && pg) nb |= 1u << g;
+                    need |= box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1) <= thr[g];
                     __builtin_amdgcn_sched_barrier(0);  // one bound at a time (temporaries)
                 }
-            }
-            if constexpr (kDyn) {
-                sneed[lane] = nb;
-                __builtin_amdgcn_wave_barrier();
             }
             sm = __ballot(need);
             base = sb;
@@ -1938,20 +1716,7 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
         }
         const int l = __builtin_ctzll(sm);
         sm &= sm - 1;
-        if constexpr (kDyn) pop_bits = (uint32_t)__builtin_amdgcn_readfirstlane((int)sneed[l]);
         return (int)(base + l);
-    };
-    auto pair_of = [&](uint32_t bits, int p, int &qa, int &qb) {  // the needed pair of pass p
-        for (int i = 0; i < 2 * p; ++i) bits &= bits - 1;
-        qa = bits ? __builtin_ctz(bits) : -1;
-        bits &= bits - 1;
-        qb = bits ? __builtin_ctz(bits) : -1;
-    };
-    auto thr_of = [&](int q) -> float {
-        float v = -__builtin_inff();
-#pragma unroll
-        for (int g = 0; g < G; ++g) v = q == g ? thr[g] : v;
-        return v;
     };
     // this lane's row of super-tile ss's tile boxes (tile ss * 32 + (lane & 31)); rows past the
     // last tile read as empty boxes (bound +inf)
@@ -1992,22 +1757,13 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
             if (rr == 0 && c == 0xFFFFu) v[0] = __builtin_nanf("");  // padding / removed
         }
     };
-    auto scan_tile = [&](uint32_t ss, int t, const float (&x)[R], uint32_t id, const float (&lb)[GH], uint32_t bits) {
+    auto scan_tile = [&](uint32_t ss, int t, const float (&x)[R], uint32_t id, const float (&lb)[GH]) {
         asm volatile("" : "+s"(qoff));
         const uint64_t p = (uint64_t)(ss * kSuperTiles + t) * kCullTile + lane;
         ++visited;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            if constexpr (kDyn) {
-                if (!((bits >> g) & 1u)) continue;
-                const int rank = __builtin_popcount(bits & ((1u << g) - 1u));
-                float v = lb[0];
-#pragma unroll
-                for (int pp = 1; pp < GH; ++pp) v = (rank >> 1) == pp ? lb[pp] : v;
-                if (!(readlane_f(v, t + ((rank & 1) ? 32 : 0)) <= thr[g])) continue;
-            } else {
-                if (!(readlane_f(lb[g % GH], t + (g < GH ? 0 : 32)) <= thr[g])) continue;
-            }
+            if (!(readlane_f(lb[g % GH], t + (g < GH ? 0 : 32)) <= thr[g])) continue;
             ++qscans;
             bool hit;  // NaN never hits
             if constexpr (SP == OMPL_GPU_SPACE_SE3) {  // chord bound first, as in the kNN walk
@@ -2016,10 +1772,6 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
                 float tt = dx * dx;
                 tt = fmaf(dy, dy, tt);
                 tt = fmaf(dz, dz, tt);
-                if constexpr (kCascade) {  // as the kNN walk's cascade: (a + b)^2 >= a^2 + b^2
-                    const float t2 = thr[g] * thr[g] * 1.0001f;
-                    if (!__ballot(w0 * w0 * tt <= t2)) continue;  // no lane can hit: nothing to count or write
-                }
                 const float c2 = chord2(x + 3, qq + 4);
                 const float c = __builtin_amdgcn_sqrtf(c2), wt = w0 * __builtin_amdgcn_sqrtf(tt);
                 hit = __ballot(fmaf(w1, c, wt) <= thr[g]) && fmaf(w1, chord_theta(c, c2), wt) <= thr[g];
@@ -2071,34 +1823,16 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
     // writes each CSR segment in tile order.
     float bx[BW];
     int ss = next_super();
-    uint32_t bits = pop_bits;
     if (ss >= 0) load_tbox((uint32_t)ss, bx);
     while (ss >= 0) {
         float lb[GH];
         bool tneed = false;
         asm volatile("" : "+s"(qoff));
-        if constexpr (kDyn) {
 #pragma unroll
-            for (int pp = 0; pp < GH; ++pp) {
-                lb[pp] = __builtin_inff();
-                int qa, qb;
-                pair_of(bits, pp, qa, qb);
-                if (qa < 0) continue;  // wave-uniform
-                const int qg = half ? qb : qa;
-                const float th = half ? thr_of(qb) : thr_of(qa);
-                if (qg >= 0) {
-                    lb[pp] = box_lb<SP, F>(bx, &qrow[qoff + qg * FS], w0, w1);
-                    tneed |= lb[pp] <= th;
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < GH; ++j) {
-                lb[j] = box_lb<SP, F>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
-                tneed |= lb[j] <= (half ? thr[GH + j] : thr[j]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
+        for (int j = 0; j < GH; ++j) {
+            lb[j] = box_lb<SP, F>(bx, &qrow[qoff + (half * GH + j) * FS], w0, w1);
+            tneed |= lb[j] <= (half ? thr[GH + j] : thr[j]);
+            __builtin_amdgcn_sched_barrier(0);
         }
         uint32_t m = fold_tiles(__ballot(tneed));
         uint32_t id = 0, idn = 0;
@@ -2112,7 +1846,6 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
                 load_raw((uint32_t)ss, t, x, id);
             }
             const int ssn = next_super();
-            const uint32_t bitsn = pop_bits;
             if (ssn >= 0) load_tbox((uint32_t)ssn, bx);
             while (have) {
                 const bool more = m != 0;
@@ -2123,7 +1856,7 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
                 }
                 float xd[R];
                 decode(x, xd);
-                scan_tile((uint32_t)ss, t, xd, id, lb, bits);
+                scan_tile((uint32_t)ss, t, xd, id, lb);
                 if (!more) break;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) x[j] = xn[j];
@@ -2131,7 +1864,6 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
                 t = tn;
             }
             ss = ssn;
-            bits = bitsn;
             continue;
         }
         float x[R], xn[R];
@@ -2141,7 +1873,6 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
             load_tile((uint32_t)ss, t, x, id);
         }
         const int ssn = next_super();
-        const uint32_t bitsn = pop_bits;
         if (ssn >= 0) load_tbox((uint32_t)ssn, bx);
         while (have) {
             const bool more = m != 0;
@@ -2150,7 +1881,7 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
                 m &= m - 1;
                 load_tile((uint32_t)ss, tn, xn, idn);
             }
-            scan_tile((uint32_t)ss, t, x, id, lb, bits);
+            scan_tile((uint32_t)ss, t, x, id, lb);
             if (!more) break;
 #pragma unroll
             for (int rr = 0; rr < R; ++rr) x[rr] = xn[rr];
@@ -2158,7 +1889,6 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
             t = tn;
         }
         ss = ssn;
-        bits = bitsn;
     }
     if (lane == 0) {
         if (!FILL) {
@@ -2276,18 +2006,11 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
         p.k2 = p.K2;
         const uint64_t ntile = std::max<uint64_t>(1, (n_end + kCullTile - 1) / kCullTile);
         const uint64_t groups = (nq + kChainCullG - 1) / kChainCullG;
-        // waves per CU the chunks aim at and the chunk cap (OMPL_GPU_CHAIN_WPC / _SMAX: A/B).  With
-        // the thresholds shared across chunks (MODE 2) more chunks only add parallelism: measured
-        // on cfg4 (8,192 milestones, 1,024 groups) 24 / 48 / 96 / 192 / 384 waves per CU ->
-        // 8.14 / 6.79 / 5.59 / 4.88 / 4.67 ms (384 reaches the 64-chunk cap)
-        static const uint64_t wpc = [] {
-            const char *v = std::getenv("OMPL_GPU_CHAIN_WPC");
-            return v ? (uint64_t)std::max(1, std::atoi(v)) : (uint64_t)384;
-        }();
-        static const uint64_t smax = [] {
-            const char *v = std::getenv("OMPL_GPU_CHAIN_SMAX");
-            return v ? (uint64_t)std::max(1, std::atoi(v)) : (uint64_t)64;
-        }();
+        // waves per CU the chunks aim at and the chunk cap.  With the thresholds shared across
+        // chunks (MODE 2) more chunks only add parallelism: measured on cfg4 (8,192 milestones,
+        // 1,024 groups) 24 / 48 / 96 / 192 / 384 waves per CU -> 8.14 / 6.79 / 5.59 / 4.88 / 4.67 ms
+        // (384 reaches the 64-chunk cap; 128 / 256 chunks: the merge eats the gain)
+        constexpr uint64_t wpc = 384, smax = 64;
         const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)num_cus * wpc + groups - 1) / groups, smax));
         const uint64_t per = (ntile + S - 1) / S;
         p.chunk_len = (uint32_t)per;  // tiles per chunk
@@ -2389,42 +2112,14 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     if (e != hipSuccess) return e;
     bool walked = false;
     float chain_qerr = 0.f;  // the culled chain scan's 16-bit screen error (certificate)
-    float knn_qerr = 0.f;    // the SE3 group walk's (certificate xerr)
     if constexpr (SP == OMPL_GPU_SPACE_SE3 || SP == OMPL_GPU_SPACE_REALVECTOR) {  // cull_supported
         if (p.cull) {
             timer_begin(st, "knn32_group_kernel");
             // (BIT*'s 64-lane lists too: cfg5k G = 2 4.08-4.14 ms, 4 4.24-4.35, 8 5.07-5.09)
-            // (A/B variant 19: at least 8 waves per SIMD, i.e. <= 64 VGPRs, against the natural 67)
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 19
-            constexpr int kWalkMinWaves = 8;
-#else
-            constexpr int kWalkMinWaves = 1;
-#endif
             constexpr int G = group_queries<SP>();
-            static const int bulk = [] {  // A/B: candidates per ballot above which the bulk merge runs
-                const char *v = std::getenv("OMPL_GPU_BULK");
-                return v ? std::atoi(v) : kBulkThreshold;
-            }();
-            static const int recheck = [] {  // A/B switch of the popped super-tile re-check
-                const char *v = std::getenv("OMPL_GPU_SUPER_RECHECK");
-                return v ? std::atoi(v) : 1;
-            }();
-            bool q16 = false;
-            if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-                if (ss->rows16 && ss->gen16 == ss->gen && se3_knn_q16_enabled()) {
-                    q16 = true;
-                    knn_qerr = (float)(se3_q16_error(sp, ss->q16) * (1.0 + 1e-5));
-                    hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, 1, true, true>), dim3((nq + G - 1) / G),
-                                       dim3(64), 0, st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox,
-                                       ss->nsuper, ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi,
-                                       ss->counters, bulk, p.k2, recheck, ss->rows16, ss->q16, knn_qerr);
-                }
-            }
-            if (!q16)
-                hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, kWalkMinWaves, true>), dim3((nq + G - 1) / G), dim3(64), 0,
-                                   st, ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper,
-                                   ss->tkey0, q32, keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters,
-                                   bulk, p.k2, recheck);
+            hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
+                               ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0, q32,
+                               keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, p.k2);
             timer_end(st);
             walked = true;
         }
@@ -2434,55 +2129,29 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             if (!ss || !ss->built) return hipErrorInvalidValue;
             // the plan's chunk count sized the lists; the store's tiles (main + tail) set their length
             const uint32_t per = (ss->ntiles + p.chunks - 1) / p.chunks;
-            // thresholds shared across the chunks (MODE 1 + 2); OMPL_GPU_CHAIN_SHARE=0: each chunk
-            // on its own (MODE 0, A/B)
-            static const int share = [] {
-                const char *v = std::getenv("OMPL_GPU_CHAIN_SHARE");
-                return v ? std::atoi(v) : 1;
-            }();
+            // thresholds shared across the chunks: the pre-pass (MODE 1) publishes each query's
+            // window bound, the chunk pass (MODE 2) tightens them by device-scope atomicMin
             unsigned long long *skey = (unsigned long long *)(ws + L.tau);
             const uint32_t ng = (nq + kChainCullG - 1) / kChainCullG;
-            // the 16-bit rows when the store's copy is current (refresh_chain_rows16; share only)
-            const bool q16 = share && ss->rows16 && ss->gen16 == ss->gen;
+            // the 16-bit rows when the store's copy is current (refresh_chain_rows16)
+            const bool q16 = ss->rows16 && ss->gen16 == ss->gen;
             const float qerr = q16 ? (float)(chain_q16_error(sp) * (1.0 + 1e-5)) : 0.f;
-            static const int kd_ord = [] {  // A/B: chunk blocks nearest the home tile first
-                const char *v = std::getenv("OMPL_GPU_CHAIN_KDORDER");
-                return v ? std::atoi(v) : 1;  // measured: 4.75-4.82 against 4.84-4.85 ms on cfg4
-            }();
-            static const bool pf = [] {  // A/B: the next tile in flight (Q16 only)
-                const char *v = std::getenv("OMPL_GPU_CHAIN_PREFETCH");
-                return v ? std::atoi(v) != 0 : false;
-            }();
-#define OMPL_AMD_CHAIN_CULL(MODE, Q, GY, CNT, KEY) OMPL_AMD_CHAIN_CULL_PF(MODE, Q, false, GY, CNT, KEY)
-#define OMPL_AMD_CHAIN_CULL_PF(MODE, Q, P, GY, CNT, KEY)                                                         \
-    hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, MODE, Q, P>), dim3(ng, GY), dim3(64), 0, st, \
-                       ss->rows, ss->rows16, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,      \
-                       (float)sp.link, sp.dim, qerr, pd, pi, CNT, KEY, kd_ord)
-            static const uint32_t tau_parts = [] {  // pre-pass parts (A/B): 16 tiles each
-                const char *v = std::getenv("OMPL_GPU_CHAIN_TAU_PARTS");
-                return (uint32_t)std::max(1, v ? std::atoi(v) : 1);
-            }();
-            if (share) {  // the parts publish with atomicMin: start from all-ones (above every key)
-                hipError_t me = hipMemsetAsync(skey, 0xFF, 8ull * nq, st);
-                if (me != hipSuccess) return me;
-            }
+#define OMPL_AMD_CHAIN_CULL(MODE, Q, GY, CNT)                                                                   \
+    hipLaunchKernelGGL((knn32_chain_cull_kernel<F, K2, kChainCullG, MODE, Q>), dim3(ng, GY), dim3(64), 0, st,   \
+                       ss->rows, ss->rows16, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, q32, keys2, nq, per,     \
+                       (float)sp.link, sp.dim, qerr, pd, pi, CNT, skey)
+            hipError_t me = hipMemsetAsync(skey, 0xFF, 8ull * nq, st);  // above every key
+            if (me != hipSuccess) return me;
             if (q16) {
-                OMPL_AMD_CHAIN_CULL(1, true, tau_parts, nullptr, skey);
+                OMPL_AMD_CHAIN_CULL(1, true, 1, nullptr);
                 timer_begin(st, "knn32_chain_cull_kernel");
-                if (pf)
-                    OMPL_AMD_CHAIN_CULL_PF(2, true, true, p.chunks, ss->counters, skey);
-                else
-                    OMPL_AMD_CHAIN_CULL(2, true, p.chunks, ss->counters, skey);
-            } else if (share) {
-                OMPL_AMD_CHAIN_CULL(1, false, tau_parts, nullptr, skey);
-                timer_begin(st, "knn32_chain_cull_kernel");
-                OMPL_AMD_CHAIN_CULL(2, false, p.chunks, ss->counters, skey);
+                OMPL_AMD_CHAIN_CULL(2, true, p.chunks, ss->counters);
             } else {
+                OMPL_AMD_CHAIN_CULL(1, false, 1, nullptr);
                 timer_begin(st, "knn32_chain_cull_kernel");
-                OMPL_AMD_CHAIN_CULL(0, false, p.chunks, ss->counters, nullptr);
+                OMPL_AMD_CHAIN_CULL(2, false, p.chunks, ss->counters);
             }
 #undef OMPL_AMD_CHAIN_CULL
-#undef OMPL_AMD_CHAIN_CULL_PF
             timer_end(st);
             chain_qerr = qerr;
             walked = true;
@@ -2491,28 +2160,12 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     if (p.cull && !walked) return hipErrorInvalidValue;
     if constexpr (SP == OMPL_GPU_SPACE_KCHAIN) if (!p.cull) {
         timer_begin(st, "knn32_wave_scan_kernel");
-        // link order of the screen (knn32_wave_scan_kernel ORD) and waves sharing each staged tile
-        // (WPB); OMPL_GPU_CHAIN_ORDER=0 restores the reference order with two exit tests and
-        // OMPL_GPU_CHAIN_WPB=1 one wave per block (A/B)
-        static const int ord = [] {
-            const char *v = std::getenv("OMPL_GPU_CHAIN_ORDER");
-            return v ? std::atoi(v) : 1;
-        }();
-        static const int wpb = [] {
-            const char *v = std::getenv("OMPL_GPU_CHAIN_WPB");
-            return v ? std::atoi(v) : 4;
-        }();
-        const uint32_t qpb = (uint32_t)(kWaveGroup * (wpb == 1 ? 1 : 4));
+        // outer links first, four waves sharing each staged tile (measured against the reference
+        // link order with two exit tests and one wave per block)
+        const uint32_t qpb = (uint32_t)(kWaveGroup * 4);
         const dim3 grid((nq + qpb - 1) / qpb, p.chunks);
-        if (ord == 0)
-            hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 0, 4>), grid, dim3(256), 0, st, f32, cap,
-                               n_end, q32, nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
-        else if (wpb == 1)
-            hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 1, 1>), grid, dim3(64), 0, st, f32, cap,
-                               n_end, q32, nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
-        else
-            hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 1, 4>), grid, dim3(256), 0, st, f32, cap,
-                               n_end, q32, nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
+        hipLaunchKernelGGL((knn32_wave_scan_kernel<F, K2, kWaveGroup, 1, 4>), grid, dim3(256), 0, st, f32, cap, n_end,
+                           q32, nq, p.chunk_len, (float)sp.link, sp.dim, pd, pi);
         timer_end(st);
         walked = true;
     }
@@ -2539,7 +2192,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
         if (pos && !ss->rows64) return hipErrorInvalidValue;
         hipLaunchKernelGGL((knn_certify_wave_kernel<SP, F, K2>), dim3((nq + QPB - 1) / QPB), b256, 0, st, pd, pi, nq,
                            perm, f64, cap, pos ? ss->ids : nullptr, pos ? ss->rows64 : nullptr, qf64, sp, b.absmax,
-                           b.qeta, b.n_live, (uint32_t)p.k2, od, oi, k, fail, fail + 1, knn_qerr);
+                           b.qeta, b.n_live, (uint32_t)p.k2, od, oi, k, fail, fail + 1, 0.f);
     } else {
         if (p.cull) return hipErrorInvalidValue;  // position lists need the wave certificate
         if constexpr (K == 64 && SP != OMPL_GPU_SPACE_KCHAIN) {
@@ -2590,19 +2243,13 @@ hipError_t run_fast_space(const DevSpace &sp, const FastPlan &p, const FastLayou
 // the last one zero) and the offsets their exclusive scan gives (nq + 2: [nq] = total,
 // [nq + 1] = longest segment)
 constexpr int kRadiusGroup = 4;  // 10^7-state radius pass: G=2 2.37 ms, G=4 2.27 ms (tiles shared by more queries)
-// the one-walk (slab) pass holds no fp64 state, so a group can be wider: each fetched tile serves
-// more queries (A/B build: OMPL_AMD_VARIANT 2 -> 8)
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 2
-constexpr int kRadiusSlabGroup = 8;
-#elif defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 18  // A/B: 2 queries per wave
-constexpr int kRadiusSlabGroup = 2;
-#else
+// the one-walk (slab) pass holds no fp64 state, so a group could be wider (each fetched tile
+// serving more queries): 8 measured no faster
 constexpr int kRadiusSlabGroup = 4;
-#endif
 
 struct RadiusLayout {
-    size_t keys, keys2, idx, perm, cub, q32u, q32, counts, off, scan, red, total;
-    size_t cub_bytes, scan_bytes, red_bytes;
+    size_t keys, keys2, idx, perm, cub, q32u, q32, counts, off, scan, total;
+    size_t cub_bytes;
 };
 
 RadiusLayout radius_layout(const DevSpace &sp, const FeatGeom &g, uint32_t nq) {
@@ -2627,13 +2274,7 @@ RadiusLayout radius_layout(const DevSpace &sp, const FeatGeom &g, uint32_t nq) {
     L.q32 = take(4ull * nq * FS);
     L.counts = take(8ull * (nq + 1));
     L.off = take(8ull * (nq + 2));
-    size_t sb = 0, rb = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)nq + 1);
-    (void)hipcub::DeviceReduce::Max(nullptr, rb, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)nq);
-    L.scan_bytes = sb;
-    L.red_bytes = rb;
-    L.scan = take(sb);
-    L.red = take(rb);
+    L.scan = take(exclusive_scan_u64_workspace((uint64_t)nq + 1));
     L.total = off;
     return L;
 }
@@ -2668,7 +2309,7 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
             const dim3 gs((nq + kRadiusSlabGroup - 1) / kRadiusSlabGroup);
             bool q16 = false;
             if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-                if (ss->rows16 && ss->gen16 == ss->gen && se3_q16_enabled()) {
+                if (ss->rows16 && ss->gen16 == ss->gen) {
                     q16 = true;
                     hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusSlabGroup, 2, true>), gs, b64, 0, st,
                                        ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32,
@@ -2689,11 +2330,8 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
                                ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64,
                                sp, b.absmax, b.qeta, r, counts, nullptr, nullptr, nullptr, nullptr, 0u);
         }
-        size_t sb = L.scan_bytes, rb = L.red_bytes;
-        if ((e = hipcub::DeviceScan::ExclusiveSum(ws + L.scan, sb, counts, offs, (int)nq + 1, st)) != hipSuccess)
-            return e;
-        if ((e = hipcub::DeviceReduce::Max(ws + L.red, rb, counts, offs + nq + 1, (int)nq, st)) != hipSuccess) return e;
-        return hipGetLastError();
+        // offsets (counts[nq] = 0: offs[nq] = offs[nq + 1] = the total) and the longest segment
+        return launch_exclusive_scan_u64(counts, (uint64_t)nq + 1, offs, ws + L.scan, st, offs + nq + 1);
     }
     timer_begin(st, "radius32_group_kernel");
     hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 1>), grid, b64, 0, st, ss->rows, ss->n_pad,
@@ -3021,101 +2659,13 @@ __global__ __launch_bounds__(BS) void kd_node_split_dim_kernel(const float *__re
     }
 }
 
-// sort key of position p at this level: (node path, extended by zeros for a node that is
-// already a leaf) << kKdQBits | its split coordinate quantised to kKdQBits bits over the node's
-// extent (0 in a leaf, which keeps it in place under the stable sort).  Quantisation only decides
-// how states with nearly equal coordinates straddle the split: the left part still gets exactly
-// floor(T/2) tiles, and every tile / super-tile box is computed from the states it holds, so the
-// walks' bounds do not depend on it.  path bits + kKdQBits <= 32 for every level the global loop
-// runs (the LDS finish takes the deep ones), so the keys are 32-bit.
+// a split coordinate quantised to kKdQBits bits over the node's extent.  Quantisation only
+// decides how states with nearly equal coordinates straddle the split: the left part still gets
+// exactly floor(T/2) tiles, and every tile / super-tile box is computed from the states it holds,
+// so the walks' bounds do not depend on it.
 __device__ __forceinline__ uint32_t kd_quant(float v, float4 ns) {
     const float x = (v - ns.y) * ns.z;
     return x > 0.f ? (x < (float)kKdQ ? (uint32_t)x : kKdQ) : 0u;
-}
-
-template <int SP, int F>
-__global__ void kd_row_keys_kernel(const float *__restrict__ W, uint32_t n, uint32_t ntiles, int level,
-                                   const float4 *__restrict__ nsplit, uint32_t *__restrict__ keys,
-                                   uint32_t *__restrict__ vals) {
-    constexpr int RW = KdRow<SP, F>::W;
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const uint32_t t = p / kCullTile;
-    uint32_t t0 = 0, T = ntiles, path = 0;
-    int l = 0;
-    for (; l < level && T > 1; ++l) {
-        const uint32_t tl = T >> 1;
-        const uint32_t right = t >= t0 + tl ? 1u : 0u;
-        path = (path << 1) | right;
-        if (right) {
-            t0 += tl;
-            T -= tl;
-        } else {
-            T = tl;
-        }
-    }
-    uint32_t q = 0;
-    if (l == level && T > 1) {
-        const float4 ns = nsplit[path];
-        q = kd_quant(W[(size_t)p * RW + (int)__float_as_uint(ns.x)], ns);
-    } else {
-        path <<= (level - l);
-    }
-    keys[p] = (path << kKdQBits) | q;
-    vals[p] = p;
-}
-
-// rows of the new order (W2[p] = W[src[p]], a wave per 64-row tile, one contiguous row read per
-// lane) and, from the rows in hand, the boxes of the new order's tiles for the next level
-template <int SP, int F>
-__global__ void kd_row_gather_boxes_kernel(const float *__restrict__ W, const uint32_t *__restrict__ src, uint32_t n,
-                                           uint32_t ntiles, float *__restrict__ W2, float *__restrict__ tb) {
-    constexpr int NB = KdRow<SP, F>::NB, RW = KdRow<SP, F>::W;
-    const uint32_t t = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (t >= ntiles) return;
-    const uint32_t p = t * kCullTile + lane;
-    float r[RW];
-    if (p < n) {
-        const float4 *w4 = reinterpret_cast<const float4 *>(W + (size_t)src[p] * RW);
-        float4 *o4 = reinterpret_cast<float4 *>(W2 + (size_t)p * RW);
-#pragma unroll
-        for (int c = 0; c < RW / 4; ++c) {
-            const float4 v = w4[c];
-            o4[c] = v;
-            r[4 * c] = v.x; r[4 * c + 1] = v.y; r[4 * c + 2] = v.z; r[4 * c + 3] = v.w;
-        }
-    }
-#pragma unroll
-    for (int d = 0; d < NB; ++d) {
-        float lo = p < n ? r[d] : __builtin_inff();
-        float hi = p < n ? r[d] : -__builtin_inff();
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            lo = fminf(lo, __shfl_xor(lo, o));
-            hi = fmaxf(hi, __shfl_xor(hi, o));
-        }
-        if (lane == 0) {
-            tb[(size_t)t * 2 * NB + d] = lo;
-            tb[(size_t)t * 2 * NB + NB + d] = hi;
-        }
-    }
-}
-
-// node records of the level (pre-order): split = first coordinate of the right part
-template <int SP, int F>
-__global__ void kd_row_split_kernel(const float *__restrict__ W, uint32_t n, uint32_t ntiles, int level,
-                                    const float4 *__restrict__ nsplit, KdNode *__restrict__ nodes) {
-    constexpr int RW = KdRow<SP, F>::W;
-    const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;
-    if (level < 31 && path >= (1u << level)) return;
-    const KdNodeRef nd = kd_node_at(ntiles, level, path);
-    if (!nd.valid || nd.T <= 1) return;
-    const uint32_t tl = nd.T >> 1;
-    const uint32_t pos = (nd.t0 + tl) * kCullTile;
-    const int d = (int)__float_as_uint(nsplit[path].x);
-    const float split = pos < n ? W[(size_t)pos * RW + d] : __builtin_inff();
-    nodes[nd.pidx] = KdNode{(uint32_t)d, split, tl, nd.pidx + tl};
 }
 
 // ---- global levels as a median partition (no sort) -----------------------------------------
@@ -3678,15 +3228,6 @@ hipError_t sorted_alloc(SortedStore *s, uint32_t pad_tiles, uint32_t max_nodes, 
 }
 
 // Full build over ids [0, n_total) whose live flag is set (n_live of them), on `st`, no sync.
-// the global k-d levels as median partitions (OMPL_GPU_KD_PART=0: one radix sort per level, A/B)
-inline bool kd_partition() {
-    static const bool b = [] {
-        const char *v = std::getenv("OMPL_GPU_KD_PART");
-        return v ? std::atoi(v) != 0 : true;
-    }();
-    return b;
-}
-
 template <int SP, int F>
 hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint64_t n_total, uint32_t n_live,
                         const uint8_t *live, SortedStore *s, hipStream_t st) {
@@ -3699,8 +3240,8 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
     if ((e = sorted_alloc<SP, F>(s, main_sup_tiles + tail_tiles, main_tiles, std::max<uint64_t>(cap, n_total), fa,
                                  st)) != hipSuccess)
         return e;
-    // scratch: flags | sel / sorted positions | keys x2 | positions | rows x2 | tile boxes | node
-    // splits | selected count | rocPRIM temp.  The two row buffers are adjacent: after the level
+    // scratch: flags | selected ids | quantised coordinates | rows x2 | tile boxes | node splits |
+    // selected count | rocPRIM temp.  The two row buffers are adjacent: after the level
     // loop they hold the fp64 features by id (feat_aos_kernel) for the rows64 gather.
     const size_t n = std::max<uint64_t>(n_total, 1);
     const uint32_t nl = std::max<uint32_t>(n_live, 1);
@@ -3711,13 +3252,10 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
     // whose nodes (ceil(main_tiles / 2^L) tiles at most) fit; kd_lds_finish_kernel does the rest
     int Lg = 0;
     while (Lg < depth && ((main_tiles + (1u << Lg) - 1) >> Lg) > kd_lds_tiles<SP, F>()) ++Lg;
-    size_t tmp_sel = 0, tmp_sort = 0;
+    size_t tmp_sel = 0;
     rocprim::counting_iterator<uint32_t> count_it(0);
     if ((e = rocprim::select(nullptr, tmp_sel, count_it, (const uint8_t *)nullptr, (uint32_t *)nullptr,
                              (uint32_t *)nullptr, n, st)) != hipSuccess)
-        return e;
-    if ((e = rocprim::radix_sort_pairs(nullptr, tmp_sort, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                       (uint32_t *)nullptr, (uint32_t *)nullptr, nl, 0, 32, st)) != hipSuccess)
         return e;
     const size_t row_bytes = std::max<size_t>(4ull * RW * nl, 4ull * fa * n);  // each half of the pair
     size_t off = 0;
@@ -3726,37 +3264,36 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
         off += align_up(b);
         return o;
     };
-    const size_t o_flags = take(n), o_sel = take(4 * n), o_k0 = take(4ull * nl), o_k1 = take(4ull * nl),
-                 o_v0 = take(4ull * nl), o_w = take(2 * row_bytes), o_tb = take(4ull * main_tiles * 2 * NB),
-                 o_ns = take(16ull * main_tiles + 16), o_cnt = take(8), o_tmp = take(std::max(tmp_sel, tmp_sort));
+    const size_t o_flags = take(n), o_sel = take(4 * n), o_k0 = take(4ull * nl), o_w = take(2 * row_bytes),
+                 o_tb = take(4ull * main_tiles * 2 * NB), o_ns = take(16ull * main_tiles + 16), o_cnt = take(8),
+                 o_tmp = take(tmp_sel);
     // median partition: bin counts per node of the deepest global level, children's boxes,
-    // per-node selections, per-chunk counts (Q, the quantised coordinates, reuses k0)
+    // per-node selections, per-chunk counts
     const size_t nodes_max = Lg > 0 ? (size_t)1 << (Lg - 1) : 1;
     const size_t o_h = take(4ull * kPartBins * nodes_max), o_cb = take(4ull * 2 * NB * 2 * nodes_max),
                  o_ps = take(8ull * nodes_max), o_pc = take(8ull * (nodes_max + main_tiles / (kPartChunk / kCullTile) + 2));
     if ((e = scratch_ensure(s, off)) != hipSuccess) return e;
     char *w = (char *)s->scratch;
     uint8_t *flags = (uint8_t *)(w + o_flags);
-    uint32_t *sel = (uint32_t *)(w + o_sel), *vals = (uint32_t *)(w + o_v0), *nsel = (uint32_t *)(w + o_cnt);
-    uint32_t *k0 = (uint32_t *)(w + o_k0), *k1 = (uint32_t *)(w + o_k1);
+    uint32_t *sel = (uint32_t *)(w + o_sel), *nsel = (uint32_t *)(w + o_cnt);
+    uint16_t *Qp = (uint16_t *)(w + o_k0);
     float *W0 = (float *)(w + o_w), *W1 = (float *)(w + o_w + row_bytes);
     float *tb = (float *)(w + o_tb);
     float4 *nsplit = (float4 *)(w + o_ns);
     uint32_t *H = (uint32_t *)(w + o_h), *cbox = (uint32_t *)(w + o_cb);
     uint2 *psel = (uint2 *)(w + o_ps), *pcnt = (uint2 *)(w + o_pc);
-    uint16_t *Qp = (uint16_t *)k0;
     const dim3 b256(256);
     if (n_total)
         hipLaunchKernelGGL(kd_live_flags_kernel, dim3((unsigned)((n_total + 255) / 256)), b256, 0, st, live, n_total,
                            flags);
-    size_t tb_bytes = std::max(tmp_sel, tmp_sort);
+    size_t tb_bytes = tmp_sel;
     if ((e = rocprim::select(w + o_tmp, tb_bytes, count_it, flags, sel, nsel, (size_t)n_total, st)) != hipSuccess)
         return e;
     hipLaunchKernelGGL((kd_rows_init_kernel<SP, F>), dim3((nl + 255) / 256), b256, 0, st, f32, cap, sel, n_live, W0);
     if (Lg > 0)
         hipLaunchKernelGGL((kd_row_tile_boxes_kernel<SP, F>), dim3((main_tiles + 3) / 4), b256, 0, st, W0, n_live,
                            main_tiles, tb);
-    for (int level = 0; level < Lg && kd_partition(); ++level) {  // the median partition levels
+    for (int level = 0; level < Lg; ++level) {  // the global levels: median partitions
         constexpr int BSL = NB * 8 * 1024 <= 150 * 1024 ? 1024 : 256;
         if (level == 0) {
             if ((main_tiles >> level) > 4096u && BSL == 1024)
@@ -3782,27 +3319,6 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
         hipLaunchKernelGGL((kd_part_scatter_kernel<SP, F>), grid, b256, 0, st, W0, W1, n_live, main_tiles, level, Qp,
                            psel, pcnt, cpn, cbox);
         std::swap(W0, W1);
-    }
-    for (int level = 0; level < Lg && !kd_partition(); ++level) {  // the radix-sort levels (A/B)
-        // few large nodes: wider blocks read their tile boxes (LDS: 2 NB floats per thread)
-        constexpr int BSL = NB * 8 * 1024 <= 150 * 1024 ? 1024 : 256;
-        if ((main_tiles >> level) > 4096u && BSL == 1024)
-            hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F, BSL>), dim3(1u << level), dim3(BSL), 0, st, tb,
-                               main_tiles, level, nsplit);
-        else
-            hipLaunchKernelGGL((kd_node_split_dim_kernel<SP, F, 256>), dim3(1u << level), b256, 0, st, tb, main_tiles,
-                               level, nsplit);
-        hipLaunchKernelGGL((kd_row_keys_kernel<SP, F>), dim3((nl + 255) / 256), b256, 0, st, W0, n_live, main_tiles,
-                           level, nsplit, k0, vals);
-        tb_bytes = std::max(tmp_sel, tmp_sort);
-        if ((e = rocprim::radix_sort_pairs(w + o_tmp, tb_bytes, k0, k1, vals, sel, n_live, 0, level + kKdQBits, st)) !=
-            hipSuccess)
-            return e;
-        hipLaunchKernelGGL((kd_row_gather_boxes_kernel<SP, F>), dim3((main_tiles + 3) / 4), b256, 0, st, W0, sel,
-                           n_live, main_tiles, W1, tb);
-        std::swap(W0, W1);
-        hipLaunchKernelGGL((kd_row_split_kernel<SP, F>), dim3(((1u << level) + 255) / 256), b256, 0, st, W0, n_live,
-                           main_tiles, level, nsplit, s->nodes);
     }
     if (Lg < depth) {  // every node of level Lg finishes its subtree in LDS
         hipLaunchKernelGGL((kd_lds_finish_kernel<SP, F>), dim3(1u << Lg), dim3(kd_lds_block<SP, F>()), 0, st, W0, W1,

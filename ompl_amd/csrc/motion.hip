@@ -137,14 +137,9 @@ static hipError_t dispatch_width(const DevSpace &sp, const DevChecker &ck, F &&l
                            ck.kind == OMPL_GPU_CHECK_CIRCLES2D ||
                            (ck.kind == OMPL_GPU_CHECK_HYPERCUBE && ck.ndim <= sp.dim));
     // the KinematicChain benchmark's 12 links (KinematicChainBenchmark.cpp:48): its checker or none
-    // (A/B build, variant 10: the 12-link chain's fixed form — measured 2.49 ms per cfg4 batch of
+    // (measured and rejected: the 12-link chain's fixed form — 2.49 ms per cfg4 batch of
     // motion checks against the runtime form's 1.13 ms: no scratch, but 290 VGPRs leave one wave
     // per SIMD, and the fp64 trigonometry and segment tests then wait on their own latencies)
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 10
-    if (sp.kind == OMPL_GPU_SPACE_KCHAIN && sp.dim == 12 &&
-        (ck.kind == OMPL_GPU_CHECK_KCHAIN || ck.kind == OMPL_GPU_CHECK_ALL_VALID))
-        return launch(std::integral_constant<int, OMPL_GPU_SPACE_KCHAIN>{}, std::integral_constant<int, 12>{});
-#endif
     if (fixed_ok) {
         if (sp.kind == OMPL_GPU_SPACE_SE3 && sp.dim == 7) return launch(std::integral_constant<int, OMPL_GPU_SPACE_SE3>{}, std::integral_constant<int, 7>{});
         if (sp.kind == OMPL_GPU_SPACE_SO3 && sp.dim == 4) return launch(std::integral_constant<int, OMPL_GPU_SPACE_SO3>{}, std::integral_constant<int, 4>{});
@@ -160,226 +155,9 @@ static hipError_t dispatch_width(const DevSpace &sp, const DevChecker &ck, F &&l
     return launch(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
 }
 
-// ---- KinematicChain: a wave per state check ------------------------------------------------
-// The chain's isValid (demos/KinematicChain.h:200-276) is ~9k fp64 operations: the 2 (n + 2)
-// joint positions, then n(n+1)/2 self and (n+1) x |env| environment segment tests.  A thread
-// per edge holds every position and fails either way (runtime width: 1.3 KB of scratch per lane;
-// 12 links unrolled: 290 VGPRs, one wave per SIMD).  Here a wave evaluates one state at a time:
-// lane i holds angle i, the cumulative angles and positions are prefix sums that lane i forms
-// itself, term by term in the reference's order (so every partial sum rounds as in the serial
-// loop), cos / sin run one per lane, the positions go to LDS, and the 364 segment tests of the
-// 12-link horn benchmark spread over the lanes (any intersection = invalid).  The motion
-// validator walks an edge's samples in the same FIFO-bisection order with the same early exit,
-// so the isValid count is the reference's.  Same arithmetic as chain_valid, bit for bit.
-// Measured on cfg4 (round 4): 1.88 ms per batch of motion checks against 1.17 ms for the
-// thread-per-edge runtime-width form — every check pays the serial prefix loops, 64 lanes of
-// sincos and all 364 tests, where a thread leaves at its first intersection — so it stays an
-// A/B form (OMPL_GPU_CHAIN_WAVE=1); the product keeps the thread-per-edge kernels.
-constexpr int kChainWaveMax = 62;  // links: positions n + 2 <= 64 lanes
-
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFFll), l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
-
-// one state, angle x (lane i < n): chain_valid's bit.  px / py: this wave's LDS rows (n + 2 each)
-__device__ bool chain_valid_wave(double x, int n, double link, const double *__restrict__ env, int nenv, double *px,
-                                 double *py) {
-    const int lane = threadIdx.x & 63;
-    double theta = 0.0;  // theta_i = x_0 + ... + x_i, in order
-    for (int j = 0; j < n; ++j) {
-        const double xj = readlane_d(x, j);
-        if (j <= lane) theta += xj;
-    }
-    double c = 0.0, sn = 0.0;
-    if (lane < n) glibc_sincos(theta, sn, c);
-    const double cl = c * link, sl = sn * link;
-    double xn = 0.0, yn = 0.0;  // position i + 1 = sum_{j <= i} (cos(theta_j) link), in order
-    for (int j = 0; j < n; ++j) {
-        const double a = readlane_d(cl, j), b = readlane_d(sl, j);
-        if (j <= lane) {
-            xn = xn + a;
-            yn = yn + b;
-        }
-    }
-    if (lane < n) {
-        px[lane + 1] = xn;
-        py[lane + 1] = yn;
-    }
-    if (lane == 0) {
-        px[0] = 0.0;
-        py[0] = 0.0;
-    }
-    if (lane == n - 1) {  // the tip: x + cos(theta) * 0.001 (KinematicChain.h)
-        px[n + 1] = xn + c * 0.001;
-        py[n + 1] = yn + sn * 0.001;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const int ns = n + 1;
-    bool hit = false;
-    for (int p = lane; p < ns * ns; p += 64) {  // self pairs i < j
-        const int i = p / ns, j = p % ns;
-        if (i < j && seg_intersect(px[i], py[i], px[i + 1], py[i + 1], px[j], py[j], px[j + 1], py[j + 1])) hit = true;
-    }
-    for (int p = lane; p < ns * nenv; p += 64) {  // environment pairs
-        const int i = p / nenv, j = p % nenv;
-        if (seg_intersect(px[i], py[i], px[i + 1], py[i + 1], env[4 * j], env[4 * j + 1], env[4 * j + 2], env[4 * j + 3]))
-            hit = true;
-    }
-    const bool any = __ballot(hit) != 0;
-    __builtin_amdgcn_wave_barrier();  // px / py are rewritten by the next check
-    return !any;
-}
-
-// chain distance (KinematicChain.h:105-124) with a lane per link, the sums in the reference's order
-__device__ double chain_dist_wave(double a, double b, int n, double link) {
-    const int lane = threadIdx.x & 63;
-    double t1 = 0.0, t2 = 0.0;
-    for (int j = 0; j < n; ++j) {
-        const double aj = readlane_d(a, j), bj = readlane_d(b, j);
-        if (j <= lane) {
-            t1 += aj;
-            t2 += bj;
-        }
-    }
-    double ddx = 0.0, ddy = 0.0;
-    if (lane < n) {
-        double s1, c1, s2, c2;
-        glibc_sincos(t1, s1, c1);
-        glibc_sincos(t2, s2, c2);
-        ddx = c1 - c2;
-        ddy = s1 - s2;
-    }
-    double dx = 0.0, dy = 0.0;
-    for (int j = 0; j < n; ++j) {
-        const double u = readlane_d(ddx, j), v = readlane_d(ddy, j);
-        if (j <= lane) {
-            dx += u;
-            dy += v;
-        }
-    }
-    const double term = lane < n ? sqrt(dx * dx + dy * dy) : 0.0;
-    double dist = 0.0;
-    for (int j = 0; j < n; ++j) dist += readlane_d(term, j);
-    return dist * link;
-}
-
-// chain_interp (KinematicChain.h:150-175) of one component
-__device__ __forceinline__ double chain_interp1(double f, double to, double t) {
-    double diff = to - f;
-    if (fabs(diff) <= kPi) return f + diff * t;
-    if (diff > 0.0)
-        diff = 2.0 * kPi - diff;
-    else
-        diff = -2.0 * kPi - diff;
-    double v = f - diff * t;
-    if (v > kPi)
-        v -= 2.0 * kPi;
-    else if (v < -kPi)
-        v += 2.0 * kPi;
-    return v;
-}
-
-// a wave per edge (4 per block): checkMotion as motion_kernel, every isValid a wave check
-__global__ __launch_bounds__(256) void motion_chain_wave_kernel(DevSpace sp, DevChecker ck, const double *__restrict__ s1,
-                                                                const double *__restrict__ s2, uint32_t m,
-                                                                uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out,
-                                                                int32_t *__restrict__ fi_out,
-                                                                unsigned long long *__restrict__ counters) {
-    __shared__ double pos[4][2][kChainWaveMax + 2];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t e = blockIdx.x * 4 + w;
-    const int n = sp.dim;
-    double *px = pos[w][0], *py = pos[w][1];
-    bool result = true;
-    uint32_t checks = 0;
-    if (e < m) {
-        const double a = lane < n ? s1[(size_t)e * n + lane] : 0.0, b = lane < n ? s2[(size_t)e * n + lane] : 0.0;
-        ++checks;
-        result = chain_valid_wave(b, n, sp.link, ck.data, ck.count, px, py);  // :96 — s2 first
-        const int nd = (result || nd_out || fi_out) ? (int)seg_count(chain_dist_wave(a, b, n, sp.link), sp.lvs0, sp.f0) : 0;
-        if (nd_out && lane == 0) nd_out[e] = nd;
-        if (result && nd >= 2) {  // level-order walk of the FIFO bisection :104-134 (as motion_kernel)
-            bool any = true;
-            for (int L = 0; any && result && L < 32; ++L) {
-                any = false;
-                const uint32_t np = 1u << L;
-                for (uint32_t p = 0; p < np && result; ++p) {
-                    int lo = 1, hi = nd - 1;
-                    bool empty = false;
-                    for (int bit = L - 1; bit >= 0; --bit) {
-                        const int mid = (lo + hi) / 2;
-                        if ((p >> bit) & 1u)
-                            lo = mid + 1;
-                        else
-                            hi = mid - 1;
-                        if (lo > hi) {
-                            empty = true;
-                            break;
-                        }
-                    }
-                    if (empty) continue;
-                    any = true;
-                    const int mid = (lo + hi) / 2;
-                    const double t = chain_interp1(a, b, (double)mid / (double)nd);
-                    ++checks;
-                    if (!chain_valid_wave(t, n, sp.link, ck.data, ck.count, px, py)) result = false;
-                }
-            }
-        }
-        if (valid && lane == 0) valid[e] = result ? 1 : 0;
-        if (fi_out) {
-            int fi = -1;
-            if (!result) {  // linear sweep :57-69, then s2 :73-79
-                for (int j = 1; j < nd; ++j) {
-                    const double t = chain_interp1(a, b, (double)j / (double)nd);
-                    if (!chain_valid_wave(t, n, sp.link, ck.data, ck.count, px, py)) {
-                        fi = j;
-                        break;
-                    }
-                }
-                if (fi < 0) fi = nd;
-            }
-            if (lane == 0) fi_out[e] = fi;
-        }
-    }
-    if (counters) {  // one atomic per counter per block
-        __shared__ unsigned long long part[3][4];
-        if (lane == 0) {
-            part[0][w] = (e < m && result) ? 1ull : 0ull;
-            part[1][w] = (e < m && !result) ? 1ull : 0ull;
-            part[2][w] = checks;
-        }
-        __syncthreads();
-        if (threadIdx.x < 3) {
-            const unsigned long long v = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] + part[threadIdx.x][3];
-            if (v) atomicAdd(&counters[threadIdx.x], v);
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void state_valid_chain_wave_kernel(DevSpace sp, DevChecker ck,
-                                                                     const double *__restrict__ s, uint32_t m,
-                                                                     uint8_t *__restrict__ valid) {
-    __shared__ double pos[4][2][kChainWaveMax + 2];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t i = blockIdx.x * 4 + w;
-    if (i >= m) return;  // wave-uniform
-    const int n = sp.dim;
-    const double x = lane < n ? s[(size_t)i * n + lane] : 0.0;
-    const bool ok = chain_valid_wave(x, n, sp.link, ck.data, ck.count, pos[w][0], pos[w][1]);
-    if (lane == 0) valid[i] = ok ? 1 : 0;
-}
-
-static bool chain_wave(const DevSpace &sp, const DevChecker &ck) {
-    static const int on = [] {  // A/B switch: OMPL_GPU_CHAIN_WAVE=1 -> the wave-per-check kernels
-        const char *v = std::getenv("OMPL_GPU_CHAIN_WAVE");
-        return v ? std::atoi(v) : 0;
-    }();
-    return on && sp.kind == OMPL_GPU_SPACE_KCHAIN && ck.kind == OMPL_GPU_CHECK_KCHAIN && sp.dim >= 1 &&
-           sp.dim <= kChainWaveMax;
-}
+// (Measured and rejected, DESIGN §8: a wave per chain state check — lane per link, positions in
+// LDS, the segment tests over the lanes — 1.88 ms per cfg4 batch of motion checks against 1.17 ms
+// for the thread-per-edge form, which leaves at its first intersection.)
 
 static bool needs_rotation(const DevSpace &sp, const DevChecker &ck) {
     if (sp.kind != OMPL_GPU_SPACE_SE3) return true;
@@ -396,11 +174,6 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
                          uint8_t *valid, int32_t *nd, int32_t *first_invalid, unsigned long long *counters,
                          hipStream_t st) {
     if (m == 0) return hipSuccess;
-    if (chain_wave(sp, ck)) {
-        hipLaunchKernelGGL(motion_chain_wave_kernel, dim3((m + 3) / 4), dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd,
-                           first_invalid, counters);
-        return hipGetLastError();
-    }
     const int rot = needs_rotation(sp, ck) ? 1 : 0;
     return dispatch_width(sp, ck, [&](auto kind, auto width) {
         hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value>), dim3((m + 255) / 256),
@@ -479,10 +252,6 @@ hipError_t launch_space_pairs(const DevSpace &sp, const double *a, const double 
 hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const double *s, uint32_t m, uint8_t *valid,
                               hipStream_t st) {
     if (m == 0) return hipSuccess;
-    if (chain_wave(sp, ck)) {
-        hipLaunchKernelGGL(state_valid_chain_wave_kernel, dim3((m + 3) / 4), dim3(256), 0, st, sp, ck, s, m, valid);
-        return hipGetLastError();
-    }
     return dispatch_width(sp, ck, [&](auto kind, auto width) {
         hipLaunchKernelGGL((state_valid_kernel<decltype(kind)::value, decltype(width)::value>), dim3((m + 255) / 256),
                            dim3(256), 0, st, sp, ck, s, m, valid);

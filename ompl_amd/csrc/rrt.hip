@@ -245,18 +245,6 @@ __global__ __launch_bounds__(256) void rrt_step_kernel(double *__restrict__ feat
 // the pollers spread over memory channels.  A waiting block gives up after kSpinLimit polls and
 // raises the abort word, which every waiter polls too: a grid that cannot progress drains (the host
 // reports it).
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 4  // phase timer build (s_memrealtime, 100 MHz)
-#define RRT_T0() uint64_t t_prev = __builtin_amdgcn_s_memrealtime()
-#define RRT_T(k)                                                 \
-    do {                                                         \
-        const uint64_t t_now = __builtin_amdgcn_s_memrealtime(); \
-        tph[k] += t_now - t_prev;                                \
-        t_prev = t_now;                                          \
-    } while (0)
-#else
-#define RRT_T0() (void)0
-#define RRT_T(k) (void)0
-#endif
 constexpr uint32_t kSpinLimit = 1u << 22;    // ~0.1 s of s_sleep(1) polls per wait
 constexpr uint32_t kRrtMaxCoopBlocks = 256;  // scanning blocks + the decider; the decider polls one flag per thread
 constexpr int kLook = 2;                     // samples the scans run ahead of the decisions
@@ -444,9 +432,6 @@ __global__ __launch_bounds__(256) void rrt_persistent_kernel(
     const int dim = sp.dim;
     uint64_t *abort_word = sync + 2, *flag = sync + kSyncFlags, *rec = sync + kSyncRec;
     double Bst = bitsd(ld_sync(&sync[kSyncB])), eta_st = bitsd(ld_sync(&sync[kSyncEta]));
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 4
-    uint64_t tph[4] = {0, 0, 0, 0};
-#endif
     if (b < nsb) {
         // ---- a scanning block
         const uint64_t lo = (uint64_t)b * slice, hi = lo + slice;
@@ -486,16 +471,13 @@ __global__ __launch_bounds__(256) void rrt_persistent_kernel(
             return !stop;
         };
         for (uint32_t s = 0; s < ns; ++s) {
-            RRT_T0();
             if (s >= (uint32_t)kLook + 1 && !process(s - kLook - 1)) return;
-            RRT_T(1);
             double qv[F];
             load_sample<SP, F>(samples + (size_t)s * dim, dim, qv);
             double wd;
             uint32_t wi;
             slice_nearest<SP, F>(feat, feat32, cap, lo, hi < n ? hi : n, qv, sp, Bst, eta_st, wd, wi, sh_row, lds_d,
                                  lds_i, lds_f);
-            RRT_T(0);
             if (threadIdx.x == 0) {  // record slot s mod R, then the flag
                 uint64_t *r = rec + ((size_t)(s % kRing) * nsb + b) * kRecWords;
                 st_sync(&r[0], dbits(wd));
@@ -505,16 +487,10 @@ __global__ __launch_bounds__(256) void rrt_persistent_kernel(
                 stores_done();
                 st_sync(&flag[b], (uint64_t)s + 1);
             }
-            RRT_T(2);
         }
         // the decisions not processed yet: their rows still go into the store
         for (uint32_t j = next_dec; j < ns;)
             if (!process(j++)) break;
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 4
-        if (threadIdx.x == 0 && (b == 0 || b == nsb - 1))
-            printf("rrt-phases block%u: scan %.2f us, wait-decision %.2f us, publish %.2f us (nsb %u, slice %lu)\n", b,
-                   tph[0] * 0.01 / ns, tph[1] * 0.01 / ns, tph[2] * 0.01 / ns, nsb, (unsigned long)slice);
-#endif
         return;
     }
     // ---- the decider
@@ -527,7 +503,6 @@ __global__ __launch_bounds__(256) void rrt_persistent_kernel(
     uint64_t n = n0;
     uint32_t j = 0;
     for (; j < ns; ++j) {
-        RRT_T0();
         const double *s = samples + (size_t)j * dim;
         if (threadIdx.x < F) sh_q[threadIdx.x] = threadIdx.x < (uint32_t)dim ? s[threadIdx.x] : 0.0;
         // 1. every slice's record of sample j
@@ -537,7 +512,6 @@ __global__ __launch_bounds__(256) void rrt_persistent_kernel(
             if (threadIdx.x == 0) st_sync(abort_word, 1);
             return;  // aborted: the host sees the abort word and fails the call
         }
-        RRT_T(0);
         double gd = __builtin_inf();
         uint32_t gi = kNoId;
         double row[F];
@@ -568,7 +542,6 @@ __global__ __launch_bounds__(256) void rrt_persistent_kernel(
             for (int f = 0; f < F; ++f) sh_row[f] = row[f];
         }
         __syncthreads();
-        RRT_T(1);
         // 3. steer, check the motion, goal test (RRT.cpp:137-187)
         const uint32_t ri = gi;
         rrt_decide<SP, kRrtWidth<SP>>([&](int c) { return sh_row[c]; }, sh_q, ri, sp, msp, ck, maxd, s1, s2, &sh_nd,
@@ -603,16 +576,11 @@ __global__ __launch_bounds__(256) void rrt_persistent_kernel(
             sh_go = !solved;
         }
         __syncthreads();
-        RRT_T(2);
         if (!sh_go) break;
     }
     if (threadIdx.x == 0) {
         *n_dev = n;
         for (int w = 0; w < kGoalWords; ++w) grec[w] = ld_sync(&sync[kSyncGoal + w]);
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 4
-        printf("rrt-phases decider: wait-flags %.2f us, merge %.2f us, decide %.2f us\n", tph[0] * 0.01 / ns,
-               tph[1] * 0.01 / ns, tph[2] * 0.01 / ns);
-#endif
     }
 }
 
@@ -658,9 +626,6 @@ hipError_t run_rrt(const DevSpace &sp, const DevSpace &msp, const DevChecker &ck
 }  // namespace
 
 uint32_t rrt_coop_blocks(int device, const DevSpace &sp, const FeatGeom &g) {
-#if defined(OMPL_AMD_VARIANT) && OMPL_AMD_VARIANT == 3
-    return 0;  // A/B build: the two-launch form
-#endif
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 0;
     const void *fn = nullptr;

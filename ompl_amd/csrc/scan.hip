@@ -1,7 +1,8 @@
 // scan.hip — exclusive prefix sums of 64-bit counts on the device (CSR offsets of the radius,
-// PRM* and RRT* paths): out[i] = in[0] + ... + in[i - 1] for i in [0, n], so out[n] is the total.
-// Three launches, no host round trip: per-1,024-element block totals, one block scanning the
-// totals, then every block's local scan plus its offset.  Wave scans by DPP-free shuffles.
+// PRM* and RRT* paths): out[i] = in[0] + ... + in[i - 1] for i in [0, n], so out[n] is the total,
+// and optionally the largest element (the radius path's longest segment).  Three launches, no host
+// round trip: per-1,024-element block totals (and maxima), one block scanning the totals, then
+// every block's local scan plus its offset.  Wave scans by shuffles.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -38,24 +39,54 @@ __device__ __forceinline__ uint64_t block_exclusive(uint64_t v, uint64_t *total)
     return off + inc - v;
 }
 
+// block maximum of one value per thread (256 threads), valid in every thread
+__device__ __forceinline__ uint64_t block_max(uint64_t v) {
+    __shared__ uint64_t wm[4];
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t u = (uint64_t)__shfl_xor((long long)v, o, 64);
+        v = u > v ? u : v;
+    }
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint64_t m = wm[0];
+    for (int i = 1; i < 4; ++i) m = wm[i] > m ? wm[i] : m;
+    __syncthreads();
+    return m;
+}
+
+// part[b] = block b's total; with MAX, part[nb + b] = its largest element
+template <bool MAX>
 __global__ __launch_bounds__(256) void scan_totals_kernel(const uint64_t *__restrict__ in, uint64_t n,
                                                           uint64_t *__restrict__ part) {
     const uint64_t b = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
-    uint64_t s = 0;
-    for (int k = 0; k < 4; ++k) s += b + k < n ? in[b + k] : 0;
+    uint64_t s = 0, m = 0;
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t v = b + k < n ? in[b + k] : 0;
+        s += v;
+        m = v > m ? v : m;
+    }
     uint64_t tot;
     block_exclusive(s, &tot);
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
+    if constexpr (MAX) {
+        m = block_max(m);
+        if (threadIdx.x == 0) part[gridDim.x + blockIdx.x] = m;
+    }
 }
 
-// one block: exclusive scan of nb block totals in place, chunk by chunk
-__global__ __launch_bounds__(256) void scan_parts_kernel(uint64_t *__restrict__ part, uint32_t nb) {
+// one block: exclusive scan of nb block totals in place, chunk by chunk; with MAX the largest of
+// the block maxima goes to *max_out
+template <bool MAX>
+__global__ __launch_bounds__(256) void scan_parts_kernel(uint64_t *__restrict__ part, uint32_t nb,
+                                                         uint64_t *__restrict__ max_out) {
     __shared__ uint64_t carry;
     if (threadIdx.x == 0) carry = 0;
     __syncthreads();
+    uint64_t m = 0;
     for (uint32_t c = 0; c < nb; c += 256) {
         const uint32_t i = c + threadIdx.x;
         const uint64_t v = i < nb ? part[i] : 0;
+        if (MAX && i < nb) m = part[nb + i] > m ? part[nb + i] : m;
         uint64_t tot;
         const uint64_t ex = block_exclusive(v, &tot);
         const uint64_t base = carry;
@@ -63,6 +94,10 @@ __global__ __launch_bounds__(256) void scan_parts_kernel(uint64_t *__restrict__ 
         __syncthreads();
         if (threadIdx.x == 0) carry = base + tot;
         __syncthreads();
+    }
+    if constexpr (MAX) {
+        m = block_max(m);
+        if (threadIdx.x == 0) *max_out = m;
     }
 }
 
@@ -85,14 +120,28 @@ __global__ __launch_bounds__(256) void scan_apply_kernel(const uint64_t *__restr
 
 }  // namespace
 
-size_t exclusive_scan_u64_workspace(uint64_t n) { return sizeof(uint64_t) * ((n + kScanBlock - 1) / kScanBlock + 1); }
+size_t exclusive_scan_u64_workspace(uint64_t n) {
+    return sizeof(uint64_t) * (2 * ((n + kScanBlock - 1) / kScanBlock) + 1);
+}
 
-hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t n, uint64_t *out, void *ws, hipStream_t st) {
-    if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+hipError_t launch_exclusive_scan_u64(const uint64_t *in, uint64_t n, uint64_t *out, void *ws, hipStream_t st,
+                                     uint64_t *max_out) {
+    if (n == 0) {
+        if (max_out) {
+            const hipError_t e = hipMemsetAsync(max_out, 0, sizeof(uint64_t), st);
+            if (e != hipSuccess) return e;
+        }
+        return hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+    }
     const uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
     uint64_t *part = (uint64_t *)ws;
-    hipLaunchKernelGGL(scan_totals_kernel, dim3(nb), dim3(256), 0, st, in, n, part);
-    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(256), 0, st, part, nb);
+    if (max_out) {
+        hipLaunchKernelGGL(scan_totals_kernel<true>, dim3(nb), dim3(256), 0, st, in, n, part);
+        hipLaunchKernelGGL(scan_parts_kernel<true>, dim3(1), dim3(256), 0, st, part, nb, max_out);
+    } else {
+        hipLaunchKernelGGL(scan_totals_kernel<false>, dim3(nb), dim3(256), 0, st, in, n, part);
+        hipLaunchKernelGGL(scan_parts_kernel<false>, dim3(1), dim3(256), 0, st, part, nb, nullptr);
+    }
     hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(256), 0, st, in, n, part, out);
     return hipGetLastError();
 }
