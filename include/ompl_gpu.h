@@ -38,6 +38,8 @@
  *                          src/ompl/geometric/planners/rrt/src/RRT.cpp:137-146
  *   ompl_gpu_rrt_grow_device  the RRT loop itself                 RRT.cpp:128-192
  *   ompl_gpu_rrtstar_batch_device  RRT*'s iterations (geometric part) RRTstar.cpp:247-542, :603-618
+ *   ompl_gpu_rrtstar_tree_* / _stage / _commit  RRT*'s cost logic (parent choice, rewiring)
+ *                          RRTstar.cpp:285-457, :620-643
  *   ompl_gpu_prm_add_milestones  PRM* causal roadmap batches      prm/src/PRM.cpp:562-596
  *   ompl_gpu_knn_merge_device  per-shard nearestK lists -> global top k (tree-sharded mode)
  *   ompl_gpu_csr_merge_device  per-shard nearestR CSR results -> one CSR (tree-sharded mode)
@@ -371,7 +373,7 @@ ompl_gpu_status ompl_gpu_rrt_solve_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, cons
  * This is the geometric part of every iteration: which states join, the neighbourhoods, and both
  * motion bits of every (neighbour, x_i) pair — checkMotion(nbh, x_i) for the parent choice in
  * cost order (:319-357) and checkMotion(x_i, nbh) for the rewiring (:414-440) — so the planner's
- * cost logic needs only lookups (ompl_amd/rrtstar.py).  None of it depends on costs.
+ * cost logic needs only lookups (ompl_gpu_rrtstar_commit below).  None of it depends on costs.
  * Inputs: d_samples ns AoS rows (device).  Outputs (device, caller-owned, ns entries each, may be
  * NULL): d_nearest[i] = id of nmotion; d_added[i] = the id x_i got, or 0xFFFFFFFF; d_inc[i] =
  * distance(nmotion, x_i) (the motion's incCost, :288); d_states[i] = x_i (dim reals).  The
@@ -395,6 +397,41 @@ ompl_gpu_status ompl_gpu_rrtstar_batch_device(ompl_gpu_nn *nn, ompl_gpu_mv *mv, 
                                               double max_distance, double k_rrt, uint32_t *d_nearest,
                                               uint32_t *d_added, double *d_inc, double *d_states,
                                               ompl_gpu_rrtstar_result *out);
+
+/* ---- RRT* cost logic -----------------------------------------------------------
+ * The tree's costs as RRTstar keeps them in its Motions (RRTstar.h:347-372: parent, incCost,
+ * cost, children), indexed by the nearest-neighbour ids, and the cost part of every iteration
+ * (RRTstar.cpp:285-457, delayCC, the path-length objective) over the device batch's results:
+ * the parent in cost order among the neighbours (:319-357), the rewiring (:414-457) with
+ * removeFromParent / updateChildCosts (:620-643), each sample in order.  Host-side; a tree
+ * belongs to one planner.  ompl_gpu_rrtstar_stage copies a batch's results to the host (device ->
+ * host, synchronous on nn's stream, under nn's lock) and queues them; ompl_gpu_rrtstar_commit
+ * processes the oldest queued batch.  stage and commit may run on two threads (the next device
+ * batch then overlaps the previous batch's cost logic); commit, add and read must not overlap.
+ * tree_add appends states: parent[j] is -1 (a start state, cost = the identity 0) or an earlier
+ * id; NULL arrays mean -1 / 0 / 0.  commit writes per sample (when not NULL; ns_cap entries
+ * available) the nearest id, the added id or -1, and the parent chosen or -1.
+ * totals: [0] rewires, [1] checkMotion calls the sequential loop makes (the bits it looks up),
+ * [2] states added, [3] neighbourhood entries, [4] samples, [5] child costs updateChildCosts
+ * rewrote. */
+typedef struct ompl_gpu_rrtstar_tree ompl_gpu_rrtstar_tree;
+ompl_gpu_status ompl_gpu_rrtstar_tree_create(ompl_gpu_rrtstar_tree **out);
+void ompl_gpu_rrtstar_tree_destroy(ompl_gpu_rrtstar_tree *t);
+ompl_gpu_status ompl_gpu_rrtstar_tree_add(ompl_gpu_rrtstar_tree *t, size_t m, const int64_t *parent,
+                                          const double *inc, const double *cost);
+ompl_gpu_status ompl_gpu_rrtstar_tree_size(const ompl_gpu_rrtstar_tree *t, size_t *n);
+ompl_gpu_status ompl_gpu_rrtstar_tree_read(const ompl_gpu_rrtstar_tree *t, size_t first, size_t m, int64_t *parent,
+                                           double *inc, double *cost);
+ompl_gpu_status ompl_gpu_rrtstar_tree_totals(const ompl_gpu_rrtstar_tree *t, uint64_t totals[6]);
+ompl_gpu_status ompl_gpu_rrtstar_stage(ompl_gpu_rrtstar_tree *t, ompl_gpu_nn *nn, size_t ns, const uint32_t *d_nearest,
+                                       const uint32_t *d_added, const double *d_inc,
+                                       const ompl_gpu_rrtstar_result *res);
+/* the same from host arrays (offsets: ns + 1 entries; a planner whose geometric part ran elsewhere) */
+ompl_gpu_status ompl_gpu_rrtstar_stage_host(ompl_gpu_rrtstar_tree *t, size_t ns, const uint32_t *nearest,
+                                            const uint32_t *added, const double *inc, const uint64_t *offsets,
+                                            const uint32_t *ids, const double *dist, const uint8_t *bits);
+ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_distance, size_t ns_cap,
+                                        int64_t *nearest, int64_t *added, int64_t *chosen, size_t *ns_out);
 
 /* ---- BIT* batch sampling -----------------------------------------------------
  * BITstar::ImplicitGraph::updateSamples before a solution exists (ImplicitGraph.cpp:924-1000: the

@@ -115,6 +115,15 @@ SIGNATURES = {
     "ompl_gpu_rrt_aborts": (C.c_int, [_P, _U64]),
     "ompl_gpu_rrtstar_batch_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, C.c_double, _P, _P, _P, _P,
                                                 C.POINTER(RrtStarResult)]),
+    "ompl_gpu_rrtstar_tree_create": (C.c_int, [C.POINTER(_P)]),
+    "ompl_gpu_rrtstar_tree_destroy": (None, [_P]),
+    "ompl_gpu_rrtstar_tree_add": (C.c_int, [_P, C.c_size_t, _P, _P, _P]),
+    "ompl_gpu_rrtstar_tree_size": (C.c_int, [_P, C.POINTER(C.c_size_t)]),
+    "ompl_gpu_rrtstar_tree_read": (C.c_int, [_P, C.c_size_t, C.c_size_t, _P, _P, _P]),
+    "ompl_gpu_rrtstar_tree_totals": (C.c_int, [_P, _U64]),
+    "ompl_gpu_rrtstar_stage": (C.c_int, [_P, _P, C.c_size_t, _P, _P, _P, C.POINTER(RrtStarResult)]),
+    "ompl_gpu_rrtstar_stage_host": (C.c_int, [_P, C.c_size_t, _P, _P, _P, _P, _P, _P, _P]),
+    "ompl_gpu_rrtstar_commit": (C.c_int, [_P, C.c_double, C.c_size_t, _P, _P, _P, C.POINTER(C.c_size_t)]),
     "ompl_gpu_csr_merge_device": (C.c_int, [_P, C.c_uint32, C.c_size_t, _P, _P, C.c_size_t, _P, _P, _P, _P]),
     "ompl_gpu_knn_merge_device": (C.c_int, [_P, _P, C.c_uint32, C.c_size_t, C.c_uint32, _P, _P, _P]),
     "ompl_gpu_rrt_solve_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, _D, C.c_double, _P, _P, _U64,

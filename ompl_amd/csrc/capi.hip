@@ -23,6 +23,7 @@
 
 #include "../../include/ompl_gpu.h"
 #include "kernels.h"
+#include "rrtstar_tree.h"
 #include "sampler_impl.h"
 #include "topk.h"
 
@@ -1848,6 +1849,58 @@ ompl_gpu_status ompl_gpu_rrtstar_batch_device(ompl_gpu_nn *h, ompl_gpu_mv *mv, c
     if (h->n_live == 0) return fail(OMPL_GPU_ERR_EMPTY, "No elements found in nearest neighbors data structure");
     HIP_OR_FAIL(hipSetDevice(h->device));
     return rrtstar_locked(h, mv, d_samples, ns, max_distance, k_rrt, d_nearest, d_added, d_inc, d_states, out);
+}
+
+// the batch's per-sample outputs and neighbourhoods to the host, queued for ompl_gpu_rrtstar_commit
+// (rrtstar_tree.cpp); under nn's lock, so that no later call on nn rewrites them meanwhile
+ompl_gpu_status ompl_gpu_rrtstar_stage(ompl_gpu_rrtstar_tree *t, ompl_gpu_nn *h, size_t ns, const uint32_t *d_nearest,
+                                       const uint32_t *d_added, const double *d_inc,
+                                       const ompl_gpu_rrtstar_result *res) {
+    if (!t || !h || !res || (ns && (!d_nearest || !d_added || !d_inc || !res->offsets)))
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (res->total && (!res->ids || !res->dist || !res->bits)) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    ompl_amd::RrtStarStaged b;
+    {
+        std::lock_guard<std::mutex> lk(t->mu);
+        if (!t->spare.empty()) {
+            b = std::move(t->spare.back());
+            t->spare.pop_back();
+        }
+    }
+    const size_t E = (size_t)res->total;
+    try {
+        b.ns = ns;
+        b.nearest.resize(ns);
+        b.added.resize(ns);
+        b.inc.resize(ns);
+        b.off.resize(ns + 1);
+        b.ids.resize(E);
+        b.dist.resize(E);
+        b.bits.resize(E);
+    } catch (const std::bad_alloc &) {
+        return fail(OMPL_GPU_ERR_OOM, "out of host memory");
+    }
+    if (ns) {
+        std::lock_guard<std::mutex> lk(h->mu);
+        HIP_OR_FAIL(hipSetDevice(h->device));
+        const hipMemcpyKind d2h = hipMemcpyDeviceToHost;
+        HIP_OR_FAIL(hipMemcpyAsync(b.nearest.data(), d_nearest, 4 * ns, d2h, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(b.added.data(), d_added, 4 * ns, d2h, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(b.inc.data(), d_inc, 8 * ns, d2h, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(b.off.data(), res->offsets, 8 * (ns + 1), d2h, h->stream));
+        if (E) {
+            HIP_OR_FAIL(hipMemcpyAsync(b.ids.data(), res->ids, 4 * E, d2h, h->stream));
+            HIP_OR_FAIL(hipMemcpyAsync(b.dist.data(), res->dist, 8 * E, d2h, h->stream));
+            HIP_OR_FAIL(hipMemcpyAsync(b.bits.data(), res->bits, E, d2h, h->stream));
+        }
+        HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+        if (b.off[ns] != E) return fail(OMPL_GPU_ERR_INVALID_ARG, "result record does not match the offsets");
+    } else {
+        b.off[0] = 0;
+    }
+    std::lock_guard<std::mutex> lk(t->mu);
+    t->staged.push_back(std::move(b));
+    return OMPL_GPU_OK;
 }
 
 // ------------------------------------------------------------------------------ RRT

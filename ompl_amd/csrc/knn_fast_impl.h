@@ -806,7 +806,6 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     // values live across the whole walk cost 29 VGPRs (69 -> 98, 7 -> 5 waves per SIMD)
     __shared__ float slb[G][64];
     bool first_round = true;  // the neighbourhood's three are always visited
-    int pop_l = -1;           // round slot of the last popped super-tile (-1: the neighbourhood's)
     auto next_super = [&]() -> int {  // next super-tile to visit, -1 when done
         for (;;) {
             if (sm && !first_round) {  // drop what the tightened thresholds exclude
@@ -821,7 +820,6 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
             if (sm) {
                 const int l = __builtin_ctzll(sm);
                 sm &= sm - 1;
-                pop_l = first_round ? -1 : l;
                 return (int)(base + l);
             }
             if (sb >= nsuper) return -1;

@@ -1,0 +1,268 @@
+// rrtstar_tree.cpp — RRT*'s cost logic over a staged device batch (host C++; see rrtstar_tree.h).
+//
+// For every sample of the batch whose state x joined the tree, in sample order, exactly as
+// RRTstar::solve with delayCC (RRTstar.cpp:285-457, the path-length objective: motionCost =
+// distance, combineCosts = +, isCostBetterThan = <):
+//   the motion as created: parent nmotion, incCost = distance(nmotion, x), cost = cost(nmotion) +
+//     incCost (:285-289);
+//   the neighbours in order of cost(nbh) + distance(nbh, x) (a stable sort: equal costs keep the
+//     (distance, id) order; the reference's std::sort leaves such ties unspecified), the first with
+//     nbh == nmotion or (distance < maxDistance and checkMotion(nbh, x)) becomes the parent, the
+//     ones before it are marked invalid (:319-357);
+//   x joins its parent's children (:410-411);
+//   rewiring, in neighbourhood order (:414-457): for each nbh != parent with cost(x) + distance <
+//     cost(nbh) and a valid motion (the cached mark, else distance < maxDistance and
+//     checkMotion(x, nbh)), nbh leaves its parent's children (removeFromParent :620-631), takes x
+//     as parent, and its subtree's costs follow (updateChildCosts :633-643).
+// The checkMotion results are the device's bits; none of the device work depends on costs.
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <numeric>
+
+#include "../../include/ompl_gpu.h"
+#include "rrtstar_tree.h"
+
+namespace ompl_amd {
+void set_last_error(const char *msg);  // capi.hip
+}
+
+using ompl_amd::RrtStarStaged;
+
+namespace {
+
+ompl_gpu_status bad(ompl_gpu_status s, const char *msg) {
+    ompl_amd::set_last_error(msg);
+    return s;
+}
+
+uint64_t update_child_costs(ompl_gpu_rrtstar_tree *t, uint32_t m) {  // RRTstar.cpp:633-643, iterative
+    auto &st = t->stack;
+    st.clear();
+    st.push_back(m);
+    uint64_t visits = 0;
+    while (!st.empty()) {
+        const uint32_t u = st.back();
+        st.pop_back();
+        const double cu = t->cost[u];
+        visits += t->children[u].size();
+        for (uint32_t c : t->children[u]) {
+            t->cost[c] = cu + t->inc[c];
+            if (!t->children[c].empty()) st.push_back(c);
+        }
+    }
+    return visits;
+}
+
+void remove_from_parent(ompl_gpu_rrtstar_tree *t, uint32_t m) {  // RRTstar.cpp:620-631
+    auto &ch = t->children[(size_t)t->parent[m]];
+    auto it = std::find(ch.begin(), ch.end(), m);
+    if (it != ch.end()) ch.erase(it);
+}
+
+void grow(ompl_gpu_rrtstar_tree *t, size_t n) {
+    if (t->parent.size() >= n) return;
+    t->parent.resize(n, -1);
+    t->inc.resize(n, 0.0);
+    t->cost.resize(n, 0.0);
+    t->children.resize(n);
+}
+
+}  // namespace
+
+extern "C" {
+
+ompl_gpu_status ompl_gpu_rrtstar_tree_create(ompl_gpu_rrtstar_tree **out) {
+    if (!out) return bad(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    *out = new (std::nothrow) ompl_gpu_rrtstar_tree();
+    return *out ? OMPL_GPU_OK : bad(OMPL_GPU_ERR_OOM, "out of host memory");
+}
+
+void ompl_gpu_rrtstar_tree_destroy(ompl_gpu_rrtstar_tree *t) { delete t; }
+
+ompl_gpu_status ompl_gpu_rrtstar_tree_add(ompl_gpu_rrtstar_tree *t, size_t m, const int64_t *parent,
+                                          const double *inc, const double *cost) {
+    if (!t) return bad(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    const size_t first = t->parent.size();
+    for (size_t j = 0; j < m; ++j) {
+        const int64_t p = parent ? parent[j] : -1;
+        if (p < -1 || p >= (int64_t)(first + j)) return bad(OMPL_GPU_ERR_INVALID_ARG, "parent must be -1 or an earlier id");
+    }
+    try {
+        grow(t, first + m);
+    } catch (const std::bad_alloc &) {
+        return bad(OMPL_GPU_ERR_OOM, "out of host memory");
+    }
+    for (size_t j = 0; j < m; ++j) {
+        const size_t v = first + j;
+        t->parent[v] = parent ? parent[j] : -1;
+        t->inc[v] = inc ? inc[j] : 0.0;
+        t->cost[v] = cost ? cost[j] : 0.0;  // a start state's cost: the identity (RRTstar.cpp:208-213)
+        if (t->parent[v] >= 0) t->children[(size_t)t->parent[v]].push_back((uint32_t)v);
+    }
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_rrtstar_tree_size(const ompl_gpu_rrtstar_tree *t, size_t *n) {
+    if (!t || !n) return bad(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    *n = t->parent.size();
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_rrtstar_tree_read(const ompl_gpu_rrtstar_tree *t, size_t first, size_t m, int64_t *parent,
+                                           double *inc, double *cost) {
+    if (!t) return bad(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (first > t->parent.size() || m > t->parent.size() - first) return bad(OMPL_GPU_ERR_INVALID_ARG, "range past the tree");
+    if (parent) std::memcpy(parent, t->parent.data() + first, sizeof(int64_t) * m);
+    if (inc) std::memcpy(inc, t->inc.data() + first, sizeof(double) * m);
+    if (cost) std::memcpy(cost, t->cost.data() + first, sizeof(double) * m);
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_rrtstar_tree_totals(const ompl_gpu_rrtstar_tree *t, uint64_t totals[6]) {
+    if (!t || !totals) return bad(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    std::memcpy(totals, t->totals, sizeof(t->totals));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_rrtstar_stage_host(ompl_gpu_rrtstar_tree *t, size_t ns, const uint32_t *nearest,
+                                            const uint32_t *added, const double *inc, const uint64_t *offsets,
+                                            const uint32_t *ids, const double *dist, const uint8_t *bits) {
+    if (!t || (ns && (!nearest || !added || !inc || !offsets))) return bad(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    const size_t E = ns ? (size_t)offsets[ns] : 0;
+    if (E && (!ids || !dist || !bits)) return bad(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    for (size_t i = 0; i < ns; ++i)
+        if (offsets[i] > offsets[i + 1]) return bad(OMPL_GPU_ERR_INVALID_ARG, "offsets must not decrease");
+    RrtStarStaged b;
+    try {
+        b.ns = ns;
+        b.nearest.assign(nearest, nearest + ns);
+        b.added.assign(added, added + ns);
+        b.inc.assign(inc, inc + ns);
+        b.off.assign(offsets, offsets + ns + 1);
+        if (!ns) b.off.assign(1, 0);
+        b.ids.assign(ids, ids + E);
+        b.dist.assign(dist, dist + E);
+        b.bits.assign(bits, bits + E);
+    } catch (const std::bad_alloc &) {
+        return bad(OMPL_GPU_ERR_OOM, "out of host memory");
+    }
+    std::lock_guard<std::mutex> lk(t->mu);
+    t->staged.push_back(std::move(b));
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_distance, size_t ns_cap,
+                                        int64_t *nearest, int64_t *added, int64_t *chosen, size_t *ns_out) {
+    if (!t) return bad(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    RrtStarStaged b;
+    {
+        std::lock_guard<std::mutex> lk(t->mu);
+        if (t->staged.empty()) return bad(OMPL_GPU_ERR_INVALID_ARG, "no staged batch");
+        if ((nearest || added || chosen) && t->staged.front().ns > ns_cap)
+            return bad(OMPL_GPU_ERR_INVALID_ARG, "output arrays shorter than the staged batch");
+        b = std::move(t->staged.front());
+        t->staged.pop_front();
+    }
+    const size_t ns = b.ns;
+    if (ns_out) *ns_out = ns;
+    const double maxd = max_distance;
+    uint64_t rewires = 0, checks = 0, nadd = 0, visits = 0;
+    try {
+        uint32_t top = 0;
+        for (size_t i = 0; i < ns; ++i)
+            if (b.added[i] != 0xFFFFFFFFu) top = std::max(top, b.added[i] + 1);
+        const size_t n = std::max(t->parent.size(), (size_t)top);  // every id the batch names is a state
+        bool ok = b.off.size() == ns + 1 && b.off[ns] == b.ids.size();
+        for (size_t i = 0; ok && i < ns; ++i) ok = b.nearest[i] < n && b.off[i] <= b.off[i + 1];
+        for (size_t j = 0; ok && j < b.ids.size(); ++j) ok = b.ids[j] < n;
+        if (!ok) return bad(OMPL_GPU_ERR_INVALID_ARG, "staged batch names ids outside the tree");
+        grow(t, top);
+        for (size_t i = 0; i < ns; ++i) {
+            const uint32_t nm = b.nearest[i], x = b.added[i];
+            if (nearest) nearest[i] = nm;
+            if (added) added[i] = x == 0xFFFFFFFFu ? -1 : (int64_t)x;
+            if (chosen) chosen[i] = -1;
+            ++checks;  // checkMotion(nmotion, x) (:282)
+            if (x == 0xFFFFFFFFu) continue;
+            const uint64_t a = b.off[i], e = b.off[i + 1];
+            const size_t nb = (size_t)(e - a);
+            const uint32_t *ids = b.ids.data() + a;
+            const double *d = b.dist.data() + a;
+            const uint8_t *bt = b.bits.data() + a;
+            double m_inc = b.inc[i], m_cost = t->cost[nm] + m_inc;
+            int64_t m_parent = nm;
+            // delayCC: neighbours in cost order, the first with a valid connection (:319-357).  The
+            // stable sort's order is the (cost, index) order, so the first valid neighbour is the
+            // valid one of least (cost, index), and the ones the loop marks invalid before it are
+            // exactly those of smaller (cost, index): two scans, no sort
+            t->costs.resize(nb);
+            t->valid.resize(nb);
+            size_t best = nb;
+            double bc = 0.0;
+            for (size_t r = 0; r < nb; ++r) {
+                const double c = t->cost[ids[r]] + d[r];
+                t->costs[r] = c;
+                if ((best == nb || c < bc) && (ids[r] == nm || (d[r] < maxd && (bt[r] & 1)))) {
+                    best = r;
+                    bc = c;
+                }
+            }
+            for (size_t r = 0; r < nb; ++r) {
+                const bool before = best == nb || t->costs[r] < bc || (t->costs[r] == bc && r < best);
+                t->valid[r] = before ? -1 : 0;
+                if ((before || r == best) && ids[r] != nm && d[r] < maxd) ++checks;  // checkMotion(nbh, x) calls
+            }
+            if (best < nb) {
+                m_inc = d[best];
+                m_cost = bc;
+                m_parent = ids[best];
+                t->valid[best] = 1;
+            }
+            // the motion joins the tree (:410-411)
+            t->parent[x] = m_parent;
+            t->inc[x] = m_inc;
+            t->cost[x] = m_cost;
+            t->children[(size_t)m_parent].push_back(x);
+            if (chosen) chosen[i] = m_parent;
+            ++nadd;
+            // rewiring (:414-457)
+            for (size_t r = 0; r < nb; ++r) {
+                const uint32_t v = ids[r];
+                if ((int64_t)v == m_parent) continue;
+                const double nc = t->cost[x] + d[r];
+                if (!(nc < t->cost[v])) continue;
+                bool ok;
+                if (t->valid[r] == 0) {
+                    ok = d[r] < maxd && (bt[r] & 2);
+                    if (d[r] < maxd) ++checks;
+                } else {
+                    ok = t->valid[r] == 1;
+                }
+                if (!ok) continue;
+                remove_from_parent(t, v);
+                t->parent[v] = x;
+                t->inc[v] = d[r];
+                t->cost[v] = nc;
+                t->children[x].push_back(v);
+                visits += update_child_costs(t, v);
+                ++rewires;
+            }
+        }
+    } catch (const std::bad_alloc &) {
+        return bad(OMPL_GPU_ERR_OOM, "out of host memory");
+    }
+    t->totals[0] += rewires;
+    t->totals[1] += checks;
+    t->totals[2] += nadd;
+    t->totals[3] += b.ids.size();
+    t->totals[4] += ns;
+    t->totals[5] += visits;
+    {
+        std::lock_guard<std::mutex> lk(t->mu);
+        if (t->spare.size() < 2) t->spare.push_back(std::move(b));  // its buffers serve a later stage
+    }
+    return OMPL_GPU_OK;
+}
+
+}  // extern "C"

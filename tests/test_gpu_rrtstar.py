@@ -4,7 +4,8 @@ the host cost logic (ompl_amd/rrtstar.py) against the oracle's sequential RRT* l
 
 * every sample's nearest state, whether it joined the tree and which parent it chose (delayCC's
   first valid neighbour in cost order, RRTstar.cpp:319-357), and the final tree — every vertex's
-  parent and cost after all rewiring (:414-457) and child-cost updates (:633-643);
+  parent and cost after all rewiring (:414-457) and child-cost updates (:633-643) — through the
+  pipelined solve_batches (native cost logic on a host thread) and the sequential solve_batch;
 * every neighbourhood nearestK(x, ceil(k_rrt ln(size + 1))) (:603-618) of sampled added states
   against the oracle's brute force over the tree as it stood (ids and order);
 * both motion bits of every neighbourhood entry against the oracle validator.
@@ -30,16 +31,11 @@ def _run(sp, ck, start, samples, batches, gpu, exact):
     maxd = 0.2 * sp.getMaximumExtent()
     planner = RRTstarGPU(sp, ck, maxd, gpu)
     planner.add_tree(start[None])
-    near, added, chosen, res_log = [], [], [], []
-    at = 0
-    for b in batches:
-        n, a, c = planner.solve_batch(samples[at:at + b])
-        near.append(n)
-        added.append(a)
-        chosen.append(c)
-        at += b
-    assert at == len(samples)
-    near, added, chosen = np.concatenate(near), np.concatenate(added), np.concatenate(chosen)
+    cuts = np.cumsum((0,) + tuple(batches))
+    assert cuts[-1] == len(samples)
+    # the pipelined form: batch i's cost logic (host thread) overlaps batch i + 1's device work
+    out = planner.solve_batches([samples[a:b] for a, b in zip(cuts[:-1], cuts[1:])])
+    near, added, chosen = (np.concatenate([o[j] for o in out]) for j in range(3))
     ref = O.rrtstar(sp, ck, start[None], [-1], [0.0], [0.0], samples, maxd, planner.k_rrt)
     radd = ref["added"].astype(np.int64)
     radd[radd == 0xFFFFFFFF] = -1
@@ -59,6 +55,7 @@ def _run(sp, ck, start, samples, batches, gpu, exact):
         np.testing.assert_allclose(planner.cost[:n], ref["cost"], rtol=1e-12, atol=0)
         np.testing.assert_allclose(planner.inc[:n], ref["inc"], rtol=1e-12, atol=1e-14)
     assert ref["rewires"] > 0 and planner.stats["rewires"] == ref["rewires"]
+    assert planner.stats["checks_used"] == ref["checks"]
     return planner, ref
 
 
