@@ -295,10 +295,13 @@ __host__ __device__ inline bool is_valid(const DevSpace &sp, const DevChecker &c
     }
 }
 
-// KinematicChain isValid (demos/KinematicChain.h:200-276) for a compile-time link count NL: the
-// joint positions and every segment pair unrolled, so the 2 (NL + 2) positions stay in registers
-// (chain_valid's runtime loops index them dynamically, which puts them in scratch).  The same
-// arithmetic in the same order, so the bit is identical.
+// KinematicChain isValid (demos/KinematicChain.h:200-276) for a compile-time link count NL.  The
+// joint positions are NL + 2-entry arrays indexed by the (wave-uniform) loop counters of the
+// pair loops, which stay loops: the compiler keeps the arrays in VGPRs and indexes them with
+// relative moves (82 VGPRs, no scratch for the 12-link chain), where the runtime-width form
+// (chain_valid) spills them to scratch (~1 GB of scratch traffic per cfg4 batch of motion
+// checks) and the fully unrolled form needed 290 VGPRs.  Same arithmetic in the same order, so
+// the bit is identical; an intersection ends the check as in the reference.
 template <int NL>
 __device__ __forceinline__ bool chain_valid_fixed(const double *s, double link, const double *env, int nenv) {
     double px[NL + 2], py[NL + 2];  // segment i = (p[i], p[i+1])
@@ -320,17 +323,20 @@ __device__ __forceinline__ bool chain_valid_fixed(const double *s, double link, 
     px[NL + 1] = x + ct * 0.001;
     py[NL + 1] = y + st * 0.001;
     constexpr int ns = NL + 1;
-#pragma unroll
-    for (int i = 0; i < ns; ++i)
-#pragma unroll
+#pragma nounroll
+    for (int i = 0; i < ns; ++i) {
+        const double ax = px[i], ay = py[i], bx = px[i + 1], by = py[i + 1];
+#pragma nounroll
         for (int j = i + 1; j < ns; ++j)
-            if (seg_intersect(px[i], py[i], px[i + 1], py[i + 1], px[j], py[j], px[j + 1], py[j + 1])) return false;
-#pragma unroll
-    for (int i = 0; i < ns; ++i)
+            if (seg_intersect(ax, ay, bx, by, px[j], py[j], px[j + 1], py[j + 1])) return false;
+    }
+#pragma nounroll
+    for (int i = 0; i < ns; ++i) {
+        const double ax = px[i], ay = py[i], bx = px[i + 1], by = py[i + 1];
         for (int j = 0; j < nenv; ++j)
-            if (seg_intersect(px[i], py[i], px[i + 1], py[i + 1], env[4 * j], env[4 * j + 1], env[4 * j + 2],
-                              env[4 * j + 3]))
+            if (seg_intersect(ax, ay, bx, by, env[4 * j], env[4 * j + 1], env[4 * j + 2], env[4 * j + 3]))
                 return false;
+    }
     return true;
 }
 

@@ -623,11 +623,15 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
     const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
     uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi,
-    unsigned long long *__restrict__ counters, int k2) {
+    unsigned long long *__restrict__ counters, int k2, float pmin) {
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
     constexpr int GH = G / 2;
+    // PK (SE3, two queries): a tile is screened for both queries at once on packed fp32, the
+    // rotation first by a certified lower bound from the quaternion dot products (below)
+    constexpr bool PK = SP == OMPL_GPU_SPACE_SE3 && G == 2;
     static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
     __shared__ __attribute__((aligned(16))) float qrow[G * FS];
+    __shared__ __attribute__((aligned(16))) float qpair[PK ? 2 * FS : 2];  // (query 0, query 1) per coordinate
     const int lane = threadIdx.x;
     const int half = lane >> 5;
     // XCD-aware group order: blocks b and b + 8 share an XCD (and its L2), so each XCD gets
@@ -638,9 +642,31 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     const uint32_t g0 = blk * G;
     for (int t = lane; t < G * FS; t += 64) {
         const uint32_t qi = g0 + t / FS;
-        qrow[t] = qi < nq ? q32[(size_t)qi * FS + t % FS] : __builtin_nanf("");
+        const float v = qi < nq ? q32[(size_t)qi * FS + t % FS] : __builtin_nanf("");
+        qrow[t] = v;
+        if constexpr (PK) qpair[2 * (t % FS) + t / FS] = v;
     }
     __syncthreads();
+    // PK's rotation bound.  For the fp32 rows p (state) and q (query), the screened chord is
+    // c2 = min(|p - q|^2, |p + q|^2) in fp32 (chord2), and exactly |p|^2 + |q|^2 - 2 |p.q| >=
+    // pmin + |q|^2 - 2 |p.q| (pmin <= every stored |p|^2: the store's norm excess qeta and the
+    // fp32 rounding, from the host).  With the fp32 dot product (error <= 2.5e-7), |q|^2 from
+    // its fp32 sum (relative error <= 5e-7), the fp32 chord's own relative error (<= 4e-7 of at
+    // most 4) and the square roots' ulps, c2lb = pmin + |q|^2 (1 - 6e-7) - 8e-6 - 2 |dot| gives
+    // sqrt(max(c2lb, 0)) <= the screened chord c, so fma(w1, that, w0 |t|) <= the chord bound
+    // fma(w1, c, w0 |t|) <= the screened distance: no lane it rejects could have been offered.
+    float kq[2] = {0.f, 0.f};
+    if constexpr (PK) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const float *qq = &qrow[g * FS + 4];
+            float n2 = qq[0] * qq[0];
+            n2 = fmaf(qq[1], qq[1], n2);
+            n2 = fmaf(qq[2], qq[2], n2);
+            n2 = fmaf(qq[3], qq[3], n2);
+            kq[g] = pmin + n2 * (1.f - 6e-7f) - 8e-6f;
+        }
+    }
     // QS: re-read the wave-uniform query rows from LDS (broadcast reads) at every tile
     // through an offset the compiler cannot see through, instead of letting it hoist all
     // G x FS values into vector registers for the whole walk (which caps occupancy)
@@ -748,6 +774,38 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     };
     auto scan_state = [&](const float (&x)[R], uint32_t id, int tin, const float (&lb)[GH]) {
         relaunder();
+        if constexpr (PK) {
+            // both queries' translation terms and rotation lower bounds in one packed pass (the
+            // translation in scan order: the same fp32 bits as the one-query form)
+            bool on[2];
+            on[0] = readlane_f(lb[0], tin) < td[0];
+            on[1] = readlane_f(lb[0], tin + 32) < td[1];
+            const f2 *qp = reinterpret_cast<const f2 *>(&qpair[qoff]);
+            f2 a = f2{x[0], x[0]} - qp[0];
+            f2 t2 = a * a;
+            a = f2{x[1], x[1]} - qp[1];
+            t2 = pk_fma(a, a, t2);
+            a = f2{x[2], x[2]} - qp[2];
+            t2 = pk_fma(a, a, t2);
+            f2 dt = f2{x[3], x[3]} * qp[4];
+            dt = pk_fma(f2{x[4], x[4]}, qp[5], dt);
+            dt = pk_fma(f2{x[5], x[5]}, qp[6], dt);
+            dt = pk_fma(f2{x[6], x[6]}, qp[7], dt);
+            const float wt[2] = {w0 * __builtin_amdgcn_sqrtf(t2.x), w0 * __builtin_amdgcn_sqrtf(t2.y)};
+            const float dd[2] = {dt.x, dt.y};
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                if (!on[g]) continue;
+                ++qscans;
+                const float clb = __builtin_amdgcn_sqrtf(fmaxf(fmaf(-2.f, fabsf(dd[g]), kq[g]), 0.f));
+                if (!__ballot(fmaf(w1, clb, wt[g]) < td[g])) continue;
+                const float c2 = chord2(x + 3, qscan(g) + 4);
+                const float c = __builtin_amdgcn_sqrtf(c2);
+                if (!__ballot(fmaf(w1, c, wt[g]) < td[g])) continue;
+                offer(g, fmaf(w1, chord_theta(c, c2), wt[g]), id);
+            }
+            return;
+        }
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             if (!(readlane_f(lb[g % GH], tin + (g < GH ? 0 : 32)) < td[g])) continue;
@@ -2117,7 +2175,8 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             constexpr int G = group_queries<SP>();
             hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
                                ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0, q32,
-                               keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, p.k2);
+                               keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, p.k2,
+                               (float)((1.0 - (double)b.qeta) * (1.0 - 4e-7)));
             timer_end(st);
             walked = true;
         }

@@ -136,10 +136,10 @@ static hipError_t dispatch_width(const DevSpace &sp, const DevChecker &ck, F &&l
     const bool fixed_ok = (ck.kind == OMPL_GPU_CHECK_ALL_VALID || ck.kind == OMPL_GPU_CHECK_SPHERES ||
                            ck.kind == OMPL_GPU_CHECK_CIRCLES2D ||
                            (ck.kind == OMPL_GPU_CHECK_HYPERCUBE && ck.ndim <= sp.dim));
-    // the KinematicChain benchmark's 12 links (KinematicChainBenchmark.cpp:48): its checker or none
-    // (measured and rejected: the 12-link chain's fixed form — 2.49 ms per cfg4 batch of
-    // motion checks against the runtime form's 1.13 ms: no scratch, but 290 VGPRs leave one wave
-    // per SIMD, and the fp64 trigonometry and segment tests then wait on their own latencies)
+    // the KinematicChain checker takes the runtime-width form.  (Measured and rejected for the
+    // 12-link chain, DESIGN §8: the pair loops fully unrolled — 290 VGPRs, 2.49 ms per cfg4 batch
+    // of motion checks; the positions in VGPRs indexed by the loop counters — no scratch, but 189
+    // VGPRs, 1.27 ms; against the runtime form's 1.14 ms.)
     if (fixed_ok) {
         if (sp.kind == OMPL_GPU_SPACE_SE3 && sp.dim == 7) return launch(std::integral_constant<int, OMPL_GPU_SPACE_SE3>{}, std::integral_constant<int, 7>{});
         if (sp.kind == OMPL_GPU_SPACE_SO3 && sp.dim == 4) return launch(std::integral_constant<int, OMPL_GPU_SPACE_SO3>{}, std::integral_constant<int, 4>{});

@@ -54,10 +54,20 @@ uint64_t update_child_costs(ompl_gpu_rrtstar_tree *t, uint32_t m) {  // RRTstar.
     return visits;
 }
 
-void remove_from_parent(ompl_gpu_rrtstar_tree *t, uint32_t m) {  // RRTstar.cpp:620-631
+// removeFromParent (RRTstar.cpp:620-631) in O(1): every state knows its slot in its parent's
+// children list, and the last child moves into the freed slot.  The order of a children list
+// changes nothing: updateChildCosts sets each child's cost from its parent's, in any order.
+void remove_from_parent(ompl_gpu_rrtstar_tree *t, uint32_t m) {
     auto &ch = t->children[(size_t)t->parent[m]];
-    auto it = std::find(ch.begin(), ch.end(), m);
-    if (it != ch.end()) ch.erase(it);
+    const uint32_t i = t->slot[m], last = ch.back();
+    ch[i] = last;
+    t->slot[last] = i;
+    ch.pop_back();
+}
+
+void add_child(ompl_gpu_rrtstar_tree *t, uint32_t p, uint32_t c) {
+    t->slot[c] = (uint32_t)t->children[p].size();
+    t->children[p].push_back(c);
 }
 
 void grow(ompl_gpu_rrtstar_tree *t, size_t n) {
@@ -66,6 +76,7 @@ void grow(ompl_gpu_rrtstar_tree *t, size_t n) {
     t->inc.resize(n, 0.0);
     t->cost.resize(n, 0.0);
     t->children.resize(n);
+    t->slot.resize(n, 0);
 }
 
 }  // namespace
@@ -98,7 +109,7 @@ ompl_gpu_status ompl_gpu_rrtstar_tree_add(ompl_gpu_rrtstar_tree *t, size_t m, co
         t->parent[v] = parent ? parent[j] : -1;
         t->inc[v] = inc ? inc[j] : 0.0;
         t->cost[v] = cost ? cost[j] : 0.0;  // a start state's cost: the identity (RRTstar.cpp:208-213)
-        if (t->parent[v] >= 0) t->children[(size_t)t->parent[v]].push_back((uint32_t)v);
+        if (t->parent[v] >= 0) add_child(t, (uint32_t)t->parent[v], (uint32_t)v);
     }
     return OMPL_GPU_OK;
 }
@@ -200,7 +211,10 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
             t->valid.resize(nb);
             size_t best = nb;
             double bc = 0.0;
+            constexpr size_t kAhead = 16;  // the costs are read by neighbour id: random over the tree
+            for (size_t r = 0; r < std::min(nb, kAhead); ++r) __builtin_prefetch(&t->cost[ids[r]]);
             for (size_t r = 0; r < nb; ++r) {
+                if (r + kAhead < nb) __builtin_prefetch(&t->cost[ids[r + kAhead]]);
                 const double c = t->cost[ids[r]] + d[r];
                 t->costs[r] = c;
                 if ((best == nb || c < bc) && (ids[r] == nm || (d[r] < maxd && (bt[r] & 1)))) {
@@ -223,7 +237,7 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
             t->parent[x] = m_parent;
             t->inc[x] = m_inc;
             t->cost[x] = m_cost;
-            t->children[(size_t)m_parent].push_back(x);
+            add_child(t, (uint32_t)m_parent, x);
             if (chosen) chosen[i] = m_parent;
             ++nadd;
             // rewiring (:414-457)
@@ -244,7 +258,7 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
                 t->parent[v] = x;
                 t->inc[v] = d[r];
                 t->cost[v] = nc;
-                t->children[x].push_back(v);
+                add_child(t, x, v);
                 visits += update_child_costs(t, v);
                 ++rewires;
             }

@@ -30,6 +30,7 @@ struct ompl_gpu_rrtstar_tree {
     std::vector<int64_t> parent;  // -1: a start state
     std::vector<double> inc, cost;
     std::vector<std::vector<uint32_t>> children;
+    std::vector<uint32_t> slot;  // each state's index in its parent's children list
     // staged batches, oldest first, and recycled buffers (stage and commit may be on two threads)
     std::mutex mu;
     std::deque<ompl_amd::RrtStarStaged> staged;

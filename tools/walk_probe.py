@@ -1,8 +1,8 @@
 """Measurement probe (not product): the batched kNN walk on the headline workload with a probe
-build of the library (make -C ompl_amd/csrc probe VARIANT=n -> tools/probe_lib/), printing
+build of the library (make -C ompl_amd/csrc probe -> tools/probe_lib/), printing
 the walk kernel's time and its event counters per launch.
 
-    OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_probe0.so python tools/walk_probe.py [--k 10]
+    OMPL_GPU_LIB=tools/probe_lib/libompl_gpu_probe.so python tools/walk_probe.py [--k 10]
 """
 import argparse
 import ctypes as C
