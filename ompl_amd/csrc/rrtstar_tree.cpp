@@ -16,6 +16,12 @@
 //     as parent, and its subtree's costs follow (updateChildCosts :633-643).
 // The checkMotion results are the device's bits; none of the device work depends on costs.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <system_error>
+#include <thread>
+#include <memory>
 #include <cstring>
 #include <new>
 #include <numeric>
@@ -36,7 +42,127 @@ ompl_gpu_status bad(ompl_gpu_status s, const char *msg) {
     return s;
 }
 
-uint64_t update_child_costs(ompl_gpu_rrtstar_tree *t, uint32_t m) {  // RRTstar.cpp:633-643, iterative
+// the states whose cost changed during one sample's rewiring (a rewired neighbour and its
+// subtree): an open-addressing set tagged by the sample's epoch, so that the rewiring loop reads
+// each neighbour's cost from the contiguous copy taken before it (cv) unless the state is in the
+// set — one random read of the tree's costs per neighbour instead of two
+struct Touched {
+    static constexpr uint32_t kSlots = 4096, kMax = 2048;
+    std::vector<uint64_t> slot = std::vector<uint64_t>(kSlots, 0);
+    uint32_t epoch = 0, count = 0;
+    bool all = false;  // too many: every read goes to the tree
+    void reset() {
+        ++epoch;
+        count = 0;
+        all = false;
+    }
+    static uint32_t hash(uint32_t v) { return (v * 0x9E3779B1u) >> 20; }
+    void add(uint32_t v) {
+        if (all) return;
+        if (++count > kMax) {
+            all = true;
+            return;
+        }
+        const uint64_t tag = ((uint64_t)epoch << 32) | v;
+        for (uint32_t h = hash(v);; h = (h + 1) & (kSlots - 1)) {
+            if ((uint32_t)(slot[h] >> 32) != epoch) {
+                slot[h] = tag;
+                return;
+            }
+            if (slot[h] == tag) return;
+        }
+    }
+    bool has(uint32_t v) const {
+        if (all) return true;
+        const uint64_t tag = ((uint64_t)epoch << 32) | v;
+        for (uint32_t h = hash(v);; h = (h + 1) & (kSlots - 1)) {
+            if ((uint32_t)(slot[h] >> 32) != epoch) return false;
+            if (slot[h] == tag) return true;
+        }
+    }
+};
+
+// A few host threads for the per-neighbour pass (the costs are read by neighbour id, random over
+// the tree: ~7 ns each on one core, so a batch's 1.8 M neighbourhood entries cost ~14 ms on one
+// thread).  Workers spin while a commit is active and sleep on a condition variable otherwise.
+class Pool {
+public:
+    explicit Pool(int nthreads) {
+        try {
+            for (int k = 1; k < nthreads; ++k) th_.emplace_back([this, k] { work(k); });
+        } catch (const std::system_error &) {  // fewer threads than asked: the caller does the rest
+        }
+        n_ = 1 + (int)th_.size();
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int size() const { return n_; }
+    void begin() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            active_.store(true);
+        }
+        cv_.notify_all();
+    }
+    void end() { active_.store(false); }
+    // f(k) on every thread k in [0, size()), the caller being thread 0; returns when all are done
+    void run(const std::function<void(int)> &f) {
+        if (n_ == 1) {
+            f(0);
+            return;
+        }
+        job_ = &f;
+        pending_.store(n_ - 1, std::memory_order_relaxed);
+        if (active_.load(std::memory_order_relaxed)) {  // the workers spin: no wake-up call
+            gen_.fetch_add(1, std::memory_order_release);
+        } else {
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                gen_.fetch_add(1, std::memory_order_release);
+            }
+            cv_.notify_all();
+        }
+        f(0);
+        while (pending_.load(std::memory_order_acquire)) __builtin_ia32_pause();
+    }
+
+private:
+    void work(int k) {
+        uint64_t seen = 0;
+        for (;;) {
+            while (gen_.load(std::memory_order_acquire) == seen) {
+                if (!active_.load(std::memory_order_relaxed)) {
+                    std::unique_lock<std::mutex> lk(mu_);
+                    cv_.wait(lk, [&] { return quit_ || active_.load() || gen_.load() != seen; });
+                    if (quit_) return;
+                } else {
+                    __builtin_ia32_pause();
+                }
+            }
+            seen = gen_.load(std::memory_order_acquire);
+            (*job_)(k);
+            pending_.fetch_sub(1, std::memory_order_release);
+        }
+    }
+    std::vector<std::thread> th_;
+    int n_ = 1;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool quit_ = false;
+    std::atomic<bool> active_{false};
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> pending_{0};
+    const std::function<void(int)> *job_ = nullptr;
+};
+
+template <class Mark>
+uint64_t update_child_costs(ompl_gpu_rrtstar_tree *t, uint32_t m, Mark &&mark) {  // RRTstar.cpp:633-643, iterative
     auto &st = t->stack;
     st.clear();
     st.push_back(m);
@@ -48,6 +174,7 @@ uint64_t update_child_costs(ompl_gpu_rrtstar_tree *t, uint32_t m) {  // RRTstar.
         visits += t->children[u].size();
         for (uint32_t c : t->children[u]) {
             t->cost[c] = cu + t->inc[c];
+            mark(c);
             if (!t->children[c].empty()) st.push_back(c);
         }
     }
@@ -109,7 +236,11 @@ ompl_gpu_status ompl_gpu_rrtstar_tree_add(ompl_gpu_rrtstar_tree *t, size_t m, co
         t->parent[v] = parent ? parent[j] : -1;
         t->inc[v] = inc ? inc[j] : 0.0;
         t->cost[v] = cost ? cost[j] : 0.0;  // a start state's cost: the identity (RRTstar.cpp:208-213)
-        if (t->parent[v] >= 0) add_child(t, (uint32_t)t->parent[v], (uint32_t)v);
+        if (t->parent[v] >= 0) {
+            add_child(t, (uint32_t)t->parent[v], (uint32_t)v);
+            // a cost that is not its parent's + incCost can rise under updateChildCosts
+            if (!(t->cost[v] == t->cost[(size_t)t->parent[v]] + t->inc[v])) t->consistent = false;
+        }
     }
     return OMPL_GPU_OK;
 }
@@ -179,6 +310,26 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
     if (ns_out) *ns_out = ns;
     const double maxd = max_distance;
     uint64_t rewires = 0, checks = 0, nadd = 0, visits = 0;
+    if (!t->touched) t->touched = std::make_shared<Touched>();
+    Touched &touched = *std::static_pointer_cast<Touched>(t->touched);
+    if (!t->pool) {
+        try {
+            t->pool = std::make_shared<Pool>((int)std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+        } catch (const std::exception &) {
+            return bad(OMPL_GPU_ERR_OOM, "no host threads");
+        }
+    }
+    Pool &pool = *std::static_pointer_cast<Pool>(t->pool);
+    struct Active {  // the workers spin for the length of the commit
+        Pool &p;
+        explicit Active(Pool &q) : p(q) { p.begin(); }
+        ~Active() { p.end(); }
+    } active(pool);
+    struct Best {
+        size_t r;
+        double c;
+    };
+    std::vector<Best> bests((size_t)pool.size());
     try {
         uint32_t top = 0;
         for (size_t i = 0; i < ns; ++i)
@@ -208,30 +359,41 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
             // valid one of least (cost, index), and the ones the loop marks invalid before it are
             // exactly those of smaller (cost, index): two scans, no sort
             t->costs.resize(nb);
-            t->valid.resize(nb);
+            t->cv.resize(nb);
+            // each thread a contiguous part: the neighbours' costs (cv), cost + distance (costs) and
+            // its part's valid candidate of least (cost, index)
+            const int T = nb >= 1024 ? pool.size() : 1;
+            auto part = [&](int k) {
+                const size_t r0 = nb * (size_t)k / (size_t)T, r1 = nb * (size_t)(k + 1) / (size_t)T;
+                size_t bi = nb;
+                double bcost = 0.0;
+                for (size_t r = r0; r < r1; ++r) {
+                    const double cr = t->cost[ids[r]];
+                    const double c = cr + d[r];
+                    t->cv[r] = cr;
+                    t->costs[r] = c;
+                    if ((bi == nb || c < bcost) && (ids[r] == nm || (d[r] < maxd && (bt[r] & 1)))) {
+                        bi = r;
+                        bcost = c;
+                    }
+                }
+                bests[(size_t)k] = Best{bi, bcost};
+            };
+            if (T > 1)
+                pool.run(part);
+            else
+                part(0);
             size_t best = nb;
             double bc = 0.0;
-            constexpr size_t kAhead = 16;  // the costs are read by neighbour id: random over the tree
-            for (size_t r = 0; r < std::min(nb, kAhead); ++r) __builtin_prefetch(&t->cost[ids[r]]);
-            for (size_t r = 0; r < nb; ++r) {
-                if (r + kAhead < nb) __builtin_prefetch(&t->cost[ids[r + kAhead]]);
-                const double c = t->cost[ids[r]] + d[r];
-                t->costs[r] = c;
-                if ((best == nb || c < bc) && (ids[r] == nm || (d[r] < maxd && (bt[r] & 1)))) {
-                    best = r;
-                    bc = c;
+            for (int k = 0; k < T; ++k)  // parts in index order: a strict < keeps the lower index on ties
+                if (bests[(size_t)k].r < nb && (best == nb || bests[(size_t)k].c < bc)) {
+                    best = bests[(size_t)k].r;
+                    bc = bests[(size_t)k].c;
                 }
-            }
-            for (size_t r = 0; r < nb; ++r) {
-                const bool before = best == nb || t->costs[r] < bc || (t->costs[r] == bc && r < best);
-                t->valid[r] = before ? -1 : 0;
-                if ((before || r == best) && ids[r] != nm && d[r] < maxd) ++checks;  // checkMotion(nbh, x) calls
-            }
             if (best < nb) {
                 m_inc = d[best];
                 m_cost = bc;
                 m_parent = ids[best];
-                t->valid[best] = 1;
             }
             // the motion joins the tree (:410-411)
             t->parent[x] = m_parent;
@@ -240,18 +402,33 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
             add_child(t, (uint32_t)m_parent, x);
             if (chosen) chosen[i] = m_parent;
             ++nadd;
-            // rewiring (:414-457)
+            // rewiring (:414-457), with the parent choice's marks: the neighbours before the parent in
+            // (cost, index) order were found invalid (-1), the parent valid (1), the rest unchecked (0)
+            touched.reset();
+            const double cx = t->cost[x];  // x is no neighbour's descendant: its cost stays
             for (size_t r = 0; r < nb; ++r) {
+                const bool before = best == nb || t->costs[r] < bc || (t->costs[r] == bc && r < best);
+                const int8_t mark = r == best ? 1 : (before ? -1 : 0);
+                if ((before || r == best) && ids[r] != nm && d[r] < maxd) ++checks;  // checkMotion(nbh, x) calls
                 const uint32_t v = ids[r];
                 if ((int64_t)v == m_parent) continue;
-                const double nc = t->cost[x] + d[r];
-                if (!(nc < t->cost[v])) continue;
+                const double nc = cx + d[r];
+                // the cost as this loop found it, or as an earlier rewire of this loop left it.  In a
+                // consistent tree (every cost = parent's cost + incCost, as RRT* keeps it) costs only
+                // fall, so nc >= the cost found means no rewire either way
+                if (t->consistent) {
+                    if (!(nc < t->cv[r])) continue;
+                    if (touched.has(v) && !(nc < t->cost[v])) continue;
+                } else {
+                    const double cur = touched.has(v) ? t->cost[v] : t->cv[r];
+                    if (!(nc < cur)) continue;
+                }
                 bool ok;
-                if (t->valid[r] == 0) {
+                if (mark == 0) {
                     ok = d[r] < maxd && (bt[r] & 2);
                     if (d[r] < maxd) ++checks;
                 } else {
-                    ok = t->valid[r] == 1;
+                    ok = mark == 1;
                 }
                 if (!ok) continue;
                 remove_from_parent(t, v);
@@ -259,7 +436,8 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
                 t->inc[v] = d[r];
                 t->cost[v] = nc;
                 add_child(t, x, v);
-                visits += update_child_costs(t, v);
+                touched.add(v);
+                visits += update_child_costs(t, v, [&](uint32_t c) { touched.add(c); });
                 ++rewires;
             }
         }

@@ -9,6 +9,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -31,14 +32,15 @@ struct ompl_gpu_rrtstar_tree {
     std::vector<double> inc, cost;
     std::vector<std::vector<uint32_t>> children;
     std::vector<uint32_t> slot;  // each state's index in its parent's children list
+    bool consistent = true;      // every cost = its parent's cost + incCost (tree_add checks)
     // staged batches, oldest first, and recycled buffers (stage and commit may be on two threads)
     std::mutex mu;
     std::deque<ompl_amd::RrtStarStaged> staged;
     std::vector<ompl_amd::RrtStarStaged> spare;
     // commit's scratch
     std::vector<uint32_t> stack;
-    std::vector<double> costs;
-    std::vector<int8_t> valid;
+    std::vector<double> costs, cv;
+    std::shared_ptr<void> touched, pool;  // rrtstar_tree.cpp Touched, Pool
     // totals: [0] rewires, [1] checkMotion calls the sequential loop would make, [2] states added,
     // [3] neighbourhood entries, [4] samples, [5] child costs updateChildCosts rewrote
     uint64_t totals[6] = {0, 0, 0, 0, 0, 0};

@@ -23,3 +23,13 @@ mkdir -p "$out/prof"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o cfg4 --output-format csv -- python -u bench.py --workload cfg4 --steps 10 --warmup 3 \
     --workloads none --no-extras --no-cpu-baseline > "$out/prof.log" 2>&1 || { tail -20 "$out/prof.log"; exit 1; }
 find "$out/prof" -name "*kernel_stats.csv" | head -1 | xargs -I{} sh -c 'head -8 {}'
+timeout -k 10 400 python -u -m pytest tests/test_gpu_rrtstar.py -m gpu -x -q --timeout 240 --timeout-method thread > "$out/pytest_rrtstar.log" 2>&1 || { tail -20 "$out/pytest_rrtstar.log"; exit 1; }
+tail -1 "$out/pytest_rrtstar.log"
+timeout -k 10 500 python -u bench.py --steps 5 --warmup 2 --workloads rrt_star --no-extras --single-query-reps 0 \
+    --rrt-iters 0 --no-cpu-baseline > "$out/rrtstar.json" 2> "$out/rrtstar.err" || { tail -30 "$out/rrtstar.err"; exit 1; }
+python - "$out/rrtstar.json" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+w = d["workloads"]["rrt_star"]
+print("rrt_star", w["value"], w["ms_per_step"], json.dumps(w["phase_ms"]))
+PY
