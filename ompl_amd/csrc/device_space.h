@@ -83,14 +83,15 @@ __host__ __device__ __forceinline__ double chain_dist_feat(const double *a, cons
 }
 
 // raw-angle chain distance (motion validator: validSegmentCount on raw states)
-__host__ __device__ __forceinline__ double chain_dist_raw(const double *a, const double *b, int n, double link) {
+__host__ __device__ __forceinline__ double chain_dist_raw(const double *a, const double *b, int n, double link,
+                                                          const double *tab = gsc::kSinCosTab) {
     double th1 = 0., th2 = 0., dx = 0., dy = 0., dist = 0.;
     for (int i = 0; i < n; ++i) {
         th1 += a[i];
         th2 += b[i];
         double s1, c1, s2, c2;
-        glibc_sincos(th1, s1, c1);
-        glibc_sincos(th2, s2, c2);
+        glibc_sincos(th1, s1, c1, tab);
+        glibc_sincos(th2, s2, c2, tab);
         dx += c1 - c2;
         dy += s1 - s2;
         dist += sqrt(dx * dx + dy * dy);
@@ -119,7 +120,8 @@ __host__ __device__ __forceinline__ uint32_t seg_count(double d, double lvs, uin
     return f * (uint32_t)ceil(d / lvs);
 }
 
-__host__ __device__ inline uint32_t valid_segment_count(const DevSpace &sp, const double *a, const double *b) {
+__host__ __device__ inline uint32_t valid_segment_count(const DevSpace &sp, const double *a, const double *b,
+                                                        const double *tab = gsc::kSinCosTab) {
     switch (sp.kind) {
     case OMPL_GPU_SPACE_REALVECTOR: return seg_count(l2_dist(a, b, sp.dim), sp.lvs0, sp.f0);
     case OMPL_GPU_SPACE_SO3: return seg_count(so3_arc(a, b), sp.lvs0, sp.f0);
@@ -131,7 +133,7 @@ __host__ __device__ inline uint32_t valid_segment_count(const DevSpace &sp, cons
         if (s1 > sc) sc = s1;
         return sc;
     }
-    default: return seg_count(chain_dist_raw(a, b, sp.dim, sp.link), sp.lvs0, sp.f0);
+    default: return seg_count(chain_dist_raw(a, b, sp.dim, sp.link, tab), sp.lvs0, sp.f0);
     }
 }
 
@@ -254,7 +256,8 @@ __host__ __device__ __forceinline__ bool seg_intersect(double a0x, double a0y, d
 
 constexpr int kChainMaxLinks = 32;
 
-__host__ __device__ inline bool chain_valid(const double *s, int n, double link, const double *env, int nenv) {
+__host__ __device__ inline bool chain_valid(const double *s, int n, double link, const double *env, int nenv,
+                                            const double *tab = gsc::kSinCosTab) {
     double px[kChainMaxLinks + 2], py[kChainMaxLinks + 2];  // segment i = (p[i], p[i+1])
     double theta = 0., x = 0., y = 0.;
     px[0] = 0.;
@@ -262,7 +265,7 @@ __host__ __device__ inline bool chain_valid(const double *s, int n, double link,
     double st = 0.0, ct = 1.0;
     for (int i = 0; i < n; ++i) {
         theta += s[i];
-        glibc_sincos(theta, st, ct);
+        glibc_sincos(theta, st, ct, tab);
         double xN = x + ct * link;
         double yN = y + st * link;
         px[i + 1] = xN;
@@ -270,7 +273,7 @@ __host__ __device__ inline bool chain_valid(const double *s, int n, double link,
         x = xN;
         y = yN;
     }
-    if (n == 0) glibc_sincos(theta, st, ct);
+    if (n == 0) glibc_sincos(theta, st, ct, tab);
     px[n + 1] = x + ct * 0.001;
     py[n + 1] = y + st * 0.001;
     const int ns = n + 1;
@@ -285,59 +288,15 @@ __host__ __device__ inline bool chain_valid(const double *s, int n, double link,
     return true;
 }
 
-__host__ __device__ inline bool is_valid(const DevSpace &sp, const DevChecker &ck, const double *s) {
+__host__ __device__ inline bool is_valid(const DevSpace &sp, const DevChecker &ck, const double *s,
+                                         const double *tab = gsc::kSinCosTab) {
     switch (ck.kind) {
     case OMPL_GPU_CHECK_ALL_VALID: return true;
     case OMPL_GPU_CHECK_HYPERCUBE: return hypercube_valid(s, ck.ndim, ck.edge);
     case OMPL_GPU_CHECK_SPHERES: return spheres_valid(s, ck.data, ck.count);
     case OMPL_GPU_CHECK_CIRCLES2D: return circles_valid(s, ck.data, ck.count);
-    default: return chain_valid(s, sp.dim, sp.link, ck.data, ck.count);
+    default: return chain_valid(s, sp.dim, sp.link, ck.data, ck.count, tab);
     }
-}
-
-// KinematicChain isValid (demos/KinematicChain.h:200-276) for a compile-time link count NL.  The
-// joint positions are NL + 2-entry arrays indexed by the (wave-uniform) loop counters of the
-// pair loops, which stay loops: the compiler keeps the arrays in VGPRs and indexes them with
-// relative moves (82 VGPRs, no scratch for the 12-link chain), where the runtime-width form
-// (chain_valid) spills them to scratch (~1 GB of scratch traffic per cfg4 batch of motion
-// checks) and the fully unrolled form needed 290 VGPRs.  Same arithmetic in the same order, so
-// the bit is identical; an intersection ends the check as in the reference.
-template <int NL>
-__device__ __forceinline__ bool chain_valid_fixed(const double *s, double link, const double *env, int nenv) {
-    double px[NL + 2], py[NL + 2];  // segment i = (p[i], p[i+1])
-    double theta = 0., x = 0., y = 0.;
-    px[0] = 0.;
-    py[0] = 0.;
-    double st = 0.0, ct = 1.0;
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-        theta += s[i];
-        glibc_sincos(theta, st, ct);
-        const double xN = x + ct * link;
-        const double yN = y + st * link;
-        px[i + 1] = xN;
-        py[i + 1] = yN;
-        x = xN;
-        y = yN;
-    }
-    px[NL + 1] = x + ct * 0.001;
-    py[NL + 1] = y + st * 0.001;
-    constexpr int ns = NL + 1;
-#pragma nounroll
-    for (int i = 0; i < ns; ++i) {
-        const double ax = px[i], ay = py[i], bx = px[i + 1], by = py[i + 1];
-#pragma nounroll
-        for (int j = i + 1; j < ns; ++j)
-            if (seg_intersect(ax, ay, bx, by, px[j], py[j], px[j + 1], py[j + 1])) return false;
-    }
-#pragma nounroll
-    for (int i = 0; i < ns; ++i) {
-        const double ax = px[i], ay = py[i], bx = px[i + 1], by = py[i + 1];
-        for (int j = 0; j < nenv; ++j)
-            if (seg_intersect(ax, ay, bx, by, env[4 * j], env[4 * j + 1], env[4 * j + 2], env[4 * j + 3]))
-                return false;
-    }
-    return true;
 }
 
 // Does the checker read the SO3 part of an SE3 state?  (None of the closed set does.)
@@ -395,7 +354,8 @@ __device__ __forceinline__ bool hypercube_valid_fixed(const double *s, int ndim,
 // is_valid (device_space.h) for the fixed forms, which never see the KinematicChain checker
 // (dispatch_width sends it to the runtime-width form)
 template <int DIM>
-__device__ __forceinline__ bool valid_t(const DevSpace &sp, const DevChecker &ck, const double *s) {
+__device__ __forceinline__ bool valid_t(const DevSpace &sp, const DevChecker &ck, const double *s,
+                                        const double *tab = gsc::kSinCosTab) {
     if constexpr (DIM > 0) {
         switch (ck.kind) {
         case OMPL_GPU_CHECK_ALL_VALID: return true;
@@ -404,19 +364,17 @@ __device__ __forceinline__ bool valid_t(const DevSpace &sp, const DevChecker &ck
         default: return circles_valid(s, ck.data, ck.count);
         }
     } else {
-        return is_valid(sp, ck, s);
+        return is_valid(sp, ck, s, tab);
     }
 }
 
-// valid_t with the space kind: the KinematicChain space at a fixed link count gets its unrolled
-// checker; every other specialisation is valid_t
+// valid_t for a kernel's (space kind, width) specialisation (the KinematicChain checker only ever
+// takes the runtime width, DIM = 0)
 template <int SP, int DIM>
-__device__ __forceinline__ bool valid_sp(const DevSpace &sp, const DevChecker &ck, const double *s) {
-    if constexpr (SP == OMPL_GPU_SPACE_KCHAIN && DIM > 0) {
-        return ck.kind == OMPL_GPU_CHECK_KCHAIN ? chain_valid_fixed<DIM>(s, sp.link, ck.data, ck.count) : true;
-    } else {
-        return valid_t<DIM>(sp, ck, s);
-    }
+__device__ __forceinline__ bool valid_sp(const DevSpace &sp, const DevChecker &ck, const double *s,
+                                         const double *tab = gsc::kSinCosTab) {
+    static_assert(SP != OMPL_GPU_SPACE_KCHAIN || DIM == 0, "the chain checker runs at the runtime width");
+    return valid_t<DIM>(sp, ck, s, tab);
 }
 
 }  // namespace ompl_amd

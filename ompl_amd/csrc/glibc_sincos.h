@@ -78,7 +78,7 @@ __host__ __device__ __forceinline__ double taylor_sin(double xx, double a, doubl
 }
 
 template <bool FMA>
-__host__ __device__ __forceinline__ double do_cos(double x, double dx) {
+__host__ __device__ __forceinline__ double do_cos(double x, double dx, const double *tab = kSinCosTab) {
     if (x < 0) dx = -dx;
     const double u = kBig + fabs(x);
     x = fabs(x) - (u - kBig) + dx;
@@ -86,13 +86,13 @@ __host__ __device__ __forceinline__ double do_cos(double x, double dx) {
     const double s = mad<FMA>(x * xx, mad<FMA>(xx, kSn5, kSn3), x);
     const double c = xx * mad<FMA>(xx, mad<FMA>(xx, kCs6, kCs4), kCs2);
     const int k = (int)(uint32_t)bits(u) << 2;
-    const double sn = kSinCosTab[k], ssn = kSinCosTab[k + 1], cs = kSinCosTab[k + 2], ccs = kSinCosTab[k + 3];
+    const double sn = tab[k], ssn = tab[k + 1], cs = tab[k + 2], ccs = tab[k + 3];
     const double cor = mad<FMA>(-sn, s, mad<FMA>(-cs, c, mad<FMA>(-s, ssn, ccs)));
     return cs + cor;
 }
 
 template <bool FMA>
-__host__ __device__ __forceinline__ double do_sin(double x, double dx) {
+__host__ __device__ __forceinline__ double do_sin(double x, double dx, const double *tab = kSinCosTab) {
     const double xold = x;
     if (fabs(x) < 0.126) return taylor_sin<FMA>(x * x, x, dx);
     if (x <= 0) dx = -dx;
@@ -103,7 +103,7 @@ __host__ __device__ __forceinline__ double do_sin(double x, double dx) {
     const double r = mad<FMA>(xx, mad<FMA>(xx, kCs6, kCs4), kCs2);
     const double c = FMA ? fma(x, dx, xx * r) : x * dx + xx * r;
     const int k = (int)(uint32_t)bits(u) << 2;
-    const double sn = kSinCosTab[k], ssn = kSinCosTab[k + 1], cs = kSinCosTab[k + 2], ccs = kSinCosTab[k + 3];
+    const double sn = tab[k], ssn = tab[k + 1], cs = tab[k + 2], ccs = tab[k + 3];
     const double cor = mad<FMA>(cs, s, mad<FMA>(-sn, c, mad<FMA>(s, ccs, ssn)));
     return copysign(sn + cor, xold);
 }
@@ -174,7 +174,8 @@ __host__ __device__ __forceinline__ double glibc_cos(double x) {
 //   |x| < 0.855469   s = do_sin(x, 0)                    c = do_cos(x, 0)
 //   |x| < 2.426265   (a, da) = pi/2 - |x|:  s = copysign(do_cos(a, da), x)   c = do_sin(a, da)
 //   else (n = quadrant)  {do_sin, do_cos}(a, da) assigned to s / c by n, signed by n & 2
-__host__ __device__ __forceinline__ void glibc_sincos(double x, double &s, double &c) {
+// tab: the table (a kernel may pass its LDS copy of gsc::kSinCosTab)
+__host__ __device__ __forceinline__ void glibc_sincos(double x, double &s, double &c, const double *tab = gsc::kSinCosTab) {
     const uint32_t k = (uint32_t)(gsc::bits(x) >> 32) & 0x7fffffffu;
     if (!(k < 0x419921fbu)) {  // outside the hot path (and inf / NaN)
         s = sin(x);
@@ -191,7 +192,7 @@ __host__ __device__ __forceinline__ void glibc_sincos(double x, double &s, doubl
     } else if (big) {
         n = gsc::reduce<false>(x, a, da);
     }
-    const double P = gsc::do_sin<false>(a, da), Q = gsc::do_cos<false>(a, da);
+    const double P = gsc::do_sin<false>(a, da, tab), Q = gsc::do_cos<false>(a, da, tab);
     if (mid) {
         s = copysign(Q, x);
         c = P;

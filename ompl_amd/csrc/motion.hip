@@ -23,12 +23,21 @@ namespace ompl_amd {
 // the runtime width, up to kChainMaxLinks): device_space.h Width / fixed_space / valid_t.
 
 template <int SP, int DIM>
-__global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
-    DevSpace sp_in, DevChecker ck, const double *__restrict__ s1, const double *__restrict__ s2, uint32_t m,
-    uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out, int32_t *__restrict__ fi_out,
-    unsigned long long *__restrict__ counters, int rot) {
+__device__ __forceinline__ void motion_body(DevSpace sp_in, DevChecker ck, const double *__restrict__ s1,
+                                            const double *__restrict__ s2, uint32_t m, uint8_t *__restrict__ valid,
+                                            int32_t *__restrict__ nd_out, int32_t *__restrict__ fi_out,
+                                            unsigned long long *__restrict__ counters, int rot) {
     const DevSpace sp = fixed_space<SP, DIM>(sp_in);
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    // the runtime-width form serves the KinematicChain: its sin / cos table (glibc's, 3.5 KB) in
+    // LDS, read 4 words per sin-cos pair at lane-dependent points
+    constexpr bool kTab = DIM == 0;
+    __shared__ double stab[kTab ? 440 : 1];
+    if constexpr (kTab) {
+        for (int i = threadIdx.x; i < 440; i += blockDim.x) stab[i] = gsc::kSinCosTab[i];
+        __syncthreads();
+    }
+    const double *tab = kTab ? stab : gsc::kSinCosTab;
     bool result = true;
     uint32_t checks = 0;
     if (e < m) {
@@ -37,10 +46,10 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
         load_state<DIM>(s1 + (size_t)e * dim, dim, a);
         load_state<DIM>(s2 + (size_t)e * dim, dim, b);
         ++checks;
-        result = valid_sp<SP, DIM>(sp, ck, b);  // :96 — s2 first, as the reference
+        result = valid_sp<SP, DIM>(sp, ck, b, tab);  // :96 — s2 first, as the reference
         // the segment count (an arc cosine for SE3) only when something reads it: the sweep of a
         // motion whose s2 is valid, the lastValid sweep, or the caller
-        const int nd = (result || nd_out || fi_out) ? (int)valid_segment_count(sp, a, b) : 0;
+        const int nd = (result || nd_out || fi_out) ? (int)valid_segment_count(sp, a, b, tab) : 0;
         if (nd_out) nd_out[e] = nd;
         if (result && nd >= 2) {
             // level-order walk of the FIFO bisection :104-134
@@ -67,7 +76,7 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
                     const int mid = (lo + hi) / 2;
                     interpolate(sp, a, b, (double)mid / (double)nd, t, rot != 0);
                     ++checks;
-                    if (!valid_sp<SP, DIM>(sp, ck, t)) result = false;
+                    if (!valid_sp<SP, DIM>(sp, ck, t, tab)) result = false;
                 }
             }
         }
@@ -78,7 +87,7 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
                 // linear sweep :57-69, then s2 :73-79
                 for (int j = 1; j < nd; ++j) {
                     interpolate(sp, a, b, (double)j / (double)nd, t, rot != 0);
-                    if (!valid_sp<SP, DIM>(sp, ck, t)) {
+                    if (!valid_sp<SP, DIM>(sp, ck, t, tab)) {
                         fi = j;
                         break;
                     }
@@ -117,6 +126,25 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
 }
 
 template <int SP, int DIM>
+__global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
+    DevSpace sp_in, DevChecker ck, const double *__restrict__ s1, const double *__restrict__ s2, uint32_t m,
+    uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out, int32_t *__restrict__ fi_out,
+    unsigned long long *__restrict__ counters, int rot) {
+    motion_body<SP, DIM>(sp_in, ck, s1, s2, m, valid, nd_out, fi_out, counters, rot);
+}
+
+// the runtime-width form (the KinematicChain's): held to 64 VGPRs for 8 waves per SIMD — its fp64
+// sin / cos chains and segment tests wait on their own latencies at the 2 waves its natural 194
+// VGPRs allow (measured per cfg4 batch of motion checks: 2 / 4 / 5 / 6 / 8 waves 1.55 / 1.18 /
+// 1.17 / 1.09 / 1.07 ms; the scratch it spills to stays in the L1 / L2)
+__global__ __launch_bounds__(256) __attribute__((flatten, amdgpu_waves_per_eu(8, 8))) void motion_rt_kernel(
+    DevSpace sp_in, DevChecker ck, const double *__restrict__ s1, const double *__restrict__ s2, uint32_t m,
+    uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out, int32_t *__restrict__ fi_out,
+    unsigned long long *__restrict__ counters, int rot) {
+    motion_body<0, 0>(sp_in, ck, s1, s2, m, valid, nd_out, fi_out, counters, rot);
+}
+
+template <int SP, int DIM>
 __global__ __launch_bounds__(256) __attribute__((flatten)) void state_valid_kernel(
     DevSpace sp_in, DevChecker ck, const double *__restrict__ s, uint32_t m, uint8_t *__restrict__ valid) {
     const DevSpace sp = fixed_space<SP, DIM>(sp_in);
@@ -136,10 +164,12 @@ static hipError_t dispatch_width(const DevSpace &sp, const DevChecker &ck, F &&l
     const bool fixed_ok = (ck.kind == OMPL_GPU_CHECK_ALL_VALID || ck.kind == OMPL_GPU_CHECK_SPHERES ||
                            ck.kind == OMPL_GPU_CHECK_CIRCLES2D ||
                            (ck.kind == OMPL_GPU_CHECK_HYPERCUBE && ck.ndim <= sp.dim));
-    // the KinematicChain checker takes the runtime-width form.  (Measured and rejected for the
-    // 12-link chain, DESIGN §8: the pair loops fully unrolled — 290 VGPRs, 2.49 ms per cfg4 batch
-    // of motion checks; the positions in VGPRs indexed by the loop counters — no scratch, but 189
-    // VGPRs, 1.27 ms; against the runtime form's 1.14 ms.)
+    // the KinematicChain checker takes the runtime-width form (motion_rt_kernel).  (Measured and
+    // rejected for the 12-link chain, DESIGN §8: the pair loops fully unrolled — 290 VGPRs, 2.49 ms
+    // per cfg4 batch of motion checks; the positions in VGPRs indexed by the loop counters — 189
+    // VGPRs, 1.27 ms at 2 waves per SIMD, 1.04 at 4, 3.39 at 6 (spills); edges walked in order of
+    // their segment counts — 0.95 ms for the walk but the ordering's atomics cost more; against
+    // the runtime form's 1.06 ms at 8 waves.)
     if (fixed_ok) {
         if (sp.kind == OMPL_GPU_SPACE_SE3 && sp.dim == 7) return launch(std::integral_constant<int, OMPL_GPU_SPACE_SE3>{}, std::integral_constant<int, 7>{});
         if (sp.kind == OMPL_GPU_SPACE_SO3 && sp.dim == 4) return launch(std::integral_constant<int, OMPL_GPU_SPACE_SO3>{}, std::integral_constant<int, 4>{});
@@ -176,8 +206,12 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
     if (m == 0) return hipSuccess;
     const int rot = needs_rotation(sp, ck) ? 1 : 0;
     return dispatch_width(sp, ck, [&](auto kind, auto width) {
-        hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value>), dim3((m + 255) / 256),
-                           dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd, first_invalid, counters, rot);
+        if constexpr (decltype(width)::value == 0)
+            hipLaunchKernelGGL(motion_rt_kernel, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd,
+                               first_invalid, counters, rot);
+        else
+            hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value>), dim3((m + 255) / 256),
+                               dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd, first_invalid, counters, rot);
         return hipGetLastError();
     });
 }
