@@ -46,8 +46,9 @@ HBM_PEAK_GBS = 8000.0                       # HBM3E spec
 F_SE3, F_L2_6, F_CHAIN = 21, 18, 84
 B_SE3 = {"f32": 28, "f64": 56}              # bytes per stored SE(3) state streamed by a scan
 # committed PMC passes per workload, newest round first (cfg5k = configs[4] in kNN mode)
-PMC_PROFILES = {w: [f"r4_{w}", f"r3_{w}"] for w in ("cfg3", "cfg2", "cfg4", "cfg5")}
-PMC_PROFILES["cfg5k"] = ["r4_cfg5k"]
+PMC_PROFILES = {w: [f"r5_{w}", f"r4_{w}", f"r3_{w}"] for w in ("cfg3", "cfg2", "cfg4", "cfg5")}
+PMC_PROFILES["cfg5k"] = ["r5_cfg5k", "r4_cfg5k"]
+PMC_PROFILES["rrt_star"] = ["r5_rrt_star"]
 DEFAULTS = {  # tree states, queries (samples / milestones / vertices) per GPU per step, k
     "cfg3": (1_000_000, 100_000, 10),
     "cfg2": (100_000, 100_000, 10),
@@ -603,6 +604,7 @@ def rrt_star_workload(torch, dev, local, stream, steps, warmup, ns=10_000, n_tre
     n_mid = n_tree + planner.stats["added"] - n_added / 2
     pairs = (n_added / steps) * n_mid  # the neighbourhood kNN's fill pass: every (added state, stored state) pair
     achieved = pairs * F_SE3 / (kern_ms * 1e-3) / 1e12
+    traffic = pmc_traffic("rrt_star", k1[2])
     line = {
         "metric": "RRT* iterations/sec (nearest + steer + checkMotion + neighbourhood + motion bits + cost logic), "
                   "SE(3) 10^6-state tree",
@@ -623,7 +625,8 @@ def rrt_star_workload(torch, dev, local, stream, steps, warmup, ns=10_000, n_tre
         "per_step": {k: (planner.stats[k] - st0[k]) / steps for k in ("rewires", "checks_used", "child_cost_updates")},
         "setup_s": setup_s,
         "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_TFLOPS["f32"], "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_TFLOPS["f32"], "traffic": None, "kernel": k1[2], "kernel_ms": kern_ms,
+                     "frac": achieved / PEAK_TFLOPS["f32"], "traffic": traffic["bytes"] if traffic else None,
+                     "traffic_source": traffic["source"] if traffic else None, "kernel": k1[2], "kernel_ms": kern_ms,
                      "algorithmic": f"the neighbourhood kNN's fp32 fill pass ({k1[2]}): every (added state, stored "
                                     f"state) pair, {pairs:.4g} per step x {F_SE3} flop"},
     }
@@ -1097,10 +1100,17 @@ def sub_args(args, spec):
     return a
 
 
+def progress(msg):
+    """a progress line on stderr (long default runs stay visibly alive)"""
+    print(f"bench [{time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
     """Run one workload: warmup, exactly args.steps timed steps bracketed by a barrier +
     synchronize on both sides (max over ranks), then the line's common fields.  Returns
     (line or None on ranks > 0, the Runner, the phase-valid fraction)."""
+    if rank == 0:
+        progress(f"{args.workload} ({args.partition}, {args.scaling}{', kNN' if args.bitstar_knn else ''}): setup")
     run = Runner(args, torch, dev, local, rank, stream, dist)
     run.stream = stream
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
@@ -1187,6 +1197,7 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
 
 def attach_cpu_baseline(line, run, args, rank, world, budget):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress(f"{args.workload}: CPU baseline")
         t0 = time.perf_counter()
         line["cpu_baseline"] = cpu_baseline(args.workload, run.sp, run.ck, run.tree, run.q_host, run.k, budget,
                                             run.radius)
@@ -1273,6 +1284,7 @@ def main():
     if (rank == 0 and world == 1 and args.workload == "cfg3" and args.partition == "replicated"
             and want_rrt_star and args.rrt_star_samples > 0):
         t0 = time.perf_counter()
+        progress("rrt_star: setup, steps, CPU baseline")
         sub = rrt_star_workload(torch, dev, local, stream, args.steps, args.warmup, ns=args.rrt_star_samples,
                                 cpu_seconds=args.sub_cpu_seconds, cpu=not args.no_cpu_baseline)
         sub["wall_s"] = time.perf_counter() - t0
