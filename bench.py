@@ -1122,6 +1122,7 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
     run.nn.profile(True)
     run.nn.kernel_time()
     scr0, fb0 = run.nn.stats()
+    rp0 = run.nn.radius_path_stats()
     c0 = run.counters()
     units = 0
     if dist:
@@ -1143,6 +1144,7 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
     kern_ms = kern_ms_total / max(kern_n, 1)
     run.nn.profile(False)
     scr1, fb1 = run.nn.stats()
+    rp1 = run.nn.radius_path_stats()
     c1 = run.counters()
     nn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     edge_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
@@ -1192,6 +1194,8 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
     elif args.workload != "cfg2":
         line["motion_checks_per_s"] = run.m * world / (mv_ms * 1e-3)
         line["motion_valid_fraction"] = valid_frac
+    if args.workload == "cfg5" and not args.bitstar_knn:  # timed nearestR calls by path
+        line["radius_walks"] = {"one_pass": rp1[0] - rp0[0], "overflowed": rp1[1] - rp0[1]}
     return line, run
 
 
@@ -1241,6 +1245,8 @@ def main():
     line, run = measure(args, torch, dev, local, rank, world, dist, stream, args.cpu_seconds)
 
     single = single_large = rrt = spheres = rrt_star = index = None
+    if rank == 0 and not args.no_extras:
+        progress(f"{args.workload}: extras")
     if rank == 0 and args.workload in ("cfg3", "cfg2") and not args.no_extras:
         index = index_maintenance(torch, run, local)
     if rank == 0 and args.workload == "cfg3" and not args.no_extras:

@@ -226,6 +226,9 @@ ompl_gpu_status ompl_gpu_nn_radius_device(ompl_gpu_nn *h, const double *d_querie
 /* Radius walk: 64-state tiles fetched and (tile, query) pairs scanned (64 distance
  * evaluations each), summed over nearestR calls.  Either output may be NULL. */
 ompl_gpu_status ompl_gpu_nn_radius_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_scanned, uint64_t *query_tiles);
+/* Culled nearestR calls answered by the one walk into per-query slabs, and those whose longest
+ * segment overflowed the slab (count walk + fill walk; the next call's slab grows to it). */
+ompl_gpu_status ompl_gpu_nn_radius_path_stats(ompl_gpu_nn *h, uint64_t *one_pass, uint64_t *two_pass);
 /* Motion endpoints of a batch of neighbour results — the edges the planners check after a
  * neighbour query: PRM checkMotion(state[n], state[m]) (PRM.cpp:577-582, from_query = 0),
  * BIT* checkMotion(vertex, sample) (BITstar.cpp:815, from_query = 1).  Edge e pairs query q

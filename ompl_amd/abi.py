@@ -110,6 +110,7 @@ SIGNATURES = {
     "ompl_gpu_steer_device": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_uint32, C.c_double, _P, _P]),
     "ompl_gpu_nn_radius_device": (C.c_int, [_P, _P, C.c_size_t, C.c_double, _P, _P, _P, C.c_uint64, _U64]),
     "ompl_gpu_nn_radius_cull_stats": (C.c_int, [_P, _U64, _U64]),
+    "ompl_gpu_nn_radius_path_stats": (C.c_int, [_P, _U64, _U64]),
     "ompl_gpu_nn_edges_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P, C.c_uint32, C.c_size_t, C.c_int, _P, _P]),
     "ompl_gpu_rrt_grow_device": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_double, _P, _P]),
     "ompl_gpu_rrt_aborts": (C.c_int, [_P, _U64]),

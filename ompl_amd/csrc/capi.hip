@@ -107,6 +107,7 @@ struct ompl_gpu_nn {
         fb_i, fb_c, fb_cd, fb_ci, slab_i, slab_d;
     uint32_t radius_slab = 64;      // per-query slab of the one-pass radius walk (adapts upward)
     uint64_t radius_one_pass = 0;   // radius calls answered by the one-pass walk
+    uint64_t radius_two_pass = 0;   // radius calls whose longest segment overflowed the slab
     DevBuf rrt_n, rrt_pd, rrt_pi;  // device RRT growth: live size + barrier words, per-block partial minima
     int rrt_coop = -1;             // persistent RRT grid size (0: two-launch form), found on first use
     int rrt_abort_streak = 0;      // consecutive aborted persistent grids (a device kept busy by others)
@@ -784,6 +785,7 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
         }
         // a slab overflowed: its query's count is a candidate count (the exact decisions run on
         // the slab), so recount exactly with the count walk before the fill walk
+        h->radius_two_pass += 1;
         HIP_OR_FAIL(launch_radius_fast(h->sp, h->g, h->feat, h->cap, &h->sorted, d_qf, (uint32_t)nq, r, b, h->ws.p,
                                        h->ws.bytes, 0, &d_off, nullptr, nullptr, h->stream));
         HIP_OR_FAIL(hipMemcpyAsync(tm, d_off + nq, sizeof(tm), hipMemcpyDeviceToHost, h->stream));
@@ -1052,6 +1054,14 @@ ompl_gpu_status ompl_gpu_nn_radius_cull_stats(ompl_gpu_nn *h, uint64_t *tiles_sc
     if (st != OMPL_GPU_OK) return st;
     if (tiles_scanned) *tiles_scanned = c[3];
     if (query_tiles) *query_tiles = c[4];
+    return OMPL_GPU_OK;
+}
+
+ompl_gpu_status ompl_gpu_nn_radius_path_stats(ompl_gpu_nn *h, uint64_t *one_pass, uint64_t *two_pass) {
+    if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (one_pass) *one_pass = h->radius_one_pass;
+    if (two_pass) *two_pass = h->radius_two_pass;
     return OMPL_GPU_OK;
 }
 

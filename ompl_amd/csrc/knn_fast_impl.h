@@ -2387,8 +2387,8 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
                                ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64,
                                sp, b.absmax, b.qeta, r, counts, nullptr, nullptr, nullptr, nullptr, 0u);
         }
-        // offsets (counts[nq] = 0: offs[nq] = offs[nq + 1] = the total) and the longest segment
-        return launch_exclusive_scan_u64(counts, (uint64_t)nq + 1, offs, ws + L.scan, st, offs + nq + 1);
+        // offsets (offs[nq] = the total) and the longest segment (offs[nq + 1])
+        return launch_exclusive_scan_u64(counts, (uint64_t)nq, offs, ws + L.scan, st, offs + nq + 1);
     }
     timer_begin(st, "radius32_group_kernel");
     hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 1>), grid, b64, 0, st, ss->rows, ss->n_pad,

@@ -206,6 +206,12 @@ class NearestNeighborsGPU(abi.Handle):
         abi.check(abi.lib.ompl_gpu_nn_radius_cull_stats(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
+    def radius_path_stats(self) -> tuple[int, int]:
+        """(culled nearestR calls answered by the one slab walk, calls that overflowed a slab)."""
+        a, b = C.c_uint64(0), C.c_uint64(0)
+        abi.check(abi.lib.ompl_gpu_nn_radius_path_stats(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def edges_device(self, d_queries: int, nq: int, d_offsets: int | None, d_ids: int, stride: int, m: int,
                      from_query: bool, d_from: int, d_to: int) -> None:
         """Motion endpoints of neighbour results (PRM.cpp:582 from_query=False, BITstar.cpp:815

@@ -55,8 +55,11 @@ def test_radius_culled_vs_oracle(gpu, name, mode):
     # the largest radius again: its longest segment overflowed the one-pass walk's first slab
     # (64 hits) above, so this call runs the single walk with the grown slab
     assert np.diff(off).max() > 64
+    paths0 = nn.radius_path_stats()
     _check_radius(nn, sp, data, q, radii[-1])
     if mode == 0:
+        one, two = nn.radius_path_stats()
+        assert paths0[1] >= 1 and (one, two) == (paths0[0] + 1, paths0[1])  # the grown slab held it
         tiles, pairs = nn.radius_cull_stats()
         assert 0 < tiles <= pairs
 
