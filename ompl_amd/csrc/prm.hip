@@ -28,10 +28,21 @@ __device__ __forceinline__ double stored_bound(const double *sd, const uint32_t 
     return si[o] == kNoId ? __builtin_inf() : sd[o];
 }
 
-__device__ __forceinline__ uint32_t stored_take(const uint32_t *si, uint32_t kq, uint32_t kj, uint32_t j) {
+// the stored entries among row j's first min(k_j, kq): one lane (short rows: PRM*'s k <= 41) ...
+__device__ __forceinline__ uint32_t stored_take_lane(const uint32_t *si, uint32_t kq, uint32_t kj, uint32_t j) {
     uint32_t c = 0;
     const uint32_t lim = kj < kq ? kj : kq;
     for (uint32_t r = 0; r < lim; ++r) c += si[(size_t)j * kq + r] != kNoId ? 1u : 0u;
+    return c;
+}
+// ... or counted over the whole wave, every lane active (every lane gets the count; a lane walking
+// RRT*'s 6,169-entry rows alone took ~0.3 ms per batch)
+__device__ __forceinline__ uint32_t stored_take(const uint32_t *si, uint32_t kq, uint32_t kj, uint32_t j) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lim = kj < kq ? kj : kq;
+    uint32_t c = 0;
+    for (uint32_t r = lane; r < lim; r += 64) c += si[(size_t)j * kq + r] != kNoId ? 1u : 0u;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
     return c;
 }
 
@@ -134,10 +145,12 @@ __global__ __launch_bounds__(256) void prm_causal_kernel(const double *__restric
         }
         cnt += (uint64_t)__popcll(bm);
     }
-    if (!FILL && lane == 0) {
-        const uint64_t len = stored_take(si, kq, kj, row) + cnt;
-        seg_len[row] = len;
-        if (seg_max) atomicMax(seg_max, (unsigned long long)len);
+    if (!FILL) {
+        const uint64_t len = stored_take(si, kq, kj, row) + cnt;  // wave-wide: every lane takes part
+        if (lane == 0) {
+            seg_len[row] = len;
+            if (seg_max) atomicMax(seg_max, (unsigned long long)len);
+        }
     }
 }
 
@@ -195,7 +208,7 @@ __global__ __launch_bounds__(64) void prm_causal_tile_kernel(const double *__res
         const double e = 2.0 * (sp.link * 8.0 * u * n * (n + 1.0) + (n + 2.0) * u * bound + sp.link * n * sqrt(2.0 * fmin));
         s_bound[lane] = bound;
         s_thr[lane] = bound < __builtin_inf() ? (float)((bound + e) * (1.0 + 16.0 * u)) : __builtin_inff();
-        s_stored[lane] = ok ? stored_take(si, kq, kj, row) : 0u;
+        s_stored[lane] = ok ? stored_take_lane(si, kq, kj, row) : 0u;
         s_cnt[lane] = 0;
         s_pos[lane] = (FILL && ok) ? seg_off[row] + s_stored[lane] : 0ull;
     }
