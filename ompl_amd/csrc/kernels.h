@@ -84,6 +84,10 @@ constexpr double kScreenMaxAbs = 1e18;
 // distance).
 constexpr int kCullTile = 64;
 constexpr int kSuperTiles = 32;
+// mega-tiles: 64 consecutive super-tiles (2,048 tiles) with the union of their boxes, so a walk
+// over a 10^7-state store tests 77 mega boxes and then only the super-tiles of the megas that
+// pass, instead of all 4,883 super-tile boxes (one lane per box, 64 per round)
+constexpr int kMegaSupers = 64;
 // queries per wave in the group walk.  Measured on MI355X (k=10, 10^5 queries, k-d tiles):
 // SE3 10^6 states G=2 2.09 ms, G=4 2.18 ms; R^6 10^5 states G=2 2.20 ms, G=4 1.50 ms.  (With
 // Morton-run tiles, SE3: G=8 4.4 ms, G=4 3.5 ms, G=2 3.2 ms; packed two-query math 3.7 ms.)
@@ -108,13 +112,14 @@ struct SortedStore {
     uint32_t *ids = nullptr;     // [n_pad] original id of each sorted slot (kNoId = padding)
     float *tbox = nullptr;       // [tiles][box_w] lo.., hi.. (, eta, pad)
     float *sbox = nullptr;       // [supers][box_w]
+    float *mbox = nullptr;       // [megas][box_w] (kMegaSupers super-tiles each)
     uint32_t *tkey0 = nullptr;   // [tiles] key of each tile = its index (queries' keys are home tiles)
     KdNode *nodes = nullptr;     // internal k-d nodes of the main tiles, pre-order (kd_order.h)
     double *rows64 = nullptr;    // [n_pad][fa] fp64 features in sorted order (AoS: one 64 B row per
                                  // SE3 state), read by the certificate; padding rows are NaN
     uint32_t *inv = nullptr;     // [cap_inv] sorted position of each id (kNoId: not placed)
     int fa = 0;                  // fp64 row width: F rounded up to a multiple of 4
-    uint32_t n = 0, n_pad = 0, ntiles = 0, nsuper = 0, nnodes = 0;
+    uint32_t n = 0, n_pad = 0, ntiles = 0, nsuper = 0, nmega = 0, nnodes = 0;
     uint32_t kd_tiles = 0;       // main tiles (leaves of the k-d tree, built on the device)
     // incremental state: the main k-d tiles hold the live ids of [0, main_covered) at the build;
     // states added since then are re-tiled along the Morton curve in the tail region, tiles

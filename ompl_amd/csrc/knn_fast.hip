@@ -43,7 +43,7 @@ bool radius_cull_supported(const DevSpace &sp) {
 }
 
 void free_sorted_store(SortedStore *s) {
-    for (void *x : {(void *)s->rows, (void *)s->ids, (void *)s->tbox, (void *)s->sbox, (void *)s->tkey0, (void *)s->nodes,
+    for (void *x : {(void *)s->rows, (void *)s->ids, (void *)s->tbox, (void *)s->sbox, (void *)s->mbox, (void *)s->tkey0, (void *)s->nodes,
                     (void *)s->rows64, (void *)s->inv, (void *)s->qcount, (void *)s->rows16, s->scratch})
         if (x) (void)hipFree(x);
     *s = SortedStore{};

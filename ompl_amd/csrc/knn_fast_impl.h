@@ -620,8 +620,8 @@ __device__ __forceinline__ float box_tgap2(const float *bx, const float *q, int 
 template <int SP, int F, int K2, int G, bool QS>
 __global__ __launch_bounds__(64) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
-    const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper,
-    const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
+    const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ mbox,
+    uint32_t nmega, const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
     uint32_t nq, float w0, float w1, float *__restrict__ pd, uint32_t *__restrict__ pi,
     unsigned long long *__restrict__ counters, int k2, float pmin) {
     constexpr int FS = Geo<SP, F>::FS, R = Geo<SP, F>::R, BW = Geo<SP, F>::BW;
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     // PK (SE3, two queries): a tile is screened for both queries at once on packed fp32, the
     // rotation first by a certified lower bound from the quaternion dot products (below)
     constexpr bool PK = SP == OMPL_GPU_SPACE_SE3 && G == 2;
-    static_assert(G % 2 == 0 && K2 <= 64, "group walk shape");
+    static_assert(G % 2 == 0 && K2 <= 64 && kMegaSupers == 64, "group walk shape");
     __shared__ __attribute__((aligned(16))) float qrow[G * FS];
     __shared__ __attribute__((aligned(16))) float qpair[PK ? 2 * FS : 2];  // (query 0, query 1) per coordinate
     const int lane = threadIdx.x;
@@ -864,6 +864,55 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     // values live across the whole walk cost 29 VGPRs (69 -> 98, 7 -> 5 waves per SIMD)
     __shared__ float slb[G][64];
     bool first_round = true;  // the neighbourhood's three are always visited
+    // mega-tiles (kMegaSupers super-tiles each): a round tests 64 mega boxes; a super-tile round
+    // then covers the 64 super-tiles of one passing mega.  A popped mega is re-checked against the
+    // tightened thresholds by its round bounds (mlb, LDS) like a popped super-tile.
+    __shared__ float mlb[G][64];
+    uint32_t mb = 0, mbase = 0;
+    uint64_t mm = 0;
+    auto next_mega = [&]() -> int {
+        for (;;) {
+            if (mm) {
+                bool keep = false;
+#pragma unroll
+                for (int g = 0; g < G; ++g) keep |= mlb[g][lane] < td[g];
+                mm &= __ballot(keep);
+            }
+            if (mm) {
+                const int l = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                return (int)(mbase + l);
+            }
+            if (mb >= nmega) return -1;
+            relaunder();
+            const uint32_t mi = mb + lane;
+            bool need = false;
+            float lbm[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) lbm[g] = __builtin_inff();
+            if (mi < nmega) {
+                float bx[BW];
+                const float4 *b4 = reinterpret_cast<const float4 *>(mbox + (size_t)mi * BW);
+#pragma unroll
+                for (int c = 0; c < BW / 4; ++c) {
+                    const float4 v = b4[c];
+                    bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    lbm[g] = box_lb<SP, F, true>(bx, &qrow[qoff + g * FS], w0, w1);
+                    need |= lbm[g] < td[g];
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) mlb[g][lane] = lbm[g];
+            __builtin_amdgcn_wave_barrier();
+            mm = __ballot(need);
+            mbase = mb;
+            mb += 64;
+        }
+    };
     auto next_super = [&]() -> int {  // next super-tile to visit, -1 when done
         for (;;) {
             if (sm && !first_round) {  // drop what the tightened thresholds exclude
@@ -880,7 +929,9 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
                 sm &= sm - 1;
                 return (int)(base + l);
             }
-            if (sb >= nsuper) return -1;
+            const int mg = next_mega();
+            if (mg < 0) return -1;
+            sb = (uint32_t)mg * kMegaSupers;
             relaunder();
 #ifdef OMPL_AMD_PROBE
             ++pr_rounds;
@@ -912,7 +963,6 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
             first_round = false;
             sm = __ballot(need);
             base = sb;
-            sb += 64;
         }
     };
     // Software pipeline: the tile boxes of the next super-tile sn are loaded while the tiles
@@ -1685,8 +1735,8 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
 template <int SP, int F, int G, int MODE, bool Q16 = false>
 __global__ OMPL_RADIUS_LB void radius32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
-    const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ q32,
-    const uint32_t *__restrict__ perm, uint32_t nq, const double *__restrict__ rows64,
+    const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ mbox,
+    uint32_t nmega, const float *__restrict__ q32, const uint32_t *__restrict__ perm, uint32_t nq, const double *__restrict__ rows64,
     const double *__restrict__ qf64, DevSpace sp, float absmax, float qeta, double r, uint64_t *__restrict__ counts,
     const uint64_t *__restrict__ offsets, uint32_t *__restrict__ out_i, double *__restrict__ out_d,
     unsigned long long *__restrict__ counters, uint32_t slab, const uint32_t *__restrict__ rows16 = nullptr,
@@ -1746,9 +1796,42 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
     // the half-waves; a translation-only pre-test before the chord bound.)
     uint32_t sb = 0, base = 0;
     uint64_t sm = 0;
+    // mega-tiles first (64 mega boxes per round), then the super-tiles of each passing mega
+    uint32_t mb = 0, mbase = 0;
+    uint64_t mm = 0;
+    auto next_mega = [&]() -> int {
+        while (!mm) {
+            if (mb >= nmega) return -1;
+            asm volatile("" : "+s"(qoff));
+            const uint32_t mi = mb + lane;
+            bool need = false;
+            if (mi < nmega) {
+                float bx[BW];
+                const float4 *b4 = reinterpret_cast<const float4 *>(mbox + (size_t)mi * BW);
+#pragma unroll
+                for (int c = 0; c < BW / 4; ++c) {
+                    const float4 v = b4[c];
+                    bx[4 * c] = v.x; bx[4 * c + 1] = v.y; bx[4 * c + 2] = v.z; bx[4 * c + 3] = v.w;
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    need |= box_lb<SP, F>(bx, &qrow[qoff + g * FS], w0, w1) <= thr[g];
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            mm = __ballot(need);
+            mbase = mb;
+            mb += 64;
+        }
+        const int l = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        return (int)(mbase + l);
+    };
     auto next_super = [&]() -> int {
         while (!sm) {
-            if (sb >= nsuper) return -1;
+            const int mg = next_mega();
+            if (mg < 0) return -1;
+            sb = (uint32_t)mg * kMegaSupers;
             asm volatile("" : "+s"(qoff));
             const uint32_t s = sb + lane;
             bool need = false;
@@ -1768,7 +1851,6 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
             }
             sm = __ballot(need);
             base = sb;
-            sb += 64;
         }
         const int l = __builtin_ctzll(sm);
         sm &= sm - 1;
@@ -2174,7 +2256,7 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
             // (BIT*'s 64-lane lists too: cfg5k G = 2 4.08-4.14 ms, 4 4.24-4.35, 8 5.07-5.09)
             constexpr int G = group_queries<SP>();
             hipLaunchKernelGGL((knn32_group_kernel<SP, F, K2, G, true>), dim3((nq + G - 1) / G), dim3(64), 0, st,
-                               ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->tkey0, q32,
+                               ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->mbox, ss->nmega, ss->tkey0, q32,
                                keys2, nq, (float)sp.w0, (float)sp.w1, pd, pi, ss->counters, p.k2,
                                (float)((1.0 - (double)b.qeta) * (1.0 - 4e-7)));
             timer_end(st);
@@ -2369,14 +2451,14 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
                 if (ss->rows16 && ss->gen16 == ss->gen) {
                     q16 = true;
                     hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusSlabGroup, 2, true>), gs, b64, 0, st,
-                                       ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32,
+                                       ss->rows, ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->mbox, ss->nmega, q32,
                                        perm, nq, ss->rows64, qf64, sp, b.absmax, b.qeta, r, counts, nullptr, out_i,
                                        out_d, ss->counters, b.slab, ss->rows16, ss->q16, se3_q16_error(sp, ss->q16));
                 }
             }
             if (!q16)
                 hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusSlabGroup, 2>), gs, b64, 0, st, ss->rows,
-                                   ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq,
+                                   ss->n_pad, ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->mbox, ss->nmega, q32, perm, nq,
                                    ss->rows64, qf64, sp, b.absmax, b.qeta, r, counts, nullptr, out_i, out_d,
                                    ss->counters, b.slab);
             timer_end(st);
@@ -2384,7 +2466,7 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
                                r, b.slab, counts, out_i, out_d);
         } else {
             hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 0>), grid, b64, 0, st, ss->rows, ss->n_pad,
-                               ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64,
+                               ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->mbox, ss->nmega, q32, perm, nq, ss->rows64, qf64,
                                sp, b.absmax, b.qeta, r, counts, nullptr, nullptr, nullptr, nullptr, 0u);
         }
         // offsets (offs[nq] = the total) and the longest segment (offs[nq + 1])
@@ -2392,7 +2474,7 @@ hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, 
     }
     timer_begin(st, "radius32_group_kernel");
     hipLaunchKernelGGL((radius32_group_kernel<SP, F, kRadiusGroup, 1>), grid, b64, 0, st, ss->rows, ss->n_pad,
-                       ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, q32, perm, nq, ss->rows64, qf64, sp,
+                       ss->ids, ss->ntiles, ss->tbox, ss->sbox, ss->nsuper, ss->mbox, ss->nmega, q32, perm, nq, ss->rows64, qf64, sp,
                        b.absmax, b.qeta, r, nullptr, offs, out_i, out_d, ss->counters, 0u);
     timer_end(st);
     return hipGetLastError();
@@ -2552,13 +2634,15 @@ __global__ void tile_box_range_kernel(const float *__restrict__ rows, uint32_t n
     }
 }
 
+// boxes of groups of `group` consecutive input boxes (tile boxes -> super-tiles, super-tile boxes
+// -> mega-tiles): output box sI covers inputs [sI * group, min((sI + 1) * group, n_in))
 template <int SP, int F>
-__global__ void super_box_range_kernel(const float *__restrict__ tbox, uint32_t ntiles, uint32_t s0, uint32_t s1,
-                                       float *__restrict__ sbox) {
+__global__ void super_box_range_kernel(const float *__restrict__ tbox, uint32_t n_in, uint32_t group, uint32_t s0,
+                                       uint32_t s1, float *__restrict__ sbox) {
     constexpr int NB = Geo<SP, F>::NB, BW = Geo<SP, F>::BW;
     const uint32_t sI = s0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (sI >= s1) return;
-    const uint32_t t0 = sI * kSuperTiles, t1 = min((sI + 1) * kSuperTiles, ntiles);
+    const uint32_t t0 = sI * group, t1 = min((sI + 1) * group, n_in);
     for (int c = 0; c < NB; ++c) {
         float lo = __builtin_inff(), hi = -__builtin_inff();
         for (uint32_t t = t0; t < t1; ++t) {
@@ -3267,6 +3351,9 @@ hipError_t sorted_alloc(SortedStore *s, uint32_t pad_tiles, uint32_t max_nodes, 
         dummy = 0;
         if ((e = grow_array(&s->sbox, dummy, (size_t)nsup * BW)) != hipSuccess) return e;
         dummy = 0;
+        if ((e = grow_array(&s->mbox, dummy, (size_t)((nsup + kMegaSupers - 1) / kMegaSupers) * BW)) != hipSuccess)
+            return e;
+        dummy = 0;
         if ((e = grow_array(&s->tkey0, dummy, (size_t)pad_tiles)) != hipSuccess) return e;
         dummy = 0;
         if ((e = grow_array(&s->qcount, dummy, ((size_t)pad_tiles + 1023) / 1024 * 1025 + 1)) != hipSuccess) return e;
@@ -3279,7 +3366,8 @@ hipError_t sorted_alloc(SortedStore *s, uint32_t pad_tiles, uint32_t max_nodes, 
     if ((e = grow_array(&s->nodes, s->cap_nodes, std::max<uint32_t>(max_nodes, 1))) != hipSuccess) return e;
     if ((e = grow_array(&s->inv, s->cap_inv, inv_cap)) != hipSuccess) return e;
     s->bytes = s->cap_pos * (4ull * R + 4 + 8ull * fa) + (s->cap_pos / kCullTile) * (4ull * BW + 4) +
-               ((s->cap_pos / kCullTile + kSuperTiles - 1) / kSuperTiles) * 4ull * BW + s->cap_nodes * sizeof(KdNode) +
+               ((s->cap_pos / kCullTile + kSuperTiles - 1) / kSuperTiles) * 4ull * BW * (kMegaSupers + 1) / kMegaSupers +
+               s->cap_nodes * sizeof(KdNode) +
                s->cap_inv * 4ull;
     return hipSuccess;
 }
@@ -3390,7 +3478,10 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
                        0u, main_sup_tiles, s->tbox);
     const uint32_t nsup = main_sup_tiles / kSuperTiles;
     hipLaunchKernelGGL((super_box_range_kernel<SP, F>), dim3((nsup + 255) / 256), b256, 0, st, s->tbox, main_sup_tiles,
-                       0u, nsup, s->sbox);
+                       (uint32_t)kSuperTiles, 0u, nsup, s->sbox);
+    const uint32_t nmeg = (nsup + kMegaSupers - 1) / kMegaSupers;
+    hipLaunchKernelGGL((super_box_range_kernel<SP, F>), dim3((nmeg + 255) / 256), b256, 0, st, s->sbox, nsup,
+                       (uint32_t)kMegaSupers, 0u, nmeg, s->mbox);
     // fp64 rows in sorted order: transpose the SoA features by id into the (now free) row
     // buffers, then one contiguous row per slot
     double *aos = (double *)(w + o_w);
@@ -3408,6 +3499,7 @@ hipError_t build_sorted(const float *f32, const double *f64, uint64_t cap, uint6
     s->tail_cap_tiles = tail_tiles;
     s->ntiles = main_sup_tiles;
     s->nsuper = nsup;
+    s->nmega = nmeg;
     s->n = n_live;
     s->covered = n_total;
     s->main_covered = n_total;
@@ -3467,13 +3559,18 @@ hipError_t append_sorted(const float *f32, const double *f64, uint64_t cap, uint
     hipLaunchKernelGGL((tile_box_range_kernel<SP, F>), dim3((tiles + 3) / 4), b256, 0, st, s->rows, s->n_pad,
                        s->tail_t0, t1, s->tbox);
     const uint32_t s0 = s->tail_t0 / kSuperTiles, s1 = (t1 + kSuperTiles - 1) / kSuperTiles;
-    hipLaunchKernelGGL((super_box_range_kernel<SP, F>), dim3((s1 - s0 + 255) / 256), b256, 0, st, s->tbox, t1, s0, s1,
-                       s->sbox);
+    hipLaunchKernelGGL((super_box_range_kernel<SP, F>), dim3((s1 - s0 + 255) / 256), b256, 0, st, s->tbox, t1,
+                       (uint32_t)kSuperTiles, s0, s1, s->sbox);
+    // the megas over the re-boxed super-tiles (the first may also hold main super-tiles: a union)
+    const uint32_t m0 = s0 / kMegaSupers, m1 = (s1 + kMegaSupers - 1) / kMegaSupers;
+    hipLaunchKernelGGL((super_box_range_kernel<SP, F>), dim3((m1 - m0 + 255) / 256), b256, 0, st, s->sbox, s1,
+                       (uint32_t)kMegaSupers, m0, m1, s->mbox);
     const uint64_t c64 = (uint64_t)(p1 - p0) * s->fa;
     hipLaunchKernelGGL(rows64_range_kernel, dim3((unsigned)((c64 + 255) / 256)), b256, 0, st, f64, cap, F, s->fa,
                        s->ids, p0, p1, s->rows64);
     s->ntiles = t1;
     s->nsuper = s1;
+    s->nmega = m1;
     s->n = p1;
     s->covered = n_total;
     return hipGetLastError();
