@@ -1249,6 +1249,12 @@ ompl_gpu_status ompl_gpu_mv_create(ompl_gpu_mv **out, const ompl_gpu_space *spac
         h->ck.data = h->ck_data;
         h->ck_host.assign(checker->data, checker->data + per * h->ck.count);
     }
+    h->ck.slack = 0.0;
+    if (checker->kind == OMPL_GPU_CHECK_KCHAIN) {  // device_space.h chain_valid's side pre-test
+        double M = std::max(1.0, std::fabs(sp.link) * sp.dim + 0.001);
+        for (double v : h->ck_host) M = std::max(M, std::fabs(v));
+        h->ck.slack = 1e-12 * M * M;
+    }
     if (e != hipSuccess) {
         ompl_gpu_mv_destroy(h);
         return fail(OMPL_GPU_ERR_DEVICE, hipGetErrorString(e));

@@ -201,6 +201,10 @@ struct DevChecker {
     double edge;
     int count;
     const double *data;  // device copy
+    // KinematicChain: the rounding slack of the segment-side pre-test (chain_valid), >= every
+    // difference between a side value computed here and the reference's s / t numerators:
+    // 1e-12 * M^2, M = max(1, the chain's reach, the largest |environment coordinate|)
+    double slack;
 };
 
 __host__ __device__ __forceinline__ bool hypercube_valid(const double *s, int ndim, double edge) {
@@ -256,8 +260,21 @@ __host__ __device__ __forceinline__ bool seg_intersect(double a0x, double a0y, d
 
 constexpr int kChainMaxLinks = 32;
 
+// KinematicChainValidityChecker::isValid (demos/KinematicChain.h:200-276): the chain's link
+// endpoints, then every pair of its segments and every (segment, environment segment) pair
+// through intersectionTest (seg_intersect) — the result is the AND of those tests, so the order
+// of the pairs does not matter.  A pair is tested only when a necessary condition for the test to
+// return true holds.  For a = (a0, a1) against b = (b0, b1), with v = b1 - b0 and the side value
+// side(p) = v x (p - b0), the test's t numerator is side(a0) and its t numerator minus the
+// denominator is side(a1) up to rounding; it returns true only if (denom > 0) t >= eps >= t - denom,
+// or (denom < 0) t < eps < t - denom — in both cases eps lies between side(a0) and side(a1)
+// (eps = FLT_EPSILON, the test's own threshold).  So when both endpoints of a have side values
+// above eps + slack, or both below eps - slack, the test returns false and is skipped (slack:
+// DevChecker::slack, far above the rounding of either computation).  For an environment
+// segment the side values of the whole chain are first bounded over the chain's bounding box
+// (side() is affine): a box entirely on one side skips all of that segment's tests.
 __host__ __device__ inline bool chain_valid(const double *s, int n, double link, const double *env, int nenv,
-                                            const double *tab = gsc::kSinCosTab) {
+                                            double slack, const double *tab = gsc::kSinCosTab) {
     double px[kChainMaxLinks + 2], py[kChainMaxLinks + 2];  // segment i = (p[i], p[i+1])
     double theta = 0., x = 0., y = 0.;
     px[0] = 0.;
@@ -277,15 +294,139 @@ __host__ __device__ inline bool chain_valid(const double *s, int n, double link,
     px[n + 1] = x + ct * 0.001;
     py[n + 1] = y + st * 0.001;
     const int ns = n + 1;
-    for (int i = 0; i < ns; ++i)
-        for (int j = i + 1; j < ns; ++j)
-            if (seg_intersect(px[i], py[i], px[i + 1], py[i + 1], px[j], py[j], px[j + 1], py[j + 1])) return false;
-    for (int i = 0; i < ns; ++i)
-        for (int j = 0; j < nenv; ++j)
-            if (seg_intersect(px[i], py[i], px[i + 1], py[i + 1], env[4 * j], env[4 * j + 1], env[4 * j + 2],
+    const double lo_t = kFltEps - slack, hi_t = kFltEps + slack;
+    // segment pairs (i, j), i < j: b = segment j
+    for (int j = 1; j < ns; ++j) {
+        const double bx = px[j], by = py[j], vx = px[j + 1] - bx, vy = py[j + 1] - by;
+        double sa = vx * (py[0] - by) - vy * (px[0] - bx);
+        for (int i = 0; i < j; ++i) {
+            const double sb = vx * (py[i + 1] - by) - vy * (px[i + 1] - bx);
+            if (!((sa > hi_t && sb > hi_t) || (sa < lo_t && sb < lo_t)) &&
+                seg_intersect(px[i], py[i], px[i + 1], py[i + 1], px[j], py[j], px[j + 1], py[j + 1]))
+                return false;
+            sa = sb;
+        }
+    }
+    double xmin = px[0], xmax = px[0], ymin = py[0], ymax = py[0];
+    for (int i = 1; i <= ns; ++i) {
+        xmin = fmin(xmin, px[i]);
+        xmax = fmax(xmax, px[i]);
+        ymin = fmin(ymin, py[i]);
+        ymax = fmax(ymax, py[i]);
+    }
+    for (int j = 0; j < nenv; ++j) {
+        const double bx = env[4 * j], by = env[4 * j + 1], vx = env[4 * j + 2] - bx, vy = env[4 * j + 3] - by;
+        const double y0 = vx * (ymin - by), y1 = vx * (ymax - by), x0 = vy * (xmin - bx), x1 = vy * (xmax - bx);
+        const double smax = fmax(y0, y1) - fmin(x0, x1), smin = fmin(y0, y1) - fmax(x0, x1);
+        if (smin > hi_t || smax < lo_t) continue;  // the whole chain on one side of b's line
+        double sa = vx * (py[0] - by) - vy * (px[0] - bx);
+        for (int i = 0; i < ns; ++i) {
+            const double sb = vx * (py[i + 1] - by) - vy * (px[i + 1] - bx);
+            if (!((sa > hi_t && sb > hi_t) || (sa < lo_t && sb < lo_t)) &&
+                seg_intersect(px[i], py[i], px[i + 1], py[i + 1], env[4 * j], env[4 * j + 1], env[4 * j + 2],
                               env[4 * j + 3]))
                 return false;
+            sa = sb;
+        }
+    }
     return true;
+}
+
+// chain_valid with the link endpoints in registers: NP >= n + 2 points, every loop unrolled to
+// NP with guards on the runtime n, so every index is a constant (the runtime form's arrays live
+// in scratch).  angle(i) yields the state's i-th joint angle — a stored state, or an interpolated
+// one computed on the fly in chain_interp's arithmetic (no state array either).  The same tests
+// in the same arithmetic as chain_valid: identical results.
+template <int NP, class Angle>
+__device__ __forceinline__ bool chain_valid_np(Angle angle, int n, double link, const double *env, int nenv,
+                                               double slack, const double *tab) {
+    double px[NP], py[NP];
+    double theta = 0., x = 0., y = 0., st = 0.0, ct = 1.0;
+    px[0] = 0.;
+    py[0] = 0.;
+#pragma unroll
+    for (int i = 0; i < NP - 2; ++i) {
+        if (i < n) {
+            __builtin_amdgcn_sched_barrier(0);  // one link at a time: no hoisted state loads
+            theta += angle(i);
+            glibc_sincos(theta, st, ct, tab);
+            x = x + ct * link;
+            y = y + st * link;
+        }
+        px[i + 1] = x;  // past n: copies of the last point (never read as a segment)
+        py[i + 1] = y;
+    }
+    if (n == 0) glibc_sincos(theta, st, ct, tab);
+    const double tx = x + ct * 0.001, ty = y + st * 0.001;
+#pragma unroll
+    for (int i = 1; i < NP; ++i)
+        if (i == n + 1) {
+            px[i] = tx;
+            py[i] = ty;
+        }
+    const int ns = n + 1;
+    const double lo_t = kFltEps - slack, hi_t = kFltEps + slack;
+#pragma unroll
+    for (int j = 1; j < NP - 1; ++j) {
+        if (j < ns) {
+            __builtin_amdgcn_sched_barrier(0);  // one segment j at a time (live ranges)
+            const double bx = px[j], by = py[j], vx = px[j + 1] - bx, vy = py[j + 1] - by;
+            double sa = vx * (py[0] - by) - vy * (px[0] - bx);
+#pragma unroll
+            for (int i = 0; i < j; ++i) {
+                const double sb = vx * (py[i + 1] - by) - vy * (px[i + 1] - bx);
+                if (!((sa > hi_t && sb > hi_t) || (sa < lo_t && sb < lo_t)) &&
+                    seg_intersect(px[i], py[i], px[i + 1], py[i + 1], px[j], py[j], px[j + 1], py[j + 1]))
+                    return false;
+                sa = sb;
+            }
+        }
+    }
+    double xmin = 0., xmax = 0., ymin = 0., ymax = 0.;  // point 0 is the origin
+#pragma unroll
+    for (int i = 1; i < NP; ++i) {
+        if (i <= ns) {
+            xmin = fmin(xmin, px[i]);
+            xmax = fmax(xmax, px[i]);
+            ymin = fmin(ymin, py[i]);
+            ymax = fmax(ymax, py[i]);
+        }
+    }
+    for (int j = 0; j < nenv; ++j) {
+        const double bx = env[4 * j], by = env[4 * j + 1], ex = env[4 * j + 2], ey = env[4 * j + 3];
+        const double vx = ex - bx, vy = ey - by;
+        const double y0 = vx * (ymin - by), y1 = vx * (ymax - by), x0 = vy * (xmin - bx), x1 = vy * (xmax - bx);
+        const double smax = fmax(y0, y1) - fmin(x0, x1), smin = fmin(y0, y1) - fmax(x0, x1);
+        if (smin > hi_t || smax < lo_t) continue;
+        double sa = vx * (py[0] - by) - vy * (px[0] - bx);
+#pragma unroll
+        for (int i = 0; i < NP - 1; ++i) {
+            if (i < ns) {
+                const double sb = vx * (py[i + 1] - by) - vy * (px[i + 1] - bx);
+                if (!((sa > hi_t && sb > hi_t) || (sa < lo_t && sb < lo_t)) &&
+                    seg_intersect(px[i], py[i], px[i + 1], py[i + 1], bx, by, ex, ey))
+                    return false;
+                sa = sb;
+            }
+        }
+    }
+    return true;
+}
+
+// chain_interp's coordinate i (demos/KinematicChain.h:150-175), for chain_valid_np
+__host__ __device__ __forceinline__ double chain_interp1(double f, double to, double t) {
+    double diff = to - f;
+    if (fabs(diff) <= kPi) return f + diff * t;
+    if (diff > 0.0)
+        diff = 2.0 * kPi - diff;
+    else
+        diff = -2.0 * kPi - diff;
+    double v = f - diff * t;
+    if (v > kPi)
+        v -= 2.0 * kPi;
+    else if (v < -kPi)
+        v += 2.0 * kPi;
+    return v;
 }
 
 __host__ __device__ inline bool is_valid(const DevSpace &sp, const DevChecker &ck, const double *s,
@@ -295,7 +436,7 @@ __host__ __device__ inline bool is_valid(const DevSpace &sp, const DevChecker &c
     case OMPL_GPU_CHECK_HYPERCUBE: return hypercube_valid(s, ck.ndim, ck.edge);
     case OMPL_GPU_CHECK_SPHERES: return spheres_valid(s, ck.data, ck.count);
     case OMPL_GPU_CHECK_CIRCLES2D: return circles_valid(s, ck.data, ck.count);
-    default: return chain_valid(s, sp.dim, sp.link, ck.data, ck.count, tab);
+    default: return chain_valid(s, sp.dim, sp.link, ck.data, ck.count, ck.slack, tab);
     }
 }
 

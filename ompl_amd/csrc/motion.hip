@@ -144,6 +144,124 @@ __global__ __launch_bounds__(256) __attribute__((flatten, amdgpu_waves_per_eu(8,
     motion_body<0, 0>(sp_in, ck, s1, s2, m, valid, nd_out, fi_out, counters, rot);
 }
 
+// KinematicChain space + KinematicChain checker (the PRM* workload): motion_body's walk with the
+// link endpoints in registers (chain_valid_np, NP >= dim + 2 points) and no state arrays — the
+// endpoints are read from the edge's rows and every sample's angles are interpolated on the fly in
+// chain_interp's arithmetic.  Same order of checks, same counts, same results as motion_body.
+// held to 4 waves per SIMD (128 VGPRs, 64 B of spills); measured per cfg4 batch of motion checks:
+// 2 / 4 / 5 waves 0.80 / 0.63 / 1.37 ms (the runtime form: 1.06 ms; with the side pre-test 1.08 —
+// its state arrays in scratch were the cost); one check site instead of three: 0.70 ms
+template <int NP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void motion_chain_kernel(DevSpace sp, DevChecker ck, const double *__restrict__ s1,
+                                                           const double *__restrict__ s2, uint32_t m,
+                                                           uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out,
+                                                           int32_t *__restrict__ fi_out,
+                                                           unsigned long long *__restrict__ counters) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ double tab[440];  // glibc's sin / cos table, read at lane-dependent points
+    for (int i = threadIdx.x; i < 440; i += blockDim.x) tab[i] = gsc::kSinCosTab[i];
+    __syncthreads();
+    bool result = true;
+    uint32_t checks = 0;
+    if (e < m) {
+        const int n = sp.dim;
+        const double *a = s1 + (size_t)e * n, *b = s2 + (size_t)e * n;
+        ++checks;
+        result = chain_valid_np<NP>([&](int i) { return b[i]; }, n, sp.link, ck.data, ck.count, ck.slack, tab);
+        const int nd = (result || nd_out || fi_out)
+                           ? (int)seg_count(chain_dist_raw(a, b, n, sp.link, tab), sp.lvs0, sp.f0)
+                           : 0;
+        if (nd_out) nd_out[e] = nd;
+        auto sample_valid = [&](int j) {
+            const double t = (double)j / (double)nd;
+            return chain_valid_np<NP>([&](int i) { return chain_interp1(a[i], b[i], t); }, n, sp.link, ck.data,
+                                      ck.count, ck.slack, tab);
+        };
+        if (result && nd >= 2) {  // level-order walk of the FIFO bisection (motion_body)
+            bool any = true;
+            for (int L = 0; any && result && L < 32; ++L) {
+                any = false;
+                const uint32_t np = 1u << L;
+                for (uint32_t p = 0; p < np && result; ++p) {
+                    int lo = 1, hi = nd - 1;
+                    bool empty = false;
+                    for (int bit = L - 1; bit >= 0; --bit) {
+                        const int mid = (lo + hi) / 2;
+                        if ((p >> bit) & 1u)
+                            lo = mid + 1;
+                        else
+                            hi = mid - 1;
+                        if (lo > hi) {
+                            empty = true;
+                            break;
+                        }
+                    }
+                    if (empty) continue;
+                    any = true;
+                    ++checks;
+                    if (!sample_valid((lo + hi) / 2)) result = false;
+                }
+            }
+        }
+        if (valid) valid[e] = result ? 1 : 0;
+        if (fi_out) {
+            int fi = -1;
+            if (!result) {
+                for (int j = 1; j < nd; ++j)
+                    if (!sample_valid(j)) {
+                        fi = j;
+                        break;
+                    }
+                if (fi < 0) fi = nd;
+            }
+            fi_out[e] = fi;
+        }
+    }
+    if (counters) {
+        unsigned long long nv = (e < m && result) ? 1ull : 0ull;
+        unsigned long long ni = (e < m && !result) ? 1ull : 0ull;
+        unsigned long long nc = checks;
+        for (int off = 32; off > 0; off >>= 1) {
+            nv += __shfl_xor(nv, off, 64);
+            ni += __shfl_xor(ni, off, 64);
+            nc += __shfl_xor(nc, off, 64);
+        }
+        __shared__ unsigned long long part[3][4];
+        const int w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) {
+            part[0][w] = nv;
+            part[1][w] = ni;
+            part[2][w] = nc;
+        }
+        __syncthreads();
+        if (threadIdx.x < 3) {
+            unsigned long long v = 0;
+            for (int i = 0; i < (int)(blockDim.x >> 6); ++i) v += part[threadIdx.x][i];
+            if (v) atomicAdd(&counters[threadIdx.x], v);
+        }
+    }
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void state_chain_kernel(DevSpace sp, DevChecker ck, const double *__restrict__ s,
+                                                          uint32_t m, uint8_t *__restrict__ valid) {
+    __shared__ double tab[440];
+    for (int i = threadIdx.x; i < 440; i += blockDim.x) tab[i] = gsc::kSinCosTab[i];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const double *x = s + (size_t)i * sp.dim;
+    valid[i] = chain_valid_np<NP>([&](int j) { return x[j]; }, sp.dim, sp.link, ck.data, ck.count, ck.slack, tab)
+                   ? 1
+                   : 0;
+}
+
+// the register forms' point counts: 14 (up to 12 links, the PRM* benchmark's chain) and 18 (16)
+static int chain_np(const DevSpace &sp, const DevChecker &ck) {
+    if (sp.kind != OMPL_GPU_SPACE_KCHAIN || ck.kind != OMPL_GPU_CHECK_KCHAIN) return 0;
+    return sp.dim <= 12 ? 14 : (sp.dim <= 16 ? 18 : 0);
+}
+
 template <int SP, int DIM>
 __global__ __launch_bounds__(256) __attribute__((flatten)) void state_valid_kernel(
     DevSpace sp_in, DevChecker ck, const double *__restrict__ s, uint32_t m, uint8_t *__restrict__ valid) {
@@ -204,6 +322,17 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
                          uint8_t *valid, int32_t *nd, int32_t *first_invalid, unsigned long long *counters,
                          hipStream_t st) {
     if (m == 0) return hipSuccess;
+    switch (chain_np(sp, ck)) {
+    case 14:
+        hipLaunchKernelGGL(motion_chain_kernel<14>, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid,
+                           nd, first_invalid, counters);
+        return hipGetLastError();
+    case 18:
+        hipLaunchKernelGGL(motion_chain_kernel<18>, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid,
+                           nd, first_invalid, counters);
+        return hipGetLastError();
+    default: break;
+    }
     const int rot = needs_rotation(sp, ck) ? 1 : 0;
     return dispatch_width(sp, ck, [&](auto kind, auto width) {
         if constexpr (decltype(width)::value == 0)
@@ -286,6 +415,15 @@ hipError_t launch_space_pairs(const DevSpace &sp, const double *a, const double 
 hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const double *s, uint32_t m, uint8_t *valid,
                               hipStream_t st) {
     if (m == 0) return hipSuccess;
+    switch (chain_np(sp, ck)) {
+    case 14:
+        hipLaunchKernelGGL(state_chain_kernel<14>, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s, m, valid);
+        return hipGetLastError();
+    case 18:
+        hipLaunchKernelGGL(state_chain_kernel<18>, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s, m, valid);
+        return hipGetLastError();
+    default: break;
+    }
     return dispatch_width(sp, ck, [&](auto kind, auto width) {
         hipLaunchKernelGGL((state_valid_kernel<decltype(kind)::value, decltype(width)::value>), dim3((m + 255) / 256),
                            dim3(256), 0, st, sp, ck, s, m, valid);
