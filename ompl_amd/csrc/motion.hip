@@ -125,12 +125,157 @@ __device__ __forceinline__ void motion_body(DevSpace sp_in, DevChecker ck, const
     }
 }
 
-template <int SP, int DIM>
+// ---- sample-parallel form (the fixed-width spaces) ---------------------------------------------
+// The thread-per-edge walk costs a wave the LONGEST of its 64 edges (nd varies along a vertex's
+// neighbour list), and the sphere field's loop waits on a scalar load per obstacle.  Here a wave
+// takes 64 edges, checks every s2 and nd lane-per-edge, then lays the interior samples of its edges
+// end to end (a wave prefix sum of nd - 1) and checks them 64 at a time, lane-per-sample: the
+// wave's cost is the MEAN segment count.  Every interior sample of an edge whose s2 is valid is
+// checked (no early exit inside an edge), so the result bit is the reference's (valid iff s2 and
+// every sample is), and the two orders of the reference are recovered exactly from the failing
+// samples: the FIFO bisection (:104-134) stops at the failing sample of smallest FIFO rank — the
+// isValid count is 1 + that rank + 1 (fifo_rank below) — and the linear lastValid sweep (:57-69)
+// at the failing sample of smallest index.
+
+// Number of non-empty intervals `d` levels below an interval of s indices in the FIFO bisection
+// (the queue holds only non-empty intervals: `x.first < mid`, `x.second > mid`, :130-133).  An
+// interval of s >= 1 indices has children of floor((s - 1) / 2) and ceil((s - 1) / 2); the sizes of
+// one level take at most two consecutive values, so a level is (v, count of v, count of v + 1).
+__device__ __forceinline__ uint32_t fifo_level_count(uint32_t s, int d) {
+    uint32_t v = s, a = 1, b = 0;
+    for (int i = 0; i < d; ++i) {
+        // children: a intervals of v -> (v - 1) >> 1 and the rest; b of v + 1 -> v >> 1 and the rest
+        const bool ha = v >= 1 && a, hb = b != 0;
+        if (!ha && !hb) return 0;
+        const uint32_t l1 = ha ? (v - 1) >> 1 : 0, h1 = ha ? v - 1 - l1 : 0;
+        const uint32_t l2 = v >> 1, h2 = v - l2;
+        const uint32_t nv = ha ? l1 : l2;  // l1 <= l2: the level's smaller size
+        uint32_t na = 0, nb = 0;
+        if (ha) {
+            na += a;                                  // l1 == nv
+            (h1 == nv ? na : nb) += a;
+        }
+        if (hb) {
+            (l2 == nv ? na : nb) += b;
+            (h2 == nv ? na : nb) += b;
+        }
+        v = nv;
+        a = na;
+        b = nb;
+    }
+    return (v >= 1 ? a : 0) + b;
+}
+
+// 0-based position of interior sample j (1 <= j <= nd - 1) in the reference's FIFO order: every
+// non-empty interval of the levels above j's, plus the non-empty intervals of j's level to the left
+// of it (those below the left siblings of j's right turns)
+__device__ inline uint32_t fifo_rank(int j, int nd) {
+    int lo = 1, hi = nd - 1, L = 0;
+    for (int mid = (lo + hi) / 2; j != mid; mid = (lo + hi) / 2, ++L) {  // j's level
+        if (j > mid) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    uint32_t r = 0;
+    for (int d = 0; d < L; ++d) r += fifo_level_count((uint32_t)(nd - 1), d);
+    lo = 1;
+    hi = nd - 1;
+    for (int d = 0; d < L; ++d) {  // again, adding the left siblings' intervals at j's level
+        const int mid = (lo + hi) / 2;
+        if (j > mid) {
+            r += fifo_level_count((uint32_t)(mid - lo), L - d - 1);
+            lo = mid + 1;
+        } else {
+            hi = mid - 1;
+        }
+    }
+    return r;
+}
+
+// ROT: the interpolation's SO3 part (false when the checker reads only the SE3 translation)
+template <int SP, int DIM, bool ROT>
 __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
     DevSpace sp_in, DevChecker ck, const double *__restrict__ s1, const double *__restrict__ s2, uint32_t m,
     uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out, int32_t *__restrict__ fi_out,
-    unsigned long long *__restrict__ counters, int rot) {
-    motion_body<SP, DIM>(sp_in, ck, s1, s2, m, valid, nd_out, fi_out, counters, rot);
+    unsigned long long *__restrict__ counters) {
+    static_assert(DIM > 0, "the sample-parallel form holds states in registers");
+    const DevSpace sp = fixed_space<SP, DIM>(sp_in);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t wbase = blockIdx.x * blockDim.x + (uint32_t)w * 64, e = wbase + lane;
+    __shared__ int s_off[4][64], s_nd[4][64], s_fj[4][64], s_fr[4][64];
+    bool s2ok = false;
+    int nd = 0;
+    if (e < m) {
+        double a[DIM], b[DIM];
+        load_state<DIM>(s1 + (size_t)e * DIM, DIM, a);
+        load_state<DIM>(s2 + (size_t)e * DIM, DIM, b);
+        s2ok = valid_sp<SP, DIM>(sp, ck, b);  // :96 — s2 first, as the reference
+        nd = (s2ok || nd_out || fi_out) ? (int)valid_segment_count(sp, a, b, gsc::kSinCosTab) : 0;
+        if (nd_out) nd_out[e] = nd;
+    }
+    // interior samples this edge contributes: the FIFO walk's (s2 valid), or the lastValid sweep's
+    const int cnt = (e < m && nd >= 2 && (s2ok || fi_out)) ? nd - 1 : 0;
+    int inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += v;
+    }
+    const int total = __shfl(inc, 63, 64);
+    s_off[w][lane] = inc - cnt;
+    s_nd[w][lane] = nd;
+    s_fj[w][lane] = 0x7FFFFFFF;
+    s_fr[w][lane] = 0x7FFFFFFF;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int k0 = 0; k0 < total; k0 += 64) {
+        const int k = k0 + lane;
+        if (k < total) {
+            int i = 0;  // the last edge whose samples start at or before k (edges with none share it)
+#pragma unroll
+            for (int step = 32; step; step >>= 1)
+                if (s_off[w][i + step] <= k) i += step;
+            const int ndi = s_nd[w][i], j = k - s_off[w][i] + 1;
+            double a[DIM], b[DIM], t[DIM];
+            load_state<DIM>(s1 + (size_t)(wbase + i) * DIM, DIM, a);
+            load_state<DIM>(s2 + (size_t)(wbase + i) * DIM, DIM, b);
+            interpolate(sp, a, b, (double)j / (double)ndi, t, ROT);
+            if (!valid_sp<SP, DIM>(sp, ck, t)) {
+                atomicMin(&s_fj[w][i], j);
+                if (counters) atomicMin(&s_fr[w][i], (int)fifo_rank(j, ndi));
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int fj = s_fj[w][lane], fr = s_fr[w][lane];
+    const bool result = s2ok && fj == 0x7FFFFFFF;
+    if (e < m) {
+        if (valid) valid[e] = result ? 1 : 0;
+        if (fi_out) fi_out[e] = result ? -1 : (fj != 0x7FFFFFFF ? fj : nd);
+    }
+    if (counters) {
+        unsigned long long nv = (e < m && result) ? 1ull : 0ull;
+        unsigned long long ni = (e < m && !result) ? 1ull : 0ull;
+        // isValid calls of the FIFO form: s2, then every interior sample, or up to the failing one
+        unsigned long long nc = e < m ? 1ull + (s2ok ? (fj == 0x7FFFFFFF ? (unsigned)cnt : (unsigned)fr + 1u) : 0u) : 0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            nv += __shfl_xor(nv, off, 64);
+            ni += __shfl_xor(ni, off, 64);
+            nc += __shfl_xor(nc, off, 64);
+        }
+        __shared__ unsigned long long part[3][4];
+        if (lane == 0) {
+            part[0][w] = nv;
+            part[1][w] = ni;
+            part[2][w] = nc;
+        }
+        __syncthreads();
+        if (threadIdx.x < 3) {
+            unsigned long long v = 0;
+            for (int q = 0; q < (int)(blockDim.x >> 6); ++q) v += part[threadIdx.x][q];
+            if (v) atomicAdd(&counters[threadIdx.x], v);
+        }
+    }
 }
 
 // the runtime-width form (the KinematicChain's): held to 64 VGPRs for 8 waves per SIMD — its fp64
@@ -242,6 +387,122 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
 }
 
+// Interior sample of FIFO rank r (0-based) of a motion of nd segments: the inverse of fifo_rank —
+// r's level by the levels' interval counts, then a descent that keeps r's position among that
+// level's intervals
+__device__ inline int fifo_sample(uint32_t r, int nd) {
+    const uint32_t S = (uint32_t)(nd - 1);
+    int L = 0;
+    for (uint32_t n = fifo_level_count(S, 0); r >= n; n = fifo_level_count(S, ++L)) r -= n;
+    int lo = 1, hi = nd - 1;
+    for (int d = 0; d < L; ++d) {
+        const int mid = (lo + hi) / 2;
+        const uint32_t nl = fifo_level_count((uint32_t)(mid - lo), L - d - 1);
+        if (r < nl) {
+            hi = mid - 1;
+        } else {
+            r -= nl;
+            lo = mid + 1;
+        }
+    }
+    return (lo + hi) / 2;
+}
+
+// The KinematicChain motion (cfg4's PRM* edges, about half of them invalid) as a compacted FIFO
+// walk: a wave takes 64 edges and, 64 samples at a time, hands its lanes the next pending samples
+// in (FIFO rank, edge) order — rank 0 of every live edge, then rank 1, ... — so every lane checks a
+// sample of some live edge instead of idling behind the wave's longest edge, and an edge stops
+// taking samples once one fails (samples of a higher rank already handed out in the same round are
+// the only extra checks).  Every rank below an edge's first failure is checked before it, so the
+// failure of smallest rank — the reference's stopping point (:122-126) — and the isValid count
+// (1 + that rank + 1) are exact.  The lastValid sweep (fi_out) takes motion_chain_kernel.
+template <int NP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void motion_chain_pool_kernel(
+    DevSpace sp, DevChecker ck, const double *__restrict__ s1, const double *__restrict__ s2, uint32_t m,
+    uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out, unsigned long long *__restrict__ counters) {
+    __shared__ double tab[440];  // glibc's sin / cos table, read at lane-dependent points
+    __shared__ int s_nd[4][64], s_fr[4][64], s_se[4][64], s_sr[4][64];
+    for (int i = threadIdx.x; i < 440; i += blockDim.x) tab[i] = gsc::kSinCosTab[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t wbase = blockIdx.x * blockDim.x + (uint32_t)w * 64, e = wbase + lane;
+    const int n = sp.dim;
+    bool s2ok = false;
+    int nd = 0;
+    if (e < m) {
+        const double *a = s1 + (size_t)e * n, *b = s2 + (size_t)e * n;
+        s2ok = chain_valid_np<NP>([&](int i) { return b[i]; }, n, sp.link, ck.data, ck.count, ck.slack, tab);
+        nd = (s2ok || nd_out) ? (int)seg_count(chain_dist_raw(a, b, n, sp.link, tab), sp.lvs0, sp.f0) : 0;
+        if (nd_out) nd_out[e] = nd;
+    }
+    const int cnt = (s2ok && nd >= 2) ? nd - 1 : 0;  // interior samples of the FIFO walk
+    int next = 0;                                      // this edge's next rank to hand out
+    bool live = cnt > 0;
+    s_nd[w][lane] = nd;
+    s_fr[w][lane] = 0x7FFFFFFF;
+    __builtin_amdgcn_wave_barrier();
+    while (__ballot(live)) {
+        // hand out up to 64 (edge, rank) pairs in (rank, edge) order: the live edges hold ranks
+        // rho or rho + 1 (the order's frontier), so rank by rank from the smallest
+        int rho = live ? next : 0x7FFFFFFF;
+#pragma unroll
+        for (int o = 32; o; o >>= 1) rho = min(rho, __shfl_xor(rho, o, 64));
+        int used = 0;
+        for (;;) {
+            const bool elig = live && next == rho && rho < cnt;
+            const uint64_t em = __ballot(elig);
+            if (!em) break;  // no live edge has rank rho left (ranks only grow)
+            const int ne = __popcll(em), take = min(ne, 64 - used);
+            const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0));
+            if (elig && pos < take) {
+                s_se[w][used + pos] = lane;
+                s_sr[w][used + pos] = rho;
+                next = rho + 1;
+            }
+            used += take;
+            if (used == 64) break;
+            ++rho;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < used) {
+            const int i = s_se[w][lane], r = s_sr[w][lane], ndi = s_nd[w][i];
+            const double *a = s1 + (size_t)(wbase + i) * n, *b = s2 + (size_t)(wbase + i) * n;
+            const double t = (double)fifo_sample((uint32_t)r, ndi) / (double)ndi;
+            if (!chain_valid_np<NP>([&](int c) { return chain_interp1(a[c], b[c], t); }, n, sp.link, ck.data,
+                                    ck.count, ck.slack, tab))
+                atomicMin(&s_fr[w][i], r);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (live && (s_fr[w][lane] != 0x7FFFFFFF || next >= cnt)) live = false;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int fr = s_fr[w][lane];
+    const bool result = s2ok && fr == 0x7FFFFFFF;
+    if (e < m && valid) valid[e] = result ? 1 : 0;
+    if (counters) {
+        unsigned long long nv = (e < m && result) ? 1ull : 0ull;
+        unsigned long long ni = (e < m && !result) ? 1ull : 0ull;
+        unsigned long long nc = e < m ? 1ull + (s2ok ? (fr == 0x7FFFFFFF ? (unsigned)cnt : (unsigned)fr + 1u) : 0u) : 0ull;
+        for (int off = 32; off > 0; off >>= 1) {
+            nv += __shfl_xor(nv, off, 64);
+            ni += __shfl_xor(ni, off, 64);
+            nc += __shfl_xor(nc, off, 64);
+        }
+        __shared__ unsigned long long part[3][4];
+        if (lane == 0) {
+            part[0][w] = nv;
+            part[1][w] = ni;
+            part[2][w] = nc;
+        }
+        __syncthreads();
+        if (threadIdx.x < 3) {
+            unsigned long long v = 0;
+            for (int q = 0; q < (int)(blockDim.x >> 6); ++q) v += part[threadIdx.x][q];
+            if (v) atomicAdd(&counters[threadIdx.x], v);
+        }
+    }
+}
+
 template <int NP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void state_chain_kernel(DevSpace sp, DevChecker ck, const double *__restrict__ s,
                                                           uint32_t m, uint8_t *__restrict__ valid) {
@@ -322,7 +583,15 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
                          uint8_t *valid, int32_t *nd, int32_t *first_invalid, unsigned long long *counters,
                          hipStream_t st) {
     if (m == 0) return hipSuccess;
-    switch (chain_np(sp, ck)) {
+    switch (chain_np(sp, ck) * (first_invalid ? 1 : -1)) {
+    case -14:
+        hipLaunchKernelGGL(motion_chain_pool_kernel<14>, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m,
+                           valid, nd, counters);
+        return hipGetLastError();
+    case -18:
+        hipLaunchKernelGGL(motion_chain_pool_kernel<18>, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m,
+                           valid, nd, counters);
+        return hipGetLastError();
     case 14:
         hipLaunchKernelGGL(motion_chain_kernel<14>, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid,
                            nd, first_invalid, counters);
@@ -338,9 +607,14 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
         if constexpr (decltype(width)::value == 0)
             hipLaunchKernelGGL(motion_rt_kernel, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd,
                                first_invalid, counters, rot);
+        else if (rot)
+            hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value, true>),
+                               dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd, first_invalid,
+                               counters);
         else
-            hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value>), dim3((m + 255) / 256),
-                               dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd, first_invalid, counters, rot);
+            hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value, false>),
+                               dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd, first_invalid,
+                               counters);
         return hipGetLastError();
     });
 }
