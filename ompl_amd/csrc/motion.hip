@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "feat_dist.h"
 #include "kernels.h"
 
 namespace ompl_amd {
@@ -191,6 +192,68 @@ __device__ inline uint32_t fifo_rank(int j, int nd) {
     return r;
 }
 
+// Sphere field on packed fp32, certified.  The reference test is fp64: dx*dx + dy*dy + dz*dz < r^2
+// with dx = c_x - s_x (device_space.h spheres_valid).  Here a pair of spheres is screened per packed
+// instruction from fp32 copies in LDS: c32 = fl32(c), r_hi = fl32(r^2 (1 + 2^-21)) >= r^2, s32 =
+// fl32(s).  With u = 2^-24 and B >= |c_i| + |s_i| for every coordinate, each fp32 difference is
+// within 2.01 u B of the exact one, so the fp32 sum of squares (one rounded product, two fmas) is
+// within 3.01 u 3 B^2 + 3 (2 B 2.01 u B + (2.01 u B)^2) <= 21.2 u B^2 of the exact sum, which the
+// fp64 sum matches to 4e-16 relative: g = fl32(D32 - r_hi) > E = 48 u B^2 proves D64 >= r^2 — the
+// sphere does not contain s.  When every sphere's g clears E the state is valid; otherwise (a
+// state inside or within E of a sphere) the exact fp64 test decides.  NaN / huge states fail the
+// screen (NaN or infinite E) and take the fp64 test too.
+constexpr int kLdsSpheres = 128;  // spheres staged in LDS (more: the fp64 test alone)
+struct SphereScreen {
+    float4 c[kLdsSpheres / 2][2];  // pair p: {cx_0, cx_1, cy_0, cy_1}, {cz_0, cz_1, rhi_0, rhi_1}
+    float mc;                      // >= every |centre coordinate| (rounded up)
+};
+
+__device__ __forceinline__ void stage_spheres(SphereScreen &ss, const double *__restrict__ c, int count) {
+    unsigned int *mcb = reinterpret_cast<unsigned int *>(&ss.mc);
+    if (threadIdx.x == 0) *mcb = 0u;
+    __syncthreads();
+    float mloc = 0.f;
+    for (int i = threadIdx.x; i < kLdsSpheres; i += blockDim.x) {
+        float x = 0.f, y = 0.f, z = 0.f, rh = -__builtin_inff();  // padding: never contains a state
+        if (i < count) {
+            x = (float)c[4 * i];
+            y = (float)c[4 * i + 1];
+            z = (float)c[4 * i + 2];
+            rh = (float)(c[4 * i + 3] * (1.0 + 0x1p-21));
+            mloc = fmaxf(mloc, fmaxf(fabsf(x), fmaxf(fabsf(y), fabsf(z))));
+        }
+        float *q = reinterpret_cast<float *>(&ss.c[i >> 1][0]);
+        const int h = i & 1;
+        q[0 + h] = x;
+        q[2 + h] = y;
+        q[4 + h] = z;
+        q[6 + h] = rh;
+    }
+    // |c| <= fl32(|c|) (1 + u): round the bound up by 2^-20 (non-negative floats order as integers)
+    atomicMax(mcb, __float_as_uint(mloc * (1.f + 0x1p-20f)));
+    __syncthreads();
+}
+
+// false: some sphere may contain s (the caller runs the exact test); true: no sphere contains s
+__device__ __forceinline__ bool spheres_clear32(const double *s, const SphereScreen &ss, int count) {
+    const float x = (float)s[0], y = (float)s[1], z = (float)s[2];
+    const float b = (ss.mc + fmaxf(fabsf(x), fmaxf(fabsf(y), fabsf(z)))) * (1.f + 0x1p-20f);
+    const float E = 48.f * 0x1p-24f * b * b;
+    const f2 nx = f2{-x, -x}, ny = f2{-y, -y}, nz = f2{-z, -z};
+    float gmin = __builtin_inff();
+#pragma unroll 2
+    for (int p = 0; p < (count + 1) >> 1; ++p) {
+        const float4 a = ss.c[p][0], q = ss.c[p][1];
+        const f2 dx = f2{a.x, a.y} + nx, dy = f2{a.z, a.w} + ny, dz = f2{q.x, q.y} + nz;
+        f2 d2 = dx * dx;
+        d2 = pk_fma(dy, dy, d2);
+        d2 = pk_fma(dz, dz, d2);
+        const f2 g = d2 - f2{q.z, q.w};
+        gmin = fminf(gmin, fminf(g.x, g.y));  // (a NaN g is dropped: the fp64 test of a NaN state passes too)
+    }
+    return gmin > E;
+}
+
 // ROT: the interpolation's SO3 part (false when the checker reads only the SE3 translation)
 template <int SP, int DIM, bool ROT>
 __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
@@ -202,6 +265,11 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t wbase = blockIdx.x * blockDim.x + (uint32_t)w * 64, e = wbase + lane;
     __shared__ int s_off[4][64], s_nd[4][64], s_fj[4][64], s_fr[4][64];
+    // the sphere field's screen (the SE3 translation / the first three reals)
+    constexpr bool kSph = (SP == OMPL_GPU_SPACE_SE3 || SP == OMPL_GPU_SPACE_REALVECTOR) && DIM >= 3;
+    __shared__ SphereScreen ss;
+    const bool sph = kSph && ck.kind == OMPL_GPU_CHECK_SPHERES && ck.count <= kLdsSpheres;
+    if (sph) stage_spheres(ss, ck.data, ck.count);
     bool s2ok = false;
     int nd = 0;
     if (e < m) {
@@ -239,7 +307,7 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
             load_state<DIM>(s1 + (size_t)(wbase + i) * DIM, DIM, a);
             load_state<DIM>(s2 + (size_t)(wbase + i) * DIM, DIM, b);
             interpolate(sp, a, b, (double)j / (double)ndi, t, ROT);
-            if (!valid_sp<SP, DIM>(sp, ck, t)) {
+            if (!(sph && spheres_clear32(t, ss, ck.count)) && !valid_sp<SP, DIM>(sp, ck, t)) {
                 atomicMin(&s_fj[w][i], j);
                 if (counters) atomicMin(&s_fr[w][i], (int)fifo_rank(j, ndi));
             }

@@ -134,3 +134,70 @@ def test_motion_states_count_limit(gpu):
     for count in (0xFFFFFFFE, 0xFFFFFFFF):
         st = abi.lib.ompl_gpu_mv_motion_states(mv._h, abi.dptr(a), abi.dptr(a), 1, count, 1, abi.dptr(out))
         assert st == abi.ERR_INVALID_ARG
+
+
+@pytest.mark.parametrize("name", ["se3_hypercube", "se3_spheres", "r6_hypercube", "chain12_horn", "r2_circles"])
+def test_motion_golden_bench_path(gpu, golden, name):
+    """The planner / bench call (no nd, no first-invalid): the lane-per-sample kernels (fixed widths:
+    samples laid end to end; KinematicChain: the compacted FIFO walk) give the golden validity bits
+    and the FIFO bisection's isValid-call count (DiscreteMotionValidator.cpp:93-145)."""
+    g = golden(f"motion_{name}.npz")
+    sp, ck = _case(name, golden)
+    mv = DiscreteMotionValidatorGPU(sp, ck, gpu)
+    np.testing.assert_array_equal(mv.checkMotions(g["s1"], g["s2"]), g["valid"])
+    assert mv.stateChecks() == int(g["checks"])
+    mv2 = DiscreteMotionValidatorGPU(sp, ck, gpu)
+    valid, nd = mv2.checkMotions(g["s1"], g["s2"], want_nd=True)
+    np.testing.assert_array_equal(valid, g["valid"])
+    np.testing.assert_array_equal(nd, g["nd"])
+    assert mv2.stateChecks() == int(g["checks"])
+
+
+def test_chain_motion_random_vs_oracle(gpu):
+    """KinematicChain motions (PRM*'s, about half invalid) through the compacted FIFO walk: bits and
+    the isValid count equal the oracle's FIFO bisection; long edges (many samples per edge, few live
+    edges per wave) included."""
+    rng = np.random.default_rng(23)
+    sp = KinematicChainSpace(12, 1.0 / 12)
+    ck = KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))
+    a = W.uniform_chain(rng, 60000, 12)
+    b = a + rng.normal(scale=0.05, size=a.shape) * rng.integers(1, 20, size=(len(a), 1))
+    b = np.mod(b + np.pi, 2 * np.pi) - np.pi
+    ok = O.is_valid(sp, ck, a)
+    a, b = a[ok], b[ok]
+    mv = DiscreteMotionValidatorGPU(sp, ck, gpu)
+    valid = mv.checkMotions(a, b)
+    ov, ond, _, checks = O.check_motions(sp, ck, a, b)
+    np.testing.assert_array_equal(valid, ov)
+    assert mv.stateChecks() == checks
+    assert 0.2 < ov.mean() < 0.9 and ond.max() >= 32
+
+
+def test_sphere_screen_knife_edge(gpu):
+    """Interior samples within ~1e-9 .. 1e-5 (relative) of a sphere surface: the packed fp32 sphere
+    screen must hand every ambiguous sample to the fp64 test, so bits and counts equal the oracle's."""
+    rng = np.random.default_rng(24)
+    sp = SE3StateSpace()
+    c, r = W.sphere_field(32, 0.1, 7)
+    ck = SpheresChecker(c, r)
+    n = 40000
+    k = rng.integers(0, len(c), n)
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    delta = rng.choice([-1e-5, -1e-7, -1e-9, 0.0, 1e-9, 1e-7, 1e-5], n)
+    m = c[k] + u * (r[k] * (1 + delta))[:, None]           # a point at the surface (+- delta)
+    tng = np.cross(u, rng.normal(size=(n, 3)))
+    tng /= np.linalg.norm(tng, axis=1, keepdims=True)
+    half = (0.02 + 0.08 * rng.random(n))[:, None] * tng
+    q = W.uniform_se3(rng, n)[:, 3:]
+    s1 = np.hstack([m - half, q])
+    s2 = np.hstack([m + half, q])                           # the t = 1/2 sample sits on m
+    mv = DiscreteMotionValidatorGPU(sp, ck, gpu)
+    valid = mv.checkMotions(s1, s2)
+    ov, ond, ofi, checks = O.check_motions(sp, ck, s1, s2)
+    np.testing.assert_array_equal(valid, ov)
+    assert mv.stateChecks() == checks
+    v2, nd, fi = DiscreteMotionValidatorGPU(sp, ck, gpu).checkMotions(s1, s2, want_nd=True, want_first_invalid=True)
+    np.testing.assert_array_equal(v2, ov)
+    np.testing.assert_array_equal(nd, ond)
+    np.testing.assert_array_equal(fi, ofi)
