@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest $tests -m gpu -x -q -p no:cacheprovider --
 rc=$?
 tail -2 "$out/pytest.log"
 [ $rc -eq 0 ] || { grep -n "FAIL\|Error\|error" "$out/pytest.log" | head -30; exit 1; }
-for w in cfg5k cfg5 cfg4 cfg3; do
+for w in ${WLS:-cfg5k cfg5 cfg4 cfg3}; do
   extra=""; wl=$w
   [ $w = cfg5k ] && { extra="--bitstar-knn"; wl=cfg5; }
   timeout -k 10 300 python -u bench.py --workload $wl $extra --steps 20 --warmup 5 --workloads none --no-extras --single-query-reps 0 \
