@@ -845,15 +845,14 @@ class Runner:
         elif a.workload == "cfg4":           # PRM: checkMotion(state[n], state[m])  PRM.cpp:582
             nn.edges_device(q, self.nq, None, self.ids.data_ptr(), self.k, self.m, False, self.s_from.data_ptr(),
                             self.s_to.data_ptr())
-        elif self.k:                         # BIT* kNN mode: checkMotion(vertex, sample)  BITstar.cpp:815
-            nn.edges_device(q, self.nq, None, self.ids.data_ptr(), self.k, self.m, True, self.s_from.data_ptr(),
-                            self.s_to.data_ptr())
-        else:                                # BIT*: checkMotion(vertex, sample)  BITstar.cpp:815
-            nn.edges_device(q, self.nq, self.off.data_ptr(), self.ids.data_ptr(), 0, self.m, True,
-                            self.s_from.data_ptr(), self.s_to.data_ptr())
+        # BIT* (cfg5, both modes): checkMotion(vertex, sample) (BITstar.cpp:815) over the neighbour
+        # result's edges read in place (ompl_gpu_mv_check_edges_device: no endpoint rows written)
         if e:
             e[2].record(self.stream)
-        if a.workload != "cfg2":
+        if a.workload == "cfg5":
+            mv.check_edges_device(nn, q, self.nq, None if self.k else self.off.data_ptr(), self.ids.data_ptr(),
+                                  self.k, self.m, True, self.valid.data_ptr())
+        elif a.workload != "cfg2":
             mv.check_device(self.s_from.data_ptr(), self.s_to.data_ptr(), self.m, self.valid.data_ptr())
         if e:
             e[3].record(self.stream)

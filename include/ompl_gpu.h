@@ -45,6 +45,8 @@
  *   ompl_gpu_csr_merge_device  per-shard nearestR CSR results -> one CSR (tree-sharded mode)
  *   ompl_gpu_nn_edges_device  the edges PRM / BIT* check after a neighbour query
  *                          prm/src/PRM.cpp:577-582, informedtrees/src/BITstar.cpp:815
+ *   ompl_gpu_mv_check_edges_device  checkMotion over those edges, read in place
+ *                          BITstar.cpp:815, PRM.cpp:582, DiscreteMotionValidator.cpp:93-145
  *
  * Distances are the reference's fp64 formulas in the reference's operation
  * order (StateSpace.cpp:1068-1076, RealVectorStateSpace.cpp:230-242,
@@ -263,6 +265,18 @@ ompl_gpu_status ompl_gpu_mv_check(ompl_gpu_mv *h, const double *s1, const double
                                   uint8_t *valid, int32_t *nd, int32_t *first_invalid);
 ompl_gpu_status ompl_gpu_mv_check_device(ompl_gpu_mv *h, const double *d_s1, const double *d_s2, size_t m,
                                          uint8_t *d_valid, int32_t *d_nd, int32_t *d_first_invalid);
+/* checkMotion over the edges of a neighbour result, without materialising them: edge e is the pair
+ * ompl_gpu_nn_edges_device(nn, ...) would write (the same d_queries / d_offsets / d_ids / stride /
+ * from_query meaning), read in place from the query rows and the stored states of nn —
+ * BITstar.cpp:815 checkMotion(vertex, sample), PRM.cpp:582 checkMotion(state[n], state[m]).
+ * d_valid[e] and the counters as ompl_gpu_mv_check_device; an edge past the last CSR segment
+ * (e >= d_offsets[nq]) reports 0 and is not counted.  Runs on the validator's stream, after the
+ * work queued on nn's stream; asynchronous.  Spaces / checkers without a fixed-width motion form
+ * (the KinematicChain, R^n other than 2 / 3 / 6) materialise the pairs in the validator's scratch
+ * (that form reads d_offsets[nq] back: it synchronises). */
+ompl_gpu_status ompl_gpu_mv_check_edges_device(ompl_gpu_mv *mv, ompl_gpu_nn *nn, const double *d_queries, size_t nq,
+                                               const uint64_t *d_offsets, const uint32_t *d_ids, uint32_t stride,
+                                               size_t m, int from_query, uint8_t *d_valid);
 ompl_gpu_status ompl_gpu_mv_counters(ompl_gpu_mv *h, uint64_t *valid, uint64_t *invalid);
 ompl_gpu_status ompl_gpu_mv_reset_counters(ompl_gpu_mv *h);
 /* total isValid() evaluations the bisection variant made (the reference's work). */

@@ -140,6 +140,7 @@ SIGNATURES = {
     "ompl_gpu_mv_sync": (C.c_int, [_P]),
     "ompl_gpu_mv_check": (C.c_int, [_P, _D, _D, C.c_size_t, _U8, _I32, _I32]),
     "ompl_gpu_mv_check_device": (C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, _P]),
+    "ompl_gpu_mv_check_edges_device": (C.c_int, [_P, _P, _P, C.c_size_t, _P, _P, C.c_uint32, C.c_size_t, C.c_int, _P]),
     "ompl_gpu_mv_counters": (C.c_int, [_P, _U64, _U64]),
     "ompl_gpu_mv_reset_counters": (C.c_int, [_P]),
     "ompl_gpu_mv_state_checks": (C.c_int, [_P, _U64]),

@@ -1327,6 +1327,73 @@ ompl_gpu_status ompl_gpu_mv_check_device(ompl_gpu_mv *h, const double *d_s1, con
     return OMPL_GPU_OK;
 }
 
+ompl_gpu_status ompl_gpu_mv_check_edges_device(ompl_gpu_mv *mv, ompl_gpu_nn *nn, const double *d_queries, size_t nq,
+                                               const uint64_t *d_offsets, const uint32_t *d_ids, uint32_t stride,
+                                               size_t m, int from_query, uint8_t *d_valid) {
+    if (!mv || !nn || (m && (!d_queries || !d_ids || !d_valid))) return fail(OMPL_GPU_ERR_INVALID_ARG, "NULL argument");
+    if (!d_offsets && m && (stride == 0 || m != nq * (size_t)stride))
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "dense neighbour ids need m == nq * stride");
+    if (mv->sp.kind != nn->sp.kind || mv->sp.dim != nn->sp.dim)
+        return fail(OMPL_GPU_ERR_INVALID_ARG, "validator and neighbour structure differ in space");
+    if (mv->device != nn->device) return fail(OMPL_GPU_ERR_INVALID_ARG, "validator and neighbour structure on different devices");
+    std::scoped_lock lk(nn->mu, mv->mu);
+    if (m == 0) return OMPL_GPU_OK;
+    if (nq == 0 || nq > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_INVALID_ARG, "query count out of range");
+    if (m > 0xFFFFFFFFull) return fail(OMPL_GPU_ERR_UNSUPPORTED, "too many edges in one call");
+    HIP_OR_FAIL(hipSetDevice(mv->device));
+    const int da = aos_width(nn);
+    if (nn->n_total) {
+        ompl_gpu_status s = ensure_aos(nn);
+        if (s != OMPL_GPU_OK) return s;
+    }
+    uint32_t *qidx = nullptr;
+    if (d_offsets) {
+        HIP_OR_FAIL(nn->edge_q.ensure(sizeof(uint32_t) * m));
+        qidx = (uint32_t *)nn->edge_q.p;
+    }
+    // the work already queued on nn's stream (the neighbour query, the AoS rows, the CSR segments)
+    // before the validator's stream reads it
+    auto order_after_nn = [&]() -> hipError_t {
+        if (nn->stream == mv->stream) return hipSuccess;
+        hipEvent_t ev;
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+        if ((e = hipEventRecord(ev, nn->stream)) == hipSuccess) e = hipStreamWaitEvent(mv->stream, ev, 0);
+        const hipError_t d = hipEventDestroy(ev);
+        return e != hipSuccess ? e : d;
+    };
+    const double *aos = nn->n_total ? (const double *)nn->raw_aos.p : nullptr;
+    if (qidx) HIP_OR_FAIL(launch_edge_query(d_offsets, (uint32_t)nq, (uint64_t)m, qidx, nn->stream));
+    HIP_OR_FAIL(order_after_nn());
+    hipError_t e = aos ? launch_motion_edges(mv->sp, mv->ck, d_queries, qidx, d_ids, stride, from_query, aos, da,
+                                             (uint32_t)m, d_valid, mv->counters, mv->stream)
+                       : hipErrorNotSupported;
+    if (e == hipErrorNotSupported) {  // no fixed-width form (or an empty structure): materialise the pairs
+        (void)hipGetLastError();
+        size_t me = m;  // a CSR's existing edges: e < offsets[nq] (read back: this form synchronises)
+        if (d_offsets) {
+            uint64_t tot = 0;
+            HIP_OR_FAIL(hipMemcpyAsync(&tot, d_offsets + nq, sizeof(tot), hipMemcpyDeviceToHost, nn->stream));
+            HIP_OR_FAIL(hipStreamSynchronize(nn->stream));
+            me = std::min<size_t>(m, tot);
+            if (me < m) HIP_OR_FAIL(hipMemsetAsync(d_valid + me, 0, m - me, mv->stream));
+            if (me == 0) return OMPL_GPU_OK;
+        }
+        m = me;
+        const size_t bytes = sizeof(double) * m * mv->sp.dim;
+        HIP_OR_FAIL(mv->s1.ensure(bytes));
+        HIP_OR_FAIL(mv->s2.ensure(bytes));
+        HIP_OR_FAIL(launch_edges(nn->sp, nn->raw, nn->cap, d_queries, (uint32_t)nq, d_offsets, d_ids, stride, m,
+                                 from_query, (double *)mv->s1.p, (double *)mv->s2.p, nn->stream, aos, da, qidx));
+        HIP_OR_FAIL(order_after_nn());
+        HIP_OR_FAIL(launch_motion(mv->sp, mv->ck, (const double *)mv->s1.p, (const double *)mv->s2.p, (uint32_t)m,
+                                  d_valid, nullptr, nullptr, mv->counters, mv->stream));
+        return OMPL_GPU_OK;
+    }
+    HIP_OR_FAIL(e);
+    return OMPL_GPU_OK;
+}
+
 ompl_gpu_status ompl_gpu_mv_counters(ompl_gpu_mv *h, uint64_t *valid, uint64_t *invalid) {
     if (!h) return fail(OMPL_GPU_ERR_INVALID_ARG, "handle is NULL");
     std::lock_guard<std::mutex> lk(h->mu);

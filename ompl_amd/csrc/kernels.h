@@ -260,6 +260,8 @@ hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_
 // motion endpoints of neighbour results: edge e pairs query q with stored state ids[e]
 // (CSR offsets, or offsets == nullptr and e = q * stride + j)
 // aos (optional): [n][da] copy of the raw states (launch_aos_rows), read instead of the SoA store
+// the CSR segment (query) of every edge e < m: qidx[e] (kNoId past offsets[nq])
+hipError_t launch_edge_query(const uint64_t *offsets, uint32_t nq, uint64_t m, uint32_t *qidx, hipStream_t st);
 hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
                         const uint64_t *offsets, const uint32_t *ids, uint32_t stride, uint64_t m, int from_query,
                         double *from, double *to, hipStream_t st, const double *aos, int da, uint32_t *qidx);
@@ -377,6 +379,11 @@ hipError_t launch_steer(const DevSpace &sp, const double *raw_soa, uint64_t cap,
 hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double *s1, const double *s2, uint32_t m,
                          uint8_t *valid, int32_t *nd, int32_t *first_invalid, unsigned long long *counters,
                          hipStream_t st);
+// the edges of a neighbour query (launch_edges' pairs) checked without materialising them; returns
+// hipErrorNotSupported for a space / checker without a fixed-width motion form
+hipError_t launch_motion_edges(const DevSpace &sp, const DevChecker &ck, const double *q, const uint32_t *qidx,
+                               const uint32_t *ids, uint32_t stride, int from_query, const double *aos, int da,
+                               uint32_t m, uint8_t *valid, unsigned long long *counters, hipStream_t st);
 hipError_t launch_state_valid(const DevSpace &sp, const DevChecker &ck, const double *s, uint32_t m, uint8_t *valid,
                               hipStream_t st);
 // getMotionStates: states per motion (SpaceInformation.cpp:201-275 with alloc = true)

@@ -834,6 +834,13 @@ __global__ void edges_copy_kernel(const double *__restrict__ raw, uint64_t cap, 
     (from_query ? to : from)[t] = id == kNoId ? qv : (aos ? aos[(uint64_t)id * da + c] : raw[(uint64_t)c * cap + id]);
 }
 
+hipError_t launch_edge_query(const uint64_t *offsets, uint32_t nq, uint64_t m, uint32_t *qidx, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(edge_query_kernel, dim3(std::min<uint32_t>(nq / 4 + 1, 8192)), dim3(256), 0, st, offsets, nq, m,
+                       qidx);
+    return hipGetLastError();
+}
+
 hipError_t launch_edges(const DevSpace &sp, const double *raw, uint64_t cap, const double *q, uint32_t nq,
                         const uint64_t *offsets, const uint32_t *ids, uint32_t stride, uint64_t m, int from_query,
                         double *from, double *to, hipStream_t st, const double *aos, int da, uint32_t *qidx) {

@@ -17,6 +17,7 @@
 
 #include "feat_dist.h"
 #include "kernels.h"
+#include "topk.h"
 
 namespace ompl_amd {
 
@@ -254,12 +255,45 @@ __device__ __forceinline__ bool spheres_clear32(const double *s, const SphereScr
     return gmin > E;
 }
 
+// Endpoint sources of the sample-parallel kernel.  PairSrc: the caller's rows s1[e], s2[e]
+// (ompl_gpu_mv_check_device).  EdgeSrc: the edges of a neighbour query read where they live —
+// the query row and the stored state's AoS row by id (ompl_gpu_mv_check_edges_device), the pairs
+// edges_copy_kernel would have materialised: a missing neighbour (kNoId) is the zero-length motion
+// from the query to itself; an edge past the last CSR segment does not exist.
+struct PairSrc {
+    const double *s1, *s2;
+    template <int DIM>
+    __device__ __forceinline__ bool load(uint32_t e, double (&a)[DIM], double (&b)[DIM]) const {
+        load_state<DIM>(s1 + (size_t)e * DIM, DIM, a);
+        load_state<DIM>(s2 + (size_t)e * DIM, DIM, b);
+        return true;
+    }
+};
+struct EdgeSrc {
+    const double *q;       // [nq][DIM] query rows
+    const uint32_t *qidx;  // CSR: the query of each edge (kNoId past the last segment); null: e / stride
+    const uint32_t *ids;   // [m] neighbour ids (kNoId: none)
+    uint32_t stride;
+    int from_query;        // 1: checkMotion(query, neighbour), 0: checkMotion(neighbour, query)
+    const double *aos;     // stored states by id, rows of da reals
+    int da;
+    template <int DIM>
+    __device__ __forceinline__ bool load(uint32_t e, double (&a)[DIM], double (&b)[DIM]) const {
+        const uint32_t qi = qidx ? qidx[e] : e / stride;
+        if (qi == kNoId) return false;
+        const uint32_t id = ids[e];
+        const double *qr = q + (size_t)qi * DIM, *sr = id == kNoId ? qr : aos + (size_t)id * da;
+        load_state<DIM>(from_query ? qr : sr, DIM, a);
+        load_state<DIM>(from_query ? sr : qr, DIM, b);
+        return true;
+    }
+};
+
 // ROT: the interpolation's SO3 part (false when the checker reads only the SE3 translation)
-template <int SP, int DIM, bool ROT>
+template <int SP, int DIM, bool ROT, class Src>
 __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
-    DevSpace sp_in, DevChecker ck, const double *__restrict__ s1, const double *__restrict__ s2, uint32_t m,
-    uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out, int32_t *__restrict__ fi_out,
-    unsigned long long *__restrict__ counters) {
+    DevSpace sp_in, DevChecker ck, Src src, uint32_t m, uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out,
+    int32_t *__restrict__ fi_out, unsigned long long *__restrict__ counters) {
     static_assert(DIM > 0, "the sample-parallel form holds states in registers");
     const DevSpace sp = fixed_space<SP, DIM>(sp_in);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -270,18 +304,27 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
     __shared__ SphereScreen ss;
     const bool sph = kSph && ck.kind == OMPL_GPU_CHECK_SPHERES && ck.count <= kLdsSpheres;
     if (sph) stage_spheres(ss, ck.data, ck.count);
-    bool s2ok = false;
+    bool s2ok = false, has = false;
     int nd = 0;
-    if (e < m) {
-        double a[DIM], b[DIM];
-        load_state<DIM>(s1 + (size_t)e * DIM, DIM, a);
-        load_state<DIM>(s2 + (size_t)e * DIM, DIM, b);
+    double a[DIM], b[DIM];
+    if (e < m) has = src.template load<DIM>(e, a, b);
+    if (has) {
         s2ok = valid_sp<SP, DIM>(sp, ck, b);  // :96 — s2 first, as the reference
         nd = (s2ok || nd_out || fi_out) ? (int)valid_segment_count(sp, a, b, gsc::kSinCosTab) : 0;
         if (nd_out) nd_out[e] = nd;
     }
+    // the coordinates the samples need (the SE3 translation alone when the checker reads only it),
+    // kept per wave in LDS: the sample lanes read their edge's endpoints from there, not again from
+    // the rows (for EdgeSrc, a query row and a stored row by id)
+    constexpr int NL = (SP == OMPL_GPU_SPACE_SE3 && !ROT) ? 3 : DIM;
+    __shared__ double s_ab[4][2][NL][64];
+#pragma unroll
+    for (int c = 0; c < NL; ++c) {
+        s_ab[w][0][c][lane] = a[c];
+        s_ab[w][1][c][lane] = b[c];
+    }
     // interior samples this edge contributes: the FIFO walk's (s2 valid), or the lastValid sweep's
-    const int cnt = (e < m && nd >= 2 && (s2ok || fi_out)) ? nd - 1 : 0;
+    const int cnt = (has && nd >= 2 && (s2ok || fi_out)) ? nd - 1 : 0;
     int inc = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -304,9 +347,12 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
                 if (s_off[w][i + step] <= k) i += step;
             const int ndi = s_nd[w][i], j = k - s_off[w][i] + 1;
             double a[DIM], b[DIM], t[DIM];
-            load_state<DIM>(s1 + (size_t)(wbase + i) * DIM, DIM, a);
-            load_state<DIM>(s2 + (size_t)(wbase + i) * DIM, DIM, b);
-            interpolate(sp, a, b, (double)j / (double)ndi, t, ROT);
+#pragma unroll
+            for (int c = 0; c < NL; ++c) {
+                a[c] = s_ab[w][0][c][i];
+                b[c] = s_ab[w][1][c][i];
+            }
+            interpolate(sp, a, b, (double)j / (double)ndi, t, ROT);  // (reads coordinates < NL only)
             if (!(sph && spheres_clear32(t, ss, ck.count)) && !valid_sp<SP, DIM>(sp, ck, t)) {
                 atomicMin(&s_fj[w][i], j);
                 if (counters) atomicMin(&s_fr[w][i], (int)fifo_rank(j, ndi));
@@ -317,15 +363,15 @@ __global__ __launch_bounds__(256) __attribute__((flatten)) void motion_kernel(
     __builtin_amdgcn_wave_barrier();
     const int fj = s_fj[w][lane], fr = s_fr[w][lane];
     const bool result = s2ok && fj == 0x7FFFFFFF;
-    if (e < m) {
+    if (e < m) {  // (an edge that does not exist reports invalid and is not counted)
         if (valid) valid[e] = result ? 1 : 0;
         if (fi_out) fi_out[e] = result ? -1 : (fj != 0x7FFFFFFF ? fj : nd);
     }
     if (counters) {
-        unsigned long long nv = (e < m && result) ? 1ull : 0ull;
-        unsigned long long ni = (e < m && !result) ? 1ull : 0ull;
+        unsigned long long nv = (has && result) ? 1ull : 0ull;
+        unsigned long long ni = (has && !result) ? 1ull : 0ull;
         // isValid calls of the FIFO form: s2, then every interior sample, or up to the failing one
-        unsigned long long nc = e < m ? 1ull + (s2ok ? (fj == 0x7FFFFFFF ? (unsigned)cnt : (unsigned)fr + 1u) : 0u) : 0ull;
+        unsigned long long nc = has ? 1ull + (s2ok ? (fj == 0x7FFFFFFF ? (unsigned)cnt : (unsigned)fr + 1u) : 0u) : 0ull;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_xor(nv, off, 64);
             ni += __shfl_xor(ni, off, 64);
@@ -676,14 +722,40 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
             hipLaunchKernelGGL(motion_rt_kernel, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd,
                                first_invalid, counters, rot);
         else if (rot)
-            hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value, true>),
-                               dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd, first_invalid,
-                               counters);
+            hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value, true, PairSrc>),
+                               dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, PairSrc{s1, s2}, m, valid, nd,
+                               first_invalid, counters);
         else
-            hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value, false>),
-                               dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid, nd, first_invalid,
-                               counters);
+            hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value, false, PairSrc>),
+                               dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, PairSrc{s1, s2}, m, valid, nd,
+                               first_invalid, counters);
         return hipGetLastError();
+    });
+}
+
+// the edges of a neighbour query checked in place (EdgeSrc); hipErrorNotSupported when the space /
+// checker has no fixed-width form (the caller materialises the pairs and calls launch_motion)
+hipError_t launch_motion_edges(const DevSpace &sp, const DevChecker &ck, const double *q, const uint32_t *qidx,
+                               const uint32_t *ids, uint32_t stride, int from_query, const double *aos, int da,
+                               uint32_t m, uint8_t *valid, unsigned long long *counters, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    if (chain_np(sp, ck)) return hipErrorNotSupported;
+    const EdgeSrc src{q, qidx, ids, stride, from_query, aos, da};
+    const int rot = needs_rotation(sp, ck) ? 1 : 0;
+    return dispatch_width(sp, ck, [&](auto kind, auto width) {
+        if constexpr (decltype(width)::value == 0) {
+            return hipErrorNotSupported;
+        } else {
+            if (rot)
+                hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value, true, EdgeSrc>),
+                                   dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, src, m, valid, nullptr, nullptr,
+                                   counters);
+            else
+                hipLaunchKernelGGL((motion_kernel<decltype(kind)::value, decltype(width)::value, false, EdgeSrc>),
+                                   dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, src, m, valid, nullptr, nullptr,
+                                   counters);
+            return hipGetLastError();
+        }
     });
 }
 

@@ -128,6 +128,14 @@ class DiscreteMotionValidatorGPU(abi.Handle):
     def sync(self) -> None:
         abi.check(abi.lib.ompl_gpu_mv_sync(self._h))
 
+    def check_edges_device(self, nn, d_queries: int, nq: int, d_offsets, d_ids: int, stride: int, m: int,
+                           from_query: bool, d_valid: int) -> None:
+        """checkMotion over the edges of a neighbour result read in place (ompl_gpu_mv_check_edges_device):
+        the pairs NearestNeighborsGPU.edges_device would write, without writing them."""
+        abi.check(abi.lib.ompl_gpu_mv_check_edges_device(self._h, nn._h, C.c_void_p(d_queries), nq,
+                                                         C.c_void_p(d_offsets or None), C.c_void_p(d_ids), stride, m,
+                                                         1 if from_query else 0, C.c_void_p(d_valid)))
+
     def check_device(self, d_s1: int, d_s2: int, m: int, d_valid: int, d_nd: int = 0, d_fi: int = 0) -> None:
         abi.check(abi.lib.ompl_gpu_mv_check_device(self._h, C.c_void_p(d_s1), C.c_void_p(d_s2), m,
                                                    C.c_void_p(d_valid), C.c_void_p(d_nd or None),

@@ -2,14 +2,16 @@
 walk against the oracle on every path, the device-resident CSR radius API, the edge
 endpoints the planners check after a neighbour query, and sequential RRT growth on device
 against the oracle's step-by-step RRT loop (RRT.cpp:128-192)."""
+import math
+
 import numpy as np
 import pytest
 
 import pyoracle as O
 from ompl_amd import DiscreteMotionValidatorGPU, NearestNeighborsGPU, abi
 from ompl_amd import workloads as W
-from ompl_amd.checkers import AllValidChecker, SpheresChecker
-from ompl_amd.spaces import RealVectorStateSpace, SE3StateSpace
+from ompl_amd.checkers import AllValidChecker, HypercubeChecker, KinematicChainChecker, SpheresChecker
+from ompl_amd.spaces import KinematicChainSpace, RealVectorStateSpace, SE3StateSpace
 from parity import assert_dist_close
 
 pytestmark = pytest.mark.gpu
@@ -180,3 +182,70 @@ def test_rrt_grow_matches_sequential_loop(gpu, case, monkeypatch):
     ids, d, _ = nn.nearestKBatch(q, 5)
     oi, od, _ = O.knn(sp, tree, q, 5)
     np.testing.assert_array_equal(ids.astype(np.int64), oi.astype(np.int64))
+
+
+@pytest.mark.parametrize("case", ["se3_spheres", "se3_hypercube", "r3_spheres", "chain12"])
+def test_check_edges_device(gpu, case):
+    """ompl_gpu_mv_check_edges_device: checkMotion over a neighbour result's edges read in place equals
+    checking the pairs edges_device materialises (validity bits and the FIFO isValid count), for a CSR
+    result with edges past the last segment, a dense kNN result with missing ids (k > n of a small
+    store: the zero-length motion), both directions; the KinematicChain takes the materialising form."""
+    rng = np.random.default_rng(91)
+    dev = f"cuda:{gpu}"
+    if case == "chain12":
+        sp = KinematicChainSpace(12, 1.0 / 12)
+        ck = KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))
+        draw = lambda n: W.uniform_chain(rng, n, 12)  # noqa: E731
+        r = 0.9
+    else:
+        c, rad = W.sphere_field(32, 0.1, 7)
+        if case == "r3_spheres":
+            sp, ck = RealVectorStateSpace(3, 0.0, 1.0), SpheresChecker(c, rad)
+            draw = lambda n: rng.uniform(0.0, 1.0, size=(n, 3))  # noqa: E731
+            r = 0.08
+        else:
+            sp = SE3StateSpace()
+            ck = SpheresChecker(c, rad) if case == "se3_spheres" else HypercubeChecker(3, 0.1)
+            draw = lambda n: W.uniform_se3(rng, n)  # noqa: E731
+            r = 0.5
+    data, q = draw(30000), draw(300)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    dq = torch.from_numpy(q).to(dev)
+    off = torch.empty(301, dtype=torch.int64, device=dev)
+    tot = nn.radius_device(dq.data_ptr(), 300, r, off.data_ptr(), 0, 0, 0)
+    assert tot > 1000
+    ids = torch.empty(tot + 37, dtype=torch.int32, device=dev)
+    dd = torch.empty(tot + 37, dtype=torch.float64, device=dev)
+    nn.radius_device(dq.data_ptr(), 300, r, off.data_ptr(), ids.data_ptr(), dd.data_ptr(), tot)
+    for from_query in (True, False):
+        for dense in (False, True):
+            if dense:
+                k, nq = 9, 300
+                small = NearestNeighborsGPU(sp, gpu)
+                small.add(data[:5])                                      # k > n: missing ids
+                ki = torch.empty((nq, k), dtype=torch.int32, device=dev)
+                kd = torch.empty((nq, k), dtype=torch.float64, device=dev)
+                small.knn_device(dq.data_ptr(), nq, k, ki.data_ptr(), kd.data_ptr())
+                src, offp, idp, stride, m = small, None, ki.data_ptr(), k, nq * k
+            else:
+                src, offp, idp, stride, m = nn, off.data_ptr(), ids.data_ptr(), 0, tot + 37  # 37 past the end
+            fr = torch.zeros((m, sp.dim), dtype=torch.float64, device=dev)
+            to = torch.zeros_like(fr)
+            src.edges_device(dq.data_ptr(), 300, offp, idp, stride, m, from_query, fr.data_ptr(), to.data_ptr())
+            src.sync()
+            n_real = tot if not dense else m
+            mv1 = DiscreteMotionValidatorGPU(sp, ck, gpu)
+            v1 = mv1.checkMotions(fr.cpu().numpy()[:n_real], to.cpu().numpy()[:n_real])
+            mv2 = DiscreteMotionValidatorGPU(sp, ck, gpu)
+            val = torch.full((m,), 7, dtype=torch.uint8, device=dev)
+            mv2.check_edges_device(src, dq.data_ptr(), 300, offp, idp, stride, m, from_query, val.data_ptr())
+            mv2.sync()
+            got = val.cpu().numpy()
+            np.testing.assert_array_equal(got[:n_real].astype(bool), v1)
+            assert (got[n_real:] == 0).all()
+            assert mv2.stateChecks() == mv1.stateChecks()
+            assert mv2.getValidMotionCount() == mv1.getValidMotionCount()
+            assert mv2.getInvalidMotionCount() == mv1.getInvalidMotionCount()
+    ov, _, _, checks = O.check_motions(sp, ck, fr.cpu().numpy(), to.cpu().numpy())
+    np.testing.assert_array_equal(v1, ov)
