@@ -501,121 +501,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
 }
 
-// Interior sample of FIFO rank r (0-based) of a motion of nd segments: the inverse of fifo_rank —
-// r's level by the levels' interval counts, then a descent that keeps r's position among that
-// level's intervals
-__device__ inline int fifo_sample(uint32_t r, int nd) {
-    const uint32_t S = (uint32_t)(nd - 1);
-    int L = 0;
-    for (uint32_t n = fifo_level_count(S, 0); r >= n; n = fifo_level_count(S, ++L)) r -= n;
-    int lo = 1, hi = nd - 1;
-    for (int d = 0; d < L; ++d) {
-        const int mid = (lo + hi) / 2;
-        const uint32_t nl = fifo_level_count((uint32_t)(mid - lo), L - d - 1);
-        if (r < nl) {
-            hi = mid - 1;
-        } else {
-            r -= nl;
-            lo = mid + 1;
-        }
-    }
-    return (lo + hi) / 2;
-}
-
-// The KinematicChain motion (cfg4's PRM* edges, about half of them invalid) as a compacted FIFO
-// walk: a wave takes 64 edges and, 64 samples at a time, hands its lanes the next pending samples
-// in (FIFO rank, edge) order — rank 0 of every live edge, then rank 1, ... — so every lane checks a
-// sample of some live edge instead of idling behind the wave's longest edge, and an edge stops
-// taking samples once one fails (samples of a higher rank already handed out in the same round are
-// the only extra checks).  Every rank below an edge's first failure is checked before it, so the
-// failure of smallest rank — the reference's stopping point (:122-126) — and the isValid count
-// (1 + that rank + 1) are exact.  The lastValid sweep (fi_out) takes motion_chain_kernel.
-template <int NP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void motion_chain_pool_kernel(
-    DevSpace sp, DevChecker ck, const double *__restrict__ s1, const double *__restrict__ s2, uint32_t m,
-    uint8_t *__restrict__ valid, int32_t *__restrict__ nd_out, unsigned long long *__restrict__ counters) {
-    __shared__ double tab[440];  // glibc's sin / cos table, read at lane-dependent points
-    __shared__ int s_nd[4][64], s_fr[4][64], s_se[4][64], s_sr[4][64];
-    for (int i = threadIdx.x; i < 440; i += blockDim.x) tab[i] = gsc::kSinCosTab[i];
-    __syncthreads();
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t wbase = blockIdx.x * blockDim.x + (uint32_t)w * 64, e = wbase + lane;
-    const int n = sp.dim;
-    bool s2ok = false;
-    int nd = 0;
-    if (e < m) {
-        const double *a = s1 + (size_t)e * n, *b = s2 + (size_t)e * n;
-        s2ok = chain_valid_np<NP>([&](int i) { return b[i]; }, n, sp.link, ck.data, ck.count, ck.slack, tab);
-        nd = (s2ok || nd_out) ? (int)seg_count(chain_dist_raw(a, b, n, sp.link, tab), sp.lvs0, sp.f0) : 0;
-        if (nd_out) nd_out[e] = nd;
-    }
-    const int cnt = (s2ok && nd >= 2) ? nd - 1 : 0;  // interior samples of the FIFO walk
-    int next = 0;                                      // this edge's next rank to hand out
-    bool live = cnt > 0;
-    s_nd[w][lane] = nd;
-    s_fr[w][lane] = 0x7FFFFFFF;
-    __builtin_amdgcn_wave_barrier();
-    while (__ballot(live)) {
-        // hand out up to 64 (edge, rank) pairs in (rank, edge) order: the live edges hold ranks
-        // rho or rho + 1 (the order's frontier), so rank by rank from the smallest
-        int rho = live ? next : 0x7FFFFFFF;
-#pragma unroll
-        for (int o = 32; o; o >>= 1) rho = min(rho, __shfl_xor(rho, o, 64));
-        int used = 0;
-        for (;;) {
-            const bool elig = live && next == rho && rho < cnt;
-            const uint64_t em = __ballot(elig);
-            if (!em) break;  // no live edge has rank rho left (ranks only grow)
-            const int ne = __popcll(em), take = min(ne, 64 - used);
-            const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0));
-            if (elig && pos < take) {
-                s_se[w][used + pos] = lane;
-                s_sr[w][used + pos] = rho;
-                next = rho + 1;
-            }
-            used += take;
-            if (used == 64) break;
-            ++rho;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (lane < used) {
-            const int i = s_se[w][lane], r = s_sr[w][lane], ndi = s_nd[w][i];
-            const double *a = s1 + (size_t)(wbase + i) * n, *b = s2 + (size_t)(wbase + i) * n;
-            const double t = (double)fifo_sample((uint32_t)r, ndi) / (double)ndi;
-            if (!chain_valid_np<NP>([&](int c) { return chain_interp1(a[c], b[c], t); }, n, sp.link, ck.data,
-                                    ck.count, ck.slack, tab))
-                atomicMin(&s_fr[w][i], r);
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (live && (s_fr[w][lane] != 0x7FFFFFFF || next >= cnt)) live = false;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const int fr = s_fr[w][lane];
-    const bool result = s2ok && fr == 0x7FFFFFFF;
-    if (e < m && valid) valid[e] = result ? 1 : 0;
-    if (counters) {
-        unsigned long long nv = (e < m && result) ? 1ull : 0ull;
-        unsigned long long ni = (e < m && !result) ? 1ull : 0ull;
-        unsigned long long nc = e < m ? 1ull + (s2ok ? (fr == 0x7FFFFFFF ? (unsigned)cnt : (unsigned)fr + 1u) : 0u) : 0ull;
-        for (int off = 32; off > 0; off >>= 1) {
-            nv += __shfl_xor(nv, off, 64);
-            ni += __shfl_xor(ni, off, 64);
-            nc += __shfl_xor(nc, off, 64);
-        }
-        __shared__ unsigned long long part[3][4];
-        if (lane == 0) {
-            part[0][w] = nv;
-            part[1][w] = ni;
-            part[2][w] = nc;
-        }
-        __syncthreads();
-        if (threadIdx.x < 3) {
-            unsigned long long v = 0;
-            for (int q = 0; q < (int)(blockDim.x >> 6); ++q) v += part[threadIdx.x][q];
-            if (v) atomicAdd(&counters[threadIdx.x], v);
-        }
-    }
-}
+// (Measured and rejected: the KinematicChain motion as a compacted FIFO walk — a wave handing its
+// lanes the next pending (FIFO rank, edge) samples of its 64 edges, every rank below an edge's first
+// failure checked first, so bits and counts stay exact — 862 us per cfg4 batch against 622 us for
+// motion_chain_kernel: about half of PRM*'s edges fail early, which the thread-per-edge walk leaves
+// at once, and the rank-to-sample mapping and extra in-round checks cost more than the balance gains.)
 
 template <int NP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void state_chain_kernel(DevSpace sp, DevChecker ck, const double *__restrict__ s,
@@ -697,15 +587,7 @@ hipError_t launch_motion(const DevSpace &sp, const DevChecker &ck, const double 
                          uint8_t *valid, int32_t *nd, int32_t *first_invalid, unsigned long long *counters,
                          hipStream_t st) {
     if (m == 0) return hipSuccess;
-    switch (chain_np(sp, ck) * (first_invalid ? 1 : -1)) {
-    case -14:
-        hipLaunchKernelGGL(motion_chain_pool_kernel<14>, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m,
-                           valid, nd, counters);
-        return hipGetLastError();
-    case -18:
-        hipLaunchKernelGGL(motion_chain_pool_kernel<18>, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m,
-                           valid, nd, counters);
-        return hipGetLastError();
+    switch (chain_np(sp, ck)) {
     case 14:
         hipLaunchKernelGGL(motion_chain_kernel<14>, dim3((m + 255) / 256), dim3(256), 0, st, sp, ck, s1, s2, m, valid,
                            nd, first_invalid, counters);

@@ -138,9 +138,9 @@ def test_motion_states_count_limit(gpu):
 
 @pytest.mark.parametrize("name", ["se3_hypercube", "se3_spheres", "r6_hypercube", "chain12_horn", "r2_circles"])
 def test_motion_golden_bench_path(gpu, golden, name):
-    """The planner / bench call (no nd, no first-invalid): the lane-per-sample kernels (fixed widths:
-    samples laid end to end; KinematicChain: the compacted FIFO walk) give the golden validity bits
-    and the FIFO bisection's isValid-call count (DiscreteMotionValidator.cpp:93-145)."""
+    """The planner / bench call (no nd, no first-invalid): the lane-per-sample kernel (fixed widths:
+    a wave's samples laid end to end; the KinematicChain's thread-per-edge walk) gives the golden
+    validity bits and the FIFO bisection's isValid-call count (DiscreteMotionValidator.cpp:93-145)."""
     g = golden(f"motion_{name}.npz")
     sp, ck = _case(name, golden)
     mv = DiscreteMotionValidatorGPU(sp, ck, gpu)
@@ -154,9 +154,8 @@ def test_motion_golden_bench_path(gpu, golden, name):
 
 
 def test_chain_motion_random_vs_oracle(gpu):
-    """KinematicChain motions (PRM*'s, about half invalid) through the compacted FIFO walk: bits and
-    the isValid count equal the oracle's FIFO bisection; long edges (many samples per edge, few live
-    edges per wave) included."""
+    """KinematicChain motions (PRM*'s, about half invalid) on the bench path (no nd / lastValid): bits
+    and the isValid count equal the oracle's FIFO bisection; long edges (up to 41 segments) included."""
     rng = np.random.default_rng(23)
     sp = KinematicChainSpace(12, 1.0 / 12)
     ck = KinematicChainChecker(W.horn_environment(12, math.log(12.0) / 12.0))
