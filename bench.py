@@ -80,6 +80,28 @@ def pmc_traffic(workload, kernel):
     return None
 
 
+def sq_issue(workload, kernel, waves, kern_ms):
+    """VALU issue utilisation of `kernel` from the committed SQ pass (tools/sq_counters.sh): VALU
+    instructions per wave (SQ_INSTS_VALU / SQ_WAVES of the sampled SQ instances) x the launch's waves x
+    4 cycles per wave64 VALU instruction (16-lane SIMDs) over 1,024 SIMDs x 2.4 GHz (the peak engine
+    clock, so a lower bound of the busy fraction) x the measured kernel time."""
+    for d in PMC_PROFILES.get(workload, ()):
+        path = os.path.join(ROOT, "profiles", d, "sq_summary.json")
+        try:
+            with open(path) as f:
+                per = json.load(f)["per_kernel_mean"]
+        except (OSError, ValueError, KeyError):
+            continue
+        for name, c in per.items():
+            if name.split("<")[0].endswith(kernel) and c.get("SQ_WAVES") and c.get("SQ_INSTS_VALU"):
+                valu = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+                salu = c.get("SQ_INSTS_SALU", 0.0) / c["SQ_WAVES"]
+                busy = valu * waves * 4 / (1024 * 2.4e9 * kern_ms * 1e-3)
+                return {"valu_per_wave": round(valu), "salu_per_wave": round(salu), "waves": waves,
+                        "valu_issue_busy": round(busy, 3), "source": os.path.relpath(path, ROOT) + f" [{name}]"}
+    return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1030,12 +1052,18 @@ class Runner:
                 what += ("; every pair counted at the full 84 flop although a wave skips the remaining links once "
                          "no lane's partial sum is below its list threshold (an upper bound of the work done)")
         achieved = pairs * flop / (kern_ms * 1e-3) / 1e12
-        return {"bound": "valu", "achieved": achieved, "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
-                "frac": achieved / PEAK_TFLOPS[dt], "traffic": traffic["bytes"] if traffic else None,
-                "kernel": kern_name, "kernel_ms": kern_ms,
-                "algorithmic": what + f"; {dt} VALU peak (compute-bound on VALU, no MFMA)",
-                "brute_force_equivalent_tflops": float(nq) * n * flop / (kern_ms * 1e-3) / 1e12,
-                "traffic_source": traffic["source"] if traffic else None}
+        out = {"bound": "valu", "achieved": achieved, "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
+               "frac": achieved / PEAK_TFLOPS[dt], "traffic": traffic["bytes"] if traffic else None,
+               "kernel": kern_name, "kernel_ms": kern_ms,
+               "algorithmic": what + f"; {dt} VALU peak (compute-bound on VALU, no MFMA)",
+               "brute_force_equivalent_tflops": float(nq) * n * flop / (kern_ms * 1e-3) / 1e12,
+               "traffic_source": traffic["source"] if traffic else None}
+        if kern_name == "knn32_group_kernel" and wl in ("cfg3", "cfg2") and not self.k > 16:
+            # the walk's waves: one per G = 2 queries (knn_fast_impl.h group_queries)
+            iss = sq_issue(wl, kern_name, (nq + 1) // 2, kern_ms)
+            if iss:
+                out["issue"] = iss
+        return out
 
     def close(self):
         """release the library handles (the next workload gets the HBM back)"""
