@@ -629,17 +629,19 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
         b.n_live = (uint32_t)h->n_live;
         const size_t wsb = knn_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus, cull);
         HIP_OR_FAIL(h->ws.ensure(wsb));
+        // the bounded re-run's counters (below), zeroed by the batch's first kernel
+        HIP_OR_FAIL(h->fb_c.ensure(sizeof(uint32_t) * (kBoundedMaxQ + 1 + nq)));
+        HIP_OR_FAIL(h->fb_cd.ensure(sizeof(double) * kBoundedMaxQ * kBoundedCap));
+        HIP_OR_FAIL(h->fb_ci.ensure(sizeof(uint32_t) * kBoundedMaxQ * kBoundedCap));
+        uint32_t *cnt = (uint32_t *)h->fb_c.p;
+        b.zero[0] = cnt;
+        b.nzero[0] = kBoundedMaxQ + 1;
         uint32_t *d_fail_count = nullptr, *d_fail_list = nullptr;
         HIP_OR_FAIL(launch_knn_fast(h->sp, h->g, h->feat, h->feat32, h->cap, n_end, cull ? &h->sorted : nullptr, d_qf,
                                     (uint32_t)nq, k, b, d_dist, d_ids, h->ws.p, h->ws.bytes, h->num_cus, h->stream,
                                     &d_fail_count, &d_fail_list));
         // exact re-run of the uncertified queries, decided on the device: the bounded pass (one
         // store read for all of them), a full scan for any that overflow its candidate cap
-        HIP_OR_FAIL(h->fb_c.ensure(sizeof(uint32_t) * (kBoundedMaxQ + 1 + nq)));
-        HIP_OR_FAIL(h->fb_cd.ensure(sizeof(double) * kBoundedMaxQ * kBoundedCap));
-        HIP_OR_FAIL(h->fb_ci.ensure(sizeof(uint32_t) * kBoundedMaxQ * kBoundedCap));
-        uint32_t *cnt = (uint32_t *)h->fb_c.p;
-        HIP_OR_FAIL(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (kBoundedMaxQ + 1), h->stream));
         HIP_OR_FAIL(launch_knn_bounded(h->sp, h->g, h->feat, h->cap, n_end, d_qf, d_fail_list, d_fail_count, k, d_dist,
                                        d_ids, cnt, (double *)h->fb_cd.p, (uint32_t *)h->fb_ci.p, h->num_cus,
                                        h->stream));

@@ -71,6 +71,10 @@ struct FastBounds {
     uint32_t slab = 0;                  // radius phase 2: hits kept per query (slab capacity)
     uint32_t n_live = 0;                // live stored states: a screening list that is not full must hold them all
     float qeta = 0.f;                   // SE3: largest |norm^2 - 1| of the stored quaternions (screen_error)
+    // per-call scratch words the first kernel of a query batch (query_rows_kernel) zeroes, so the
+    // batch needs no memset launches: the re-run counters (C ABI), the home-key bins, the fail count
+    uint32_t *zero[3] = {nullptr, nullptr, nullptr};
+    uint32_t nzero[3] = {0u, 0u, 0u};
 };
 // The fp32 screens assume coordinates far from fp32 overflow: with |x| < kScreenMaxAbs every
 // squared fp32 distance is finite (the C ABI takes the exact fp64 path otherwise).

@@ -144,6 +144,10 @@ __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, Fa
                                   const KdNode *__restrict__ nodes, uint32_t ntiles) {
     constexpr int FS = Geo<SP, F>::FS;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        if (b.zero[r])
+            for (uint32_t t = i; t < b.nzero[r]; t += gridDim.x * blockDim.x) b.zero[r][t] = 0u;
     if (i >= nq) return;
     const double *s = qf + (size_t)i * F;
     float o[FS];
@@ -237,13 +241,15 @@ __global__ void home_scatter_kernel(const uint32_t *__restrict__ keys, const uin
 }
 inline hipError_t sort_home_keys(char *cub, size_t cub_bytes, const uint32_t *keys, uint32_t *keys2,
                                  const uint32_t *idx, uint32_t *perm, uint32_t nq, int key_bits, hipStream_t st,
-                                 uint32_t *qcount = nullptr, uint32_t bins = 0) {
+                                 uint32_t *qcount = nullptr, uint32_t bins = 0, bool zeroed = false) {
     // the counting sort (measured 0.081-0.083 ms against 0.113-0.115 ms for the radix sort of the
     // nn phase outside the walk on cfg3); the radix sort stays for Morton keys (32 bits)
     if (qcount && bins && key_bits < 32 && cub_bytes >= 4ull * nq) {
         uint32_t *slot = (uint32_t *)cub;  // the radix sort's temporary storage holds the slots
-        hipError_t e = hipMemsetAsync(qcount, 0, 4ull * bins, st);
-        if (e != hipSuccess) return e;
+        if (!zeroed) {  // (query_rows_kernel zeroes the bins when the caller listed them)
+            const hipError_t e = hipMemsetAsync(qcount, 0, 4ull * bins, st);
+            if (e != hipSuccess) return e;
+        }
         const uint32_t nb = (bins + 1023) / 1024;
         uint32_t *bsum = qcount + nb * 1024;  // qcount holds the bins padded to 1,024, then the block sums
         hipLaunchKernelGGL(home_count_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, keys, nq, qcount, slot);
@@ -2236,18 +2242,21 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     uint32_t *pi = (uint32_t *)(ws + L.pi);
     uint32_t *fail = (uint32_t *)(ws + L.fail);
     const dim3 b256(256);
-    hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys, idx,
-                       (p.cull && ss) ? ss->nodes : nullptr, (p.cull && ss) ? ss->kd_tiles : 0u);
     // home-tile keys are below kd_tiles: sort only their bits (half the radix passes at 10^6
     // states); Morton keys use all 32
     const bool home_keys = p.cull && ss && ss->nodes && ss->kd_tiles > 1;
     const int key_bits = home_keys ? 32 - __builtin_clz(ss->kd_tiles - 1) : 32;
+    FastBounds bz = b;  // + the home-key bins and the fail count, zeroed by query_rows_kernel
+    bz.zero[1] = home_keys ? ss->qcount : nullptr;
+    bz.nzero[1] = home_keys ? ss->kd_tiles : 0u;
+    bz.zero[2] = fail;
+    bz.nzero[2] = 1u;
+    hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, bz, q32u, keys, idx,
+                       (p.cull && ss) ? ss->nodes : nullptr, (p.cull && ss) ? ss->kd_tiles : 0u);
     hipError_t e = sort_home_keys(ws + L.cub, L.cub_bytes, keys, keys2, idx, perm, nq, key_bits, st,
-                                  home_keys ? ss->qcount : nullptr, home_keys ? ss->kd_tiles : 0u);
+                                  home_keys ? ss->qcount : nullptr, home_keys ? ss->kd_tiles : 0u, true);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
-    e = hipMemsetAsync(fail, 0, 4, st);
-    if (e != hipSuccess) return e;
     bool walked = false;
     float chain_qerr = 0.f;  // the culled chain scan's 16-bit screen error (certificate)
     if constexpr (SP == OMPL_GPU_SPACE_SE3 || SP == OMPL_GPU_SPACE_REALVECTOR) {  // cull_supported
