@@ -406,6 +406,88 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
             // (cost, index) order were found invalid (-1), the parent valid (1), the rest unchecked (0)
             touched.reset();
             const double cx = t->cost[x];  // x is no neighbour's descendant: its cost stays
+            if (t->consistent) {
+                // costs only fall in a consistent tree, so a neighbour whose cost as read before the loop
+                // (cv) x cannot lower never becomes a candidate later: the pool collects, in index
+                // order, the neighbours x can lower (and counts the parent choice's checkMotion calls);
+                // the sequential loop visits only those, with the tree bookkeeping of the candidates a
+                // few ahead prefetched (the rewires' random reads were the cost of this loop)
+                auto scan = [&](int k) {
+                    const size_t r0 = nb * (size_t)k / (size_t)T, r1 = nb * (size_t)(k + 1) / (size_t)T;
+                    auto &cl = t->cand[(size_t)k];
+                    cl.clear();
+                    uint64_t ck = 0;
+                    for (size_t r = r0; r < r1; ++r) {
+                        const bool before = best == nb || t->costs[r] < bc || (t->costs[r] == bc && r < best);
+                        if ((before || r == best) && ids[r] != nm && d[r] < maxd) ++ck;  // checkMotion(nbh, x)
+                        if ((int64_t)ids[r] == m_parent) continue;
+                        if (cx + d[r] < t->cv[r]) cl.push_back((uint32_t)r);
+                    }
+                    t->cand_checks[(size_t)k] = ck;
+                };
+                t->cand.resize((size_t)pool.size());
+                t->cand_checks.resize((size_t)pool.size());
+                if (T > 1)
+                    pool.run(scan);
+                else
+                    scan(0);
+                for (int k = 0; k < T; ++k) {
+                    checks += t->cand_checks[(size_t)k];
+                    const auto &cl = t->cand[(size_t)k];
+                    const size_t nc_ = cl.size();
+                    for (size_t q = 0; q < nc_; ++q) {
+                        // (hints only: a rewire may move what they point at)
+                        if (q + 12 < nc_) {
+                            const uint32_t v = ids[cl[q + 12]];
+                            __builtin_prefetch(&t->parent[v]);
+                            __builtin_prefetch(&t->slot[v]);
+                            __builtin_prefetch(&t->children[v]);
+                            __builtin_prefetch(&t->cost[v], 1);
+                            __builtin_prefetch(&t->inc[v], 1);
+                        }
+                        if (q + 6 < nc_) {
+                            const uint32_t v = ids[cl[q + 6]];
+                            const int64_t p = t->parent[v];
+                            if (p >= 0) __builtin_prefetch(&t->children[(size_t)p]);
+                        }
+                        if (q + 3 < nc_) {
+                            const uint32_t v = ids[cl[q + 3]];
+                            const int64_t p = t->parent[v];
+                            if (p >= 0) {
+                                const auto &ch = t->children[(size_t)p];
+                                if (!ch.empty()) {
+                                    __builtin_prefetch(ch.data() + t->slot[v], 1);
+                                    __builtin_prefetch(ch.data() + ch.size() - 1);
+                                    __builtin_prefetch(&t->slot[ch.back()], 1);
+                                }
+                            }
+                        }
+                        const size_t r = cl[q];
+                        const bool before = best == nb || t->costs[r] < bc || (t->costs[r] == bc && r < best);
+                        const int8_t mark = r == best ? 1 : (before ? -1 : 0);
+                        const uint32_t v = ids[r];
+                        const double nc = cx + d[r];
+                        if (touched.has(v) && !(nc < t->cost[v])) continue;
+                        bool ok;
+                        if (mark == 0) {
+                            ok = d[r] < maxd && (bt[r] & 2);
+                            if (d[r] < maxd) ++checks;
+                        } else {
+                            ok = mark == 1;
+                        }
+                        if (!ok) continue;
+                        remove_from_parent(t, v);
+                        t->parent[v] = x;
+                        t->inc[v] = d[r];
+                        t->cost[v] = nc;
+                        add_child(t, x, v);
+                        touched.add(v);
+                        visits += update_child_costs(t, v, [&](uint32_t c) { touched.add(c); });
+                        ++rewires;
+                    }
+                }
+                continue;
+            }
             for (size_t r = 0; r < nb; ++r) {
                 const bool before = best == nb || t->costs[r] < bc || (t->costs[r] == bc && r < best);
                 const int8_t mark = r == best ? 1 : (before ? -1 : 0);

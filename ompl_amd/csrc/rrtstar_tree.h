@@ -40,6 +40,8 @@ struct ompl_gpu_rrtstar_tree {
     // commit's scratch
     std::vector<uint32_t> stack;
     std::vector<double> costs, cv;
+    std::vector<std::vector<uint32_t>> cand;  // per pool thread: rewiring candidates (neighbour index)
+    std::vector<uint64_t> cand_checks;        // per pool thread: parent-choice checkMotion count
     std::shared_ptr<void> touched, pool;  // rrtstar_tree.cpp Touched, Pool
     // totals: [0] rewires, [1] checkMotion calls the sequential loop would make, [2] states added,
     // [3] neighbourhood entries, [4] samples, [5] child costs updateChildCosts rewrote
