@@ -831,7 +831,10 @@ class Runner:
             self.ids = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
             self.dd = torch.empty(max(m, 1), dtype=torch.float64, device=dev)
         self.m = m
-        self.s_from = torch.empty((max(m, 1), dim), dtype=torch.float64, device=dev)
+        # endpoint rows: the steered motions (cfg3 / cfg2) and the tree-sharded cfg5 edges; the
+        # replicated cfg5 step checks its edges in place (ompl_gpu_mv_check_edges_device)
+        rows = 1 if (wl == "cfg5" and not self.tree_mode) else max(m, 1)
+        self.s_from = torch.empty((rows, dim), dtype=torch.float64, device=dev)
         self.s_to = torch.empty_like(self.s_from)
         self.valid = torch.empty(max(m, 1), dtype=torch.uint8, device=dev)
         self.maxd = 0.2 * self.sp.getMaximumExtent()                    # RRT range default (SelfConfig.cpp:98)
