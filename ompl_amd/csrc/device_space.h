@@ -4,8 +4,9 @@
 // the distance the NN plugin's verify mode compares against), so host and device agree bit for
 // bit.  The KinematicChain's cos / sin are glibc's own algorithm (glibc_sincos.h: the device math
 // library differs from glibc by an ulp on 3 % of the arguments, enough to flip validity bits and
-// segment counts at the chain's knife edges); SO3's acos is the device library's (<= 1 ulp from
-// glibc: SO3 / SE3 distances are compared within 4 ulps).  This translation unit is
+// segment counts at the chain's knife edges); SO3's acos is glibc's own too (glibc_acos.h: the
+// device library's differs from glibc's by an ulp on up to 2 % of the arguments near 1, which moved
+// SO3 / SE3 distances, steered rotations and segment counts off the reference's bits).  This translation unit is
 // compiled with -ffp-contract=off: no multiply-add is fused, matching the
 // reference x86-64 build (CMakeModules/CompilerSettings.cmake:8, no -march).
 //
@@ -21,6 +22,7 @@
 #include <stdint.h>
 
 #include "../../include/ompl_gpu.h"
+#include "glibc_acos.h"
 #include "glibc_sincos.h"
 
 namespace ompl_amd {
@@ -64,7 +66,7 @@ __host__ __device__ __forceinline__ double l2_dist(const double *a, const double
 __host__ __device__ __forceinline__ double so3_arc(const double *p, const double *q) {
     double dq = fabs(p[0] * q[0] + p[1] * q[1] + p[2] * q[2] + p[3] * q[3]);
     if (dq > 1.0 - kQuatNormErr) return 0.0;
-    return acos(dq);
+    return glibc_acos(dq);
 }
 
 // chain distance from precomputed cumulative cos/sin features (cs[0..n) = cos, cs[n..2n) = sin)

@@ -174,7 +174,7 @@ def test_rrt_grow_matches_sequential_loop(gpu, case, monkeypatch):
     np.testing.assert_array_equal(near.cpu().numpy().astype(np.int64), en)
     np.testing.assert_array_equal(added.cpu().numpy().astype(np.uint32).astype(np.int64), ea)
     assert nn.size() == len(tree) > len(tree0)
-    np.testing.assert_allclose(nn.states(), tree, rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(nn.states(), tree)
     assert mv.getValidMotionCount() == int((ea != abi.NO_ID32).sum())
     assert mv.getValidMotionCount() + mv.getInvalidMotionCount() == 300
     # the grown store answers queries like a store built by add()

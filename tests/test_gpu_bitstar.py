@@ -102,11 +102,11 @@ def test_nearest_samples(gpu, use_k):
         oi, od, oc = O.knn(sp, data, vertices, g.k)
         np.testing.assert_array_equal(cnt, oc)
         np.testing.assert_array_equal(ids.astype(np.int64), oi.astype(np.int64))
-        np.testing.assert_allclose(d, od, rtol=0, atol=1e-12)
+        np.testing.assert_array_equal(d, od)
     else:
         off, ids, d = res
         oo, oi, od = O.radius(sp, data, vertices, g.r)
         np.testing.assert_array_equal(off, oo)
         np.testing.assert_array_equal(ids.astype(np.int64), oi.astype(np.int64))
-        np.testing.assert_allclose(d, od, rtol=0, atol=1e-12)
+        np.testing.assert_array_equal(d, od)
         assert int(off[-1]) > 0

@@ -98,8 +98,8 @@ def test_state_validity_random(gpu):
 def test_get_motion_states(gpu, name, count, endpoints):
     """SpaceInformation::getMotionStates (SpaceInformation.cpp:201-275, alloc = true) on the
     device against the oracle: same number of states, endpoints copied, interior samples at
-    j / (count + 1).  R^n and the chain (arithmetic only) are bit-identical; SO3 / SE3 slerp
-    differs from glibc only through sin / acos (a few ulps)."""
+    j / (count + 1), bit-identical in every space (SO3 / SE3 slerp: glibc's own acos and sin on
+    the device)."""
     from ompl_amd.spaces import SO3StateSpace
     rng = np.random.default_rng(91)
     sp = {"se3": SE3StateSpace, "so3": SO3StateSpace, "r6": lambda: RealVectorStateSpace(6),
@@ -112,10 +112,7 @@ def test_get_motion_states(gpu, name, count, endpoints):
     got = mv.getMotionStates(a, b, count, endpoints)
     want = O.motion_states(sp, a, b, count, endpoints)
     assert got.shape == want.shape == (300, count + (2 if endpoints else 0), sp.dim)
-    if name in ("r6", "chain12"):
-        np.testing.assert_array_equal(got, want)
-    else:
-        np.testing.assert_allclose(got, want, rtol=0, atol=4e-15)
+    np.testing.assert_array_equal(got, want)
     if endpoints:
         np.testing.assert_array_equal(got[:, 0], a)
         np.testing.assert_array_equal(got[:, -1], b)

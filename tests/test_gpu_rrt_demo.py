@@ -62,7 +62,7 @@ def test_rigid_body_planning_rrt_matches_oracle(gpu, seed):
     sol_i, tree, parent = _oracle_rrt(sp, start, goal, samples, planner.getRange())
     assert sol_i == iters - 1                         # solved at the same iteration
     assert planner.nn.size() == len(tree)
-    np.testing.assert_allclose(planner.nn.states(), tree, rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(planner.nn.states(), tree)
     assert planner.parent == parent
     assert path[0] == 0 and path[-1] == len(tree) - 1
     assert np.allclose(planner.nn.states()[path[-1]], goal, atol=0)

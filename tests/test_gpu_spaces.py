@@ -12,9 +12,9 @@ getMotionStates kernels use), not only on the oracle (test_oracle.py):
 
 The spaces are the ones on the hot path: R^3 / R^6, SO3, SE3 and the 12-link KinematicChain.
 Random states come from the reference's sampler streams (RNG::setSeed(42)).  Beside the
-properties, every device distance is compared with the oracle restatement: bit-identical for
-R^n and the chain (its cos / sin are glibc's algorithm on the device too, glibc_sincos.h), within
-4 ulp for SO3 / SE3 (the device's acos may differ from glibc's by an ulp)."""
+properties, every device distance is compared with the oracle restatement: bit-identical in every
+space (the chain's cos / sin and SO3's acos are glibc's algorithms on the device too,
+glibc_sincos.h / glibc_acos.h)."""
 import math
 
 import numpy as np
@@ -45,10 +45,6 @@ def _setup(name, gpu):
     return sp, DiscreteMotionValidatorGPU(sp, AllValidChecker(), gpu), smp
 
 
-def _ulps(a, b):
-    return np.abs(a - b) / np.spacing(np.maximum(np.abs(a), np.abs(b)))
-
-
 @pytest.mark.parametrize("name", list(SPACES))
 def test_state_space_test_distance(gpu, name):
     """testDistance (StateSpaceTest.h:72-90): d(s1,s1) ~ 0, d12 > 0, d12 ~ d21, on the device."""
@@ -62,11 +58,8 @@ def test_state_space_test_distance(gpu, name):
     assert np.all(np.abs(d12 - d21)[differ] < EPS)
     # the device metric against the oracle restatement (the reference's operation order)
     od = np.array([O.distance(sp, a, b) for a, b in zip(s1, s2)])
-    if name in ("r3", "r6", "chain12"):
-        # the chain from raw angles: the device's cos / sin are glibc's algorithm (glibc_sincos.h)
-        assert np.array_equal(d12, od)
-    else:
-        assert np.all(_ulps(d12, od) <= 4)
+    # the chain from raw angles and SO3's arc: glibc's cos / sin / acos on the device too
+    assert np.array_equal(d12, od)
 
 
 @pytest.mark.parametrize("name", list(SPACES))
@@ -90,10 +83,7 @@ def test_state_space_test_interpolation(gpu, name):
     t = np.linspace(0.0, 1.0, N)
     si = mv.interpolate(s1, s2, t)
     oi = np.array([O.interpolate(sp, a, b, x) for a, b, x in zip(s1, s2, t)])
-    if name in ("r3", "r6", "chain12"):
-        assert np.array_equal(si, oi)
-    else:
-        np.testing.assert_allclose(si, oi, rtol=0, atol=1e-15)
+    np.testing.assert_array_equal(si, oi)
 
 
 def test_so3_simple_known_answers(gpu):

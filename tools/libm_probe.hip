@@ -1,13 +1,14 @@
 // libm_probe.hip — measurement tool (not product): the device math library's sin / cos / acos
 // against the host's, on the argument ranges the hot path uses (cumulative KinematicChain angles
 // |theta| <= 12 pi; SO3 |q1 . q2| in [0, 1]).  Reads n doubles from argv[1], writes
-// sin, cos, acos of each and the glibc restatement's sin, cos, sincos (ompl_amd/csrc/glibc_sincos.h) to
-// argv[2] (7 n doubles, the last two = sincos); tools/libm_probe.py compares with glibc.
+// sin, cos, acos of each and the glibc restatements' sin, cos, sincos, acos (ompl_amd/csrc/glibc_sincos.h, glibc_acos.h) to
+// argv[2] (8 n doubles: sin, cos, acos, glibc sin, cos, sincos (2), acos); tools/libm_probe.py compares with glibc.
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
 #include <vector>
 
+#include "../ompl_amd/csrc/glibc_acos.h"
 #include "../ompl_amd/csrc/glibc_sincos.h"
 
 __global__ void probe(const double *x, size_t n, double *o) {
@@ -20,6 +21,7 @@ __global__ void probe(const double *x, size_t n, double *o) {
     o[3 * n + i] = ompl_amd::glibc_sin(v);
     o[4 * n + i] = ompl_amd::glibc_cos(v);
     ompl_amd::glibc_sincos(v, o[5 * n + i], o[6 * n + i]);
+    o[8 * n + i] = ompl_amd::glibc_acos(fabs(v) <= 1.0 ? v : 0.5);
 }
 
 int main(int argc, char **argv) {
@@ -33,12 +35,12 @@ int main(int argc, char **argv) {
     fclose(f);
     const size_t n = x.size();
     double *dx, *dout;
-    if (hipMalloc(&dx, n * sizeof(double)) != hipSuccess || hipMalloc(&dout, 7 * n * sizeof(double)) != hipSuccess)
+    if (hipMalloc(&dx, n * sizeof(double)) != hipSuccess || hipMalloc(&dout, 8 * n * sizeof(double)) != hipSuccess)
         return 3;
     hipMemcpy(dx, x.data(), n * sizeof(double), hipMemcpyHostToDevice);
     hipLaunchKernelGGL(probe, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dx, n, dout);
-    std::vector<double> out(7 * n);
-    if (hipMemcpy(out.data(), dout, 7 * n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return 4;
+    std::vector<double> out(8 * n);
+    if (hipMemcpy(out.data(), dout, 8 * n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return 4;
     hipFree(dx);
     hipFree(dout);
     FILE *g = fopen(argv[2], "wb");
