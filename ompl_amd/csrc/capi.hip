@@ -217,6 +217,7 @@ struct ompl_gpu_mv {
     unsigned long long *counters = nullptr;  // valid, invalid, isValid calls
     std::mutex mu;
     DevBuf s1, s2, valid, nd, fi, ms;
+    DevBuf edge_q;  // per-edge CSR segment (query) of ompl_gpu_mv_check_edges_device, written on this stream
 };
 
 extern "C" {
@@ -1349,24 +1350,25 @@ ompl_gpu_status ompl_gpu_mv_check_edges_device(ompl_gpu_mv *mv, ompl_gpu_nn *nn,
         if (s != OMPL_GPU_OK) return s;
     }
     uint32_t *qidx = nullptr;
-    if (d_offsets) {
-        HIP_OR_FAIL(nn->edge_q.ensure(sizeof(uint32_t) * m));
-        qidx = (uint32_t *)nn->edge_q.p;
+    if (d_offsets) {  // validator-owned: written and read on the validator's stream only
+        HIP_OR_FAIL(mv->edge_q.ensure(sizeof(uint32_t) * m));
+        qidx = (uint32_t *)mv->edge_q.p;
     }
-    // the work already queued on nn's stream (the neighbour query, the AoS rows, the CSR segments)
-    // before the validator's stream reads it
-    auto order_after_nn = [&]() -> hipError_t {
-        if (nn->stream == mv->stream) return hipSuccess;
+    // `from`'s queued work before `to`'s stream goes on: nn -> mv before the validator reads the
+    // neighbour result and the AoS rows; mv -> nn at the end, so no later work on nn's stream (a
+    // query overwriting its scratch, an add growing the AoS rows) runs while the motion kernel reads
+    auto order = [&](hipStream_t from, hipStream_t to) -> hipError_t {
+        if (from == to) return hipSuccess;
         hipEvent_t ev;
         hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
         if (e != hipSuccess) return e;
-        if ((e = hipEventRecord(ev, nn->stream)) == hipSuccess) e = hipStreamWaitEvent(mv->stream, ev, 0);
+        if ((e = hipEventRecord(ev, from)) == hipSuccess) e = hipStreamWaitEvent(to, ev, 0);
         const hipError_t d = hipEventDestroy(ev);
         return e != hipSuccess ? e : d;
     };
     const double *aos = nn->n_total ? (const double *)nn->raw_aos.p : nullptr;
-    if (qidx) HIP_OR_FAIL(launch_edge_query(d_offsets, (uint32_t)nq, (uint64_t)m, qidx, nn->stream));
-    HIP_OR_FAIL(order_after_nn());
+    HIP_OR_FAIL(order(nn->stream, mv->stream));
+    if (qidx) HIP_OR_FAIL(launch_edge_query(d_offsets, (uint32_t)nq, (uint64_t)m, qidx, mv->stream));
     hipError_t e = aos ? launch_motion_edges(mv->sp, mv->ck, d_queries, qidx, d_ids, stride, from_query, aos, da,
                                              (uint32_t)m, d_valid, mv->counters, mv->stream)
                        : hipErrorNotSupported;
@@ -1375,8 +1377,8 @@ ompl_gpu_status ompl_gpu_mv_check_edges_device(ompl_gpu_mv *mv, ompl_gpu_nn *nn,
         size_t me = m;  // a CSR's existing edges: e < offsets[nq] (read back: this form synchronises)
         if (d_offsets) {
             uint64_t tot = 0;
-            HIP_OR_FAIL(hipMemcpyAsync(&tot, d_offsets + nq, sizeof(tot), hipMemcpyDeviceToHost, nn->stream));
-            HIP_OR_FAIL(hipStreamSynchronize(nn->stream));
+            HIP_OR_FAIL(hipMemcpyAsync(&tot, d_offsets + nq, sizeof(tot), hipMemcpyDeviceToHost, mv->stream));
+            HIP_OR_FAIL(hipStreamSynchronize(mv->stream));
             me = std::min<size_t>(m, tot);
             if (me < m) HIP_OR_FAIL(hipMemsetAsync(d_valid + me, 0, m - me, mv->stream));
             if (me == 0) return OMPL_GPU_OK;
@@ -1386,13 +1388,14 @@ ompl_gpu_status ompl_gpu_mv_check_edges_device(ompl_gpu_mv *mv, ompl_gpu_nn *nn,
         HIP_OR_FAIL(mv->s1.ensure(bytes));
         HIP_OR_FAIL(mv->s2.ensure(bytes));
         HIP_OR_FAIL(launch_edges(nn->sp, nn->raw, nn->cap, d_queries, (uint32_t)nq, d_offsets, d_ids, stride, m,
-                                 from_query, (double *)mv->s1.p, (double *)mv->s2.p, nn->stream, aos, da, qidx));
-        HIP_OR_FAIL(order_after_nn());
+                                 from_query, (double *)mv->s1.p, (double *)mv->s2.p, mv->stream, aos, da, qidx));
         HIP_OR_FAIL(launch_motion(mv->sp, mv->ck, (const double *)mv->s1.p, (const double *)mv->s2.p, (uint32_t)m,
                                   d_valid, nullptr, nullptr, mv->counters, mv->stream));
+        HIP_OR_FAIL(order(mv->stream, nn->stream));
         return OMPL_GPU_OK;
     }
     HIP_OR_FAIL(e);
+    HIP_OR_FAIL(order(mv->stream, nn->stream));
     return OMPL_GPU_OK;
 }
 

@@ -225,6 +225,10 @@ ompl_gpu_status ompl_gpu_rrtstar_tree_add(ompl_gpu_rrtstar_tree *t, size_t m, co
     for (size_t j = 0; j < m; ++j) {
         const int64_t p = parent ? parent[j] : -1;
         if (p < -1 || p >= (int64_t)(first + j)) return bad(OMPL_GPU_ERR_INVALID_ARG, "parent must be -1 or an earlier id");
+        // a start state's cost is the objective's identity (RRTstar.cpp:208-213): with any other
+        // cost a rewire could reach a root, which has no parent to leave (:620-631)
+        if (p == -1 && cost && !(cost[j] == 0.0))
+            return bad(OMPL_GPU_ERR_INVALID_ARG, "a start state (parent -1) must have cost 0");
     }
     try {
         grow(t, first + m);
@@ -339,6 +343,17 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
         for (size_t i = 0; ok && i < ns; ++i) ok = b.nearest[i] < n && b.off[i] <= b.off[i + 1];
         for (size_t j = 0; ok && j < b.ids.size(); ++j) ok = b.ids[j] < n;
         if (!ok) return bad(OMPL_GPU_ERR_INVALID_ARG, "staged batch names ids outside the tree");
+        // the added ids are new (>= the tree's size), strictly increasing, and each added state's
+        // nearest state and neighbours are earlier states
+        uint64_t next = t->parent.size();
+        for (size_t i = 0; ok && i < ns; ++i) {
+            const uint32_t x = b.added[i];
+            if (x == 0xFFFFFFFFu) continue;
+            ok = x >= next && b.nearest[i] < x;
+            next = (uint64_t)x + 1;
+            for (uint64_t j = b.off[i]; ok && j < b.off[i + 1]; ++j) ok = b.ids[j] < x;
+        }
+        if (!ok) return bad(OMPL_GPU_ERR_INVALID_ARG, "staged batch: added ids not new and increasing, or neighbours not earlier");
         grow(t, top);
         for (size_t i = 0; i < ns; ++i) {
             const uint32_t nm = b.nearest[i], x = b.added[i];
@@ -466,6 +481,7 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
                         const bool before = best == nb || t->costs[r] < bc || (t->costs[r] == bc && r < best);
                         const int8_t mark = r == best ? 1 : (before ? -1 : 0);
                         const uint32_t v = ids[r];
+                        if (t->parent[v] < 0) continue;  // a start state keeps no parent (cost 0: never lowered)
                         const double nc = cx + d[r];
                         if (touched.has(v) && !(nc < t->cost[v])) continue;
                         bool ok;
@@ -493,7 +509,7 @@ ompl_gpu_status ompl_gpu_rrtstar_commit(ompl_gpu_rrtstar_tree *t, double max_dis
                 const int8_t mark = r == best ? 1 : (before ? -1 : 0);
                 if ((before || r == best) && ids[r] != nm && d[r] < maxd) ++checks;  // checkMotion(nbh, x) calls
                 const uint32_t v = ids[r];
-                if ((int64_t)v == m_parent) continue;
+                if ((int64_t)v == m_parent || t->parent[v] < 0) continue;  // a start state keeps no parent
                 const double nc = cx + d[r];
                 // the cost as this loop found it, or as an earlier rewire of this loop left it.  In a
                 // consistent tree (every cost = parent's cost + incCost, as RRT* keeps it) costs only

@@ -249,3 +249,45 @@ def test_check_edges_device(gpu, case):
             assert mv2.getInvalidMotionCount() == mv1.getInvalidMotionCount()
     ov, _, _, checks = O.check_motions(sp, ck, fr.cpu().numpy(), to.cpu().numpy())
     np.testing.assert_array_equal(v1, ov)
+
+
+def test_check_edges_device_back_to_back_streams(gpu):
+    """two CSR check_edges_device calls with different query sets on the handles' own (separate,
+    non-blocking) streams, synchronised only at the end: the second call's scratch
+    (the per-edge query index, the neighbour query's results) must not be overwritten while the
+    first call's motion kernel still reads it — every bit against the oracle validator."""
+    rng = np.random.default_rng(17)
+    dev = f"cuda:{gpu}"
+    sp = SE3StateSpace()
+    c, rad = W.sphere_field(32, 0.1, 7)
+    ck = SpheresChecker(c, rad)
+    data = W.uniform_se3(rng, 50000)
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    mv = DiscreteMotionValidatorGPU(sp, ck, gpu)
+    r, nq = 0.45, 400
+    qs = [W.uniform_se3(rng, nq) for _ in range(3)]
+    caps = []
+    for q in qs:  # sizes first (synchronous), then the timed-style back-to-back calls
+        off = torch.empty(nq + 1, dtype=torch.int64, device=dev)
+        dq = torch.from_numpy(q).to(dev)
+        caps.append(nn.radius_device(dq.data_ptr(), nq, r, off.data_ptr(), 0, 0, 0))
+    torch.cuda.synchronize()
+    bufs = [(q, torch.from_numpy(q).to(dev), torch.empty(nq + 1, dtype=torch.int64, device=dev),
+             torch.empty(cap, dtype=torch.int32, device=dev), torch.empty(cap, dtype=torch.float64, device=dev),
+             torch.full((cap,), 7, dtype=torch.uint8, device=dev)) for q, cap in zip(qs, caps)]
+    torch.cuda.synchronize()  # the buffers' fills (torch's stream) before the library's streams write them
+    for (q, dq, off, ids, dd, val), cap in zip(bufs, caps):
+        m = nn.radius_device(dq.data_ptr(), nq, r, off.data_ptr(), ids.data_ptr(), dd.data_ptr(), cap)
+        assert m == cap
+        mv.check_edges_device(nn, dq.data_ptr(), nq, off.data_ptr(), ids.data_ptr(), 0, m, True, val.data_ptr())
+    nn.sync()
+    mv.sync()
+    for q, _, off, ids, _, val in bufs:
+        o = off.cpu().numpy().astype(np.int64)
+        i = ids.cpu().numpy().astype(np.int64)
+        s1 = np.repeat(q, np.diff(o), axis=0)
+        ov = O.check_motions_mt(sp, ck, s1, data[i], 16)
+        np.testing.assert_array_equal(val.cpu().numpy().astype(bool), ov)
+    mv.close()
+    nn.close()

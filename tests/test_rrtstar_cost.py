@@ -158,6 +158,30 @@ def test_cost_logic_se3_hypercube_existing_tree():
     _run(sp, ck, tree, parent, inc, cost, samples, (200, 600))
 
 
+def test_cost_logic_inconsistent_tree():
+    """an existing tree whose costs are not parent's cost + incCost (each edge's share scaled by
+    0.6-1.4: costs still grow along every path, as any RRT* tree's must — an ancestor cheaper than
+    its descendant is what keeps a rewire from closing a cycle), so the commit takes its general
+    rewiring loop (costs may rise under updateChildCosts) — against the sequential loop"""
+    sp = RealVectorStateSpace(3)
+    c, r = W.sphere_field(32, 0.1, 7)
+    ck = SpheresChecker(c, r)
+    S.set_seed(11)
+    x = S.StateSampler(sp).sample_uniform(3000)
+    v = O.is_valid(sp, ck, x)
+    tree = x[v][:200]
+    parent = np.full(len(tree), -1, np.int64)
+    inc = np.zeros(len(tree))
+    for j in range(1, len(tree)):
+        oi, od, _ = O.knn(sp, tree[:j], tree[j][None], 1)
+        parent[j], inc[j] = int(oi[0, 0]), od[0, 0]
+    f = np.random.default_rng(3).uniform(0.6, 1.4, len(tree))
+    cost = np.zeros(len(tree))
+    for j in range(1, len(tree)):
+        cost[j] = cost[parent[j]] + inc[j] * f[j]  # no longer parent's cost + incCost
+    _run(sp, ck, tree, parent, inc, cost, x[v][200:500], (100, 200))
+
+
 def test_commit_rejects_bad_batches():
     tree = _Tree()
     tree.add([-1], [0.0], [0.0])
@@ -171,4 +195,16 @@ def test_commit_rejects_bad_batches():
     # a parent that is not an earlier id
     p = np.array([3], np.int64)
     assert abi.lib.ompl_gpu_rrtstar_tree_add(tree.h, 1, _p(p), None, None) == abi.ERR_INVALID_ARG
+    # a start state with a cost other than the identity
+    p, cc = np.array([-1], np.int64), np.array([0.5])
+    assert abi.lib.ompl_gpu_rrtstar_tree_add(tree.h, 1, _p(p), None, _p(cc)) == abi.ERR_INVALID_ARG
+    # an added id that is not new (0 exists), and a neighbour that is not earlier than the added state
+    for added, ids in (([0], [0]), ([1], [1])):
+        tree.stage([0], added, [0.1], [0, 1], ids, [0.1], [3])
+        assert abi.lib.ompl_gpu_rrtstar_commit(tree.h, 1.0, 1, _p(near), None, None, C.byref(got)) == \
+            abi.ERR_INVALID_ARG
+    # added ids out of order
+    tree.stage([0, 0], [2, 1], [0.1, 0.1], [0, 1, 2], [0, 0], [0.1, 0.1], [3, 3])
+    near2 = np.empty(2, np.int64)
+    assert abi.lib.ompl_gpu_rrtstar_commit(tree.h, 1.0, 2, _p(near2), None, None, C.byref(got)) == abi.ERR_INVALID_ARG
     tree.close()
