@@ -8,7 +8,6 @@
 // Ids are insertion indices, as the reference NN stores copies of _T in insertion
 // order (NearestNeighborsLinear.h:78-88); the C++ wrapper maps id <-> _T.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -815,24 +814,12 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
             *res_d = sd;
             return OMPL_GPU_OK;
         }
-        // long segments: two stable radix passes, by id and then by distance
-        size_t tb1 = 0, tb2 = 0;
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb1, (const uint32_t *)ui, si,
-                                                                (const double *)ud, sd, (int)tot, (int)nq, d_qoff,
-                                                                d_qoff + 1, 0, 32, h->stream));
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb2, (const double *)sd, ud,
-                                                                (const uint32_t *)si, ui, (int)tot, (int)nq, d_qoff,
-                                                                d_qoff + 1, 0, 64, h->stream));
-        HIP_OR_FAIL(h->tmp.ensure(std::max(tb1, tb2)));
-        tb1 = tb2 = h->tmp.bytes;
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb1, (const uint32_t *)ui, si,
-                                                                (const double *)ud, sd, (int)tot, (int)nq, d_qoff,
-                                                                d_qoff + 1, 0, 32, h->stream));
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb2, (const double *)sd, ud,
-                                                                (const uint32_t *)si, ui, (int)tot, (int)nq, d_qoff,
-                                                                d_qoff + 1, 0, 64, h->stream));
-        *res_i = ui;
-        *res_d = ud;
+        // long segments: the merge-pass segmented sort by (distance, id)
+        HIP_OR_FAIL(h->tmp.ensure(segment_sort_workspace(tot)));
+        int second = 0;
+        HIP_OR_FAIL(launch_segment_sort(d_qoff, (uint32_t)nq, tot, tm[1], ui, ud, si, sd, h->tmp.p, h->stream, &second));
+        *res_i = second ? si : ui;
+        *res_d = second ? sd : ud;
         return OMPL_GPU_OK;
     }
     // exact fp64 scan (OMPL_GPU_EXACT_ONLY / set_exact, SO3, KCHAIN): hits per (query, chunk)
@@ -846,13 +833,14 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
     HIP_OR_FAIL(hipMemcpyAsync(cnt.data(), h->counts.p, sizeof(uint32_t) * nc, hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     std::vector<uint64_t> off(nc), qoff(nq + 1);
-    uint64_t tot = 0;
+    uint64_t tot = 0, longest = 0;
     for (size_t q = 0; q < nq; ++q) {
         qoff[q] = tot;
         for (uint32_t c = 0; c < p.chunks; ++c) {
             off[q * p.chunks + c] = tot;
             tot += cnt[q * p.chunks + c];
         }
+        longest = std::max<uint64_t>(longest, tot - qoff[q]);
     }
     qoff[nq] = tot;
     *total = tot;
@@ -871,17 +859,13 @@ static ompl_gpu_status radius_features_locked(ompl_gpu_nn *h, const double *d_qf
         HIP_OR_FAIL(launch_radius_fill(h->sp, h->g, p, h->feat, h->cap, n_end, d_qf, (uint32_t)nq, r,
                                        (const uint64_t *)h->offsets.p, (uint32_t *)h->ids.p, (double *)h->dists.p,
                                        h->stream));
-        size_t tb = 0;
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(
-            nullptr, tb, (const double *)h->dists.p, (double *)h->sorted_d.p, (const uint32_t *)h->ids.p,
-            (uint32_t *)h->sorted_ids.p, (int)tot, (int)nq, d_qoff, d_qoff + 1, 0, 64, h->stream));
-        HIP_OR_FAIL(h->tmp.ensure(tb));
-        tb = h->tmp.bytes;
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(
-            h->tmp.p, tb, (const double *)h->dists.p, (double *)h->sorted_d.p, (const uint32_t *)h->ids.p,
-            (uint32_t *)h->sorted_ids.p, (int)tot, (int)nq, d_qoff, d_qoff + 1, 0, 64, h->stream));
-        *res_i = (const uint32_t *)h->sorted_ids.p;
-        *res_d = (const double *)h->sorted_d.p;
+        HIP_OR_FAIL(h->tmp.ensure(segment_sort_workspace(tot)));
+        int second = 0;
+        HIP_OR_FAIL(launch_segment_sort(d_qoff, (uint32_t)nq, tot, longest, (uint32_t *)h->ids.p, (double *)h->dists.p,
+                                        (uint32_t *)h->sorted_ids.p, (double *)h->sorted_d.p, h->tmp.p, h->stream,
+                                        &second));
+        *res_i = (const uint32_t *)(second ? h->sorted_ids.p : h->ids.p);
+        *res_d = (const double *)(second ? h->sorted_d.p : h->dists.p);
     }
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));  // the host offset vectors are released on return
     return OMPL_GPU_OK;
@@ -1627,24 +1611,15 @@ ompl_gpu_status prm_batch_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *
     }
     if (tot && longest <= kRankSortMax) {  // every segment fits a wave's LDS: rank placement by (distance, id)
         HIP_OR_FAIL(launch_segment_rank_sort(off, ci, cd, (uint32_t)rows, sii, sdd, h->stream));
-    } else if (tot) {  // long segments: two stable radix passes, by id and then by distance
-        size_t tb1 = 0, tb2 = 0;
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb1, (const uint32_t *)ci, sii,
-                                                                (const double *)cd, sdd, (int)tot, (int)rows, off,
-                                                                off + 1, 0, 32, h->stream));
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb2, (const double *)sdd, cd,
-                                                                (const uint32_t *)sii, ci, (int)tot, (int)rows, off,
-                                                                off + 1, 0, 64, h->stream));
-        HIP_OR_FAIL(h->tmp.ensure(std::max(tb1, tb2)));
-        tb1 = tb2 = h->tmp.bytes;
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb1, (const uint32_t *)ci, sii,
-                                                                (const double *)cd, sdd, (int)tot, (int)rows, off,
-                                                                off + 1, 0, 32, h->stream));
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb2, (const double *)sdd, cd,
-                                                                (const uint32_t *)sii, ci, (int)tot, (int)rows, off,
-                                                                off + 1, 0, 64, h->stream));
-        std::swap(cd, sdd);  // the result is in (cd, ci): read it from there
-        std::swap(ci, sii);
+    } else if (tot) {  // long segments: the merge-pass segmented sort by (distance, id)
+        HIP_OR_FAIL(h->tmp.ensure(segment_sort_workspace(tot)));
+        int second = 0;
+        HIP_OR_FAIL(launch_segment_sort(off, (uint32_t)rows, tot, longest, ci, cd, sii, sdd, h->tmp.p, h->stream,
+                                        &second));
+        if (!second) {  // the result is in (cd, ci): read it from there
+            std::swap(cd, sdd);
+            std::swap(ci, sii);
+        }
     }
     HIP_OR_FAIL(launch_prm_take(sii, sdd, off, dkj + j0, (uint32_t)rows, k_cap, d_nbr, d_cnt, d_dist, h->stream));
     if (!mv) return add_locked(h, states, m, nullptr, bf, braw);  // lazy: edge validity unknown (LazyPRM.cpp:302)
@@ -1839,6 +1814,7 @@ ompl_gpu_status rrtstar_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_
     HIP_OR_FAIL(launch_exclusive_scan_u64(len, m, off, R.scan.p, st));
     uint64_t hdr[2] = {0, 0};  // total, longest
     HIP_OR_FAIL(hipMemcpyAsync(&hdr[0], off + m, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipMemcpyAsync(&hdr[1], len + m + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipStreamSynchronize(st));
     const uint64_t tot = hdr[0];
     HIP_OR_FAIL(R.cd.ensure(sizeof(double) * std::max<uint64_t>(tot, 1)));
@@ -1878,18 +1854,11 @@ ompl_gpu_status rrtstar_locked(ompl_gpu_nn *h, ompl_gpu_mv *mv, const double *d_
         HIP_OR_FAIL(R.bits.ensure(sizeof(double) * std::max<uint64_t>(tot, 1)));
         uint32_t *sii = (uint32_t *)R.sorti.p;
         double *sdd = (double *)R.bits.p;
-        size_t tb1 = 0, tb2 = 0;
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb1, (const uint32_t *)ci, sii, (const double *)cd,
-                                                                sdd, (int)tot, (int)m, off, off + 1, 0, 32, st));
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb2, (const double *)sdd, cd, (const uint32_t *)sii,
-                                                                ci, (int)tot, (int)m, off, off + 1, 0, 64, st));
-        HIP_OR_FAIL(h->tmp.ensure(std::max(tb1, tb2)));
-        tb1 = tb2 = h->tmp.bytes;
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb1, (const uint32_t *)ci, sii, (const double *)cd,
-                                                                sdd, (int)tot, (int)m, off, off + 1, 0, 32, st));
-        HIP_OR_FAIL(hipcub::DeviceSegmentedRadixSort::SortPairs(h->tmp.p, tb2, (const double *)sdd, cd, (const uint32_t *)sii,
-                                                                ci, (int)tot, (int)m, off, off + 1, 0, 64, st));
-        HIP_OR_FAIL(launch_rrtstar_take(off, ci, cd, ooff, m, oi, odist, oseg, st));
+        HIP_OR_FAIL(h->tmp.ensure(segment_sort_workspace(tot)));
+        int second = 0;
+        HIP_OR_FAIL(launch_segment_sort(off, (uint32_t)m, tot, std::max<uint64_t>(hdr[1], 1), ci, cd, sii, sdd, h->tmp.p,
+                                        st, &second));
+        HIP_OR_FAIL(launch_rrtstar_take(off, second ? sii : ci, second ? sdd : cd, ooff, m, oi, odist, oseg, st));
     }
     // 4. both motion bits of every neighbourhood entry: checkMotion(nbh, x_j), checkMotion(x_j, nbh)
     s = ensure_aos(h);

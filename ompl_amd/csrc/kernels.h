@@ -261,6 +261,12 @@ constexpr uint32_t kRankSortMax = 1024;
 // in_stride != 0: segment q is read from [q * in_stride, ...) (a radius slab) instead of offsets[q]
 hipError_t launch_segment_rank_sort(const uint64_t *offsets, const uint32_t *in_i, const double *in_d, uint32_t nq,
                                     uint32_t *out_i, double *out_d, hipStream_t st, uint32_t in_stride = 0);
+// every segment [off[s], off[s + 1]) of (i0, d0) sorted by (distance, id), segments of any length
+// (max_len >= the longest): bottom-up merge passes between (i0, d0) and (i1, d1); *in_second says
+// which pair holds the result.  ws: segment_sort_workspace(n) bytes.
+size_t segment_sort_workspace(uint64_t n);
+hipError_t launch_segment_sort(const uint64_t *off, uint32_t nseg, uint64_t n, uint64_t max_len, uint32_t *i0,
+                               double *d0, uint32_t *i1, double *d1, void *ws, hipStream_t st, int *in_second);
 // motion endpoints of neighbour results: edge e pairs query q with stored state ids[e]
 // (CSR offsets, or offsets == nullptr and e = q * stride + j)
 // aos (optional): [n][da] copy of the raw states (launch_aos_rows), read instead of the SoA store

@@ -40,7 +40,7 @@
 // Included by one translation unit per space (knn_fast_{se3,so3,rv}.hip) so that the
 // template instantiations compile in parallel; knn_fast.hip holds the dispatch.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // (rocPRIM block primitives need memset declared)
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
@@ -193,13 +193,16 @@ __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, Fa
 // queries sorted by home tile.  Home-tile keys (< bins = the k-d tiles) take a counting sort over
 // the whole grid — a count kernel whose atomicAdd also hands each query its slot inside its tile,
 // a one-block exclusive scan of the bins, a scatter: three launches; queries of one tile land in
-// any order, which only changes how the walk's groups are formed, never a result.  Morton keys
-// (32 bits, no k-d tree) take the library radix sort.  (Measured and rejected in round 3: a
-// one-block LDS counting sort, one CU doing every atomic and write: nn phase 1.41 -> 1.48 ms.)
+// any order, which only changes how the walk's groups are formed, never a result.  Wider keys
+// (32-bit Morton codes when there is no k-d tree; the tail's Morton / home keys) are counted by
+// their top 16 bits (key >> shift): 65,536 cells of the Morton curve, order inside a cell
+// arbitrary — a coarser curve, still exact (tile order never changes a result).  (Measured and
+// rejected in round 3: a one-block LDS counting sort, one CU doing every atomic and write: nn
+// phase 1.41 -> 1.48 ms.)
 __global__ void home_count_kernel(const uint32_t *__restrict__ keys, uint32_t nq, uint32_t *__restrict__ cnt,
-                                  uint32_t *__restrict__ slot) {
+                                  uint32_t *__restrict__ slot, int shift) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nq) slot[i] = atomicAdd(&cnt[keys[i]], 1u);
+    if (i < nq) slot[i] = atomicAdd(&cnt[keys[i] >> shift], 1u);
 }
 // exclusive scan of the bin counts in two levels: each block of 1,024 bins in place (coalesced,
 // one block scan) with its total to bsum, then the block totals by one block; the scatter adds
@@ -232,35 +235,50 @@ __global__ __launch_bounds__(1024) void home_scan_blocks_kernel(uint32_t *__rest
 __global__ void home_scatter_kernel(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ idx,
                                     const uint32_t *__restrict__ slot, uint32_t nq, const uint32_t *__restrict__ start,
                                     const uint32_t *__restrict__ bsum, uint32_t *__restrict__ keys2,
-                                    uint32_t *__restrict__ perm) {
+                                    uint32_t *__restrict__ perm, int shift) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nq) return;
-    const uint32_t k = keys[i], p = bsum[k >> 10] + start[k] + slot[i];
+    const uint32_t k = keys[i], c = k >> shift, p = bsum[c >> 10] + start[c] + slot[i];
     keys2[p] = k;
     perm[p] = idx[i];
 }
-inline hipError_t sort_home_keys(char *cub, size_t cub_bytes, const uint32_t *keys, uint32_t *keys2,
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+constexpr int kCountBitsMax = 16;  // counting-sort cells of a wide key: its top 16 bits
+// scratch of sort_home_keys without a caller's bin array: the slots, then 2^16 bins padded to
+// 1,024 and their block sums
+inline size_t home_sort_bytes(uint32_t n) {
+    return align_up(4ull * std::max<uint32_t>(n, 1)) + 4ull * ((1u << kCountBitsMax) / 1024 * 1025 + 1);
+}
+// (keys, idx) -> (keys2, perm) ordered by key >> shift; shift = 0 with a caller's bin array
+// (qcount, bins > every key: the k-d home tiles), else the key's top kCountBitsMax of key_bits
+inline hipError_t sort_home_keys(char *ws, size_t ws_bytes, const uint32_t *keys, uint32_t *keys2,
                                  const uint32_t *idx, uint32_t *perm, uint32_t nq, int key_bits, hipStream_t st,
                                  uint32_t *qcount = nullptr, uint32_t bins = 0, bool zeroed = false) {
-    // the counting sort (measured 0.081-0.083 ms against 0.113-0.115 ms for the radix sort of the
-    // nn phase outside the walk on cfg3); the radix sort stays for Morton keys (32 bits)
-    if (qcount && bins && key_bits < 32 && cub_bytes >= 4ull * nq) {
-        uint32_t *slot = (uint32_t *)cub;  // the radix sort's temporary storage holds the slots
-        if (!zeroed) {  // (query_rows_kernel zeroes the bins when the caller listed them)
-            const hipError_t e = hipMemsetAsync(qcount, 0, 4ull * bins, st);
-            if (e != hipSuccess) return e;
-        }
-        const uint32_t nb = (bins + 1023) / 1024;
-        uint32_t *bsum = qcount + nb * 1024;  // qcount holds the bins padded to 1,024, then the block sums
-        hipLaunchKernelGGL(home_count_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, keys, nq, qcount, slot);
-        hipLaunchKernelGGL(home_scan_kernel, dim3(nb), dim3(1024), 0, st, qcount, bins, bsum);
-        hipLaunchKernelGGL(home_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, bsum, nb);
-        hipLaunchKernelGGL(home_scatter_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, keys, idx, slot, nq, qcount,
-                           bsum, keys2, perm);
-        return hipGetLastError();
+    // the counting sort (measured 0.081-0.083 ms against 0.113-0.115 ms for a radix sort of the
+    // nn phase outside the walk on cfg3)
+    if (nq == 0) return hipSuccess;
+    if (ws_bytes < 4ull * nq) return hipErrorInvalidValue;
+    uint32_t *slot = (uint32_t *)ws;
+    int shift = 0;
+    if (!(qcount && bins)) {  // own bins after the slots: the key's top bits
+        if (ws_bytes < home_sort_bytes(nq)) return hipErrorInvalidValue;
+        shift = std::max(0, key_bits - kCountBitsMax);
+        bins = (uint32_t)((((uint64_t)1 << key_bits) - 1) >> shift) + 1;
+        qcount = (uint32_t *)(ws + align_up(4ull * nq));
+        zeroed = false;
     }
-    size_t cb = cub_bytes;
-    return hipcub::DeviceRadixSort::SortPairs(cub, cb, keys, keys2, idx, perm, (int)nq, 0, key_bits, st);
+    if (!zeroed) {  // (query_rows_kernel zeroes the bins when the caller listed them)
+        const hipError_t e = hipMemsetAsync(qcount, 0, 4ull * bins, st);
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t nb = (bins + 1023) / 1024;
+    uint32_t *bsum = qcount + nb * 1024;  // qcount holds the bins padded to 1,024, then the block sums
+    hipLaunchKernelGGL(home_count_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, keys, nq, qcount, slot, shift);
+    hipLaunchKernelGGL(home_scan_kernel, dim3(nb), dim3(1024), 0, st, qcount, bins, bsum);
+    hipLaunchKernelGGL(home_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, bsum, nb);
+    hipLaunchKernelGGL(home_scatter_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, keys, idx, slot, nq, qcount,
+                       bsum, keys2, perm, shift);
+    return hipGetLastError();
 }
 
 template <int FS>
@@ -2195,7 +2213,6 @@ FastPlan fast_plan(const DevSpace &sp, uint32_t nq, uint32_t k, uint64_t n_end, 
     return p;
 }
 
-inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct FastLayout {
     size_t keys, keys2, idx, perm, cub, q32u, q32, pd, pi, fail, tau, total;
@@ -2214,10 +2231,7 @@ FastLayout fast_layout(const DevSpace &sp, const FeatGeom &g, const FastPlan &p,
     L.keys2 = take(4ull * nq);
     L.idx = take(4ull * nq);
     L.perm = take(4ull * nq);
-    size_t cb = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                             (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nq, 0, 32);
-    L.cub_bytes = std::max<size_t>(cb, 4ull * nq);  // also the counting sort's per-query slots
+    L.cub_bytes = home_sort_bytes(nq);  // the counting sort's per-query slots (+ its bins for wide keys)
     L.cub = take(L.cub_bytes);
     const int FS = sp.kind == OMPL_GPU_SPACE_SE3 ? 8 : g.F;
     L.q32u = take(4ull * nq * FS);
@@ -2412,10 +2426,7 @@ RadiusLayout radius_layout(const DevSpace &sp, const FeatGeom &g, uint32_t nq) {
     L.keys2 = take(4ull * nq);
     L.idx = take(4ull * nq);
     L.perm = take(4ull * nq);
-    size_t cb = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                             (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nq, 0, 32);
-    L.cub_bytes = std::max<size_t>(cb, 4ull * nq);  // also the counting sort's per-query slots
+    L.cub_bytes = home_sort_bytes(nq);  // the counting sort's per-query slots (+ its bins for wide keys)
     L.cub = take(L.cub_bytes);
     const int FS = sp.kind == OMPL_GPU_SPACE_SE3 ? 8 : g.F;
     L.q32u = take(4ull * nq * FS);
@@ -3553,9 +3564,7 @@ hipError_t append_sorted(const float *f32, const double *f64, uint64_t cap, uint
     }
     const uint32_t n_tail = (uint32_t)n_tail64;
     if (n_tail == 0) return hipSuccess;
-    size_t cub = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                             (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n_tail, 0, 32);
+    const size_t cub = home_sort_bytes(n_tail);
     size_t off = 0;
     auto take = [&](size_t bb) {
         const size_t o = off;
@@ -3571,8 +3580,9 @@ hipError_t append_sorted(const float *f32, const double *f64, uint64_t cap, uint
     const dim3 b256(256);
     hipLaunchKernelGGL((tail_keys_kernel<SP, F>), dim3((n_tail + 255) / 256), b256, 0, st, f32, cap, s->main_covered,
                        n_tail, b, s->nodes, s->kd_tiles, k0, i0);
-    if ((e = hipcub::DeviceRadixSort::SortPairs(w + o_cub, cub, k0, k1, i0, i1, (int)n_tail, 0, 32, st)) != hipSuccess)
-        return e;
+    // Morton keys: 32 bits; the chain's home tiles: below kd_tiles
+    const int key_bits = SP == OMPL_GPU_SPACE_KCHAIN ? (s->kd_tiles > 1 ? 32 - __builtin_clz(s->kd_tiles - 1) : 1) : 32;
+    if ((e = sort_home_keys(w + o_cub, cub, k0, k1, i0, i1, n_tail, key_bits, st)) != hipSuccess) return e;
     const uint32_t tiles = (n_tail + kCullTile - 1) / kCullTile;
     const uint32_t p0 = s->tail_t0 * kCullTile, p1 = p0 + tiles * kCullTile;
     hipLaunchKernelGGL((sorted_gather_kernel<SP, F>), dim3((p1 - p0 + 255) / 256), b256, 0, st, f32, cap, i1, n_tail,

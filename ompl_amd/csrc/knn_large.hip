@@ -13,7 +13,7 @@
 //   4. stable segmented radix sort by fp64 distance -> (distance, id) order; the first k
 //      of each query's segment are the answer (exact, as the reference's ascending list).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // (rocPRIM block primitives need memset declared)
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
@@ -387,15 +387,14 @@ hipError_t run_large(const DevSpace &sp, const double *f64, const float *f32, ui
         const dim3 gb((nqb + kTile - 1) / kTile, p.chunks);
         hipLaunchKernelGGL((select_kernel<SP, F, true>), gb, dim3(kTile), 0, st, f32, f64, cap, n_end, q32, qf64, q0,
                            q1, p.chunk_len, p.chunks, sp, radius, nullptr, d_off, cd, ci);
-        size_t tb = 0;
-        TRYB(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, cd, sd, ci, si, (int)run, (int)nqb, d_seg,
-                                                          d_seg + 1, 0, 64, st));
-        TRYB(hipMalloc(&tmp, std::max<size_t>(tb, 1)));
-        TRYB(hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, tb, cd, sd, ci, si, (int)run, (int)nqb, d_seg,
-                                                          d_seg + 1, 0, 64, st));
+        uint64_t longest = 0;
+        for (uint32_t ql = 0; ql < nqb; ++ql) longest = std::max<uint64_t>(longest, seg[ql + 1] - seg[ql]);
+        TRYB(hipMalloc(&tmp, segment_sort_workspace(run)));
+        int second = 0;  // (distance, id) order: the candidates' ties by id
+        TRYB(launch_segment_sort(d_seg, nqb, run, longest, ci, cd, si, sd, tmp, st, &second));
         const uint64_t nout = (uint64_t)nqb * k;
-        hipLaunchKernelGGL(take_first_k_kernel, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, st, sd, si, d_seg,
-                           q0, nqb, k, out_d, out_i);
+        hipLaunchKernelGGL(take_first_k_kernel, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, st,
+                           second ? sd : cd, second ? si : ci, d_seg, q0, nqb, k, out_d, out_i);
         TRYB(hipStreamSynchronize(st));
         free_batch();
 #undef TRYB

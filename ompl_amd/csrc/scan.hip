@@ -3,6 +3,10 @@
 // and optionally the largest element (the radius path's longest segment).  Three launches, no host
 // round trip: per-1,024-element block totals (and maxima), one block scanning the totals, then
 // every block's local scan plus its offset.  Wave scans by shuffles.
+//
+// Also the segmented sort by (distance, id) for segments too long for a wave's LDS rank sort
+// (knn.hip segment_rank_sort_kernel, <= kRankSortMax): bottom-up merge passes, each element placing
+// itself by a binary search in its partner run (merge path), ping-pong buffers.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -118,7 +122,76 @@ __global__ __launch_bounds__(256) void scan_apply_kernel(const uint64_t *__restr
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 255) out[n] = part[blockIdx.x] + tot;
 }
 
+// (distance, id) as one total order: the distance's bits made monotone (NaN above +inf)
+__device__ __forceinline__ uint64_t dist_order(double d) {
+    const uint64_t u = (uint64_t)__double_as_longlong(d);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__global__ void segment_of_kernel(const uint64_t *__restrict__ off, uint32_t nseg, uint64_t n,
+                                  uint32_t *__restrict__ seg) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    uint32_t lo = 0, hi = nseg;  // the last segment whose start is <= t
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= t) lo = mid; else hi = mid;
+    }
+    seg[t] = lo;
+}
+
+// one pass: runs of w elements of a segment merged pairwise; an element of the left run counts the
+// partner's elements ordered before it, one of the right run those ordered before or equal
+__global__ void merge_pass_kernel(const uint64_t *__restrict__ off, const uint32_t *__restrict__ seg, uint64_t n,
+                                  uint64_t w, const uint32_t *__restrict__ in_i, const double *__restrict__ in_d,
+                                  uint32_t *__restrict__ out_i, double *__restrict__ out_d) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t s = seg[t];
+    const uint64_t a = off[s], b = off[s + 1], p = t - a, r = p / w;
+    const uint64_t pa = a + (r ^ 1) * w, pb = pa + w < b ? pa + w : b;
+    const uint32_t id = in_i[t];
+    const double d = in_d[t];
+    if (pa >= b) {  // the segment's last run has no partner this pass
+        out_i[t] = id;
+        out_d[t] = d;
+        return;
+    }
+    const uint64_t key = dist_order(d);
+    const bool left = (r & 1) == 0;
+    uint64_t lo = pa, hi = pb;  // first partner element not ordered before this one
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const uint64_t km = dist_order(in_d[mid]);
+        const uint32_t im = in_i[mid];
+        const bool before = left ? (km < key || (km == key && im < id)) : (km < key || (km == key && im <= id));
+        if (before) lo = mid + 1; else hi = mid;
+    }
+    const uint64_t pos = a + (r & ~1ull) * w + (p - r * w) + (lo - pa);
+    out_i[pos] = id;
+    out_d[pos] = d;
+}
+
 }  // namespace
+
+size_t segment_sort_workspace(uint64_t n) { return sizeof(uint32_t) * (n ? n : 1); }
+
+hipError_t launch_segment_sort(const uint64_t *off, uint32_t nseg, uint64_t n, uint64_t max_len, uint32_t *i0,
+                               double *d0, uint32_t *i1, double *d1, void *ws, hipStream_t st, int *in_second) {
+    *in_second = 0;
+    if (n == 0 || nseg == 0 || max_len < 2) return hipSuccess;
+    uint32_t *seg = (uint32_t *)ws;
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(segment_of_kernel, dim3(blocks), dim3(256), 0, st, off, nseg, n, seg);
+    int cur = 0;
+    for (uint64_t w = 1; w < max_len; w <<= 1) {
+        hipLaunchKernelGGL(merge_pass_kernel, dim3(blocks), dim3(256), 0, st, off, seg, n, w, cur ? i1 : i0,
+                           cur ? d1 : d0, cur ? i0 : i1, cur ? d0 : d1);
+        cur ^= 1;
+    }
+    *in_second = cur;
+    return hipGetLastError();
+}
 
 size_t exclusive_scan_u64_workspace(uint64_t n) {
     return sizeof(uint64_t) * (2 * ((n + kScanBlock - 1) / kScanBlock) + 1);

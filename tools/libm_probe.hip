@@ -40,7 +40,13 @@ int main(int argc, char **argv) {
     hipMemcpy(dx, x.data(), n * sizeof(double), hipMemcpyHostToDevice);
     hipLaunchKernelGGL(probe, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dx, n, dout);
     std::vector<double> out(8 * n);
-    if (hipMemcpy(out.data(), dout, 8 * n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return 4;
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out.data(), dout, 8 * n * sizeof(double), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        fprintf(stderr, "libm_probe: %s\n", hipGetErrorString(e));
+        return 4;
+    }
     hipFree(dx);
     hipFree(dout);
     FILE *g = fopen(argv[2], "wb");
