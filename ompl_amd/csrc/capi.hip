@@ -642,17 +642,16 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
                                     &d_fail_count, &d_fail_list));
         // exact re-run of the uncertified queries, decided on the device: the bounded pass (one
         // store read for all of them), a full scan for any that overflow its candidate cap
-        HIP_OR_FAIL(launch_knn_bounded(h->sp, h->g, h->feat, h->cap, n_end, d_qf, d_fail_list, d_fail_count, k, d_dist,
-                                       d_ids, cnt, (double *)h->fb_cd.p, (uint32_t *)h->fb_ci.p, h->num_cus,
-                                       h->stream));
-        h->fast_queries += nq;
+        // (stats_dev: the re-run statistics, accumulated by the re-run's last kernel)
         HIP_OR_FAIL(h->stats_dev.ensure(2 * sizeof(unsigned long long)));
         if (!h->stats_init) {
             HIP_OR_FAIL(hipMemsetAsync(h->stats_dev.p, 0, 2 * sizeof(unsigned long long), h->stream));
             h->stats_init = true;
         }
-        HIP_OR_FAIL(launch_count_add(d_fail_count, cnt + kBoundedMaxQ, (unsigned long long *)h->stats_dev.p,
-                                     h->stream));
+        HIP_OR_FAIL(launch_knn_bounded(h->sp, h->g, h->feat, h->cap, n_end, d_qf, d_fail_list, d_fail_count, k, d_dist,
+                                       d_ids, cnt, (double *)h->fb_cd.p, (uint32_t *)h->fb_ci.p, h->num_cus,
+                                       h->stream, (unsigned long long *)h->stats_dev.p));
+        h->fast_queries += nq;
         return OMPL_GPU_OK;
     }
     if (h->fast && screen_safe(h) && h->rows32 && stream32_supported(h->sp, h->g, (uint32_t)nq, k)) {

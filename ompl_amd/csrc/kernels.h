@@ -236,9 +236,7 @@ constexpr uint32_t kBoundedMaxQ = 512;
 hipError_t launch_knn_bounded(const DevSpace &sp, const FeatGeom &g, const double *feat, uint64_t cap,
                               uint64_t n_end, const double *qf, const uint32_t *list, const uint32_t *d_nlist,
                               uint32_t k, double *od, uint32_t *oi, uint32_t *counts, double *cand_d,
-                              uint32_t *cand_i, int num_cus, hipStream_t st);
-// acc[0] += *a; acc[1] += *b (device-side statistics, one thread)
-hipError_t launch_count_add(const uint32_t *a, const uint32_t *b, unsigned long long *acc, hipStream_t st);
+                              uint32_t *cand_i, int num_cus, hipStream_t st, unsigned long long *stats = nullptr);
 // gather rows q = list[i] of an AoS [*][F] fp64 array into dst[i]; scatter results back
 hipError_t launch_gather_rows(const double *src, int F, const uint32_t *list, uint32_t n, double *dst, hipStream_t st);
 hipError_t launch_scatter_results(const double *d, const uint32_t *ids, uint32_t k, const uint32_t *list, uint32_t n,

@@ -290,10 +290,16 @@ __global__ __launch_bounds__(256) void knn_full_list_kernel(const double *__rest
                                                             const uint32_t *__restrict__ count_ptr,
                                                             const uint32_t *__restrict__ list, DevSpace sp,
                                                             uint32_t out_k, double *__restrict__ out_d,
-                                                            uint32_t *__restrict__ out_i) {
+                                                            uint32_t *__restrict__ out_i,
+                                                            const uint32_t *__restrict__ fail_ptr,
+                                                            unsigned long long *__restrict__ stats) {
     __shared__ double lds_d[4 * K];
     __shared__ uint32_t lds_i[4 * K];
     const uint32_t count = *count_ptr;
+    if (stats && blockIdx.x == 0 && threadIdx.x == 0) {  // the re-run statistics (ompl_gpu_nn_stats)
+        stats[0] += *fail_ptr;
+        stats[1] += count;
+    }
     for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
         const uint32_t q = list[e];
         double qf[F];
@@ -322,7 +328,8 @@ __global__ __launch_bounds__(256) void knn_full_list_kernel(const double *__rest
 template <int SP, int F, int NMAX>
 hipError_t run_knn_bounded(const DevSpace &sp, const double *feat, uint64_t cap, uint64_t n_end, const double *qf,
                            const uint32_t *list, const uint32_t *d_nlist, uint32_t k, double *od, uint32_t *oi,
-                           uint32_t *counts, double *cand_d, uint32_t *cand_i, int num_cus, hipStream_t st) {
+                           uint32_t *counts, double *cand_d, uint32_t *cand_i, int num_cus, hipStream_t st,
+                           unsigned long long *stats) {
     constexpr int ITEMS = F <= 8 ? 4 : 1;
     const uint64_t blocks = (n_end + 256 * ITEMS - 1) / (256 * ITEMS);
     hipLaunchKernelGGL((knn_bounded_kernel<SP, F, NMAX, ITEMS>), dim3((uint32_t)blocks), dim3(256), 0, st, feat, cap,
@@ -335,7 +342,7 @@ hipError_t run_knn_bounded(const DevSpace &sp, const double *feat, uint64_t cap,
 #define OMPL_AMD_FULL(KK)                                                                                       \
     case KK:                                                                                                   \
         hipLaunchKernelGGL((knn_full_list_kernel<SP, F, NMAX, KK>), grid, dim3(256), 0, st, feat, cap, n_end, qf, \
-                           ov_count, ov_list, sp, k, od, oi);                                                  \
+                           ov_count, ov_list, sp, k, od, oi, d_nlist, stats);                                  \
         break;
         OMPL_AMD_FULL(1)
         OMPL_AMD_FULL(4)
@@ -744,10 +751,10 @@ hipError_t launch_knn(const DevSpace &sp, const FeatGeom &g, const double *feat,
 hipError_t launch_knn_bounded(const DevSpace &sp, const FeatGeom &g, const double *feat, uint64_t cap,
                               uint64_t n_end, const double *qf, const uint32_t *list, const uint32_t *d_nlist,
                               uint32_t k, double *od, uint32_t *oi, uint32_t *counts, double *cand_d,
-                              uint32_t *cand_i, int num_cus, hipStream_t st) {
+                              uint32_t *cand_i, int num_cus, hipStream_t st, unsigned long long *stats) {
     if (k == 0) return hipSuccess;
     OMPL_AMD_SPACE_DISPATCH(run_knn_bounded, sp, feat, cap, n_end, qf, list, d_nlist, k, od, oi, counts, cand_d, cand_i,
-                            num_cus, st)
+                            num_cus, st, stats)
 }
 
 RadiusPlan radius_plan(uint32_t nq, uint64_t n_end, int num_cus) {

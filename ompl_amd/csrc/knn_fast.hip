@@ -255,19 +255,6 @@ hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t
     return hipGetLastError();
 }
 
-namespace {
-__global__ void count_add_kernel(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b,
-                                 unsigned long long *__restrict__ acc) {
-    acc[0] += *a;
-    acc[1] += *b;
-}
-}  // namespace
-
-hipError_t launch_count_add(const uint32_t *a, const uint32_t *b, unsigned long long *acc, hipStream_t st) {
-    hipLaunchKernelGGL(count_add_kernel, dim3(1), dim3(1), 0, st, a, b, acc);
-    return hipGetLastError();
-}
-
 hipError_t launch_gather_rows(const double *src, int F, const uint32_t *list, uint32_t n, double *dst, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(gather_rows_kernel, dim3((n * F + 255) / 256), dim3(256), 0, st, src, F, list, n, dst);

@@ -141,7 +141,8 @@ __device__ __forceinline__ uint32_t kd_home_tile(const float *c, const KdNode *_
 template <int SP, int F>
 __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, FastBounds b, float *__restrict__ q32u,
                                   uint32_t *__restrict__ keys, uint32_t *__restrict__ idx,
-                                  const KdNode *__restrict__ nodes, uint32_t ntiles) {
+                                  const KdNode *__restrict__ nodes, uint32_t ntiles, uint32_t *__restrict__ qcnt = nullptr,
+                                  uint32_t *__restrict__ slot = nullptr) {
     constexpr int FS = Geo<SP, F>::FS;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 #pragma unroll
@@ -181,7 +182,9 @@ __global__ void query_rows_kernel(const double *__restrict__ qf, uint32_t nq, Fa
         } else {
             for (int d = 0; d < Geo<SP, F>::NB; ++d) c[d] = o[d];
         }
-        keys[i] = kd_home_tile(c, nodes, ntiles);
+        const uint32_t k = kd_home_tile(c, nodes, ntiles);
+        keys[i] = k;
+        if (qcnt) slot[i] = atomicAdd(&qcnt[k], 1u);  // the counting sort's count (home_place_kernel)
     } else {
         float c[kKeyDims];
         key_coords<SP>(x, c, b.nkey);
@@ -243,6 +246,70 @@ __global__ void home_scatter_kernel(const uint32_t *__restrict__ keys, const uin
     perm[p] = idx[i];
 }
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+// The home-key sort over the store's persistent bins (SortedStore::qcount: counts | start | block
+// sums), which stay zero between calls — zeroed once when allocated, and by home_bins_scan_kernel
+// as it reads them: query_rows_kernel counts (slot = its atomicAdd), the scan turns each block of
+// 1,024 counts into exclusive prefixes in start[] with the block's total in bsum, and
+// home_place_kernel puts each query at (prefix of the block totals) + start + slot, writing its
+// key and its fp32 row in sorted order.  Three launches instead of six (count, two scans, scatter,
+// row gather, and the zeroing of the bins).
+__global__ __launch_bounds__(1024) void home_bins_scan_kernel(uint32_t *__restrict__ cnt, uint32_t bins,
+                                                              uint32_t *__restrict__ start,
+                                                              uint32_t *__restrict__ bsum) {
+    using BlockScan = rocprim::block_scan<uint32_t, 1024>;
+    __shared__ typename BlockScan::storage_type sh;
+    const uint32_t b = blockIdx.x * 1024 + threadIdx.x;
+    const uint32_t c = b < bins ? cnt[b] : 0u;
+    uint32_t pre = 0, tot = 0;
+    BlockScan().exclusive_scan(c, pre, 0u, tot, sh);
+    if (b < bins) {
+        start[b] = pre;
+        cnt[b] = 0u;  // ready for the next call
+    }
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+template <int FS>
+__global__ __launch_bounds__(256) void home_place_kernel(const uint32_t *__restrict__ keys,
+                                                         const uint32_t *__restrict__ slot, uint32_t nq,
+                                                         const uint32_t *__restrict__ start,
+                                                         const uint32_t *__restrict__ bsum, uint32_t nb,
+                                                         const float *__restrict__ q32u, uint32_t *__restrict__ keys2,
+                                                         uint32_t *__restrict__ perm, float *__restrict__ q32) {
+    __shared__ uint32_t boff[1024];  // exclusive prefix of the block totals, 1,024 at a time
+    __shared__ uint32_t carry;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t k = i < nq ? keys[i] : 0u, kb = k >> 10;
+    uint32_t off = 0;
+    if (threadIdx.x == 0) carry = 0;
+    for (uint32_t c0 = 0; c0 < nb; c0 += 1024) {  // uniform trip count
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < 1024; t += blockDim.x) boff[t] = c0 + t < nb ? bsum[c0 + t] : 0u;
+        __syncthreads();
+        if (threadIdx.x == 0) {  // serial scan of <= 1,024 block totals (153 at 10^7 states)
+            uint32_t run = carry;
+            const uint32_t m = nb - c0 < 1024 ? nb - c0 : 1024;
+            for (uint32_t t = 0; t < m; ++t) {
+                const uint32_t v = boff[t];
+                boff[t] = run;
+                run += v;
+            }
+            carry = run;
+        }
+        __syncthreads();
+        if (i < nq && kb >= c0 && kb < c0 + 1024) off = boff[kb - c0];
+    }
+    if (i >= nq) return;
+    const uint32_t p = off + start[k] + slot[i];
+    keys2[p] = k;
+    perm[p] = i;
+#pragma unroll
+    for (int f = 0; f < FS; ++f) q32[(size_t)p * FS + f] = q32u[(size_t)i * FS + f];
+}
+// words of SortedStore::qcount for `tiles` bins: counts and start padded to 1,024, the block sums
+inline size_t home_bins_words(uint32_t tiles) {
+    const size_t nb = ((size_t)tiles + 1023) / 1024;
+    return 2 * nb * 1024 + nb + 1;
+}
 constexpr int kCountBitsMax = 16;  // counting-sort cells of a wide key: its top 16 bits
 // scratch of sort_home_keys without a caller's bin array: the slots, then 2^16 bins padded to
 // 1,024 and their block sums
@@ -288,6 +355,34 @@ __global__ void query_gather_kernel(const float *__restrict__ q32u, const uint32
     if (t >= nq * (uint32_t)FS) return;
     const uint32_t qs = t / FS, f = t % FS;
     q32[t] = q32u[(size_t)perm[qs] * FS + f];
+}
+
+// queries ordered by key for the walks: the home-key sort when the store has a k-d tree
+// (home_keys), else the counting sort on the Morton key's top bits + a row gather
+template <int SP, int F>
+hipError_t sort_queries(const double *qf64, uint32_t nq, const FastBounds &b, const SortedStore *ss, bool home_keys,
+                        char *ws, size_t ws_bytes, float *q32u, uint32_t *keys, uint32_t *keys2, uint32_t *idx,
+                        uint32_t *perm, float *q32, hipStream_t st, const KdNode *nodes, uint32_t ntiles) {
+    constexpr int FS = Geo<SP, F>::FS;
+    const dim3 b256(256);
+    if (home_keys) {
+        const uint32_t bins = ss->kd_tiles, nb = (bins + 1023) / 1024;
+        uint32_t *cnt = ss->qcount, *start = cnt + (size_t)nb * 1024, *bsum = start + (size_t)nb * 1024;
+        uint32_t *slot = (uint32_t *)ws;
+        if (ws_bytes < 4ull * nq) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys, idx,
+                           nodes, ntiles, cnt, slot);
+        hipLaunchKernelGGL(home_bins_scan_kernel, dim3(nb), dim3(1024), 0, st, cnt, bins, start, bsum);
+        hipLaunchKernelGGL((home_place_kernel<FS>), dim3((nq + 255) / 256), b256, 0, st, keys, slot, nq, start, bsum,
+                           nb, q32u, keys2, perm, q32);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys, idx,
+                       nodes, ntiles, nullptr, nullptr);
+    const hipError_t e = sort_home_keys(ws, ws_bytes, keys, keys2, idx, perm, nq, 32, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
+    return hipGetLastError();
 }
 
 // ---- screening --------------------------------------------------------------------------
@@ -2248,7 +2343,6 @@ template <int SP, int F, int K2, int K>
 hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, char *ws, const float *f32,
                     const double *f64, uint64_t cap, uint64_t n_end, const SortedStore *ss, const double *qf64,
                     uint32_t nq, uint32_t k, const FastBounds &b, double *od, uint32_t *oi, hipStream_t st) {
-    constexpr int FS = Geo<SP, F>::FS;
     uint32_t *keys = (uint32_t *)(ws + L.keys), *keys2 = (uint32_t *)(ws + L.keys2);
     uint32_t *idx = (uint32_t *)(ws + L.idx), *perm = (uint32_t *)(ws + L.perm);
     float *q32u = (float *)(ws + L.q32u), *q32 = (float *)(ws + L.q32);
@@ -2256,21 +2350,15 @@ hipError_t run_fast(const DevSpace &sp, const FastPlan &p, const FastLayout &L, 
     uint32_t *pi = (uint32_t *)(ws + L.pi);
     uint32_t *fail = (uint32_t *)(ws + L.fail);
     const dim3 b256(256);
-    // home-tile keys are below kd_tiles: sort only their bits (half the radix passes at 10^6
-    // states); Morton keys use all 32
+    // home-tile keys (a k-d tree): the fused counting sort over the store's bins; else Morton keys
     const bool home_keys = p.cull && ss && ss->nodes && ss->kd_tiles > 1;
-    const int key_bits = home_keys ? 32 - __builtin_clz(ss->kd_tiles - 1) : 32;
-    FastBounds bz = b;  // + the home-key bins and the fail count, zeroed by query_rows_kernel
-    bz.zero[1] = home_keys ? ss->qcount : nullptr;
-    bz.nzero[1] = home_keys ? ss->kd_tiles : 0u;
+    FastBounds bz = b;  // + the fail count, zeroed by query_rows_kernel
     bz.zero[2] = fail;
     bz.nzero[2] = 1u;
-    hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, bz, q32u, keys, idx,
-                       (p.cull && ss) ? ss->nodes : nullptr, (p.cull && ss) ? ss->kd_tiles : 0u);
-    hipError_t e = sort_home_keys(ws + L.cub, L.cub_bytes, keys, keys2, idx, perm, nq, key_bits, st,
-                                  home_keys ? ss->qcount : nullptr, home_keys ? ss->kd_tiles : 0u, true);
+    hipError_t e = sort_queries<SP, F>(qf64, nq, bz, ss, home_keys, ws + L.cub, L.cub_bytes, q32u, keys, keys2, idx,
+                                       perm, q32, st, (p.cull && ss) ? ss->nodes : nullptr,
+                                       (p.cull && ss) ? ss->kd_tiles : 0u);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
     bool walked = false;
     float chain_qerr = 0.f;  // the culled chain scan's 16-bit screen error (certificate)
     if constexpr (SP == OMPL_GPU_SPACE_SE3 || SP == OMPL_GPU_SPACE_REALVECTOR) {  // cull_supported
@@ -2442,27 +2530,24 @@ template <int SP, int F>
 hipError_t run_radius_fast(const DevSpace &sp, const RadiusLayout &L, char *ws, const double *f64, uint64_t cap,
                            const SortedStore *ss, const double *qf64, uint32_t nq, double r, const FastBounds &b,
                            int phase, uint32_t *out_i, double *out_d, hipStream_t st) {
-    constexpr int FS = Geo<SP, F>::FS;
     uint32_t *keys = (uint32_t *)(ws + L.keys), *keys2 = (uint32_t *)(ws + L.keys2);
     uint32_t *idx = (uint32_t *)(ws + L.idx), *perm = (uint32_t *)(ws + L.perm);
     float *q32u = (float *)(ws + L.q32u), *q32 = (float *)(ws + L.q32);
     uint64_t *counts = (uint64_t *)(ws + L.counts), *offs = (uint64_t *)(ws + L.off);
-    const dim3 grid((nq + kRadiusGroup - 1) / kRadiusGroup), b64(64), b256(256);
+    const dim3 grid((nq + kRadiusGroup - 1) / kRadiusGroup), b64(64);
     if (!ss->rows64) return hipErrorInvalidValue;
     (void)f64;
     (void)cap;
     hipError_t e;
     if (phase == 2 && (b.slab == 0 || !out_i || !out_d)) return hipErrorInvalidValue;
     if (phase == 0 || phase == 2) {
-        hipLaunchKernelGGL((query_rows_kernel<SP, F>), dim3((nq + 255) / 256), b256, 0, st, qf64, nq, b, q32u, keys,
-                           idx, ss->nodes, ss->kd_tiles);
         const bool home_keys = ss->nodes && ss->kd_tiles > 1;
-        const int key_bits = home_keys ? 32 - __builtin_clz(ss->kd_tiles - 1) : 32;  // home tiles
-        if ((e = sort_home_keys(ws + L.cub, L.cub_bytes, keys, keys2, idx, perm, nq, key_bits, st,
-                                home_keys ? ss->qcount : nullptr, home_keys ? ss->kd_tiles : 0u)) != hipSuccess)
+        FastBounds bz = b;  // + the walk's candidate total, zeroed by query_rows_kernel
+        bz.zero[2] = (uint32_t *)(counts + nq);
+        bz.nzero[2] = 2u;
+        if ((e = sort_queries<SP, F>(qf64, nq, bz, ss, home_keys, ws + L.cub, L.cub_bytes, q32u, keys, keys2, idx, perm,
+                                     q32, st, ss->nodes, ss->kd_tiles)) != hipSuccess)
             return e;
-        hipLaunchKernelGGL((query_gather_kernel<FS>), dim3((nq * FS + 255) / 256), b256, 0, st, q32u, perm, nq, q32);
-        if ((e = hipMemsetAsync(counts + nq, 0, 8, st)) != hipSuccess) return e;
         if (phase == 2) {
             timer_begin(st, "radius32_group_kernel");
             const dim3 gs((nq + kRadiusSlabGroup - 1) / kRadiusSlabGroup);
@@ -3389,7 +3474,9 @@ hipError_t sorted_alloc(SortedStore *s, uint32_t pad_tiles, uint32_t max_nodes, 
         dummy = 0;
         if ((e = grow_array(&s->tkey0, dummy, (size_t)pad_tiles)) != hipSuccess) return e;
         dummy = 0;
-        if ((e = grow_array(&s->qcount, dummy, ((size_t)pad_tiles + 1023) / 1024 * 1025 + 1)) != hipSuccess) return e;
+        if ((e = grow_array(&s->qcount, dummy, home_bins_words(pad_tiles))) != hipSuccess) return e;
+        // the home-key bins are zero between calls (home_bins_scan_kernel re-zeroes what it reads)
+        if ((e = hipMemsetAsync(s->qcount, 0, 4 * home_bins_words(pad_tiles), st)) != hipSuccess) return e;
         s->cap_pos = n_pad;
         hipLaunchKernelGGL(iota_kernel, dim3((pad_tiles + 255) / 256), dim3(256), 0, st, s->tkey0, pad_tiles);
         if ((e = hipGetLastError()) != hipSuccess) return e;
