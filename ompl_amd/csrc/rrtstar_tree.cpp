@@ -119,13 +119,9 @@ public:
         }
         job_ = &f;
         pending_.store(n_ - 1, std::memory_order_relaxed);
-        if (active_.load(std::memory_order_relaxed)) {  // the workers spin: no wake-up call
-            gen_.fetch_add(1, std::memory_order_release);
-        } else {
-            {
-                std::lock_guard<std::mutex> lk(mu_);
-                gen_.fetch_add(1, std::memory_order_release);
-            }
+        gen_.fetch_add(1, std::memory_order_seq_cst);
+        if (sleepers_.load(std::memory_order_seq_cst) > 0) {  // wake the workers that stopped spinning
+            { std::lock_guard<std::mutex> lk(mu_); }
             cv_.notify_all();
         }
         f(0);
@@ -133,17 +129,32 @@ public:
     }
 
 private:
+    // a worker spins for the next job while the pool is active, at most kSpin pauses after its last
+    // one (the two pool phases of a sample are microseconds apart), then sleeps until a job or the
+    // end: a sequential stretch of the commit (the rewiring loop) or the time between commits does
+    // not keep the host cores busy
+    static constexpr int kSpin = 1 << 14;
     void work(int k) {
         uint64_t seen = 0;
         for (;;) {
+            int spins = 0;
             while (gen_.load(std::memory_order_acquire) == seen) {
-                if (!active_.load(std::memory_order_relaxed)) {
-                    std::unique_lock<std::mutex> lk(mu_);
-                    cv_.wait(lk, [&] { return quit_ || active_.load() || gen_.load() != seen; });
-                    if (quit_) return;
-                } else {
+                if (active_.load(std::memory_order_relaxed) && spins < kSpin) {
+                    ++spins;
                     __builtin_ia32_pause();
+                    continue;
                 }
+                sleepers_.fetch_add(1, std::memory_order_seq_cst);
+                {
+                    std::unique_lock<std::mutex> lk(mu_);
+                    cv_.wait(lk, [&] { return quit_ || gen_.load(std::memory_order_seq_cst) != seen; });
+                }
+                sleepers_.fetch_sub(1, std::memory_order_seq_cst);
+                {
+                    std::lock_guard<std::mutex> lk(mu_);
+                    if (quit_) return;
+                }
+                spins = 0;
             }
             seen = gen_.load(std::memory_order_acquire);
             (*job_)(k);
@@ -156,6 +167,7 @@ private:
     std::condition_variable cv_;
     bool quit_ = false;
     std::atomic<bool> active_{false};
+    std::atomic<int> sleepers_{0};
     std::atomic<uint64_t> gen_{0};
     std::atomic<int> pending_{0};
     const std::function<void(int)> *job_ = nullptr;

@@ -115,3 +115,39 @@ def test_realvector_simple_known_answers(gpu):
     assert abs(mv.distance(s0, s0)[0]) < 1e-3
     np.testing.assert_array_equal(mv.interpolate(s0, s0, 0.6), s0)
     assert abs(mv.interpolate(s0, s1, 0.5)[0, 2] - 0.5) < 1e-3
+
+
+def test_so3_arc_every_acos_branch(gpu):
+    """SO3 arcLength (SO3StateSpace.cpp:254-262) and slerp (:289-318) on the device against the
+    oracle (glibc) at every branch of glibc's acos (e_asin.c: |x| < 2^-54, < 0.125, the table
+    intervals up to 0.96875, the square-root form below 1) and its interval edges: q1 = identity,
+    q2 = (sqrt(1 - c^2), 0, 0, c), so |q1 . q2| = |c| exactly; bit-identical distances and
+    interpolated states, SO3 and SE3."""
+    rng = np.random.default_rng(5)
+    edges = [2.0 ** -54, 0.125, 0.25, 0.5, 0.75, 0.921875, 0.953125, 0.96875, 1.0 - 1e-9, 1.0 - 2e-9]
+    cs = []
+    for e in edges:
+        cs += [np.nextafter(e, 0.0), e, np.nextafter(e, 2.0)]
+    lo = [0.0] + edges[:-1]
+    for a, b in zip(lo, edges):
+        cs += list(rng.uniform(a, b, 40))
+    cs += list(np.ldexp(rng.uniform(0.5, 1.0, 20), -rng.integers(1, 60, 20)))  # tiny
+    cs += list(1.0 - np.ldexp(rng.uniform(0.5, 1.0, 40), -rng.integers(10, 30, 40)))  # near 1 (above the cut too)
+    c = np.array(cs, dtype=np.float64)
+    c = np.concatenate([c, -c])  # the sign: |q1 . q2|
+    c = c[np.abs(c) <= 1.0]
+    n = len(c)
+    q1 = np.tile([0.0, 0.0, 0.0, 1.0], (n, 1))
+    q2 = np.stack([np.sqrt(1.0 - c * c), np.zeros(n), np.zeros(n), c], axis=1)
+    t = rng.uniform(0.0, 1.0, n)
+    for sp, a, b in ((SO3StateSpace(), q1, q2),
+                     (SE3StateSpace(), np.hstack([rng.uniform(0, 1, (n, 3)), q1]),
+                      np.hstack([rng.uniform(0, 1, (n, 3)), q2]))):
+        mv = DiscreteMotionValidatorGPU(sp, AllValidChecker(), gpu)
+        d = mv.distance(a, b)
+        od = np.array([O.distance(sp, x, y) for x, y in zip(a, b)])
+        np.testing.assert_array_equal(d, od)
+        si = mv.interpolate(a, b, t)
+        oi = np.array([O.interpolate(sp, x, y, s) for x, y, s in zip(a, b, t)])
+        np.testing.assert_array_equal(si, oi)
+        mv.close()
