@@ -143,6 +143,10 @@ def parse():
                     help="configs measured after the headline into the line's `workloads` record: 'auto' = "
                          f"{','.join(SUB_WORKLOADS)} when the headline is cfg3 replicated, 'none', or a comma list")
     ap.add_argument("--sub-cpu-seconds", type=float, default=6.0, help="CPU baseline budget of each sub-workload")
+    ap.add_argument("--lanes", type=int, default=3,
+                    help="steps in flight for workloads whose batches are independent (cfg3, cfg2, cfg5 kNN): step i "
+                         "runs on stream i %% lanes with its own NN / validator handles over the same tree, so the next "
+                         "step's walk fills the CUs the current walk's tail leaves idle (1 = one stream)")
     ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
                     help="file for the full record (the stdout line is the compact form); '' = none")
     a = ap.parse_args()
@@ -849,8 +853,39 @@ class Runner:
         self.s_to = torch.empty_like(self.s_from)
         self.valid = torch.empty(max(m, 1), dtype=torch.uint8, device=dev)
         self.maxd = 0.2 * self.sp.getMaximumExtent()                    # RRT range default (SelfConfig.cpp:98)
+        # steps in flight: the batches of cfg3 / cfg2 / cfg5's kNN mode are independent (a step adds
+        # nothing to the tree), so step i runs on lane i % L — its own stream, NN and validator
+        # handles over the same tree, its own outputs — and step i + 1's walk starts on the CUs that
+        # step i's walk tail (its last groups) and the small kernels after it leave idle.  cfg4's
+        # causal PRM* batches and the radius mode (a host read of the result size per call) keep one.
+        self.stream = stream
+        keys = ("nn", "mv", "stream", "ids", "dd", "s_from", "s_to", "valid")
+        self.lanes = [{key: getattr(self, key) for key in keys}]
+        nl = max(1, getattr(args, "lanes", 1))
+        if self.tree_mode or not (wl in ("cfg3", "cfg2") or (wl == "cfg5" and self.k)):
+            nl = 1
+        for _ in range(nl - 1):
+            ln = {"stream": torch.cuda.Stream(dev), "nn": NearestNeighborsGPU(self.sp, local),
+                  "mv": DiscreteMotionValidatorGPU(self.sp, self.ck, local)}
+            ln["nn"].set_exact(args.exact)
+            ln["nn"].add(self.tree)
+            ln["nn"].set_stream(ln["stream"].cuda_stream)
+            ln["mv"].set_stream(ln["stream"].cuda_stream)
+            for key in ("ids", "dd", "s_from", "s_to", "valid"):
+                ln[key] = torch.empty_like(getattr(self, key))
+            self.lanes.append(ln)
+        self.si = 0
+
+    def use_lane(self, i):
+        for key, v in self.lanes[i].items():
+            setattr(self, key, v)
+
+    def next_lane(self):
+        self.use_lane(self.si % len(self.lanes))
+        self.si += 1
 
     def step(self, e=None):
+        self.next_lane()
         a, nn, mv, q = self.args, self.nn, self.mv, self.queries.data_ptr()
         if a.workload == "cfg4":  # one causal PRM* batch (synchronous: its kNN, scan, edges, insert)
             if e:
@@ -988,7 +1023,8 @@ class Runner:
     def config(self, world):
         a = self.args
         base = {"tree_states": a.tree, "queries_per_gpu": self.nq,
-                "parallelism": f"queries sharded over {world} GPU(s), tree replicated"}
+                "parallelism": f"queries sharded over {world} GPU(s), tree replicated",
+                "steps_in_flight": len(self.lanes)}
         if self.strong:
             base.update(queries_per_gpu=None, queries_per_step=self.global_q, queries_this_rank=self.nq,
                         parallelism=(f"a fixed global batch of {self.global_q} samples split over {world} GPU(s) "
@@ -1081,13 +1117,36 @@ class Runner:
 
     def close(self):
         """release the library handles (the next workload gets the HBM back)"""
-        for h in (self.nn, self.mv):
-            h.close()
+        for ln in self.lanes:
+            for h in (ln["nn"], ln["mv"]):
+                h.close()
 
     def counters(self):
-        k = self.nn.cull_stats()
-        r = self.nn.radius_cull_stats()
-        return {"kq": k[2], "rq": r[1]}
+        """walk counters summed over the lanes' handles"""
+        kq = sum(ln["nn"].cull_stats()[2] for ln in self.lanes)
+        rq = sum(ln["nn"].radius_cull_stats()[1] for ln in self.lanes)
+        return {"kq": kq, "rq": rq}
+
+    def profile(self, on):
+        for ln in self.lanes:
+            ln["nn"].profile(on)
+
+    def kernel_time(self):
+        """(total ms, launches, name) of the dominant kernel over every lane (HIP events on each
+        handle's own stream)"""
+        tot, n, name = 0.0, 0, ""
+        for ln in self.lanes:
+            ms, c, nm = ln["nn"].kernel_time()
+            tot, n, name = tot + ms, n + c, nm or name
+        return tot, n, name
+
+    def stats(self):
+        s = [ln["nn"].stats() for ln in self.lanes]
+        return sum(x[0] for x in s), sum(x[1] for x in s)
+
+    def radius_path_stats(self):
+        s = [ln["nn"].radius_path_stats() for ln in self.lanes]
+        return [sum(x[i] for x in s) for i in range(len(s[0]))]
 
 
 def spawn_ranks(n):
@@ -1159,8 +1218,8 @@ def _short(s, n):
 def _compact_roofline(r, full=True):
     if not r:
         return None
-    keys = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms") if full else \
-        ("frac", "kernel_ms", "traffic")
+    keys = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms", "kernel_ms_isolated",
+            "frac_isolated") if full else ("frac", "kernel_ms", "traffic", "frac_isolated")
     out = {k: _sig(r.get(k)) for k in keys if k in r}
     if full and r.get("issue"):
         out["issue"] = {k: _sig(v) for k, v in r["issue"].items() if k != "source"}
@@ -1256,17 +1315,16 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
     if rank == 0:
         progress(f"{args.workload} ({args.partition}, {args.scaling}{', kNN' if args.bitstar_knn else ''}): setup")
     run = Runner(args, torch, dev, local, rank, stream, dist)
-    run.stream = stream
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, len(run.lanes))):  # every lane warm
         run.step()
     torch.cuda.synchronize(dev)
     if run.tree_mode and args.workload == "cfg3":
         run.owned = torch.zeros((), dtype=torch.int64, device=dev)
-    run.nn.profile(True)
-    run.nn.kernel_time()
-    scr0, fb0 = run.nn.stats()
-    rp0 = run.nn.radius_path_stats()
+    run.profile(True)
+    run.kernel_time()
+    scr0, fb0 = run.stats()
+    rp0 = run.radius_path_stats()
     c0 = run.counters()
     units = 0
     if dist:
@@ -1284,12 +1342,21 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
     if run.tree_mode and args.workload == "cfg3":  # motion checks of the samples whose nearest state this rank owns
         units += int(run.owned.item())
         run.m = int(run.last_owned.item())
-    kern_ms_total, kern_n, kern_name = run.nn.kernel_time()
+    kern_ms_total, kern_n, kern_name = run.kernel_time()
     kern_ms = kern_ms_total / max(kern_n, 1)
-    run.nn.profile(False)
-    scr1, fb1 = run.nn.stats()
-    rp1 = run.nn.radius_path_stats()
+    scr1, fb1 = run.stats()
+    rp1 = run.radius_path_stats()
     c1 = run.counters()
+    iso_ms = None
+    if len(run.lanes) > 1:  # the dominant kernel alone: a few steps on one lane, one at a time
+        for _ in range(3):
+            run.si = 0
+            run.step()
+            torch.cuda.synchronize(dev)
+        iso_total, iso_n, _ = run.kernel_time()  # (cumulative since profiling started)
+        iso_ms = (iso_total - kern_ms_total) / max(iso_n - kern_n, 1)
+    run.profile(False)
+    run.use_lane(0)
     nn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     edge_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     mv_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
@@ -1330,6 +1397,13 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
         "fast_path": {"screened": scr1 - scr0, "exact_reruns": fb1 - fb0},
         "roofline": run.roofline(kern_ms, kern_name, c0, c1, max(args.steps, 1)),
     }
+    if iso_ms:  # the kernel's duration without a second step in flight, and the roofline fraction at it
+        r = line["roofline"]
+        r["kernel_ms_isolated"] = iso_ms
+        r["frac_isolated"] = r["frac"] * kern_ms / iso_ms
+    if len(run.lanes) > 1:
+        line["phase_ms"]["note"] = (f"{len(run.lanes)} steps in flight: a phase's HIP events (on its lane's stream) also "
+                                    "span the other lanes' kernels running meanwhile")
     if args.workload == "cfg4":  # one synchronous call per step: kNN, causal scan, edges and insert together
         line["phase_ms"] = {"prm_batch": nn_ms}
         line["edges_checked_per_s"] = run.m * world / (nn_ms * 1e-3)

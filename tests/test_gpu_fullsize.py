@@ -342,3 +342,31 @@ def test_random_access_pattern(gpu):
     builds, appends = nn.index_stats()
     assert builds >= 2 and appends >= 1  # removals forced rebuilds; adds went to the tail
     nn.close()
+
+
+def test_cfg3_steps_in_flight_identical(gpu):
+    """bench's steps in flight (--lanes 2: alternate steps on two streams, each lane its own NN /
+    validator handles over the same tree) give every step the same neighbours, steered motions and
+    validity bits as the one-stream step — no lane reads another's scratch"""
+    import torch
+
+    import bench
+
+    t, q, k = bench.DEFAULTS["cfg3"]
+    outs = {}
+    for lanes in (1, 2):
+        a = argparse.Namespace(workload="cfg3", tree=t, queries=20000, k=k, exact=False, partition="replicated",
+                               warmup=0, steps=4, bitstar_knn=False, lanes=lanes)
+        dev = torch.device("cuda", 0)
+        run = bench.Runner(a, torch, dev, 0, 0, torch.cuda.Stream(dev))
+        assert len(run.lanes) == lanes
+        res = []
+        for _ in range(4):  # back to back, synchronised only at the end
+            run.step()
+            res.append({n: getattr(run, n) for n in ("ids", "dd", "s_to", "valid")})
+        torch.cuda.synchronize(dev)
+        outs[lanes] = [{n: v.cpu().numpy() for n, v in r.items()} for r in res]
+        run.close()
+    for a1, a2 in zip(outs[1], outs[2]):
+        for n in a1:
+            np.testing.assert_array_equal(a1[n], a2[n])

@@ -124,7 +124,7 @@ def test_so3_arc_every_acos_branch(gpu):
     q2 = (sqrt(1 - c^2), 0, 0, c), so |q1 . q2| = |c| exactly; bit-identical distances and
     interpolated states, SO3 and SE3."""
     rng = np.random.default_rng(5)
-    edges = [2.0 ** -54, 0.125, 0.25, 0.5, 0.75, 0.921875, 0.953125, 0.96875, 1.0 - 1e-9, 1.0 - 2e-9]
+    edges = [2.0 ** -54, 0.125, 0.25, 0.5, 0.75, 0.921875, 0.953125, 0.96875, 1.0 - 2e-9, 1.0 - 1e-9]
     cs = []
     for e in edges:
         cs += [np.nextafter(e, 0.0), e, np.nextafter(e, 2.0)]
