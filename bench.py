@@ -859,11 +859,13 @@ class Runner:
         # step i's walk tail (its last groups) and the small kernels after it leave idle.  cfg4's
         # causal PRM* batches and the radius mode (a host read of the result size per call) keep one.
         self.stream = stream
-        keys = ("nn", "mv", "stream", "ids", "dd", "s_from", "s_to", "valid")
+        keys = ("nn", "mv", "stream", "ids", "dd", "s_from", "s_to", "valid") + (("off",) if hasattr(self, "off") else ())
         self.lanes = [{key: getattr(self, key) for key in keys}]
         nl = max(1, getattr(args, "lanes", 1))
-        if self.tree_mode or not (wl in ("cfg3", "cfg2") or (wl == "cfg5" and self.k)):
+        if self.tree_mode or wl not in ("cfg3", "cfg2", "cfg5"):
             nl = 1
+        # the radius mode reads each call's result size on the host: its lanes get host threads
+        self.threaded = nl > 1 and wl == "cfg5" and not self.k
         for _ in range(nl - 1):
             ln = {"stream": torch.cuda.Stream(dev), "nn": NearestNeighborsGPU(self.sp, local),
                   "mv": DiscreteMotionValidatorGPU(self.sp, self.ck, local)}
@@ -871,7 +873,7 @@ class Runner:
             ln["nn"].add(self.tree)
             ln["nn"].set_stream(ln["stream"].cuda_stream)
             ln["mv"].set_stream(ln["stream"].cuda_stream)
-            for key in ("ids", "dd", "s_from", "s_to", "valid"):
+            for key in ("ids", "dd", "s_from", "s_to", "valid") + (("off",) if "off" in self.lanes[0] else ()):
                 ln[key] = torch.empty_like(getattr(self, key))
             self.lanes.append(ln)
         self.si = 0
@@ -901,32 +903,57 @@ class Runner:
         if self.tree_mode:
             (self.step_tree_radius if a.workload == "cfg5" else self.step_tree)(e)
             return
+        self.m = self.step_on(self.lanes[(self.si - 1) % len(self.lanes)], e)
+
+    def step_on(self, L, e=None):
+        """one replicated step of cfg3 / cfg2 / cfg5 on lane L (its handles, stream and outputs);
+        returns the step's edge count.  Touches no Runner state: lanes may run on their own host
+        threads (threaded_lanes)."""
+        a, nn, mv, q, st = self.args, L["nn"], L["mv"], self.queries.data_ptr(), L["stream"]
         if e:
-            e[0].record(self.stream)
+            e[0].record(st)
+        m = self.m
         if a.workload == "cfg5" and not self.k:
-            self.m = nn.radius_device(q, self.nq, self.radius, self.off.data_ptr(), self.ids.data_ptr(),
-                                      self.dd.data_ptr(), self.cap)
+            m = nn.radius_device(q, self.nq, self.radius, L["off"].data_ptr(), L["ids"].data_ptr(), L["dd"].data_ptr(),
+                                 self.cap)
         else:
-            nn.knn_device(q, self.nq, self.k, self.ids.data_ptr(), self.dd.data_ptr())
+            nn.knn_device(q, self.nq, self.k, L["ids"].data_ptr(), L["dd"].data_ptr())
         if e:
-            e[1].record(self.stream)
+            e[1].record(st)
         if a.workload in ("cfg3", "cfg2"):   # RRT extend: nearest -> steer (RRT.cpp:137-146)
-            nn.steer_device(q, self.nq, self.ids.data_ptr(), self.k, self.maxd, self.s_from.data_ptr(),
-                            self.s_to.data_ptr())
-        elif a.workload == "cfg4":           # PRM: checkMotion(state[n], state[m])  PRM.cpp:582
-            nn.edges_device(q, self.nq, None, self.ids.data_ptr(), self.k, self.m, False, self.s_from.data_ptr(),
-                            self.s_to.data_ptr())
+            nn.steer_device(q, self.nq, L["ids"].data_ptr(), self.k, self.maxd, L["s_from"].data_ptr(),
+                            L["s_to"].data_ptr())
         # BIT* (cfg5, both modes): checkMotion(vertex, sample) (BITstar.cpp:815) over the neighbour
         # result's edges read in place (ompl_gpu_mv_check_edges_device: no endpoint rows written)
         if e:
-            e[2].record(self.stream)
+            e[2].record(st)
         if a.workload == "cfg5":
-            mv.check_edges_device(nn, q, self.nq, None if self.k else self.off.data_ptr(), self.ids.data_ptr(),
-                                  self.k, self.m, True, self.valid.data_ptr())
+            mv.check_edges_device(nn, q, self.nq, None if self.k else L["off"].data_ptr(), L["ids"].data_ptr(),
+                                  self.k, m, True, L["valid"].data_ptr())
         elif a.workload != "cfg2":
-            mv.check_device(self.s_from.data_ptr(), self.s_to.data_ptr(), self.m, self.valid.data_ptr())
+            mv.check_device(L["s_from"].data_ptr(), L["s_to"].data_ptr(), m, L["valid"].data_ptr())
         if e:
-            e[3].record(self.stream)
+            e[3].record(st)
+        return m
+
+    def run_threaded(self, steps, ev):
+        """the timed steps with one host thread per lane (lane j takes steps j, j + L, ...): a lane
+        whose call waits on the host (nearestR reads its result size) leaves the other lanes' host
+        threads free to keep their streams fed.  Returns the units issued."""
+        import torch
+        from concurrent.futures import ThreadPoolExecutor
+
+        nl = len(self.lanes)
+
+        def lane(j):
+            torch.cuda.set_device(self.dev)
+            for s in range(j, steps, nl):
+                self.step_on(self.lanes[j], ev[s] if ev else None)
+            return len(range(j, steps, nl))
+
+        with ThreadPoolExecutor(nl) as ex:
+            n = sum(ex.map(lane, range(nl)))
+        return n * self.units_per_step()
 
     def step_tree_radius(self, e=None):
         """Tree-sharded BIT* batch (cfg5 radius): every rank answers every vertex's nearestR on its
@@ -1331,9 +1358,12 @@ def measure(args, torch, dev, local, rank, world, dist, stream, cpu_seconds):
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        run.step(ev[s])
-        units += run.units_per_step()
+    if run.threaded:
+        units = run.run_threaded(args.steps, ev)
+    else:
+        for s in range(args.steps):
+            run.step(ev[s])
+            units += run.units_per_step()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
