@@ -143,7 +143,7 @@ def parse():
                     help="configs measured after the headline into the line's `workloads` record: 'auto' = "
                          f"{','.join(SUB_WORKLOADS)} when the headline is cfg3 replicated, 'none', or a comma list")
     ap.add_argument("--sub-cpu-seconds", type=float, default=6.0, help="CPU baseline budget of each sub-workload")
-    ap.add_argument("--lanes", type=int, default=3,
+    ap.add_argument("--lanes", type=int, default=2,
                     help="steps in flight for workloads whose batches are independent (cfg3, cfg2, cfg5 kNN): step i "
                          "runs on stream i %% lanes with its own NN / validator handles over the same tree, so the next "
                          "step's walk fills the CUs the current walk's tail leaves idle (1 = one stream)")

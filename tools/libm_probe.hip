@@ -21,7 +21,7 @@ __global__ void probe(const double *x, size_t n, double *o) {
     o[3 * n + i] = ompl_amd::glibc_sin(v);
     o[4 * n + i] = ompl_amd::glibc_cos(v);
     ompl_amd::glibc_sincos(v, o[5 * n + i], o[6 * n + i]);
-    o[8 * n + i] = ompl_amd::glibc_acos(fabs(v) <= 1.0 ? v : 0.5);
+    o[7 * n + i] = ompl_amd::glibc_acos(fabs(v) <= 1.0 ? v : 0.5);
 }
 
 int main(int argc, char **argv) {
