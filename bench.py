@@ -46,9 +46,9 @@ HBM_PEAK_GBS = 8000.0                       # HBM3E spec
 F_SE3, F_L2_6, F_CHAIN = 21, 18, 84
 B_SE3 = {"f32": 28, "f64": 56}              # bytes per stored SE(3) state streamed by a scan
 # committed PMC passes per workload, newest round first (cfg5k = configs[4] in kNN mode)
-PMC_PROFILES = {w: [f"r5_{w}", f"r4_{w}", f"r3_{w}"] for w in ("cfg3", "cfg2", "cfg4", "cfg5")}
-PMC_PROFILES["cfg5k"] = ["r5_cfg5k", "r4_cfg5k"]
-PMC_PROFILES["rrt_star"] = ["r5_rrt_star"]
+PMC_PROFILES = {w: [f"r6_{w}", f"r5_{w}", f"r4_{w}", f"r3_{w}"] for w in ("cfg3", "cfg2", "cfg4", "cfg5")}
+PMC_PROFILES["cfg5k"] = ["r6_cfg5k", "r5_cfg5k", "r4_cfg5k"]
+PMC_PROFILES["rrt_star"] = ["r6_rrt_star", "r5_rrt_star"]
 DEFAULTS = {  # tree states, queries (samples / milestones / vertices) per GPU per step, k
     "cfg3": (1_000_000, 100_000, 10),
     "cfg2": (100_000, 100_000, 10),
