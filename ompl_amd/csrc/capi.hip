@@ -515,7 +515,7 @@ static bool screen_safe(const ompl_gpu_nn *h) {
 }
 
 #ifdef OMPL_AMD_PROBE
-constexpr int kCullCounters = 12;  // + walk event counters of the probe build (tools/probe)
+constexpr int kCullCounters = 23;  // + walk event counters and timers of the probe build (tools/walk_probe.py)
 #else
 constexpr int kCullCounters = 5;
 #endif
@@ -630,12 +630,12 @@ static ompl_gpu_status knn_features_locked(ompl_gpu_nn *h, const double *d_qf, s
         const size_t wsb = knn_fast_workspace_bytes(h->sp, h->g, (uint32_t)nq, k, n_end, h->num_cus, cull);
         HIP_OR_FAIL(h->ws.ensure(wsb));
         // the bounded re-run's counters (below), zeroed by the batch's first kernel
-        HIP_OR_FAIL(h->fb_c.ensure(sizeof(uint32_t) * (kBoundedMaxQ + 1 + nq)));
+        HIP_OR_FAIL(h->fb_c.ensure(sizeof(uint32_t) * (kBoundedMaxQ + 2 + nq)));
         HIP_OR_FAIL(h->fb_cd.ensure(sizeof(double) * kBoundedMaxQ * kBoundedCap));
         HIP_OR_FAIL(h->fb_ci.ensure(sizeof(uint32_t) * kBoundedMaxQ * kBoundedCap));
         uint32_t *cnt = (uint32_t *)h->fb_c.p;
         b.zero[0] = cnt;
-        b.nzero[0] = kBoundedMaxQ + 1;
+        b.nzero[0] = kBoundedMaxQ + 2;
         uint32_t *d_fail_count = nullptr, *d_fail_list = nullptr;
         HIP_OR_FAIL(launch_knn_fast(h->sp, h->g, h->feat, h->feat32, h->cap, n_end, cull ? &h->sorted : nullptr, d_qf,
                                     (uint32_t)nq, k, b, d_dist, d_ids, h->ws.p, h->ws.bytes, h->num_cus, h->stream,

@@ -14,7 +14,7 @@ constexpr int kMaxK = 64;           // largest register top-K bucket
 // walk statistics counters (SortedStore::counters): kCounterSlots copies of kCounterStride words,
 // a wave adds into copy blockIdx.x % kCounterSlots (same-address atomics from every wave of a
 // 25,000-wave launch would serialise at the L2); readers sum the copies
-constexpr int kCounterSlots = 64, kCounterStride = 16;
+constexpr int kCounterSlots = 64, kCounterStride = 24;
 constexpr uint32_t kStreamMaxQ = 64; // below this many queries the stream mapping is used
 
 // Optional HIP-event bracket around the dominant kernel of a launch (the scan), armed by
@@ -227,10 +227,10 @@ hipError_t launch_to_fp32(const double *feat64, uint64_t cap, int rows, uint64_t
 // (device count).  The first kBoundedMaxQ take the bounded pass: od / oi hold the certificate's
 // exact lists (row q = query q, k entries), whose k-th distance bounds the answer, and the exact
 // top-k overwrites them; queries with more than kBoundedCap candidates (and list entries past
-// kBoundedMaxQ) take a full exact scan.  counts (device, kBoundedMaxQ + 1 + nq words, the first
-// kBoundedMaxQ + 1 zeroed by the caller) returns at [kBoundedMaxQ] the number of full scans and
-// at [kBoundedMaxQ + 1 ..] their query indices.  cand_d / cand_i hold kBoundedMaxQ * kBoundedCap
-// entries.
+// kBoundedMaxQ) take a full exact scan.  counts (device, kBoundedMaxQ + 2 + nq words, the first
+// kBoundedMaxQ + 2 zeroed by the caller) returns at [kBoundedMaxQ] the number of full scans and
+// at [kBoundedMaxQ + 2 ..] their query indices ([kBoundedMaxQ + 1]: the launch's grid barrier).
+// cand_d / cand_i hold kBoundedMaxQ * kBoundedCap entries.  One launch of num_cus blocks.
 constexpr uint32_t kBoundedCap = 1024;
 constexpr uint32_t kBoundedMaxQ = 512;
 hipError_t launch_knn_bounded(const DevSpace &sp, const FeatGeom &g, const double *feat, uint64_t cap,

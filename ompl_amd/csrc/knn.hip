@@ -187,121 +187,134 @@ __global__ __launch_bounds__(256) void knn_stream_merge_kernel(const double *__r
 // sort of that set yields the exact (distance, id) top-k — the same answer as the full
 // stream re-run, at one read of the store for all failed queries together instead of one
 // per query.  A query with more than kBoundedCap such states overflows to the full scan.
-// The list length is read on the device (no host round trip): the kernels are launched
-// with fixed grids and return at once when nothing failed.
-template <int SP, int F, int NMAX, int ITEMS>
-__global__ __launch_bounds__(256) void knn_bounded_kernel(const double *__restrict__ feat, uint64_t cap,
-                                                          uint64_t n_end, const double *__restrict__ qfeat,
-                                                          const uint32_t *__restrict__ list,
-                                                          const uint32_t *__restrict__ nlist_ptr,
-                                                          const double *__restrict__ out_d, uint32_t out_k,
-                                                          DevSpace sp, uint32_t *__restrict__ counts,
-                                                          double *__restrict__ cand_d, uint32_t *__restrict__ cand_i) {
-    const uint32_t nlist = min(*nlist_ptr, kBoundedMaxQ);
-    if (nlist == 0) return;
-    const uint64_t base = (uint64_t)blockIdx.x * (256 * ITEMS) + threadIdx.x;
-    double sf[ITEMS][F];
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it) {
-        const uint64_t g = base + (uint64_t)it * 256;
-#pragma unroll
-        for (int f = 0; f < F; ++f) sf[it][f] = g < n_end ? feat[(uint64_t)f * cap + g] : __builtin_nan("");
+//
+// One persistent launch (a block per CU) runs the three phases — the bounded pass, the
+// per-query rank select, the full scans of the overflow list — separated by grid-wide
+// barriers.  The failed-query count is read on the device (no host round trip): when nothing
+// failed, every block returns at once, so the common batch pays one small launch instead of
+// three (two of them store-sized grids).  All blocks are co-resident (one per CU, whatever
+// else runs beside them eventually drains), so the barriers cannot deadlock.
+
+// grid-wide barrier: each thread releases its phase's writes at agent scope (the L2s of the
+// XCDs are not coherent with each other), thread 0 of each block counts in and waits for the
+// target on the monotone counter, and every thread acquires before the next phase
+__device__ __forceinline__ void rerun_grid_sync(uint32_t *ctr, uint32_t target) {
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(4);
     }
-    for (uint32_t j = 0; j < nlist; ++j) {
-        const uint32_t q = list[j];
-        const double b = out_d[(size_t)q * out_k + out_k - 1];
-        double qv[F];
-#pragma unroll
-        for (int f = 0; f < F; ++f) qv[f] = qfeat[(size_t)q * F + f];
+    __syncthreads();
+    __threadfence();
+}
+
+template <int SP, int F, int NMAX, int ITEMS, int K>
+__global__ __launch_bounds__(256) void knn_rerun_kernel(const double *__restrict__ feat, uint64_t cap, uint64_t n_end,
+                                                        const double *__restrict__ qfeat,
+                                                        const uint32_t *__restrict__ list,
+                                                        const uint32_t *__restrict__ nlist_ptr, DevSpace sp,
+                                                        uint32_t out_k, double *__restrict__ out_d,
+                                                        uint32_t *__restrict__ out_i, uint32_t *__restrict__ counts,
+                                                        double *__restrict__ cand_d, uint32_t *__restrict__ cand_i,
+                                                        unsigned long long *__restrict__ stats) {
+    const uint32_t total = *nlist_ptr;
+    if (total == 0) return;  // the common batch: every query certified
+    const uint32_t nlist = min(total, kBoundedMaxQ);
+    uint32_t *ov_count = counts + kBoundedMaxQ, *bar = counts + kBoundedMaxQ + 1, *ov_list = counts + kBoundedMaxQ + 2;
+
+    // phase 1: the bounded pass — chunks of 256 * ITEMS states, block-strided
+    const uint64_t nchunk = (n_end + 256 * ITEMS - 1) / (256 * ITEMS);
+    for (uint64_t c = blockIdx.x; c < nchunk; c += gridDim.x) {
+        const uint64_t base = c * (256 * ITEMS) + threadIdx.x;
+        double sf[ITEMS][F];
 #pragma unroll
         for (int it = 0; it < ITEMS; ++it) {
-            double d;
-            if constexpr (SP == OMPL_GPU_SPACE_SE3) {
-                // as knn_stream_kernel: the translation term alone bounds the distance below
-                const double a = sp.w0 * l2_dist(sf[it], qv, 3);
-                if (!(a <= b)) continue;
-                d = 0.0;
-                d += a;
-                d += sp.w1 * so3_arc(sf[it] + 3, qv + 3);
-            } else {
-                d = feat_dist<SP, F, NMAX>(sf[it], qv, sp);
-            }
-            if (d <= b) {  // NaN (unused / removed slot) never passes
-                const uint32_t slot = atomicAdd(&counts[j], 1u);
-                if (slot < kBoundedCap) {
-                    cand_d[(size_t)j * kBoundedCap + slot] = d;
-                    cand_i[(size_t)j * kBoundedCap + slot] = (uint32_t)(base + (uint64_t)it * 256);
+            const uint64_t g = base + (uint64_t)it * 256;
+#pragma unroll
+            for (int f = 0; f < F; ++f) sf[it][f] = g < n_end ? feat[(uint64_t)f * cap + g] : __builtin_nan("");
+        }
+        for (uint32_t j = 0; j < nlist; ++j) {
+            const uint32_t q = list[j];
+            const double b = out_d[(size_t)q * out_k + out_k - 1];
+            double qv[F];
+#pragma unroll
+            for (int f = 0; f < F; ++f) qv[f] = qfeat[(size_t)q * F + f];
+#pragma unroll
+            for (int it = 0; it < ITEMS; ++it) {
+                double d;
+                if constexpr (SP == OMPL_GPU_SPACE_SE3) {
+                    // as knn_stream_kernel: the translation term alone bounds the distance below
+                    const double a = sp.w0 * l2_dist(sf[it], qv, 3);
+                    if (!(a <= b)) continue;
+                    d = 0.0;
+                    d += a;
+                    d += sp.w1 * so3_arc(sf[it] + 3, qv + 3);
+                } else {
+                    d = feat_dist<SP, F, NMAX>(sf[it], qv, sp);
+                }
+                if (d <= b) {  // NaN (unused / removed slot) never passes
+                    const uint32_t slot = atomicAdd(&counts[j], 1u);
+                    if (slot < kBoundedCap) {
+                        cand_d[(size_t)j * kBoundedCap + slot] = d;
+                        cand_i[(size_t)j * kBoundedCap + slot] = (uint32_t)(base + (uint64_t)it * 256);
+                    }
                 }
             }
         }
     }
-}
+    rerun_grid_sync(bar, gridDim.x);
 
-// block j < nlist: rank-sort query list[j]'s candidates by (distance, id) in LDS and write the
-// first out_k into its output row; too many (or, impossibly, too few) candidates put the query
-// on the overflow list (counts[kBoundedMaxQ] = its length, entries from counts + kBoundedMaxQ + 1).
-// The last block moves list entries beyond kBoundedMaxQ (not re-run here) to the overflow list.
-__global__ __launch_bounds__(256) void knn_bounded_select_kernel(const uint32_t *__restrict__ list,
-                                                                 const uint32_t *__restrict__ nlist_ptr,
-                                                                 uint32_t *__restrict__ counts,
-                                                                 const double *__restrict__ cand_d,
-                                                                 const uint32_t *__restrict__ cand_i, uint32_t out_k,
-                                                                 double *__restrict__ out_d,
-                                                                 uint32_t *__restrict__ out_i) {
-    __shared__ double sd[kBoundedCap];
-    __shared__ uint32_t si[kBoundedCap];
-    const uint32_t total = *nlist_ptr, nlist = min(total, kBoundedMaxQ);
-    uint32_t *ov_count = counts + kBoundedMaxQ, *ov_list = counts + kBoundedMaxQ + 1;
-    if (blockIdx.x == kBoundedMaxQ) {  // excess list entries: straight to the full scan
-        for (uint32_t e = kBoundedMaxQ + threadIdx.x; e < total; e += blockDim.x) ov_list[atomicAdd(ov_count, 1u)] = list[e];
-        return;
-    }
-    const uint32_t j = blockIdx.x;
-    if (j >= nlist) return;
-    const uint32_t q = list[j];
-    const uint32_t c = counts[j];
-    if (c > kBoundedCap || c < out_k) {
-        if (threadIdx.x == 0) ov_list[atomicAdd(ov_count, 1u)] = q;
-        return;
-    }
-    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
-        sd[e] = cand_d[(size_t)j * kBoundedCap + e];
-        si[e] = cand_i[(size_t)j * kBoundedCap + e];
-    }
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
-        const double d = sd[e];
-        const uint32_t id = si[e];
-        uint32_t rank = 0;
-        for (uint32_t m = 0; m < c; ++m) rank += (sd[m] < d || (sd[m] == d && si[m] < id)) ? 1u : 0u;
-        if (rank < out_k) {
-            out_d[(size_t)q * out_k + rank] = d;
-            out_i[(size_t)q * out_k + rank] = id;
+    // phase 2: entry j < nlist rank-sorts its candidates by (distance, id) in LDS and writes the
+    // first out_k into its output row; too many (or, impossibly, too few) candidates put the
+    // query on the overflow list.  Entry kBoundedMaxQ moves list entries beyond kBoundedMaxQ
+    // (not re-run by the bounded pass) to the overflow list.
+    {
+        __shared__ double sd[kBoundedCap];
+        __shared__ uint32_t si[kBoundedCap];
+        for (uint32_t j = blockIdx.x; j <= kBoundedMaxQ; j += gridDim.x) {
+            if (j == kBoundedMaxQ) {
+                for (uint32_t e = kBoundedMaxQ + threadIdx.x; e < total; e += blockDim.x)
+                    ov_list[atomicAdd(ov_count, 1u)] = list[e];
+            } else if (j < nlist) {
+                const uint32_t q = list[j];
+                const uint32_t c = counts[j];
+                if (c > kBoundedCap || c < out_k) {
+                    if (threadIdx.x == 0) ov_list[atomicAdd(ov_count, 1u)] = q;
+                } else {
+                    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
+                        sd[e] = cand_d[(size_t)j * kBoundedCap + e];
+                        si[e] = cand_i[(size_t)j * kBoundedCap + e];
+                    }
+                    __syncthreads();
+                    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
+                        const double d = sd[e];
+                        const uint32_t id = si[e];
+                        uint32_t rank = 0;
+                        for (uint32_t m = 0; m < c; ++m) rank += (sd[m] < d || (sd[m] == d && si[m] < id)) ? 1u : 0u;
+                        if (rank < out_k) {
+                            out_d[(size_t)q * out_k + rank] = d;
+                            out_i[(size_t)q * out_k + rank] = id;
+                        }
+                    }
+                }
+            }
+            __syncthreads();  // LDS reuse by the block's next entry
         }
     }
-}
+    rerun_grid_sync(bar, 2 * gridDim.x);
 
-// full exact scan of the overflow list: persistent blocks, block b answers overflow entries
-// b, b + gridDim.x, ...; each block scans the whole store for its query (per-thread register
-// top-K, block selection) — the rare path (more than kBoundedCap states within the bound).
-template <int SP, int F, int NMAX, int K>
-__global__ __launch_bounds__(256) void knn_full_list_kernel(const double *__restrict__ feat, uint64_t cap,
-                                                            uint64_t n_end, const double *__restrict__ qfeat,
-                                                            const uint32_t *__restrict__ count_ptr,
-                                                            const uint32_t *__restrict__ list, DevSpace sp,
-                                                            uint32_t out_k, double *__restrict__ out_d,
-                                                            uint32_t *__restrict__ out_i,
-                                                            const uint32_t *__restrict__ fail_ptr,
-                                                            unsigned long long *__restrict__ stats) {
+    // phase 3: full exact scan of the overflow list, block b answering entries b, b + gridDim.x,
+    // ... (per-thread register top-K, block selection) — the rare path
     __shared__ double lds_d[4 * K];
     __shared__ uint32_t lds_i[4 * K];
-    const uint32_t count = *count_ptr;
+    const uint32_t count = *ov_count;
     if (stats && blockIdx.x == 0 && threadIdx.x == 0) {  // the re-run statistics (ompl_gpu_nn_stats)
-        stats[0] += *fail_ptr;
+        stats[0] += total;
         stats[1] += count;
     }
     for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
-        const uint32_t q = list[e];
+        const uint32_t q = ov_list[e];
         double qf[F];
 #pragma unroll
         for (int f = 0; f < F; ++f) qf[f] = qfeat[(size_t)q * F + f];
@@ -331,25 +344,19 @@ hipError_t run_knn_bounded(const DevSpace &sp, const double *feat, uint64_t cap,
                            uint32_t *counts, double *cand_d, uint32_t *cand_i, int num_cus, hipStream_t st,
                            unsigned long long *stats) {
     constexpr int ITEMS = F <= 8 ? 4 : 1;
-    const uint64_t blocks = (n_end + 256 * ITEMS - 1) / (256 * ITEMS);
-    hipLaunchKernelGGL((knn_bounded_kernel<SP, F, NMAX, ITEMS>), dim3((uint32_t)blocks), dim3(256), 0, st, feat, cap,
-                       n_end, qf, list, d_nlist, od, k, sp, counts, cand_d, cand_i);
-    hipLaunchKernelGGL(knn_bounded_select_kernel, dim3(kBoundedMaxQ + 1), dim3(256), 0, st, list, d_nlist, counts,
-                       cand_d, cand_i, k, od, oi);
-    const uint32_t *ov_count = counts + kBoundedMaxQ, *ov_list = counts + kBoundedMaxQ + 1;
-    const dim3 grid((unsigned)std::max(num_cus, 1));
+    const dim3 grid((unsigned)std::max(num_cus, 1));  // one block per CU: co-resident (the barriers)
     switch (k_bucket(k)) {
-#define OMPL_AMD_FULL(KK)                                                                                       \
-    case KK:                                                                                                   \
-        hipLaunchKernelGGL((knn_full_list_kernel<SP, F, NMAX, KK>), grid, dim3(256), 0, st, feat, cap, n_end, qf, \
-                           ov_count, ov_list, sp, k, od, oi, d_nlist, stats);                                  \
+#define OMPL_AMD_RERUN(KK)                                                                                          \
+    case KK:                                                                                                       \
+        hipLaunchKernelGGL((knn_rerun_kernel<SP, F, NMAX, ITEMS, KK>), grid, dim3(256), 0, st, feat, cap, n_end, qf, \
+                           list, d_nlist, sp, k, od, oi, counts, cand_d, cand_i, stats);                           \
         break;
-        OMPL_AMD_FULL(1)
-        OMPL_AMD_FULL(4)
-        OMPL_AMD_FULL(16)
-        OMPL_AMD_FULL(32)
-        OMPL_AMD_FULL(64)
-#undef OMPL_AMD_FULL
+        OMPL_AMD_RERUN(1)
+        OMPL_AMD_RERUN(4)
+        OMPL_AMD_RERUN(16)
+        OMPL_AMD_RERUN(32)
+        OMPL_AMD_RERUN(64)
+#undef OMPL_AMD_RERUN
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -808,6 +808,22 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     uint32_t visited = 0, qscans = 0;  // tiles fetched; (tile, query) scans
 #ifdef OMPL_AMD_PROBE
     uint32_t pr_offers = 0, pr_bulk = 0, pr_ins = 0, pr_supers = 0, pr_rounds = 0, pr_empty = 0, pr_skip = 0;
+    // probe timers (shader clock, per wave): the masks of popped super-tiles, the wait for a fetched
+    // tile, its scan, next_super (its mega / super rounds' box loads and bounds), the whole walk
+    uint64_t pt_mask = 0, pt_wait = 0, pt_scan = 0, pt_next = 0, pt_pro = 0, pt_issue = 0, pt_tail = 0, pt_offer = 0, pt_cwait = 0, pt_dummy = 0;
+    const uint64_t pt_start = __builtin_amdgcn_s_memtime();
+#define OMPL_PT(acc, ...)                                          \
+    do {                                                            \
+        __builtin_amdgcn_sched_barrier(0);                          \
+        const uint64_t pt_a = __builtin_amdgcn_s_memtime();         \
+        __builtin_amdgcn_sched_barrier(0);                          \
+        __VA_ARGS__;                                                \
+        __builtin_amdgcn_sched_barrier(0);                          \
+        acc += __builtin_amdgcn_s_memtime() - pt_a;                 \
+        __builtin_amdgcn_sched_barrier(0);                          \
+    } while (0)
+#else
+#define OMPL_PT(acc, ...) do { __VA_ARGS__; } while (0)
 #endif
 
     // tiles of super-tile s some query may still need; lb[j]: this lane's bound for tile
@@ -861,6 +877,10 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     // tied with the K2-th entry stays out, which the certificate allows (every excluded
     // element still has a screened distance >= the final K2-th distance)
     auto offer = [&](int g, float d, uint32_t id) {
+#ifdef OMPL_AMD_PROBE
+            const uint64_t pt_o = __builtin_amdgcn_s_memtime();
+            struct PtO { uint64_t &acc; uint64_t t0; __device__ ~PtO() { acc += __builtin_amdgcn_s_memtime() - t0; } } pt_od{pt_offer, pt_o};
+#endif
             uint64_t bm = __ballot(d < td[g]);
 #ifdef OMPL_AMD_PROBE
             ++pr_offers;
@@ -947,21 +967,17 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
             }
         }
     };
-    // start at the super-tile holding the group's middle query on the Morton curve
+    // start at the super-tile holding the group's middle query's home tile.  The store's tile
+    // keys are the tile indices (SortedStore::tkey0 = iota) and a query's key is its home tile,
+    // so the last tile whose key is <= the query's is min(key, ntiles - 1): no search (the binary
+    // search over tkey0 it replaces was a chain of 14 dependent loads at the start of every wave)
+    (void)tkey0;
     const uint32_t key = qkeys[min(g0 + G / 2, nq - 1)];
-    uint32_t lo = 0, hi = ntiles;  // first tile with tkey0 > key
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (tkey0[mid] <= key)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    const uint32_t s0 = (lo > 0 ? lo - 1 : 0) / kSuperTiles;
+    const uint32_t th = min(key, ntiles - 1);
+    const uint32_t s0 = th / kSuperTiles;
     // scan the middle query's home tile (its k-d leaf) first, for every query of the group:
     // the thresholds start near the final K2-th distances, so the box tests that follow
     // exclude more tiles; the home tile is then dropped from its super-tile's mask
-    const uint32_t th = min(key, ntiles - 1);
     {
         float x[R];
         uint32_t id;
@@ -1108,6 +1124,11 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     bool have = false;  // x holds a fetched tile of s
     int sn = next_super();
     if (sn >= 0) load_tbox((uint32_t)sn, bx);
+#ifdef OMPL_AMD_PROBE
+    __builtin_amdgcn_sched_barrier(0);
+    pt_pro = __builtin_amdgcn_s_memtime() - pt_start;
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     // one site each for the mask, the fetch, the scan and next_super (every inlined copy of
     // next_super's round adds its box-bound temporaries to the live set of its site)
     for (;;) {
@@ -1116,21 +1137,28 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
         bool got = false, cross = false, consumed = false;
         uint32_t mn = 0;
         float lbn[GH];
+#ifdef OMPL_AMD_PROBE
+        OMPL_PT(pt_dummy, (void)0);  // the timer's own cost
+#endif
         if (!m && sn >= 0) {
-            mn = mask_of(sn, lbn);
+            OMPL_PT(pt_mask, mn = mask_of(sn, lbn));
             consumed = true;
             cross = mn != 0;
         }
         uint32_t &mf = cross ? mn : m;
-        if (mf) {
+        OMPL_PT(pt_issue, if (mf) {
             tn = __builtin_ctz(mf);
             mf &= mf - 1;
             load_state((uint32_t)(cross ? sn : s) * kSuperTiles + tn, xn, idn);
             got = true;
-        }
+        });
         if (have) {  // the list ids are sorted positions: recomputed, not carried in a VGPR
             const uint32_t pid = ((uint32_t)s * kSuperTiles + (uint32_t)t) * kCullTile + (uint32_t)lane;
-            scan_state(x, pid, t, lb);
+#ifdef OMPL_AMD_PROBE
+            OMPL_PT(pt_wait, asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]),
+                                          "v"(x[R - 1])));
+#endif
+            OMPL_PT(pt_scan, scan_state(x, pid, t, lb));
             ++visited;
         }
         if (cross) {
@@ -1140,15 +1168,29 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
             for (int j = 0; j < GH; ++j) lb[j] = lbn[j];
         }
         if (consumed) {  // after the scan: a round's box loads wait behind it, not before
-            sn = next_super();
+            OMPL_PT(pt_next, sn = next_super());
             if (sn >= 0) load_tbox((uint32_t)sn, bx);
         }
+#ifdef OMPL_AMD_PROBE
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t pt_t = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         bool still = false;  // drop the tiles of s that the tightened thresholds exclude
 #pragma unroll
         for (int j = 0; j < GH; ++j) still |= lb[j] < (half ? td[GH + j] : td[j]);
         m &= fold_tiles(__ballot(still));
         have = got;
+#ifdef OMPL_AMD_PROBE
+        __builtin_amdgcn_sched_barrier(0);
+        pt_tail += __builtin_amdgcn_s_memtime() - pt_t;
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         if (got) {
+#ifdef OMPL_AMD_PROBE
+            OMPL_PT(pt_cwait, asm volatile("" ::"v"(xn[0]), "v"(xn[1]), "v"(xn[2]), "v"(xn[3]), "v"(xn[4]), "v"(xn[5]),
+                                           "v"(xn[R - 1])));
+#endif
 #pragma unroll
             for (int r = 0; r < R; ++r) x[r] = xn[r];
             t = tn;
@@ -1169,8 +1211,20 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
         atomicAdd(&cs[9], (unsigned long long)pr_rounds);
         atomicAdd(&cs[10], (unsigned long long)pr_empty);
         atomicAdd(&cs[11], (unsigned long long)pr_skip);
+        atomicAdd(&cs[12], (unsigned long long)(__builtin_amdgcn_s_memtime() - pt_start));
+        atomicAdd(&cs[13], (unsigned long long)pt_pro);
+        atomicAdd(&cs[14], (unsigned long long)pt_mask);
+        atomicAdd(&cs[15], (unsigned long long)pt_issue);
+        atomicAdd(&cs[16], (unsigned long long)pt_wait);
+        atomicAdd(&cs[17], (unsigned long long)pt_scan);
+        atomicAdd(&cs[18], (unsigned long long)pt_offer);
+        atomicAdd(&cs[19], (unsigned long long)pt_next);
+        atomicAdd(&cs[20], (unsigned long long)pt_tail);
+        atomicAdd(&cs[21], (unsigned long long)pt_cwait);
+        atomicAdd(&cs[22], (unsigned long long)pt_dummy);
 #endif
     }
+#undef OMPL_PT
 #pragma unroll
     for (int g = 0; g < G; ++g)
         if (g0 + g < nq && lane < K2) {

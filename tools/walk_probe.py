@@ -39,12 +39,12 @@ def main():
     nn.knn_device(dq.data_ptr(), a.queries, a.k, ids.data_ptr(), dd.data_ptr())
     nn.sync()
     f = getattr(abi.lib, "ompl_gpu_probe_counters", None)
-    cnt = (C.c_uint64 * 12)()
+    cnt = (C.c_uint64 * 23)()
 
     def counters():
         if f is None:
-            return [0] * 12
-        f(nn._h, cnt, 12)
+            return [0] * 23
+        f(nn._h, cnt, 23)
         return list(cnt)
 
     c0 = counters()
@@ -57,9 +57,17 @@ def main():
     c1 = counters()
     per = [(y - x) / a.reps for x, y in zip(c0, c1)]
     keys = ["tiles", "tiles_bruteforce", "qscans", "radius_tiles", "radius_qscans", "offers", "bulk_merges",
-            "insertions", "supertile_masks", "super_rounds", "empty_masks", "recheck_skips"]
+            "insertions", "supertile_masks", "super_rounds", "empty_masks", "recheck_skips", "walk_cycles",
+            "prologue_cycles", "mask_cycles", "issue_cycles", "tile_wait_cycles", "scan_cycles",
+            "offer_cycles (inside scan)", "next_super_cycles", "loop_tail_cycles", "copy_wait_cycles",
+            "timer_overhead_cycles (one per iteration)"]
     out = {"lib": os.path.basename(abi.LIB_PATH), "kernel": name, "kernel_ms": (ms1 - ms0) / max(n1 - n0, 1),
-           "per_query": {k: v / a.queries for k, v in zip(keys, per) if v}, "reruns": nn.stats()[1]}
+           "per_query": {k: v / a.queries for k, v in zip(keys, per) if v}, "reruns": nn.stats()[1],
+           # the timers are per wave (two queries): shader-clock cycles per wave and their shares
+           "per_wave_cycles": {k: 2 * v / a.queries for k, v in zip(keys, per) if "_cycles" in k}}
+    wc = out["per_wave_cycles"].get("walk_cycles", 0)
+    if wc:
+        out["cycle_shares"] = {k: v / wc for k, v in out["per_wave_cycles"].items()}
     # spot parity against the exact path on a few queries
     ref = NearestNeighborsGPU(sp, 0)
     ref.set_mode(1)
