@@ -894,22 +894,26 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
                 td[g] = kdist(tk[g]);
                 return;
             }
+            // every lane that passed the offer's threshold is shifted into the 64-lane list in
+            // turn, with no re-test against the threshold its predecessors tightened: a candidate
+            // above the new k2-th entry lands at a position >= k2 (or falls off the end), so the
+            // first k2 entries — all the walk and its output read — are those of the one-by-one
+            // insertion with a test each, and the k2-th entry is read once, after the loop (the
+            // serial readlane -> 64-bit compare -> branch chain per candidate is gone)
             const uint64_t mk = kpack(d, id);
             while (bm) {
                 const int l = __builtin_ctzll(bm);
                 bm &= bm - 1;
                 const uint64_t ck = readlane_k(mk, l);
-                if (ck < tk[g]) {
 #ifdef OMPL_AMD_PROBE
-                    ++pr_ins;
+                ++pr_ins;
 #endif
-                    const uint64_t pv = shr1_k(Lk[g], 0ull);
-                    const bool lt_prev = lane > 0 && ck < pv;
-                    Lk[g] = lt_prev ? pv : (ck < Lk[g] ? ck : Lk[g]);
-                    tk[g] = readlane_k(Lk[g], k2 - 1);
-                    td[g] = kdist(tk[g]);
-                }
+                const uint64_t pv = shr1_k(Lk[g], 0ull);
+                const bool lt_prev = lane > 0 && ck < pv;
+                Lk[g] = lt_prev ? pv : (ck < Lk[g] ? ck : Lk[g]);
             }
+            tk[g] = readlane_k(Lk[g], k2 - 1);
+            td[g] = kdist(tk[g]);
     };
     auto scan_state = [&](const float (&x)[R], uint32_t id, int tin, const float (&lb)[GH]) {
         relaunder();
