@@ -699,8 +699,43 @@ __device__ __forceinline__ uint64_t shfl_k(uint64_t v, int src) {
 __device__ __forceinline__ uint64_t shfl_xor_k(uint64_t v, int j) {
     return ((uint64_t)(uint32_t)__shfl_xor((int)(v >> 32), j) << 32) | (uint32_t)__shfl_xor((int)v, j);
 }
-__device__ __forceinline__ void bitonic_step_k(uint64_t &k, int j, bool keep_min) {
-    const uint64_t o = shfl_xor_k(k, j);
+// the value of lane ^ j without the LDS crossbar (ds_bpermute waits on lgkmcnt at every stage of
+// a serial network): DPP inside a row of 16 — quad_perm for j = 1, 2, row_shl / row_shr by 4 for
+// j = 4, row_ror:8 for j = 8 — and gfx950's permlane swaps across rows (permlane16_swap trades the
+// odd rows of its first operand with the even rows of its second, permlane32_swap the upper half
+// of the first with the lower half of the second; with both operands v, lane l finds its partner
+// in the first result iff bit j of l is set).  j is a compile-time constant after unrolling.
+__device__ __forceinline__ uint32_t xor_lane_u(uint32_t v, int j, int lane) {
+    switch (j) {
+    case 1: return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+    case 2: return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+    case 4: {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x104, 0xF, 0xF, false);  // row_shl:4
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+        return (lane & 4) ? dn : up;
+    }
+    case 8: return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    case 16: {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    }
+    default: {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    }
+    }
+}
+__device__ __forceinline__ uint64_t xor_lane_k(uint64_t v, int j, int lane) {
+    return ((uint64_t)xor_lane_u((uint32_t)(v >> 32), j, lane) << 32) | xor_lane_u((uint32_t)v, j, lane);
+}
+// the value of lane 63 - lane = lane ^ 63: row_mirror (lane ^ 15 inside each row), then ^ 16, ^ 32
+__device__ __forceinline__ uint64_t reverse_lanes_k(uint64_t v, int lane) {
+    auto mirror = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x140, 0xF, 0xF, false); };
+    const uint64_t m = ((uint64_t)mirror((uint32_t)(v >> 32)) << 32) | mirror((uint32_t)v);
+    return xor_lane_k(xor_lane_k(m, 16, lane), 32, lane);
+}
+__device__ __forceinline__ void bitonic_step_k(uint64_t &k, int j, bool keep_min, int lane) {
+    const uint64_t o = xor_lane_k(k, j, lane);
     if ((o < k) == keep_min) k = o;
 }
 // wave_merge_sorted on packed keys: candidates c (non-candidates kMaxKey) into the sorted list L
@@ -708,11 +743,11 @@ __device__ __forceinline__ void wave_merge_sorted_k(uint64_t &L, uint64_t c, int
 #pragma unroll
     for (int k = 2; k <= 64; k <<= 1)
 #pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) bitonic_step_k(c, j, ((lane & j) == 0) == ((lane & k) == 0));
-    const uint64_t r = shfl_k(c, 63 - lane);
+        for (int j = k >> 1; j > 0; j >>= 1) bitonic_step_k(c, j, ((lane & j) == 0) == ((lane & k) == 0), lane);
+    const uint64_t r = reverse_lanes_k(c, lane);
     if (r < L) L = r;
 #pragma unroll
-    for (int j = 32; j > 0; j >>= 1) bitonic_step_k(L, j, (lane & j) == 0);
+    for (int j = 32; j > 0; j >>= 1) bitonic_step_k(L, j, (lane & j) == 0, lane);
 }
 // candidates in one ballot above which the bulk merge is used.  Measured (G = 4): SE3 1.58 /
 // 1.42 / 1.41 ms at 64 / 8 / 32; R^6 1.60 / 1.12 / 1.13 / 1.21 ms at 64 / 8 / 16 / 32
