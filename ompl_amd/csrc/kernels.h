@@ -111,8 +111,19 @@ struct Q16Geo {
     float lo[8], step[8], inv[8];
 };
 
+// Sorted-store rows are blocked by tile (round 6; were [row][n_pad] SoA): tile t (positions
+// 64 t .. 64 t + 63) holds its R rows in segments of 4 rows — the last one R mod 4 wide — and each
+// segment is position-major, the 4 values of one position side by side, so a wave reads a tile
+// with one 16-byte load per lane per full segment (a contiguous 1 KB per instruction) and one
+// narrower load for the remainder, instead of one 4-byte load per row.
+__host__ __device__ __forceinline__ uint64_t blk_index(uint64_t p, int r, int R) {
+    const int s = r >> 2, w = 4 * s + 4 <= R ? 4 : R - 4 * s;
+    return (p >> 6) * (uint64_t)(64 * R) + (uint64_t)s * 256 + (p & 63) * (uint64_t)w + (uint64_t)(r & 3);
+}
 struct SortedStore {
-    float *rows = nullptr;       // [rows32][n_pad] (SE3 quaternions sign-canonical: w >= 0)
+    float *rows = nullptr;       // R rows per position, blocked by tile (blk_index; SE3 quaternions
+                                 // sign-canonical: w >= 0)
+    int rw = 0;                  // R: fp32 rows per position
     uint32_t *ids = nullptr;     // [n_pad] original id of each sorted slot (kNoId = padding)
     float *tbox = nullptr;       // [tiles][box_w] lo.., hi.. (, eta, pad)
     float *sbox = nullptr;       // [supers][box_w]
@@ -135,10 +146,12 @@ struct SortedStore {
     uint64_t main_covered = 0, covered = 0, removed = 0;
     size_t cap_pos = 0, cap_nodes = 0, cap_inv = 0;  // allocated positions / nodes / inv entries
     uint32_t *qcount = nullptr;  // [pad_tiles + 1] per-tile query counts of the home-key counting sort
-    // KinematicChain: the joint positions as 16-bit fixed point, two per word, [F / 2][n_pad]
-    // (chain_q16_code), re-encoded from `rows` when the store changed (gen != gen16)
-    // SE3 (the radius walk): the 7 coordinates as 16-bit codes over q16 (4 words per state)
+    // KinematicChain: the joint positions as 16-bit fixed point, two per word, F / 2 words per
+    // position (chain_q16_code), re-encoded from `rows` when the store changed (gen != gen16)
+    // SE3 (the radius walk): the 7 coordinates as 16-bit codes over q16 (4 words per position);
+    // blocked by tile like `rows` (blk_index with w16 words)
     uint32_t *rows16 = nullptr;
+    int w16 = 0;
     size_t cap16 = 0;
     uint64_t gen = 0, gen16 = ~0ull;
     Q16Geo q16{};

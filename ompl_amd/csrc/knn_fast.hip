@@ -50,16 +50,17 @@ void free_sorted_store(SortedStore *s) {
 }
 
 namespace {
-__global__ void tombstone_kernel(const uint32_t *__restrict__ inv, uint64_t id, float *__restrict__ rows,
-                                 uint32_t *__restrict__ rows16) {
+__global__ void tombstone_kernel(const uint32_t *__restrict__ inv, uint64_t id, float *__restrict__ rows, int rw,
+                                 uint32_t *__restrict__ rows16, int w16) {
     const uint32_t p = inv[id];
     if (p == kNoId) return;
-    rows[p] = __builtin_nanf("");  // row 0 of the fp32 copy: every distance is NaN
-    if (rows16) rows16[p] |= 0xFFFFu;  // the 16-bit copy's NaN marker (coordinate 0)
+    rows[blk_index(p, 0, rw)] = __builtin_nanf("");  // row 0 of the fp32 copy: every distance is NaN
+    if (rows16) rows16[blk_index(p, 0, w16)] |= 0xFFFFu;  // the 16-bit copy's NaN marker (coordinate 0)
 }
-// thread = sorted position: the F = 2 nm fp32 coordinates (SoA, stride n_pad) to nm words
+// thread = sorted position: the F = 2 nm fp32 coordinates to nm words (both tile-blocked)
 __global__ void chain_rows16_kernel(const float *__restrict__ rows, uint32_t n_pad, uint32_t n, int nm,
                                     uint32_t *__restrict__ r16) {
+    (void)n_pad;
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     bool dead = false;
@@ -68,27 +69,28 @@ __global__ void chain_rows16_kernel(const float *__restrict__ rows, uint32_t n_p
         uint32_t c[2];
         for (int h = 0; h < 2; ++h) {
             const int f = 2 * w + h, li = f < nm ? f : f - nm;
-            const float v = rows[(size_t)f * n_pad + p];
+            const float v = rows[blk_index(p, f, 2 * nm)];
             dead |= !(v == v);
             const float t = rintf((v + (float)(li + 1)) * (kChainQ16 / (float)(2 * (li + 1))));
             c[h] = (uint32_t)fminf(fmaxf(t, 0.f), kChainQ16);
         }
         const uint32_t word = c[0] | (c[1] << 16);
         if (w == 0) w0 = word;
-        else r16[(size_t)w * n_pad + p] = word;
+        else r16[blk_index(p, w, nm)] = word;
     }
-    r16[p] = dead ? (w0 | 0xFFFFu) : w0;
+    r16[blk_index(p, 0, nm)] = dead ? (w0 | 0xFFFFu) : w0;
 }
 // thread = sorted position: the 7 SE3 coordinates to 4 words (the last half unused)
 __global__ void se3_rows16_kernel(const float *__restrict__ rows, uint32_t n_pad, uint32_t n, Q16Geo q,
                                   uint32_t *__restrict__ r16) {
+    (void)n_pad;
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     bool dead = false;
     uint32_t c[8];
 #pragma unroll
     for (int f = 0; f < 7; ++f) {
-        const float v = rows[(size_t)f * n_pad + p];
+        const float v = rows[blk_index(p, f, 7)];
         dead |= !(v == v);
         const float t = rintf((v - q.lo[f]) * q.inv[f]);
         c[f] = (uint32_t)fminf(fmaxf(t, 0.f), kQ16Max);
@@ -96,7 +98,7 @@ __global__ void se3_rows16_kernel(const float *__restrict__ rows, uint32_t n_pad
     c[7] = 0u;
     if (dead) c[0] = 0xFFFFu;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) r16[(size_t)w * n_pad + p] = c[2 * w] | (c[2 * w + 1] << 16);
+    for (int w = 0; w < 4; ++w) r16[blk_index(p, w, 4)] = c[2 * w] | (c[2 * w + 1] << 16);
 }
 }  // namespace
 
@@ -116,6 +118,7 @@ hipError_t refresh_se3_rows16(const double *lo, const double *hi, SortedStore *s
     const uint32_t n = s->ntiles * kCullTile;
     hipLaunchKernelGGL(se3_rows16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, s->rows, s->n_pad, n, q, s->rows16);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    s->w16 = 4;
     s->q16 = q;
     s->gen16 = s->gen;
     return hipSuccess;
@@ -159,6 +162,7 @@ hipError_t refresh_chain_rows16(const FeatGeom &g, SortedStore *s, hipStream_t s
     hipLaunchKernelGGL(chain_rows16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, s->rows, s->n_pad, n, nm,
                        s->rows16);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    s->w16 = nm;
     s->gen16 = s->gen;
     return hipSuccess;
 }
@@ -167,7 +171,8 @@ hipError_t tombstone_sorted_store(SortedStore *s, uint64_t id, hipStream_t st) {
     if (!s->built || id >= s->covered || id >= s->cap_inv) return hipSuccess;
     // a current 16-bit copy is patched in place and stays current
     const bool q16 = s->rows16 && s->gen16 == s->gen;
-    hipLaunchKernelGGL(tombstone_kernel, dim3(1), dim3(1), 0, st, s->inv, id, s->rows, q16 ? s->rows16 : nullptr);
+    hipLaunchKernelGGL(tombstone_kernel, dim3(1), dim3(1), 0, st, s->inv, id, s->rows, s->rw, q16 ? s->rows16 : nullptr,
+                       s->w16);
     s->removed += 1;
     s->gen += 1;
     if (q16) s->gen16 = s->gen;

@@ -67,6 +67,35 @@ struct Geo {
     static constexpr int BW = SP == OMPL_GPU_SPACE_SE3 ? 16 : 2 * F;
 };
 
+// one tile's R rows for this lane (position 64 t + lane) from the tile-blocked store (kernels.h
+// blk_index): a 16-byte load per full segment of 4 rows, one 4 / 8 / 12-byte load for the rest
+template <int R, typename T>
+__device__ __forceinline__ void load_blk(const T *__restrict__ rows, uint32_t t, int lane, T (&x)[R]) {
+    static_assert(sizeof(T) == 4, "32-bit rows");
+    const T *b = rows + (uint64_t)t * (64 * R);
+#pragma unroll
+    for (int s = 0; s < R / 4; ++s) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(b + s * 256 + lane * 4);
+        x[4 * s] = __builtin_bit_cast(T, v.x);
+        x[4 * s + 1] = __builtin_bit_cast(T, v.y);
+        x[4 * s + 2] = __builtin_bit_cast(T, v.z);
+        x[4 * s + 3] = __builtin_bit_cast(T, v.w);
+    }
+    constexpr int Q = R % 4, S = R / 4;
+    if constexpr (Q == 1) {
+        x[R - 1] = b[S * 256 + lane];
+    } else if constexpr (Q == 2) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(b + S * 256 + lane * 2);
+        x[R - 2] = __builtin_bit_cast(T, v.x);
+        x[R - 1] = __builtin_bit_cast(T, v.y);
+    } else if constexpr (Q == 3) {
+        const T *q = b + S * 256 + lane * 3;
+        x[R - 3] = q[0];
+        x[R - 2] = q[1];
+        x[R - 1] = q[2];
+    }
+}
+
 __device__ __forceinline__ float abs1(float x) {  // |x| clamped to 1; NaN stays NaN
     float a = fabsf(x);
     return a > 1.f ? 1.f : a;
@@ -899,10 +928,10 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     };
     auto load_state = [&](uint32_t t, float (&x)[R], uint32_t &id) {
         const uint64_t p = (uint64_t)t * kCullTile + lane;
-#pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = rows[(uint64_t)r * n_pad + p];
+        load_blk<R>(rows, t, lane, x);
         id = (uint32_t)p;  // lists hold sorted positions; the certificate maps them to ids
         (void)ids;
+        (void)n_pad;
     };
     // scan tile tin (index inside its super-tile) against every query whose own box bound
     // lb (held by lane tin + 32 * (g / GH)) is still below its threshold: the tile was
@@ -1551,11 +1580,7 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
         }
     };
     uint32_t visited = 0, qscans = 0;
-    auto load_raw = [&](uint32_t t, uint32_t (&w)[NM]) {
-        const uint64_t p = (uint64_t)t * kCullTile + lane;
-#pragma unroll
-        for (int j = 0; j < NM; ++j) w[j] = rows16[(uint64_t)j * n_pad + p];
-    };
+    auto load_raw = [&](uint32_t t, uint32_t (&w)[NM]) { load_blk<NM>(rows16, t, lane, w); };
     auto decode = [&](const uint32_t (&w)[NM], float (&x)[F]) {
 #pragma unroll
         for (int j = 0; j < NM; ++j) {
@@ -1565,14 +1590,12 @@ __global__ __launch_bounds__(64) void knn32_chain_cull_kernel(
         if ((w[0] & 0xFFFFu) == 0xFFFFu) x[0] = __builtin_nanf("");  // padding / removed
     };
     auto load_tile = [&](uint32_t t, float (&x)[F]) {
-        const uint64_t p = (uint64_t)t * kCullTile + lane;
         if constexpr (Q16) {
             uint32_t w[NM];
             load_raw(t, w);
             decode(w, x);
         } else {
-#pragma unroll
-            for (int f = 0; f < F; ++f) x[f] = rows[(uint64_t)f * n_pad + p];
+            load_blk<F>(rows, t, lane, x);
         }
     };
     // query g against the lane's state x, outermost links first (|P_i(a) - P_i(b)| grows with
@@ -2087,16 +2110,14 @@ __global__ OMPL_RADIUS_LB void radius32_group_kernel(
     };
     auto load_tile = [&](uint32_t ss, int t, float (&x)[R], uint32_t &id) {
         const uint64_t p = (uint64_t)(ss * kSuperTiles + t) * kCullTile + lane;
-#pragma unroll
-        for (int rr = 0; rr < R; ++rr) x[rr] = rows[(uint64_t)rr * n_pad + p];
+        load_blk<R>(rows, ss * kSuperTiles + t, lane, x);
         id = ids[p];
     };
     // Q16: a tile in flight stays raw (4 words per lane) and is decoded when it is scanned, so
     // the next tile's loads overlap the current scan
     auto load_raw = [&](uint32_t ss, int t, uint32_t (&w)[4], uint32_t &id) {
         const uint64_t p = (uint64_t)(ss * kSuperTiles + t) * kCullTile + lane;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = rows16[(uint64_t)j * n_pad + p];
+        load_blk<4>(rows16, ss * kSuperTiles + t, lane, w);
         id = ids[p];
     };
     auto decode = [&](const uint32_t (&w)[4], float (&v)[R]) {
@@ -2737,12 +2758,12 @@ __global__ void sorted_gather_kernel(const float *__restrict__ f32, uint64_t cap
                 for (int r = 3; r < 7; ++r) x[r] = -x[r];
         }
 #pragma unroll
-        for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = x[r];
+        for (int r = 0; r < R; ++r) rows[blk_index(p, r, R)] = x[r];
         ids[p] = id;
         inv[id] = p;
     } else {
 #pragma unroll
-        for (int r = 0; r < R; ++r) rows[(size_t)r * n_pad + p] = __builtin_nanf("");
+        for (int r = 0; r < R; ++r) rows[blk_index(p, r, R)] = __builtin_nanf("");
         ids[p] = kNoId;
     }
 }
@@ -2793,10 +2814,12 @@ __global__ void tile_box_range_kernel(const float *__restrict__ rows, uint32_t n
     const uint32_t t = t0 + blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (t >= t1) return;
-    const uint32_t p = t * kCullTile + lane;
+    float xr[Geo<SP, F>::R];
+    load_blk<Geo<SP, F>::R>(rows, t, lane, xr);
+    (void)n_pad;
     float x[NB];
 #pragma unroll
-    for (int c = 0; c < NB; ++c) x[c] = rows[(size_t)c * n_pad + p];
+    for (int c = 0; c < NB; ++c) x[c] = xr[c];
     const bool ok = x[0] == x[0];  // padding / removed
     float eta = 0.f;
     if constexpr (SP == OMPL_GPU_SPACE_SE3) {
@@ -3475,12 +3498,12 @@ __global__ void kd_rows_store_kernel(const float *__restrict__ W, uint32_t n, ui
         }
         const uint32_t id = __float_as_uint(r[NB]);
 #pragma unroll
-        for (int c = 0; c < R; ++c) rows[(size_t)c * n_pad + p] = r[c];
+        for (int c = 0; c < R; ++c) rows[blk_index(p, c, R)] = r[c];
         ids[p] = id;
         inv[id] = p;
     } else {
 #pragma unroll
-        for (int c = 0; c < R; ++c) rows[(size_t)c * n_pad + p] = __builtin_nanf("");
+        for (int c = 0; c < R; ++c) rows[blk_index(p, c, R)] = __builtin_nanf("");
         ids[p] = kNoId;
     }
 }
@@ -3550,7 +3573,8 @@ hipError_t sorted_alloc(SortedStore *s, uint32_t pad_tiles, uint32_t max_nodes, 
     const size_t n_pad = (size_t)pad_tiles * kCullTile;
     const uint32_t nsup = (pad_tiles + kSuperTiles - 1) / kSuperTiles;
     hipError_t e;
-    if (n_pad > s->cap_pos) {  // rows are laid out with stride n_pad: reallocate all row arrays together
+    s->rw = R;
+    if (n_pad > s->cap_pos) {  // reallocate all per-position arrays together
         size_t dummy = 0;
         if ((e = grow_array(&s->rows, dummy, (size_t)R * n_pad)) != hipSuccess) return e;
         dummy = 0;
