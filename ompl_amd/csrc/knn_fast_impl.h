@@ -784,6 +784,22 @@ __device__ __forceinline__ void wave_merge_sorted_k(uint64_t &L, uint64_t c, int
 // 1.29-1.30 ms, cfg5k 4.06 / 4.10 / 3.93-3.97 / 4.03 / 4.29 ms, cfg2 flat (profiles/r4_ab)
 constexpr int kBulkThreshold = 16;
 
+// LDS-DMA bookkeeping.  The compiler does not order an LDS read after the global_load_lds that
+// fills it (ROCm 7.2 emits no vmcnt for it), so the waits are explicit: vmcnt(0) before reading a
+// filled slot (at that point the DMA is the only vector memory op the walk has in flight),
+// lgkmcnt(0) before the slot is refilled (its reads have returned).  s_waitcnt simm16 on gfx9:
+// vmcnt[3:0] | expcnt << 4 | lgkmcnt << 8 | vmcnt[5:4] << 14.
+__device__ __forceinline__ void lds_dma_wait_all() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void lds_reads_done() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    asm volatile("" ::: "memory");
+}
+
 // translation part of box_lb<SE3>: the squared gap of query row q to box bx
 __device__ __forceinline__ float box_tgap2(const float *bx, const float *q, int NB) {
     float tg = 0.f;
@@ -801,7 +817,11 @@ __device__ __forceinline__ float box_tgap2(const float *bx, const float *q, int 
 // passes; square-root-free rejects before the chord; a translation-only first mask pass; tiles
 // from a 16-bit copy.)
 template <int SP, int F, int K2, int G, bool QS>
-__global__ __launch_bounds__(64) void knn32_group_kernel(
+// (amdgpu_waves_per_eu(8): with the next super-tile's boxes in LDS the walk fits 64 VGPRs and,
+// with the scalar registers it then spills to VGPR lanes, 8 waves per SIMD instead of 7 — cfg3's
+// walk 1.022-1.028 against 1.046-1.049 ms isolated on one box, cfg5k and cfg2 unchanged; the
+// boxes in LDS at 7 waves were slower, 8 waves with the boxes in registers spill to scratch)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ mbox,
     uint32_t nmega, const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
@@ -895,7 +915,7 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     // this lane's row of super-tile s's tile boxes (tile s * 32 + (lane & 31)); rows past
     // the last tile read as empty boxes (lo = +inf, hi = -inf), whose bound is +inf, so no
     // tile past the end is ever fetched (a NaN box would not do: fmaxf drops NaN)
-    auto load_tbox = [&](uint32_t s, float (&bx)[BW]) {
+    auto load_tbox_regs = [&](uint32_t s, float (&bx)[BW]) {
         const uint32_t t = s * kSuperTiles + (lane & 31);
         if (t < ntiles) {
             const float4 *b4 = reinterpret_cast<const float4 *>(tbox + (size_t)t * BW);
@@ -1175,10 +1195,51 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     // bound; the super-tile after sn is popped (a round's box loads included) only after that
     // scan.  Masks use the thresholds of their moment; every tile is re-checked against the
     // current thresholds before it is scanned.  (Measured: 1.27-1.29 -> 1.25-1.26 ms on cfg3.)
-    float bx[BW];
+    // the next super-tile's 32 tile boxes: staged in LDS by LDS-DMA (BW / 8 loads of 1 KB, no
+    // registers held across the scans) when the record width allows, else in registers
+    constexpr bool kLdsBox = BW % 8 == 0;
+    __shared__ __attribute__((aligned(16))) float tbs[kLdsBox ? kSuperTiles * BW : 4];
+    float bx[kLdsBox ? 1 : BW];
+    auto load_tbox = [&](uint32_t sv) {
+        if constexpr (kLdsBox) {
+            lds_reads_done();  // the previous boxes were read out of the slot
+            const char *blk = reinterpret_cast<const char *>(tbox + (size_t)sv * kSuperTiles * BW);
+#pragma unroll
+            for (int j = 0; j < BW / 8; ++j) {
+                // this lane's 16 bytes of piece j; a piece past the last tile reads the first box
+                // instead (never used: mask_of gives tiles past the end empty boxes)
+                const uint32_t off = (uint32_t)j * 1024u + (uint32_t)lane * 16u;
+                const bool in = sv * kSuperTiles + off / (BW * 4) < ntiles;
+                __builtin_amdgcn_global_load_lds((const void *)(in ? blk + off : reinterpret_cast<const char *>(tbox)),
+                                                 (void *)(tbs + j * 256), 16, 0, 0);
+            }
+        } else {
+            load_tbox_regs(sv, bx);
+        }
+    };
     const uint32_t home_s = th / kSuperTiles;
     auto mask_of = [&](int sv, float (&l)[GH]) -> uint32_t {
-        uint32_t mm = tile_mask(bx, l);
+        uint32_t mm;
+        if constexpr (kLdsBox) {
+            float bl[BW];
+            lds_dma_wait_all();  // the boxes' DMA (and nothing later is in flight here)
+            const uint32_t t = (uint32_t)sv * kSuperTiles + (lane & 31);
+            if (t < ntiles) {
+                const float4 *b4 = reinterpret_cast<const float4 *>(tbs + (lane & 31) * BW);
+#pragma unroll
+                for (int c = 0; c < BW / 4; ++c) {
+                    const float4 v = b4[c];
+                    bl[4 * c] = v.x; bl[4 * c + 1] = v.y; bl[4 * c + 2] = v.z; bl[4 * c + 3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < BW; ++c) bl[c] = c < Geo<SP, F>::NB ? __builtin_inff() : -__builtin_inff();
+                if constexpr (SP == OMPL_GPU_SPACE_SE3) bl[2 * Geo<SP, F>::NB] = bl[2 * Geo<SP, F>::NB + 1] = 0.f;
+            }
+            mm = tile_mask(bl, l);
+        } else {
+            mm = tile_mask(bx, l);
+        }
         if ((uint32_t)sv == home_s) mm &= ~(1u << (th % kSuperTiles));  // scanned first
 #ifdef OMPL_AMD_PROBE
         if (!mm) ++pr_empty;
@@ -1191,7 +1252,7 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
     int t = 0, tn = 0, s = -1;
     bool have = false;  // x holds a fetched tile of s
     int sn = next_super();
-    if (sn >= 0) load_tbox((uint32_t)sn, bx);
+    if (sn >= 0) load_tbox((uint32_t)sn);
 #ifdef OMPL_AMD_PROBE
     __builtin_amdgcn_sched_barrier(0);
     pt_pro = __builtin_amdgcn_s_memtime() - pt_start;
@@ -1237,7 +1298,7 @@ __global__ __launch_bounds__(64) void knn32_group_kernel(
         }
         if (consumed) {  // after the scan: a round's box loads wait behind it, not before
             OMPL_PT(pt_next, sn = next_super());
-            if (sn >= 0) load_tbox((uint32_t)sn, bx);
+            if (sn >= 0) load_tbox((uint32_t)sn);
         }
 #ifdef OMPL_AMD_PROBE
         __builtin_amdgcn_sched_barrier(0);
@@ -1961,7 +2022,9 @@ __global__ __launch_bounds__(256) void knn_certify_wave_kernel(const float *__re
 // MODE 2 (SLAB) counts like MODE 0 and also writes the first `slab` hits of each query to its
 // fixed-size slab, so that one walk suffices when no query has more hits than that.
 // (Measured and rejected: 7 / 8 waves per SIMD from the compiler — 72 / 64 VGPRs with 24 / 68 B
-// of scratch spills — against the default's 80 VGPRs, 6 waves.)
+// of scratch spills — against the default's 80 VGPRs, 6 waves; round 6: the next super-tile's
+// boxes staged in LDS by LDS-DMA, 69 VGPRs at 7 waves / 64 at 8 without scratch — 1.24-1.26 /
+// 1.27-1.28 against 1.19-1.22 ms.)
 #define OMPL_RADIUS_LB __launch_bounds__(64)
 // Q16 (SE3, MODE 2; Q16 = false reads the fp32 rows): the tiles come from the 16-bit copy
 // (SortedStore::rows16, 16 B per state against 28), decoded to fp32 once per tile; every
