@@ -817,11 +817,13 @@ __device__ __forceinline__ float box_tgap2(const float *bx, const float *q, int 
 // passes; square-root-free rejects before the chord; a translation-only first mask pass; tiles
 // from a 16-bit copy.)
 template <int SP, int F, int K2, int G, bool QS>
-// (amdgpu_waves_per_eu(8): with the next super-tile's boxes in LDS the walk fits 64 VGPRs and,
-// with the scalar registers it then spills to VGPR lanes, 8 waves per SIMD instead of 7 — cfg3's
-// walk 1.022-1.028 against 1.046-1.049 ms isolated on one box, cfg5k and cfg2 unchanged; the
-// boxes in LDS at 7 waves were slower, 8 waves with the boxes in registers spill to scratch)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void knn32_group_kernel(
+// (amdgpu_waves_per_eu(8), lists of up to 32 lanes: with the next super-tile's boxes in LDS the
+// walk fits 64 VGPRs and, with the scalar registers it then spills to VGPR lanes, 8 waves per SIMD
+// instead of 7 — cfg3's walk 1.022-1.028 against 1.046-1.049 ms isolated on one box, cfg2
+// unchanged; the boxes in LDS at 7 waves were slower, 8 waves with the boxes in registers spill to
+// scratch.  BIT*'s 64-lane lists keep the boxes in registers at 7 waves: 8 waves were no faster
+// (3.22-3.25 against 3.20-3.22 ms) and read 8 % more bytes, the LDS boxes at 7 waves were slower.)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K2 == 64 ? 7 : 8))) void knn32_group_kernel(
     const float *__restrict__ rows, uint32_t n_pad, const uint32_t *__restrict__ ids, uint32_t ntiles,
     const float *__restrict__ tbox, const float *__restrict__ sbox, uint32_t nsuper, const float *__restrict__ mbox,
     uint32_t nmega, const uint32_t *__restrict__ tkey0, const float *__restrict__ q32, const uint32_t *__restrict__ qkeys,
@@ -1197,7 +1199,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void kn
     // current thresholds before it is scanned.  (Measured: 1.27-1.29 -> 1.25-1.26 ms on cfg3.)
     // the next super-tile's 32 tile boxes: staged in LDS by LDS-DMA (BW / 8 loads of 1 KB, no
     // registers held across the scans) when the record width allows, else in registers
-    constexpr bool kLdsBox = BW % 8 == 0;
+    constexpr bool kLdsBox = BW % 8 == 0 && K2 < 64;
     __shared__ __attribute__((aligned(16))) float tbs[kLdsBox ? kSuperTiles * BW : 4];
     float bx[kLdsBox ? 1 : BW];
     auto load_tbox = [&](uint32_t sv) {
