@@ -111,8 +111,8 @@ def sq_issue(workload, kernel, waves, kern_ms):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="cfg3", choices=sorted(DEFAULTS))
     ap.add_argument("--tree", type=int, default=None)
     ap.add_argument("--queries", type=int, default=None, help="samples / milestones / vertices per GPU per step")
@@ -1206,7 +1206,7 @@ def spawn_ranks(n):
     sys.exit(rc)
 
 
-SUB_WORKLOADS = {  # the default line's `workloads` record: every other config, same steps / warmup
+SUB_WORKLOADS = {  # the default line's `workloads` record: every other config, same steps / warmup (cfg4: at most 5 / 2, sub_args)
     # the headline's strong-scaling forms: 10^5 samples in total over the N GPUs on the replicated
     # tree, and the tree sharded over the ranks (every sample answered by every shard, merged)
     "cfg3_strong": {"workload": "cfg3", "scaling": "strong"},
@@ -1227,6 +1227,10 @@ def sub_args(args, spec):
     a.scaling = spec.get("scaling", "weak")
     a.tree, a.queries, a.k = DEFAULTS[a.workload]
     a.exact = False
+    if a.workload == "cfg4":
+        # each PRM* batch grows the roadmap by 8,192 milestones: 2 + 5 batches keep it within 6 % of
+        # the configuration's 10^6 vertices (20 + 10 would take it to 1.25 * 10^6)
+        a.steps, a.warmup = min(a.steps, 5), min(a.warmup, 2)
     return a
 
 
