@@ -1329,6 +1329,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(K2 == 64 ? 7
             break;
         }
     }
+    // every staged box DMA was consumed by a mask before the loop could end; wait anyway, so that no
+    // LDS-DMA can land in LDS the next workgroup on this CU already owns
+    if constexpr (kLdsBox) lds_dma_wait_all();
     if (counters && lane == 0) {
         unsigned long long *cs = counters + (blockIdx.x % kCounterSlots) * kCounterStride;
         atomicAdd(&cs[0], (unsigned long long)visited);  // tiles scanned
