@@ -321,6 +321,32 @@ def test_bounded_rerun_se3_near_rotations(gpu):
     assert_knn_parity(ids, d, oi, od, 10)
 
 
+def test_rerun_beyond_bounded_capacity(gpu):
+    """More uncertified queries than the bounded pass takes (512): the persistent re-run launch
+    (knn.hip knn_rerun_kernel: bounded pass, rank select, full scans between grid-wide barriers)
+    moves the excess to the full-scan list in its second phase and answers it in its third; every
+    list must still be the oracle's, and a second batch on the same handle (the barrier counter
+    re-zeroed by the batch's first kernel) must be too."""
+    rng = np.random.default_rng(38)
+    sp = SE3StateSpace()
+    n = 30000
+    v = rng.normal(0, 1e-3, (n, 3))
+    quat = np.column_stack([v, np.ones(n)])
+    quat /= np.linalg.norm(quat, axis=1, keepdims=True)
+    data = np.column_stack([rng.uniform(0, 1, (n, 3)) * 0.02, quat])
+    nn = NearestNeighborsGPU(sp, gpu)
+    nn.add(data)
+    for rep in range(2):
+        q = data[rng.choice(n, 1500, replace=False)].copy()
+        q[:, :3] += rng.normal(0, 1e-4, (1500, 3))
+        s0, f0 = nn.stats()
+        ids, d, _ = nn.nearestKBatch(q, 10)
+        s1, f1 = nn.stats()
+        assert s1 - s0 == 1500 and f1 - f0 > 512, (rep, f1 - f0)
+        oi, od = _oracle_ext(sp, data, q, 10)
+        assert_knn_parity(ids, d, oi, od, 10)
+
+
 def test_bounded_rerun_overflow_takes_full_path(gpu):
     """2,000 identical copies of one state: every query next to it has more than the bounded
     re-run's candidate cap (1,024) at d <= its k-th distance, so the full exact scan answers."""
